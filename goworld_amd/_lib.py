@@ -1,0 +1,146 @@
+"""ctypes binding of libgwaoi.so (include/gwaoi.h, include/gwaoi_tools.h).
+
+The product path is the HIP library only: if libgwaoi.so is missing or cannot be loaded this module
+raises; there is no CPU fallback. Import torch (if at all) BEFORE this module so the process uses
+one HIP runtime (torch's bundled libamdhip64.so.7 and /opt/rocm's share the soname).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(HERE, "libgwaoi.so")
+
+GWAOI_OK = 0
+GWAOI_ERR_INVALID = -1
+GWAOI_ERR_STATE = -2
+GWAOI_ERR_HIP = -3
+GWAOI_ERR_NOMEM = -4
+GWAOI_ERR_DEVICE_CHECK = -5
+GWAOI_EV_ENTER = 0x80000000
+GWAOI_EV_SLOT_MASK = 0x7FFFFFFF
+GWAOI_TICK_DEVICE_EVENTS = 1
+
+# every symbol declared by include/gwaoi.h and include/gwaoi_tools.h
+ABI_SYMBOLS = (
+    "gwaoi_create", "gwaoi_create_spaces", "gwaoi_destroy", "gwaoi_set_stream", "gwaoi_enter",
+    "gwaoi_enter_space", "gwaoi_stage_enters", "gwaoi_leave", "gwaoi_moved", "gwaoi_stage_moves", "gwaoi_stage_moves_device",
+    "gwaoi_tick", "gwaoi_tick_ex", "gwaoi_count", "gwaoi_export_relation", "gwaoi_set_timing",
+    "gwaoi_get_stats", "gwaoi_reset_stats", "gwaoi_version", "gwaoi_last_error",
+)
+TOOL_SYMBOLS = (
+    "gwaoi_device_count", "gwaoi_dev_malloc", "gwaoi_dev_free", "gwaoi_dev_htod", "gwaoi_dev_dtoh",
+    "gwaoi_dev_sync", "gwaoi_wl_init", "gwaoi_wl_step", "gwaoi_wl_iota", "gwaoi_debug_set_next_seq",
+    "gwaoi_debug_set_cells_per_dist",
+)
+
+
+class GwaoiError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"gwaoi error {code}: {msg}")
+        self.code = code
+
+
+class Event(ctypes.Structure):
+    _fields_ = [("mover", ctypes.c_uint32), ("other", ctypes.c_uint32)]
+
+
+class Events(ctypes.Structure):
+    _fields_ = [
+        ("events", ctypes.POINTER(Event)),
+        ("count", ctypes.c_uint64),
+        ("n_enter", ctypes.c_uint64),
+        ("n_leave", ctypes.c_uint64),
+        ("n_subticks", ctypes.c_uint32),
+        ("n_ops", ctypes.c_uint32),
+    ]
+
+
+class SpaceDesc(ctypes.Structure):
+    _fields_ = [("dist", ctypes.c_float), ("min_x", ctypes.c_float), ("min_z", ctypes.c_float),
+                ("max_x", ctypes.c_float), ("max_z", ctypes.c_float)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("ticks", ctypes.c_uint64),
+        ("ms_apply", ctypes.c_double),
+        ("ms_grid", ctypes.c_double),
+        ("ms_sweep", ctypes.c_double),
+        ("ms_order", ctypes.c_double),
+        ("ms_total", ctypes.c_double),
+        ("sweep_movers", ctypes.c_uint64),
+        ("events", ctypes.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def load(path: str = SO_PATH):
+    """Load libgwaoi.so (raises if it is missing: build it with `python -m goworld_amd.build`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"libgwaoi.so not found at {path}: run `python -m goworld_amd.build` "
+                          "(the AOI engine has no CPU fallback)")
+    L = ctypes.CDLL(path)
+    u32 = ctypes.c_uint32
+    u64 = ctypes.c_uint64
+    f32 = ctypes.c_float
+    vp = ctypes.c_void_p
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    f32p = ctypes.POINTER(ctypes.c_float)
+    mgrp = ctypes.POINTER(vp)
+    sig = {
+        "gwaoi_create": ([f32, u32, ctypes.c_int, mgrp], ctypes.c_int),
+        "gwaoi_create_spaces": ([ctypes.POINTER(SpaceDesc), u32, u32, ctypes.c_int, mgrp], ctypes.c_int),
+        "gwaoi_destroy": ([vp], ctypes.c_int),
+        "gwaoi_set_stream": ([vp, vp], ctypes.c_int),
+        "gwaoi_enter": ([vp, u32, f32, f32], ctypes.c_int),
+        "gwaoi_enter_space": ([vp, u32, u32, f32, f32], ctypes.c_int),
+        "gwaoi_stage_enters": ([vp, u32, u32p, f32p, f32p, u32], ctypes.c_int),
+        "gwaoi_leave": ([vp, u32], ctypes.c_int),
+        "gwaoi_moved": ([vp, u32, f32, f32], ctypes.c_int),
+        "gwaoi_stage_moves": ([vp, u32p, f32p, f32p, u32], ctypes.c_int),
+        "gwaoi_stage_moves_device": ([vp, vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_tick": ([vp, ctypes.POINTER(Events)], ctypes.c_int),
+        "gwaoi_tick_ex": ([vp, u32, ctypes.POINTER(Events)], ctypes.c_int),
+        "gwaoi_count": ([vp, u32p, u32p], ctypes.c_int),
+        "gwaoi_export_relation": ([vp, u32p, u32p, u64, ctypes.POINTER(u64)], ctypes.c_int),
+        "gwaoi_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
+        "gwaoi_get_stats": ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
+        "gwaoi_reset_stats": ([vp], ctypes.c_int),
+        "gwaoi_version": ([], ctypes.c_char_p),
+        "gwaoi_last_error": ([], ctypes.c_char_p),
+        "gwaoi_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        "gwaoi_dev_malloc": ([ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)], ctypes.c_int),
+        "gwaoi_dev_free": ([ctypes.c_int, vp], ctypes.c_int),
+        "gwaoi_dev_htod": ([ctypes.c_int, vp, vp, ctypes.c_size_t], ctypes.c_int),
+        "gwaoi_dev_dtoh": ([ctypes.c_int, vp, vp, ctypes.c_size_t], ctypes.c_int),
+        "gwaoi_dev_sync": ([ctypes.c_int], ctypes.c_int),
+        "gwaoi_wl_init": ([ctypes.c_int, vp, vp, u32, u64, f32], ctypes.c_int),
+        "gwaoi_wl_step": ([ctypes.c_int, vp, vp, vp, vp, u32, u64, u64, f32, f32], ctypes.c_int),
+        "gwaoi_wl_iota": ([ctypes.c_int, vp, u32], ctypes.c_int),
+        "gwaoi_debug_set_next_seq": ([vp, u32], ctypes.c_int),
+        "gwaoi_debug_set_cells_per_dist": ([vp, f32], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != GWAOI_OK:
+        raise GwaoiError(rc, (load().gwaoi_last_error() or b"").decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = load().gwaoi_device_count(ctypes.byref(n))
+    return n.value if rc == GWAOI_OK else 0

@@ -1,0 +1,58 @@
+"""Build libgwaoi.so (hand-written HIP for gfx950) in-tree: goworld_amd/libgwaoi.so.
+
+Called by __graft_entry__.build(); runnable as `python -m goworld_amd.build`. hipcc cross-compiles
+for gfx950 without a GPU. IEEE binary32 semantics are part of the product's contract (bit-exact
+AOI events), hence -ffp-contract=off and preserved denormals.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libgwaoi.so")
+SOURCES = ["gwaoi_kernels.hip", "gwaoi_runtime.hip"]
+HEADERS = ["gwaoi_internal.h"]
+PUBLIC = ["gwaoi.h", "gwaoi_tools.h", "gwaoi_workload.h"]
+ARCH = os.environ.get("GWAOI_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for p in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if p and os.path.exists(p):
+            return p
+    return "hipcc"
+
+
+def _stale() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", f) for f in PUBLIC]
+    deps.append(os.path.abspath(__file__))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return OUT
+    cmd = [
+        hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+        "-ffp-contract=off", "-fno-fast-math", "-fno-gpu-flush-denormals-to-zero",
+        "-Wall", "-Wno-unused-result", "-Wno-unused-value",
+        f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
+        *[os.path.join(CSRC, f) for f in SOURCES],
+        "-o", OUT + ".tmp",
+    ]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

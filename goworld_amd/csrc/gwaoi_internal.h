@@ -1,0 +1,127 @@
+// gwaoi_internal.h — data layout shared by the gfx950 kernels (gwaoi_kernels.hip) and the host
+// runtime (gwaoi_runtime.hip). See DESIGN.md "Data layout in HBM".
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gw {
+
+// Op kinds staged by the host (the reference's three AOIManager calls, Space.go:211/221, 243, 259).
+enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2 };
+
+// Device-side error bits (device-staged batches are validated on the GPU).
+enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u };
+
+// Counters block in device memory (one 64-B line).
+enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_N = 16 };
+
+// Cell geometry of one Space inside one grid snapshot. A grid is a counting sort of every present
+// entity by cell key = base + cz * ncx + cx; the cells of one row of one Space are contiguous, so a
+// query box is (rows) x (one contiguous segment per row).
+struct Geom {
+  float x0, z0;   // origin of cell (0,0)
+  float inv_c;    // 1 / cell side
+  float D;        // AOI distance of the Space (manager-wide per Space, as NewXZListAOIManager)
+  int32_t ncx, ncz;
+  uint32_t base;  // first cell key of this Space
+  uint32_t pad;
+};
+
+// One grid snapshot: all present entities sorted by cell. ent[j] = {x bits, z bits, slot, seq}.
+struct GridView {
+  const uint4* ent;
+  const uint32_t* cs;    // cell_start[ncells + 1]
+  const uint32_t* side;  // side[j] = op seq of entry j's slot this pass (old-grid role), else stale
+  const Geom* geom;      // [nspaces]
+};
+
+struct ApplyArgs {
+  const uint32_t* op_slot;
+  const float* op_x;
+  const float* op_z;
+  const uint8_t* op_kind;    // null => all OP_MOVE (device-staged batch)
+  const uint32_t* op_space;  // space of OP_ENTER ops
+  uint32_t n_ops;
+  uint32_t base;             // seq of op 0; op i gets seq base + i
+  uint32_t cap;
+  uint32_t batch;            // pass id, for duplicate detection of device-staged batches
+  int check;                 // validate (device-staged)
+  float* pos_x;
+  float* pos_z;
+  uint32_t* seq;             // 0 = absent
+  uint32_t* space_of;
+  float* old_x;
+  float* old_z;
+  uint32_t* old_seq;
+  uint32_t* stamp;
+  uint32_t* old_side;        // side array of the old grid
+  const uint32_t* old_gidx;  // slot -> entry index in the old grid
+  uint32_t* ctr;
+};
+
+struct BinArgs {
+  const float* pos_x;
+  const float* pos_z;
+  const uint32_t* seq;
+  const uint32_t* space_of;
+  const Geom* geom;
+  uint32_t cap;
+  uint32_t* key_of;
+  uint32_t* local_of;
+  uint32_t* cs;      // counts, then (after scan) cell_start
+  uint4* ent;
+  uint32_t* gidx;
+};
+
+struct SweepArgs {
+  GridView og;  // old grid: state at the start of the pass
+  GridView ng;  // new grid: state at the end of the pass
+  const float* old_x;
+  const float* old_z;
+  const uint32_t* old_seq;
+  const uint32_t* space_of;
+  uint32_t base;    // seq of op 0 of this pass
+  uint32_t n_new;   // entries in the new grid
+  const uint32_t* op_slot;    // for the leave path
+  const uint32_t* leave_ops;  // op indices of OP_LEAVE ops
+  uint32_t n_leaves;
+  uint4* ev_tmp;    // {rank, local index within rank, mover, other|kind}
+  uint32_t ev_cap;
+  uint32_t* rank_cnt;
+  uint32_t* ctr;
+};
+
+struct RelArgs {
+  GridView g;
+  const float* pos_x;
+  const float* pos_z;
+  const uint32_t* seq;
+  const uint32_t* space_of;
+  uint32_t cap;
+  const uint32_t* row_ptr;  // null in the count pass
+  uint32_t* row_cnt;        // count pass output
+  uint32_t* cols;
+};
+
+// ---- launchers (gwaoi_kernels.hip) ----
+void launch_apply(const ApplyArgs& a, hipStream_t st);
+void launch_bin_count(const BinArgs& a, hipStream_t st);
+void launch_bin_scatter(const BinArgs& a, hipStream_t st);
+// In-place exclusive scan of d[0..n); d[n-1] must be 0 on entry if the total is wanted there.
+// part: scratch of scan_part_words(n) words.
+void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st);
+uint32_t scan_part_words(uint32_t n);
+void launch_sweep(const SweepArgs& a, hipStream_t st);
+void launch_sweep_leaves(const SweepArgs& a, hipStream_t st);
+void launch_place(const uint4* ev_tmp, const uint32_t* ctr, uint32_t ev_cap, const uint32_t* rank_off,
+                  uint2* ev_out, hipStream_t st);
+void launch_slice_sort(const uint32_t* rank_off, uint32_t n_ops, uint2* ev_out, hipStream_t st);
+void launch_relation(const RelArgs& a, hipStream_t st);
+void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, hipStream_t st);
+void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st);
+void launch_wl_step(const float* xp, const float* zp, float* xo, float* zo, uint32_t n, uint64_t seed,
+                    uint64_t tick, float L, float s, hipStream_t st);
+void launch_iota(uint32_t* d, uint32_t n, hipStream_t st);
+
+}  // namespace gw

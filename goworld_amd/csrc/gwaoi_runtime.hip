@@ -1,0 +1,1020 @@
+// gwaoi_runtime.hip — host runtime of libgwaoi: manager state, op staging, the per-tick pipeline
+// and the C ABI of include/gwaoi.h (the drop-in boundary for go-aoi's AOIManager,
+// /root/reference/engine/entity/Space.go:33,105,211,221,243,259).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "gwaoi.h"
+#include "gwaoi_internal.h"
+#include "gwaoi_tools.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+#define HIPCHK(x)                                                                               \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) {                                                                     \
+      set_err("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_));                   \
+      return GWAOI_ERR_HIP;                                                                     \
+    }                                                                                           \
+  } while (0)
+
+#define RCHK(x)              \
+  do {                       \
+    int r_ = (x);            \
+    if (r_ != GWAOI_OK) return r_; \
+  } while (0)
+
+constexpr uint32_t kSeqLimit = 0x7ff00000u;  // renormalise seqs before they pass this
+
+template <class T>
+int dalloc(T** p, size_t n) {
+  *p = nullptr;
+  if (!n) n = 1;
+  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+  if (e != hipSuccess) {
+    set_err("hipMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+    *p = nullptr;
+    return GWAOI_ERR_NOMEM;
+  }
+  return GWAOI_OK;
+}
+
+template <class T>
+int halloc(T** p, size_t n) {
+  *p = nullptr;
+  if (!n) n = 1;
+  hipError_t e = hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault);
+  if (e != hipSuccess) {
+    set_err("hipHostMalloc(%zu bytes): %s", n * sizeof(T), hipGetErrorString(e));
+    *p = nullptr;
+    return GWAOI_ERR_NOMEM;
+  }
+  return GWAOI_OK;
+}
+
+struct SpaceHost {
+  gwaoi_space_desc desc;
+  bool auto_extent;
+  // auto-extent tracking (host-staged coordinates)
+  float seen_minx, seen_minz, seen_maxx, seen_maxz;
+  bool seen_any;
+  // extent the current geometry covers
+  float gx0, gz0, gx1, gz1;
+};
+
+struct Grid {
+  uint4* ent = nullptr;
+  uint32_t* cs = nullptr;
+  uint32_t* side = nullptr;
+  uint32_t* gidx = nullptr;
+  gw::Geom* d_geom = nullptr;
+  std::vector<gw::Geom> h_geom;  // what d_geom holds
+  uint32_t ncells = 0;
+};
+
+}  // namespace
+
+struct gwaoi_mgr {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  uint32_t cap = 0;
+  uint32_t nspaces = 0;
+  std::vector<SpaceHost> spaces;
+  float cells_per_dist = 2.0f;
+  uint32_t max_cells = 0;
+  bool broken = false;
+
+  // ---- host mirror of the staged state ----
+  std::vector<uint8_t> h_present;
+  std::vector<uint32_t> h_space_of;
+  std::vector<uint32_t> h_stamp;  // pass id the slot was staged in
+  uint32_t pass_id = 1;           // id of the pass being staged
+  uint32_t n_present = 0;         // after staged ops
+  uint32_t n_present_dev = 0;     // after the last executed pass
+
+  // ---- staged ops (pinned) ----
+  uint32_t* h_op_slot = nullptr;
+  float* h_op_x = nullptr;
+  float* h_op_z = nullptr;
+  uint8_t* h_op_kind = nullptr;
+  uint32_t* h_op_space = nullptr;
+  uint32_t* h_leaves = nullptr;
+  uint32_t n_ops = 0, n_leaves = 0;
+  bool geom_dirty = true;
+  // device-staged batch
+  const uint32_t* dv_slot = nullptr;
+  const float* dv_x = nullptr;
+  const float* dv_z = nullptr;
+  uint32_t dv_n = 0;
+
+  // ---- device state ----
+  float *pos_x = nullptr, *pos_z = nullptr, *old_x = nullptr, *old_z = nullptr;
+  uint32_t *seq = nullptr, *space_of = nullptr, *old_seq = nullptr, *stamp = nullptr;
+  uint32_t *key_of = nullptr, *local_of = nullptr;
+  uint32_t *d_op_slot = nullptr, *d_op_space = nullptr, *d_leaves = nullptr;
+  float *d_op_x = nullptr, *d_op_z = nullptr;
+  uint8_t* d_op_kind = nullptr;
+  Grid grid[2];
+  int cur = 0;  // grid holding the current state
+  uint32_t next_seq = 1;
+  uint32_t* rank_cnt = nullptr;  // [cap + 1]
+  uint32_t* part = nullptr;
+  uint32_t part_words = 0;
+  uint32_t* ctr = nullptr;       // [CTR_N]
+  uint32_t* h_ctr = nullptr;     // pinned
+  // events
+  uint4* ev_tmp = nullptr;
+  uint2* ev_out = nullptr;   // device, accumulated over the passes of one tick
+  gwaoi_event* h_ev = nullptr;  // pinned, accumulated over the passes of one tick
+  uint64_t ev_cap = 0;       // capacity of ev_out / h_ev
+  uint32_t tmp_cap = 0;      // capacity of ev_tmp
+  uint64_t tick_events = 0, tick_enter = 0;  // accumulated over the passes since the last tick
+  uint32_t tick_passes = 0, tick_ops = 0;
+  bool acc_open = false;                      // a pass ran since the last gwaoi_tick
+
+  // timing
+  bool timing = false;
+  hipEvent_t tev[5] = {};
+  gwaoi_stats stats = {};
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// geometry
+
+void space_extent(const SpaceHost& sh, float* x0, float* z0, float* x1, float* z1) {
+  if (!sh.auto_extent) {
+    *x0 = sh.desc.min_x;
+    *z0 = sh.desc.min_z;
+    *x1 = sh.desc.max_x;
+    *z1 = sh.desc.max_z;
+    return;
+  }
+  if (!sh.seen_any) {
+    *x0 = *z0 = -1000.0f;  // Space.GetSpaceRange default (Space.go:51-53)
+    *x1 = *z1 = 1000.0f;
+    return;
+  }
+  const float D = sh.desc.dist;
+  const float wx = sh.seen_maxx - sh.seen_minx, wz = sh.seen_maxz - sh.seen_minz;
+  *x0 = sh.seen_minx - 0.125f * wx - D;
+  *x1 = sh.seen_maxx + 0.125f * wx + D;
+  *z0 = sh.seen_minz - 0.125f * wz - D;
+  *z1 = sh.seen_maxz + 0.125f * wz + D;
+}
+
+void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
+  out.resize(m->nspaces);
+  const uint64_t share = std::max<uint64_t>(16, m->max_cells / std::max<uint32_t>(1, m->nspaces));
+  uint32_t base = 0;
+  for (uint32_t s = 0; s < m->nspaces; ++s) {
+    SpaceHost& sh = m->spaces[s];
+    float x0, z0, x1, z1;
+    space_extent(sh, &x0, &z0, &x1, &z1);
+    if (!std::isfinite(x0) || !std::isfinite(x1) || !(x1 > x0)) { x0 = -1000.f; x1 = 1000.f; }
+    if (!std::isfinite(z0) || !std::isfinite(z1) || !(z1 > z0)) { z0 = -1000.f; z1 = 1000.f; }
+    double c = (double)sh.desc.dist / (double)m->cells_per_dist;
+    if (!(c > 0)) c = 1.0;
+    auto dims = [&](double cc, int64_t* nx, int64_t* nz) {
+      *nx = (int64_t)(((double)x1 - x0) / cc) + 1;
+      *nz = (int64_t)(((double)z1 - z0) / cc) + 1;
+    };
+    int64_t nx, nz;
+    dims(c, &nx, &nz);
+    while ((uint64_t)(nx * nz) > share || nx > (1 << 22) || nz > (1 << 22)) {
+      c *= 1.25;
+      dims(c, &nx, &nz);
+    }
+    gw::Geom g;
+    g.x0 = x0;
+    g.z0 = z0;
+    g.inv_c = (float)(1.0 / c);
+    g.D = sh.desc.dist;
+    g.ncx = (int32_t)nx;
+    g.ncz = (int32_t)nz;
+    g.base = base;
+    g.pad = 0;
+    base += (uint32_t)(nx * nz);
+    sh.gx0 = x0;
+    sh.gz0 = z0;
+    sh.gx1 = x1;
+    sh.gz1 = z1;
+    out[s] = g;
+  }
+}
+
+uint32_t total_cells(const std::vector<gw::Geom>& g) {
+  uint32_t t = 0;
+  for (auto& x : g) t += (uint32_t)(x.ncx * x.ncz);
+  return t;
+}
+
+bool same_geom(const std::vector<gw::Geom>& a, const std::vector<gw::Geom>& b) {
+  return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(gw::Geom)) == 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+
+int ensure_events(gwaoi_mgr* m, uint64_t need_out, uint32_t need_tmp, uint64_t keep) {
+  if (need_tmp > m->tmp_cap) {
+    uint32_t nc = std::max<uint32_t>(need_tmp, m->tmp_cap * 2);
+    if (m->ev_tmp) hipFree(m->ev_tmp);
+    m->ev_tmp = nullptr;
+    RCHK(dalloc(&m->ev_tmp, nc));
+    m->tmp_cap = nc;
+  }
+  if (need_out > m->ev_cap) {
+    uint64_t nc = std::max<uint64_t>(need_out, m->ev_cap * 2);
+    uint2* nd = nullptr;
+    gwaoi_event* nh = nullptr;
+    RCHK(dalloc(&nd, nc));
+    int r = halloc(&nh, nc);
+    if (r) {
+      hipFree(nd);
+      return r;
+    }
+    if (keep) {
+      HIPCHK(hipMemcpyAsync(nd, m->ev_out, keep * sizeof(uint2), hipMemcpyDeviceToDevice, m->stream));
+      std::memcpy(nh, m->h_ev, keep * sizeof(gwaoi_event));
+      HIPCHK(hipStreamSynchronize(m->stream));
+    }
+    if (m->ev_out) hipFree(m->ev_out);
+    if (m->h_ev) hipHostFree(m->h_ev);
+    m->ev_out = nd;
+    m->h_ev = nh;
+    m->ev_cap = nc;
+  }
+  return GWAOI_OK;
+}
+
+int upload_geom(gwaoi_mgr* m, Grid& g, const std::vector<gw::Geom>& geo) {
+  if (same_geom(g.h_geom, geo)) return GWAOI_OK;
+  g.h_geom = geo;
+  g.ncells = total_cells(geo);
+  HIPCHK(hipMemcpyAsync(g.d_geom, g.h_geom.data(), geo.size() * sizeof(gw::Geom), hipMemcpyHostToDevice,
+                        m->stream));
+  return GWAOI_OK;
+}
+
+// Build grid `gi` from the per-slot state (pos, seq, space_of).
+int build_grid(gwaoi_mgr* m, int gi) {
+  Grid& g = m->grid[gi];
+  HIPCHK(hipMemsetAsync(g.cs, 0, (size_t)(g.ncells + 1) * sizeof(uint32_t), m->stream));
+  gw::BinArgs b;
+  b.pos_x = m->pos_x;
+  b.pos_z = m->pos_z;
+  b.seq = m->seq;
+  b.space_of = m->space_of;
+  b.geom = g.d_geom;
+  b.cap = m->cap;
+  b.key_of = m->key_of;
+  b.local_of = m->local_of;
+  b.cs = g.cs;
+  b.ent = g.ent;
+  b.gidx = g.gidx;
+  gw::launch_bin_count(b, m->stream);
+  gw::launch_scan(g.cs, g.ncells + 1, m->part, m->stream);
+  gw::launch_bin_scatter(b, m->stream);
+  HIPCHK(hipGetLastError());
+  return GWAOI_OK;
+}
+
+// Rank-compress every present slot's seq (order preserved) when the counter nears its limit.
+int renormalise(gwaoi_mgr* m) {
+  HIPCHK(hipStreamSynchronize(m->stream));
+  std::vector<uint32_t> q(m->cap);
+  HIPCHK(hipMemcpy(q.data(), m->seq, m->cap * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  std::vector<std::pair<uint32_t, uint32_t>> v;
+  v.reserve(m->n_present_dev);
+  for (uint32_t s = 0; s < m->cap; ++s)
+    if (q[s]) v.emplace_back(q[s], s);
+  std::sort(v.begin(), v.end());
+  for (size_t i = 0; i < v.size(); ++i) q[v[i].second] = (uint32_t)i + 1;
+  HIPCHK(hipMemcpy(m->seq, q.data(), m->cap * sizeof(uint32_t), hipMemcpyHostToDevice));
+  for (int gi = 0; gi < 2; ++gi)
+    HIPCHK(hipMemsetAsync(m->grid[gi].side, 0, (size_t)m->cap * sizeof(uint32_t), m->stream));
+  RCHK(build_grid(m, m->cur));
+  m->next_seq = (uint32_t)v.size() + 1;
+  HIPCHK(hipStreamSynchronize(m->stream));
+  return GWAOI_OK;
+}
+
+void reset_tick(gwaoi_mgr* m) {
+  m->tick_events = 0;
+  m->tick_enter = 0;
+  m->tick_passes = 0;
+  m->tick_ops = 0;
+}
+
+// Run the device pipeline over the staged batch (host ops or the device batch). Events accumulate
+// (device buffer always, host buffer when copy_events) until the next gwaoi_tick returns them.
+int run_pass(gwaoi_mgr* m, bool copy_events) {
+  const bool dev = m->dv_n != 0;
+  const uint32_t n_ops = dev ? m->dv_n : m->n_ops;
+  if (!n_ops) return GWAOI_OK;
+  if (!m->acc_open) {
+    reset_tick(m);
+    m->acc_open = true;
+  }
+  if ((uint64_t)m->next_seq + n_ops >= kSeqLimit) RCHK(renormalise(m));
+  const uint32_t base = m->next_seq;
+  m->next_seq += n_ops;
+  const int og = m->cur, ng = m->cur ^ 1;
+  hipStream_t st = m->stream;
+
+  // geometry of the new grid: the latest geometry (recomputed when auto extents grew)
+  std::vector<gw::Geom> geo = m->grid[og].h_geom;
+  if (m->geom_dirty) {
+    compute_geometry(m, geo);
+    m->geom_dirty = false;
+  }
+  RCHK(upload_geom(m, m->grid[ng], geo));
+
+  if (m->timing) HIPCHK(hipEventRecord(m->tev[0], st));
+  if (!dev) {
+    HIPCHK(hipMemcpyAsync(m->d_op_slot, m->h_op_slot, n_ops * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->d_op_x, m->h_op_x, n_ops * sizeof(float), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->d_op_z, m->h_op_z, n_ops * sizeof(float), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->d_op_kind, m->h_op_kind, n_ops, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->d_op_space, m->h_op_space, n_ops * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    if (m->n_leaves)
+      HIPCHK(hipMemcpyAsync(m->d_leaves, m->h_leaves, m->n_leaves * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipMemsetAsync(m->ctr, 0, gw::CTR_N * sizeof(uint32_t), st));
+
+  gw::ApplyArgs a;
+  a.op_slot = dev ? m->dv_slot : m->d_op_slot;
+  a.op_x = dev ? m->dv_x : m->d_op_x;
+  a.op_z = dev ? m->dv_z : m->d_op_z;
+  a.op_kind = dev ? nullptr : m->d_op_kind;
+  a.op_space = m->d_op_space;
+  a.n_ops = n_ops;
+  a.base = base;
+  a.cap = m->cap;
+  a.batch = m->pass_id;
+  a.check = dev ? 1 : 0;
+  a.pos_x = m->pos_x;
+  a.pos_z = m->pos_z;
+  a.seq = m->seq;
+  a.space_of = m->space_of;
+  a.old_x = m->old_x;
+  a.old_z = m->old_z;
+  a.old_seq = m->old_seq;
+  a.stamp = m->stamp;
+  a.old_side = m->grid[og].side;
+  a.old_gidx = m->grid[og].gidx;
+  a.ctr = m->ctr;
+  gw::launch_apply(a, st);
+  HIPCHK(hipGetLastError());
+  if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
+
+  RCHK(build_grid(m, ng));
+  if (m->timing) HIPCHK(hipEventRecord(m->tev[2], st));
+
+  const uint32_t n_new = dev ? m->n_present_dev : m->n_present;
+  const uint64_t keep = m->tick_events;
+  // events: expected count is small; grow and re-run the (pure) sweep on overflow
+  for (int attempt = 0;; ++attempt) {
+    HIPCHK(hipMemsetAsync(m->rank_cnt, 0, (size_t)(n_ops + 1) * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(m->ctr, 0, 1 * sizeof(uint32_t), st));           // CTR_EVENTS
+    HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
+    gw::SweepArgs s;
+    s.og = {m->grid[og].ent, m->grid[og].cs, m->grid[og].side, m->grid[og].d_geom};
+    s.ng = {m->grid[ng].ent, m->grid[ng].cs, m->grid[ng].side, m->grid[ng].d_geom};
+    s.old_x = m->old_x;
+    s.old_z = m->old_z;
+    s.old_seq = m->old_seq;
+    s.space_of = m->space_of;
+    s.base = base;
+    s.n_new = n_new;
+    s.op_slot = a.op_slot;
+    s.leave_ops = m->d_leaves;
+    s.n_leaves = dev ? 0 : m->n_leaves;
+    s.ev_tmp = m->ev_tmp;
+    s.ev_cap = m->tmp_cap;
+    s.rank_cnt = m->rank_cnt;
+    s.ctr = m->ctr;
+    gw::launch_sweep(s, st);
+    gw::launch_sweep_leaves(s, st);
+    HIPCHK(hipGetLastError());
+    if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
+    gw::launch_scan(m->rank_cnt, n_ops + 1, m->part, st);
+    HIPCHK(hipMemcpyAsync(m->h_ctr, m->ctr, gw::CTR_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (m->h_ctr[gw::CTR_ERR]) {
+      m->broken = true;
+      set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
+              "capacity); the manager is unusable",
+              m->h_ctr[gw::CTR_ERR]);
+      return GWAOI_ERR_DEVICE_CHECK;
+    }
+    const uint32_t nev = m->h_ctr[gw::CTR_EVENTS];
+    if (nev > m->tmp_cap || keep + nev > m->ev_cap) {
+      RCHK(ensure_events(m, keep + nev, nev, keep));
+      if (attempt < 3) continue;
+      set_err("event buffer overflow persisted");
+      return GWAOI_ERR_NOMEM;
+    }
+    uint2* out = m->ev_out + keep;
+    gw::launch_place(m->ev_tmp, m->ctr, m->tmp_cap, m->rank_cnt, out, st);
+    gw::launch_slice_sort(m->rank_cnt, n_ops, out, st);
+    HIPCHK(hipGetLastError());
+    if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
+    if (copy_events && nev)
+      HIPCHK(hipMemcpyAsync(m->h_ev + keep, out, (size_t)nev * sizeof(uint2), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    m->tick_events += nev;
+    m->tick_enter += m->h_ctr[gw::CTR_ENTER];
+    if (m->timing) {
+      float t01, t12, t23, t34, t04;
+      HIPCHK(hipEventElapsedTime(&t01, m->tev[0], m->tev[1]));
+      HIPCHK(hipEventElapsedTime(&t12, m->tev[1], m->tev[2]));
+      HIPCHK(hipEventElapsedTime(&t23, m->tev[2], m->tev[3]));
+      HIPCHK(hipEventElapsedTime(&t34, m->tev[3], m->tev[4]));
+      HIPCHK(hipEventElapsedTime(&t04, m->tev[0], m->tev[4]));
+      m->stats.ticks++;
+      m->stats.ms_apply += t01;
+      m->stats.ms_grid += t12;
+      m->stats.ms_sweep += t23;
+      m->stats.ms_order += t34;
+      m->stats.ms_total += t04;
+      m->stats.sweep_movers += n_ops;
+      m->stats.events += nev;
+    }
+    break;
+  }
+  m->cur = ng;
+  m->tick_passes++;
+  m->tick_ops += n_ops;
+  m->n_ops = 0;
+  m->n_leaves = 0;
+  m->dv_n = 0;
+  m->dv_slot = nullptr;
+  m->dv_x = m->dv_z = nullptr;
+  m->pass_id++;
+  m->n_present_dev = m->n_present;
+  return GWAOI_OK;
+}
+
+int check_mgr(const gwaoi_mgr* m) {
+  if (!m) {
+    set_err("null manager");
+    return GWAOI_ERR_INVALID;
+  }
+  if (m->broken) {
+    set_err("manager is unusable after a failed device-staged batch");
+    return GWAOI_ERR_STATE;
+  }
+  return GWAOI_OK;
+}
+
+int set_dev(const gwaoi_mgr* m) {
+  HIPCHK(hipSetDevice(m->device));
+  return GWAOI_OK;
+}
+
+// Before staging an op on `slot`: a slot may appear once per pass; a second op flushes the batch.
+int before_stage(gwaoi_mgr* m, uint32_t slot) {
+  if (m->dv_n) RCHK(run_pass(m, true));
+  if (m->h_stamp[slot] == m->pass_id) RCHK(run_pass(m, true));
+  return GWAOI_OK;
+}
+
+void note_coord(gwaoi_mgr* m, uint32_t space, float x, float z) {
+  SpaceHost& sh = m->spaces[space];
+  if (!sh.auto_extent) return;
+  if (!std::isfinite(x) || !std::isfinite(z)) return;
+  if (!sh.seen_any) {
+    sh.seen_minx = sh.seen_maxx = x;
+    sh.seen_minz = sh.seen_maxz = z;
+    sh.seen_any = true;
+    m->geom_dirty = true;
+    return;
+  }
+  sh.seen_minx = std::min(sh.seen_minx, x);
+  sh.seen_maxx = std::max(sh.seen_maxx, x);
+  sh.seen_minz = std::min(sh.seen_minz, z);
+  sh.seen_maxz = std::max(sh.seen_maxz, z);
+  if (x < sh.gx0 || x > sh.gx1 || z < sh.gz0 || z > sh.gz1) m->geom_dirty = true;
+}
+
+void stage(gwaoi_mgr* m, uint32_t slot, uint8_t kind, float x, float z, uint32_t space) {
+  const uint32_t i = m->n_ops++;
+  m->h_op_slot[i] = slot;
+  m->h_op_x[i] = x;
+  m->h_op_z[i] = z;
+  m->h_op_kind[i] = kind;
+  m->h_op_space[i] = space;
+  if (kind == gw::OP_LEAVE) m->h_leaves[m->n_leaves++] = i;
+  m->h_stamp[slot] = m->pass_id;
+}
+
+void free_all(gwaoi_mgr* m) {
+  hipSetDevice(m->device);
+  if (m->stream) hipStreamSynchronize(m->stream);
+  void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->stamp,
+                   m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_op_x, m->d_op_z,
+                   m->d_op_kind, m->rank_cnt, m->part, m->ctr, m->ev_tmp, m->ev_out};
+  for (void* p : dptrs)
+    if (p) hipFree(p);
+  for (int gi = 0; gi < 2; ++gi) {
+    Grid& g = m->grid[gi];
+    void* gp[] = {g.ent, g.cs, g.side, g.gidx, g.d_geom};
+    for (void* p : gp)
+      if (p) hipFree(p);
+  }
+  void* hptrs[] = {m->h_op_slot, m->h_op_x, m->h_op_z, m->h_op_kind, m->h_op_space, m->h_leaves, m->h_ctr,
+                   m->h_ev};
+  for (void* p : hptrs)
+    if (p) hipHostFree(p);
+  for (auto& e : m->tev)
+    if (e) hipEventDestroy(e);
+  if (m->own_stream) hipStreamDestroy(m->own_stream);
+}
+
+int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capacity, int device,
+                gwaoi_mgr** out) {
+  if (!out || !spaces || !nspaces || !capacity || capacity > 0x7fffffffu) {
+    set_err("gwaoi_create: invalid argument");
+    return GWAOI_ERR_INVALID;
+  }
+  *out = nullptr;
+  for (uint32_t s = 0; s < nspaces; ++s) {
+    if (!(spaces[s].dist > 0) || !std::isfinite(spaces[s].dist)) {
+      set_err("space %u: AOI distance must be > 0 (Space.EnableAOI panics otherwise, Space.go:92-94)", s);
+      return GWAOI_ERR_INVALID;
+    }
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    set_err("no HIP device available");
+    return GWAOI_ERR_HIP;
+  }
+  if (device < 0 || device >= ndev) {
+    set_err("device %d out of range (%d devices)", device, ndev);
+    return GWAOI_ERR_INVALID;
+  }
+  gwaoi_mgr* m = new (std::nothrow) gwaoi_mgr();
+  if (!m) return GWAOI_ERR_NOMEM;
+  m->device = device;
+  m->cap = capacity;
+  m->nspaces = nspaces;
+  m->spaces.resize(nspaces);
+  for (uint32_t s = 0; s < nspaces; ++s) {
+    SpaceHost& sh = m->spaces[s];
+    std::memset(&sh, 0, sizeof sh);
+    sh.desc = spaces[s];
+    sh.auto_extent = !(spaces[s].max_x > spaces[s].min_x && spaces[s].max_z > spaces[s].min_z);
+  }
+  m->max_cells = (uint32_t)std::min<uint64_t>(0x7fffffffu, std::max<uint64_t>(4096, 2ull * capacity) + 16ull * nspaces);
+  m->h_present.assign(capacity, 0);
+  m->h_space_of.assign(capacity, 0);
+  m->h_stamp.assign(capacity, 0);
+  int r = GWAOI_OK;
+  auto chk = [&](int x) {
+    if (r == GWAOI_OK) r = x;
+  };
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&m->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    set_err("stream creation failed on device %d", device);
+    delete m;
+    return GWAOI_ERR_HIP;
+  }
+  m->stream = m->own_stream;
+  const size_t C = capacity;
+  chk(dalloc(&m->pos_x, C));
+  chk(dalloc(&m->pos_z, C));
+  chk(dalloc(&m->old_x, C));
+  chk(dalloc(&m->old_z, C));
+  chk(dalloc(&m->seq, C));
+  chk(dalloc(&m->space_of, C));
+  chk(dalloc(&m->old_seq, C));
+  chk(dalloc(&m->stamp, C));
+  chk(dalloc(&m->key_of, C));
+  chk(dalloc(&m->local_of, C));
+  chk(dalloc(&m->d_op_slot, C));
+  chk(dalloc(&m->d_op_space, C));
+  chk(dalloc(&m->d_leaves, C));
+  chk(dalloc(&m->d_op_x, C));
+  chk(dalloc(&m->d_op_z, C));
+  chk(dalloc(&m->d_op_kind, C));
+  chk(dalloc(&m->rank_cnt, C + 1));
+  m->part_words = gw::scan_part_words(std::max<uint32_t>(m->max_cells, capacity) + 1);
+  chk(dalloc(&m->part, m->part_words));
+  chk(dalloc(&m->ctr, gw::CTR_N));
+  chk(halloc(&m->h_ctr, gw::CTR_N));
+  chk(halloc(&m->h_op_slot, C));
+  chk(halloc(&m->h_op_x, C));
+  chk(halloc(&m->h_op_z, C));
+  chk(halloc(&m->h_op_kind, C));
+  chk(halloc(&m->h_op_space, C));
+  chk(halloc(&m->h_leaves, C));
+  for (int gi = 0; gi < 2; ++gi) {
+    Grid& g = m->grid[gi];
+    chk(dalloc(&g.ent, C));
+    chk(dalloc(&g.cs, (size_t)m->max_cells + 1));
+    chk(dalloc(&g.side, C));
+    chk(dalloc(&g.gidx, C));
+    chk(dalloc(&g.d_geom, nspaces));
+  }
+  if (r == GWAOI_OK) r = ensure_events(m, std::max<uint64_t>(1u << 16, C / 2), (uint32_t)std::max<uint64_t>(1u << 16, C / 2), 0);
+  for (auto& e : m->tev)
+    if (r == GWAOI_OK && hipEventCreate(&e) != hipSuccess) {
+      set_err("hipEventCreate failed");
+      r = GWAOI_ERR_HIP;
+    }
+  if (r == GWAOI_OK) {
+    hipStream_t st = m->stream;
+    auto z = [&](void* p, size_t bytes) {
+      if (r == GWAOI_OK && hipMemsetAsync(p, 0, bytes, st) != hipSuccess) {
+        set_err("hipMemsetAsync failed");
+        r = GWAOI_ERR_HIP;
+      }
+    };
+    z(m->pos_x, C * 4);
+    z(m->pos_z, C * 4);
+    z(m->seq, C * 4);
+    z(m->space_of, C * 4);
+    z(m->stamp, C * 4);
+    for (int gi = 0; gi < 2; ++gi) {
+      z(m->grid[gi].side, C * 4);
+      z(m->grid[gi].gidx, C * 4);
+    }
+    std::vector<gw::Geom> geo;
+    compute_geometry(m, geo);
+    m->geom_dirty = false;
+    for (int gi = 0; gi < 2 && r == GWAOI_OK; ++gi) {
+      r = upload_geom(m, m->grid[gi], geo);
+      z(m->grid[gi].cs, ((size_t)m->grid[gi].ncells + 1) * 4);
+    }
+    if (r == GWAOI_OK && hipStreamSynchronize(st) != hipSuccess) {
+      set_err("initialisation failed");
+      r = GWAOI_ERR_HIP;
+    }
+  }
+  if (r != GWAOI_OK) {
+    free_all(m);
+    delete m;
+    return r;
+  }
+  *out = m;
+  return GWAOI_OK;
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+
+extern "C" {
+
+const char* gwaoi_version(void) { return "gwaoi 0.1.0 (gfx950)"; }
+const char* gwaoi_last_error(void) { return g_err.c_str(); }
+
+int gwaoi_create(float dist, uint32_t capacity, int device, gwaoi_mgr** out) {
+  gwaoi_space_desc d = {dist, 0.f, 0.f, 0.f, 0.f};
+  return create_impl(&d, 1, capacity, device, out);
+}
+
+int gwaoi_create_spaces(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capacity, int device,
+                        gwaoi_mgr** out) {
+  return create_impl(spaces, nspaces, capacity, device, out);
+}
+
+int gwaoi_destroy(gwaoi_mgr* m) {
+  if (!m) return GWAOI_OK;
+  free_all(m);
+  delete m;
+  return GWAOI_OK;
+}
+
+int gwaoi_set_stream(gwaoi_mgr* m, void* s) {
+  if (!m) return GWAOI_ERR_INVALID;
+  RCHK(set_dev(m));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  m->stream = s ? (hipStream_t)s : m->own_stream;
+  return GWAOI_OK;
+}
+
+int gwaoi_enter_space(gwaoi_mgr* m, uint32_t space, uint32_t slot, float x, float z) {
+  RCHK(check_mgr(m));
+  if (slot >= m->cap || space >= m->nspaces) {
+    set_err("enter: slot %u / space %u out of range", slot, space);
+    return GWAOI_ERR_INVALID;
+  }
+  if (m->h_present[slot]) {
+    set_err("enter: slot %u is already in a Space", slot);
+    return GWAOI_ERR_STATE;
+  }
+  RCHK(set_dev(m));
+  RCHK(before_stage(m, slot));
+  note_coord(m, space, x, z);
+  stage(m, slot, gw::OP_ENTER, x, z, space);
+  m->h_present[slot] = 1;
+  m->h_space_of[slot] = space;
+  m->n_present++;
+  return GWAOI_OK;
+}
+
+int gwaoi_enter(gwaoi_mgr* m, uint32_t slot, float x, float z) { return gwaoi_enter_space(m, 0, slot, x, z); }
+
+int gwaoi_stage_enters(gwaoi_mgr* m, uint32_t space, const uint32_t* slots, const float* x, const float* z,
+                       uint32_t n) {
+  RCHK(check_mgr(m));
+  if (n && (!slots || !x || !z)) {
+    set_err("stage_enters: null array");
+    return GWAOI_ERR_INVALID;
+  }
+  for (uint32_t i = 0; i < n; ++i) RCHK(gwaoi_enter_space(m, space, slots[i], x[i], z[i]));
+  return GWAOI_OK;
+}
+
+int gwaoi_leave(gwaoi_mgr* m, uint32_t slot) {
+  RCHK(check_mgr(m));
+  if (slot >= m->cap) {
+    set_err("leave: slot %u out of range", slot);
+    return GWAOI_ERR_INVALID;
+  }
+  if (!m->h_present[slot]) {
+    set_err("leave: slot %u is not in a Space", slot);
+    return GWAOI_ERR_STATE;
+  }
+  RCHK(set_dev(m));
+  RCHK(before_stage(m, slot));
+  stage(m, slot, gw::OP_LEAVE, 0.f, 0.f, m->h_space_of[slot]);
+  m->h_present[slot] = 0;
+  m->n_present--;
+  return GWAOI_OK;
+}
+
+int gwaoi_moved(gwaoi_mgr* m, uint32_t slot, float x, float z) {
+  RCHK(check_mgr(m));
+  if (slot >= m->cap) {
+    set_err("moved: slot %u out of range", slot);
+    return GWAOI_ERR_INVALID;
+  }
+  if (!m->h_present[slot]) {
+    set_err("moved: slot %u is not in a Space", slot);
+    return GWAOI_ERR_STATE;
+  }
+  RCHK(set_dev(m));
+  RCHK(before_stage(m, slot));
+  note_coord(m, m->h_space_of[slot], x, z);
+  stage(m, slot, gw::OP_MOVE, x, z, m->h_space_of[slot]);
+  return GWAOI_OK;
+}
+
+int gwaoi_stage_moves(gwaoi_mgr* m, const uint32_t* slots, const float* x, const float* z, uint32_t n) {
+  RCHK(check_mgr(m));
+  if (n && (!slots || !x || !z)) {
+    set_err("stage_moves: null array");
+    return GWAOI_ERR_INVALID;
+  }
+  for (uint32_t i = 0; i < n; ++i) RCHK(gwaoi_moved(m, slots[i], x[i], z[i]));
+  return GWAOI_OK;
+}
+
+int gwaoi_stage_moves_device(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                             uint32_t n) {
+  RCHK(check_mgr(m));
+  if (n && (!d_slots || !d_x || !d_z)) {
+    set_err("stage_moves_device: null array");
+    return GWAOI_ERR_INVALID;
+  }
+  if (n > m->cap) {
+    set_err("stage_moves_device: %u ops > capacity %u", n, m->cap);
+    return GWAOI_ERR_INVALID;
+  }
+  RCHK(set_dev(m));
+  if (m->n_ops || m->dv_n) RCHK(run_pass(m, true));
+  m->dv_slot = d_slots;
+  m->dv_x = d_x;
+  m->dv_z = d_z;
+  m->dv_n = n;
+  return GWAOI_OK;
+}
+
+int gwaoi_tick_ex(gwaoi_mgr* m, uint32_t flags, gwaoi_events* out) {
+  RCHK(check_mgr(m));
+  RCHK(set_dev(m));
+  const bool copy = !(flags & GWAOI_TICK_DEVICE_EVENTS);
+  // Passes forced earlier by re-staging a slot (before_stage) already accumulated their events.
+  int r = run_pass(m, copy);
+  if (r) return r;
+  if (!m->acc_open) reset_tick(m);  // nothing ran since the last tick
+  m->acc_open = false;
+  if (out) {
+    out->events = copy ? m->h_ev : (const gwaoi_event*)m->ev_out;
+    out->count = m->tick_events;
+    out->n_enter = m->tick_enter;
+    out->n_leave = m->tick_events - m->tick_enter;
+    out->n_subticks = m->tick_passes;
+    out->n_ops = m->tick_ops;
+  }
+  return GWAOI_OK;
+}
+
+int gwaoi_tick(gwaoi_mgr* m, gwaoi_events* out) { return gwaoi_tick_ex(m, 0, out); }
+
+int gwaoi_count(const gwaoi_mgr* m, uint32_t* n_present, uint32_t* n_staged) {
+  if (!m) return GWAOI_ERR_INVALID;
+  if (n_present) *n_present = m->n_present;
+  if (n_staged) *n_staged = m->dv_n ? m->dv_n : m->n_ops;
+  return GWAOI_OK;
+}
+
+int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint64_t cols_cap, uint64_t* nnz) {
+  RCHK(check_mgr(m));
+  if (!row_ptr || !nnz || (cols_cap && !cols)) {
+    set_err("export_relation: null argument");
+    return GWAOI_ERR_INVALID;
+  }
+  RCHK(set_dev(m));
+  if (m->n_ops || m->dv_n) {
+    RCHK(run_pass(m, false));
+    m->acc_open = false;  // events of the flushed batch are discarded (documented in gwaoi.h)
+    reset_tick(m);
+  }
+  hipStream_t st = m->stream;
+  const Grid& g = m->grid[m->cur];
+  uint32_t* d_rp = nullptr;
+  RCHK(dalloc(&d_rp, (size_t)m->cap + 1));
+  gw::RelArgs a;
+  a.g = {g.ent, g.cs, g.side, g.d_geom};
+  a.pos_x = m->pos_x;
+  a.pos_z = m->pos_z;
+  a.seq = m->seq;
+  a.space_of = m->space_of;
+  a.cap = m->cap;
+  a.row_ptr = nullptr;
+  a.row_cnt = d_rp;
+  a.cols = nullptr;
+  hipError_t e = hipMemsetAsync(d_rp + m->cap, 0, sizeof(uint32_t), st);
+  gw::launch_relation(a, st);
+  gw::launch_scan(d_rp, m->cap + 1, m->part, st);
+  uint32_t total = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&total, d_rp + m->cap, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    hipFree(d_rp);
+    set_err("export_relation: %s", hipGetErrorString(e));
+    return GWAOI_ERR_HIP;
+  }
+  *nnz = total;
+  if (total > cols_cap) {
+    hipFree(d_rp);
+    set_err("export_relation: cols_cap %llu < nnz %u", (unsigned long long)cols_cap, total);
+    return GWAOI_ERR_INVALID;
+  }
+  uint32_t* d_cols = nullptr;
+  int r = dalloc(&d_cols, std::max<uint32_t>(total, 1));
+  if (r) {
+    hipFree(d_rp);
+    return r;
+  }
+  a.row_ptr = d_rp;
+  a.cols = d_cols;
+  gw::launch_relation(a, st);
+  gw::launch_row_sort(d_rp, m->cap, d_cols, st);
+  e = hipMemcpyAsync(row_ptr, d_rp, ((size_t)m->cap + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && total)
+    e = hipMemcpyAsync(cols, d_cols, (size_t)total * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  hipFree(d_rp);
+  hipFree(d_cols);
+  if (e != hipSuccess) {
+    set_err("export_relation: %s", hipGetErrorString(e));
+    return GWAOI_ERR_HIP;
+  }
+  return GWAOI_OK;
+}
+
+int gwaoi_set_timing(gwaoi_mgr* m, int enable) {
+  if (!m) return GWAOI_ERR_INVALID;
+  m->timing = enable != 0;
+  return GWAOI_OK;
+}
+
+int gwaoi_get_stats(const gwaoi_mgr* m, gwaoi_stats* out) {
+  if (!m || !out) return GWAOI_ERR_INVALID;
+  *out = m->stats;
+  return GWAOI_OK;
+}
+
+int gwaoi_reset_stats(gwaoi_mgr* m) {
+  if (!m) return GWAOI_ERR_INVALID;
+  m->stats = gwaoi_stats{};
+  return GWAOI_OK;
+}
+
+// ---- tooling (include/gwaoi_tools.h) ----
+
+int gwaoi_device_count(int* n) {
+  if (!n) return GWAOI_ERR_INVALID;
+  *n = 0;
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) {
+    *n = 0;
+    set_err("hipGetDeviceCount: %s", hipGetErrorString(e));
+    return GWAOI_ERR_HIP;
+  }
+  return GWAOI_OK;
+}
+
+int gwaoi_dev_malloc(int device, size_t bytes, void** out) {
+  if (!out) return GWAOI_ERR_INVALID;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMalloc(out, bytes ? bytes : 1));
+  return GWAOI_OK;
+}
+
+int gwaoi_dev_free(int device, void* p) {
+  HIPCHK(hipSetDevice(device));
+  if (p) HIPCHK(hipFree(p));
+  return GWAOI_OK;
+}
+
+int gwaoi_dev_htod(int device, void* dst, const void* src, size_t bytes) {
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return GWAOI_OK;
+}
+
+int gwaoi_dev_dtoh(int device, void* dst, const void* src, size_t bytes) {
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return GWAOI_OK;
+}
+
+int gwaoi_dev_sync(int device) {
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipDeviceSynchronize());
+  return GWAOI_OK;
+}
+
+int gwaoi_wl_init(int device, float* d_x, float* d_z, uint32_t n, uint64_t seed, float L) {
+  HIPCHK(hipSetDevice(device));
+  gw::launch_wl_init(d_x, d_z, n, seed, L, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return GWAOI_OK;
+}
+
+int gwaoi_wl_step(int device, const float* d_xprev, const float* d_zprev, float* d_xout, float* d_zout, uint32_t n,
+                  uint64_t seed, uint64_t tick, float L, float s) {
+  HIPCHK(hipSetDevice(device));
+  gw::launch_wl_step(d_xprev, d_zprev, d_xout, d_zout, n, seed, tick, L, s, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return GWAOI_OK;
+}
+
+int gwaoi_wl_iota(int device, uint32_t* d, uint32_t n) {
+  HIPCHK(hipSetDevice(device));
+  gw::launch_iota(d, n, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
+  RCHK(check_mgr(m));
+  if (next_seq < m->next_seq || next_seq >= kSeqLimit) {
+    set_err("debug_set_next_seq: must be in [%u, %u)", m->next_seq, kSeqLimit);
+    return GWAOI_ERR_INVALID;
+  }
+  m->next_seq = next_seq;
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_cells_per_dist(gwaoi_mgr* m, float cpd) {
+  RCHK(check_mgr(m));
+  if (!(cpd > 0) || cpd > 64) return GWAOI_ERR_INVALID;
+  m->cells_per_dist = cpd;
+  m->geom_dirty = true;
+  return GWAOI_OK;
+}
+
+}  // extern "C"

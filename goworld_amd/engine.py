@@ -1,0 +1,214 @@
+"""Thin numpy-facing handle over one libgwaoi manager (include/gwaoi.h).
+
+`Engine` is what tests and bench.py drive; `goworld_amd.aoi` builds the go-aoi-shaped interface
+(AOI / AOICallback / AOIManager) on top of it.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+def _u32p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
+def _f32p(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+class Engine:
+    """One AOI manager on one GPU: a single Space (dist) or several Spaces (spaces=[(dist, bounds)])."""
+
+    def __init__(self, dist: Optional[float] = None, capacity: int = 1 << 16, device: int = 0,
+                 bounds: Optional[Sequence[float]] = None, spaces: Optional[Sequence] = None):
+        L = _lib.load()
+        self._L = L
+        self.capacity = int(capacity)
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        if spaces is None:
+            if dist is None:
+                raise ValueError("dist or spaces required")
+            spaces = [(dist, bounds)]
+        descs = (_lib.SpaceDesc * len(spaces))()
+        for i, (d, b) in enumerate(spaces):
+            descs[i].dist = float(d)
+            if b is not None:
+                descs[i].min_x, descs[i].min_z, descs[i].max_x, descs[i].max_z = [float(v) for v in b]
+        check(L.gwaoi_create_spaces(descs, len(spaces), self.capacity, self.device, ctypes.byref(h)))
+        self._h = h
+        self.nspaces = len(spaces)
+
+    # ---- lifecycle ----
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._L.gwaoi_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # ---- ops (the reference's Enter / Leave / Moved) ----
+    def enter(self, slot: int, x: float, z: float, space: int = 0):
+        check(self._L.gwaoi_enter_space(self._h, space, slot, x, z))
+
+    def stage_enters(self, slots, x, z, space: int = 0):
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        xa = np.ascontiguousarray(x, dtype=np.float32)
+        za = np.ascontiguousarray(z, dtype=np.float32)
+        check(self._L.gwaoi_stage_enters(self._h, space, _u32p(s), _f32p(xa), _f32p(za), len(s)))
+
+    def leave(self, slot: int):
+        check(self._L.gwaoi_leave(self._h, slot))
+
+    def moved(self, slot: int, x: float, z: float):
+        check(self._L.gwaoi_moved(self._h, slot, x, z))
+
+    def stage_moves(self, slots, x, z):
+        s = np.ascontiguousarray(slots, dtype=np.uint32)
+        xa = np.ascontiguousarray(x, dtype=np.float32)
+        za = np.ascontiguousarray(z, dtype=np.float32)
+        check(self._L.gwaoi_stage_moves(self._h, _u32p(s), _f32p(xa), _f32p(za), len(s)))
+
+    def stage_moves_device(self, d_slots: int, d_x: int, d_z: int, n: int):
+        check(self._L.gwaoi_stage_moves_device(self._h, ctypes.c_void_p(d_slots), ctypes.c_void_p(d_x),
+                                                ctypes.c_void_p(d_z), n))
+
+    def set_stream(self, stream_ptr: int):
+        check(self._L.gwaoi_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
+
+    # ---- tick ----
+    def tick(self) -> np.ndarray:
+        """Apply staged ops; returns the events as an (n, 2) uint32 array [mover, other|kind] in
+        canonical replay order (copied out of the manager's pinned buffer)."""
+        ev = _lib.Events()
+        check(self._L.gwaoi_tick(self._h, ctypes.byref(ev)))
+        self.last = ev
+        n = int(ev.count)
+        if n == 0:
+            return np.zeros((0, 2), dtype=np.uint32)
+        p = ctypes.cast(ev.events, ctypes.POINTER(ctypes.c_uint32))
+        return np.ctypeslib.as_array(p, shape=(2 * n,)).reshape(n, 2).copy()
+
+    def tick_raw(self) -> _lib.Events:
+        """Apply staged ops, events copied to the manager's pinned host buffer (not to numpy)."""
+        ev = _lib.Events()
+        check(self._L.gwaoi_tick(self._h, ctypes.byref(ev)))
+        self.last = ev
+        return ev
+
+    def tick_device(self) -> _lib.Events:
+        """Apply staged ops, leave the events in device memory; returns the Events record."""
+        ev = _lib.Events()
+        check(self._L.gwaoi_tick_ex(self._h, _lib.GWAOI_TICK_DEVICE_EVENTS, ctypes.byref(ev)))
+        self.last = ev
+        return ev
+
+    def count(self):
+        p = ctypes.c_uint32()
+        s = ctypes.c_uint32()
+        check(self._L.gwaoi_count(self._h, ctypes.byref(p), ctypes.byref(s)))
+        return p.value, s.value
+
+    def relation(self):
+        """CSR (row_ptr[capacity+1], cols) of the current neighbour relation, rows ascending."""
+        rp = np.zeros(self.capacity + 1, dtype=np.uint32)
+        nnz = ctypes.c_uint64(0)
+        cap = 1 << 16
+        while True:
+            cols = np.zeros(cap, dtype=np.uint32)
+            rc = self._L.gwaoi_export_relation(self._h, _u32p(rp), _u32p(cols), cap, ctypes.byref(nnz))
+            if rc == _lib.GWAOI_OK:
+                return rp, cols[: nnz.value]
+            if rc == _lib.GWAOI_ERR_INVALID and nnz.value > cap:
+                cap = int(nnz.value)
+                continue
+            check(rc)
+
+    # ---- timing ----
+    def set_timing(self, on: bool = True):
+        check(self._L.gwaoi_set_timing(self._h, 1 if on else 0))
+
+    def stats(self) -> dict:
+        st = _lib.Stats()
+        check(self._L.gwaoi_get_stats(self._h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in _lib.Stats._fields_}
+
+    def reset_stats(self):
+        check(self._L.gwaoi_reset_stats(self._h))
+
+    # ---- test hooks ----
+    def debug_set_next_seq(self, v: int):
+        check(self._L.gwaoi_debug_set_next_seq(self._h, v))
+
+    def debug_set_cells_per_dist(self, v: float):
+        check(self._L.gwaoi_debug_set_cells_per_dist(self._h, v))
+
+
+class DeviceBuffer:
+    """Raw device allocation via libgwaoi (no torch dependency)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        L = _lib.load()
+        self._L = L
+        self.device = device
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(L.gwaoi_dev_malloc(device, self.nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes
+        check(self._L.gwaoi_dev_htod(self.device, ctypes.c_void_p(self.ptr), a.ctypes.data_as(ctypes.c_void_p),
+                                     a.nbytes))
+
+    def download(self, dtype, count: int, offset_bytes: int = 0) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        check(self._L.gwaoi_dev_dtoh(self.device, out.ctypes.data_as(ctypes.c_void_p),
+                                     ctypes.c_void_p(self.ptr + offset_bytes), out.nbytes))
+        return out
+
+    def free(self):
+        if self.ptr:
+            self._L.gwaoi_dev_free(self.device, ctypes.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def wl_init(device: int, d_x: int, d_z: int, n: int, seed: int, L: float):
+    check(_lib.load().gwaoi_wl_init(device, ctypes.c_void_p(d_x), ctypes.c_void_p(d_z), n, seed, L))
+
+
+def wl_step(device: int, d_xp: int, d_zp: int, d_xo: int, d_zo: int, n: int, seed: int, tick: int, L: float,
+            s: float = 1.0):
+    check(_lib.load().gwaoi_wl_step(device, ctypes.c_void_p(d_xp), ctypes.c_void_p(d_zp), ctypes.c_void_p(d_xo),
+                                    ctypes.c_void_p(d_zo), n, seed, tick, L, s))
+
+
+def wl_iota(device: int, d: int, n: int):
+    check(_lib.load().gwaoi_wl_iota(device, ctypes.c_void_p(d), n))

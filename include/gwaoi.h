@@ -1,0 +1,148 @@
+/*
+ * gwaoi.h — C ABI of the MI355X-native, tick-batched AOI engine (libgwaoi.so).
+ *
+ * This is the drop-in boundary for GoWorld's AOI hot path. In the reference the path is the
+ * go-aoi v0.2.0 (rev 5e9d879, /root/reference/Gopkg.lock:155-159) interface
+ *
+ *     type AOIManager interface { Enter(aoi *AOI, x, y Coord); Leave(aoi *AOI); Moved(aoi *AOI, x, y Coord) }
+ *     func NewXZListAOIManager(aoidist Coord) AOIManager
+ *     type AOICallback interface { OnEnterAOI(other *AOI); OnLeaveAOI(other *AOI) }
+ *
+ * held by engine/entity/Space.go:33, constructed at Space.go:105 and called at Space.go:211,221,243,259;
+ * the callbacks are implemented by *Entity at engine/entity/Entity.go:227-233. Each entry point below
+ * names the reference call it replaces.
+ *
+ * Contract (mirrors the reference's):
+ *   - Identity is a dense uint32 "slot" (cgo may not retain Go pointers); the Go side keeps slot -> *AOI.
+ *   - One manager is driven by one thread at a time (GameService main goroutine, GameService.go:88-192).
+ *   - No exceptions cross the ABI: every function returns GWAOI_OK (0) or a negative GWAOI_ERR_* code;
+ *     gwaoi_last_error() gives a message (thread-local). Misuse the reference would panic on
+ *     (Enter twice, Leave/Moved of an absent AOI) is reported as GWAOI_ERR_STATE instead.
+ *   - Ops are STAGED and applied by gwaoi_tick() in staging order. The events returned are exactly the
+ *     pair events the reference would have raised by running the same calls one by one:
+ *       Enter(m)  -> ENTER(m,o) for every present o inside m's box,
+ *       Leave(m)  -> LEAVE(m,o) for every current neighbour o,
+ *       Moved(m)  -> LEAVE(m,o) for neighbours now outside m's new box, ENTER(m,o) for new ones,
+ *     where "o inside m's box" is the go-aoi float32 predicate
+ *       fl32(m.x-D) <= o.x <= fl32(m.x+D)  &&  fl32(m.z-D) <= o.z <= fl32(m.z+D).
+ *     Each pair event stands for the two reference callbacks m.OnXAOI(o) then o.OnXAOI(m).
+ *     Staging a slot that already has an op in the current batch first flushes the batch (a
+ *     "sub-tick"), so the sequential semantics hold for ANY call sequence.
+ *   - Events are ordered canonically: by staging order of the mover, then LEAVE before ENTER, then
+ *     other-slot ascending. Replaying them in this order reproduces a valid sequential execution of the
+ *     reference (the reference's own order inside one Moved follows Go map iteration, i.e. is random).
+ */
+#ifndef GWAOI_H
+#define GWAOI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GWAOI_OK 0
+#define GWAOI_ERR_INVALID (-1)  /* bad argument (null pointer, slot >= capacity, bad space id, dist <= 0) */
+#define GWAOI_ERR_STATE (-2)    /* Enter of a present slot, Leave/Moved of an absent slot */
+#define GWAOI_ERR_HIP (-3)      /* HIP runtime failure (no GPU, launch failure, ...) */
+#define GWAOI_ERR_NOMEM (-4)    /* device or pinned host allocation failed */
+#define GWAOI_ERR_DEVICE_CHECK (-5) /* device-staged batch failed validation (duplicate / absent slot) */
+
+#define GWAOI_EV_ENTER 0x80000000u /* bit 31 of gwaoi_event.other: 1 = ENTER, 0 = LEAVE */
+#define GWAOI_EV_SLOT_MASK 0x7fffffffu
+
+typedef struct gwaoi_mgr gwaoi_mgr;
+
+/* One pair event: the reference's mover.OnXAOI(other); other.OnXAOI(mover). 8 bytes. */
+typedef struct {
+  uint32_t mover; /* slot whose Enter/Leave/Moved raised the event */
+  uint32_t other; /* other slot | GWAOI_EV_ENTER for enter events */
+} gwaoi_event;
+
+/* Events of one gwaoi_tick(). `events` points into memory owned by the manager (host-pinned, or
+ * device memory with GWAOI_TICK_DEVICE_EVENTS), valid until the next gwaoi_tick*/ /* call. */
+typedef struct {
+  const gwaoi_event* events;
+  uint64_t count;
+  uint64_t n_enter;
+  uint64_t n_leave;
+  uint32_t n_subticks; /* device pipeline passes this tick ran (>1 when a slot was staged twice) */
+  uint32_t n_ops;      /* ops applied */
+} gwaoi_events;
+
+/* One AOI Space inside a manager. A manager may batch many independent Spaces. */
+typedef struct {
+  float dist;                 /* AOI distance D of the Space (Space.EnableAOI(d), Space.go:91-105) */
+  float min_x, min_z;         /* grid extent hint. Correctness never depends on it: entities outside */
+  float max_x, max_z;         /* are clamped into edge cells (only slower). min >= max => auto extent. */
+} gwaoi_space_desc;
+
+/* Replaces aoi.NewXZListAOIManager(aoidist) (Space.go:105) for one Space. capacity = max slot + 1. */
+int gwaoi_create(float dist, uint32_t capacity, int device, gwaoi_mgr** out);
+/* Many Spaces in one manager (one pipeline pass per tick for all of them). */
+int gwaoi_create_spaces(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capacity, int device,
+                        gwaoi_mgr** out);
+int gwaoi_destroy(gwaoi_mgr* mgr);
+
+/* Run the manager's work on a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream).
+ * NULL restores the manager's own stream. */
+int gwaoi_set_stream(gwaoi_mgr* mgr, void* hip_stream);
+
+/* XZListAOIManager.Enter(aoi, x, z)  <- Space.enter (Space.go:211,221). Staged. */
+int gwaoi_enter(gwaoi_mgr* mgr, uint32_t slot, float x, float z);
+int gwaoi_enter_space(gwaoi_mgr* mgr, uint32_t space, uint32_t slot, float x, float z);
+/* n Enter calls in array order into one Space (bulk load: EntityManager.RestoreFreezedEntities ->
+ * restoreEntity -> Space.enter(isRestore) -> aoiMgr.Enter, EntityManager.go:591-652, Space.go:218-223). */
+int gwaoi_stage_enters(gwaoi_mgr* mgr, uint32_t space, const uint32_t* slots, const float* x, const float* z,
+                       uint32_t n);
+/* XZListAOIManager.Leave(aoi)  <- Space.leave (Space.go:243). Staged. */
+int gwaoi_leave(gwaoi_mgr* mgr, uint32_t slot);
+/* XZListAOIManager.Moved(aoi, x, z)  <- Space.move (Space.go:259). Staged. */
+int gwaoi_moved(gwaoi_mgr* mgr, uint32_t slot, float x, float z);
+/* n Moved calls in array order (GameService.HandleSyncPositionYawFromClient loop, GameService.go:398-410). */
+int gwaoi_stage_moves(gwaoi_mgr* mgr, const uint32_t* slots, const float* x, const float* z, uint32_t n);
+/* Same, from DEVICE arrays (inputs resident in HBM). Must be the only ops of the batch; slots must be
+ * distinct and present — checked on the device, reported by gwaoi_tick as GWAOI_ERR_DEVICE_CHECK
+ * (the manager is then unusable and must be destroyed). The arrays must stay valid until gwaoi_tick. */
+int gwaoi_stage_moves_device(gwaoi_mgr* mgr, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                             uint32_t n);
+
+/* Apply every staged op; blocks until the events are on the host (or in device memory, see flags). */
+#define GWAOI_TICK_DEVICE_EVENTS 1u /* leave events in device memory (no D2H copy) */
+int gwaoi_tick(gwaoi_mgr* mgr, gwaoi_events* out);
+int gwaoi_tick_ex(gwaoi_mgr* mgr, uint32_t flags, gwaoi_events* out);
+
+/* Number of present slots / staged ops. */
+int gwaoi_count(const gwaoi_mgr* mgr, uint32_t* n_present, uint32_t* n_staged);
+
+/* Export the current relation N (the union of every entity's InterestedIn set, Entity.go:53) as CSR
+ * over slots: row_ptr has capacity+1 entries, cols[row_ptr[s] .. row_ptr[s+1]) = neighbours of s in
+ * ascending slot order. Pending ops are flushed first (their events are discarded: call gwaoi_tick
+ * first if you need them). If cols_cap is too small, *nnz is set and GWAOI_ERR_INVALID returned. */
+int gwaoi_export_relation(gwaoi_mgr* mgr, uint32_t* row_ptr, uint32_t* cols, uint64_t cols_cap,
+                          uint64_t* nnz);
+
+/* Per-stage device time of the pipeline, accumulated over ticks while timing is enabled (hipEvents on
+ * the manager's stream). */
+typedef struct {
+  uint64_t ticks;          /* pipeline passes timed */
+  double ms_apply;         /* op application + per-slot bookkeeping */
+  double ms_grid;          /* cell binning + counting sort (count, scan, scatter) */
+  double ms_sweep;         /* neighbour sweep + event emission (the dominant kernel) */
+  double ms_order;         /* canonical event ordering (scan, place, slice sort) */
+  double ms_total;         /* first to last kernel of the pass */
+  uint64_t sweep_movers;   /* movers processed by the sweep */
+  uint64_t events;         /* events emitted */
+} gwaoi_stats;
+int gwaoi_set_timing(gwaoi_mgr* mgr, int enable);
+int gwaoi_get_stats(const gwaoi_mgr* mgr, gwaoi_stats* out);
+int gwaoi_reset_stats(gwaoi_mgr* mgr);
+
+/* Library version string and the thread-local message of the last failing call. */
+const char* gwaoi_version(void);
+const char* gwaoi_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GWAOI_H */

@@ -1,0 +1,41 @@
+/*
+ * gwaoi_tools.h — bench / test tooling exported by libgwaoi.so next to the AOI ABI (gwaoi.h).
+ * Not part of the drop-in boundary: no reference interface corresponds to these. They let tests and
+ * bench.py keep inputs resident in HBM without depending on PyTorch for device memory.
+ */
+#ifndef GWAOI_TOOLS_H
+#define GWAOI_TOOLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int gwaoi_device_count(int* n);
+int gwaoi_dev_malloc(int device, size_t bytes, void** out);
+int gwaoi_dev_free(int device, void* p);
+int gwaoi_dev_htod(int device, void* dst, const void* src, size_t bytes);
+int gwaoi_dev_dtoh(int device, void* dst, const void* src, size_t bytes);
+int gwaoi_dev_sync(int device);
+
+/* Device generator of include/gwaoi_workload.h (bit-identical to the host functions there).
+ * wl_init: positions at tick 0.  wl_step: x_out = step(x_prev) for `tick` (x_out may alias x_prev).
+ * wl_iota: d[i] = i. All run on the null stream of `device` and are synchronous. */
+int gwaoi_wl_init(int device, float* d_x, float* d_z, uint32_t n, uint64_t seed, float L);
+int gwaoi_wl_step(int device, const float* d_xprev, const float* d_zprev, float* d_xout, float* d_zout,
+                  uint32_t n, uint64_t seed, uint64_t tick, float L, float s);
+int gwaoi_wl_iota(int device, uint32_t* d, uint32_t n);
+
+/* Test hook: set the manager's next op sequence number (exercises the sequence renormalisation that
+ * otherwise runs every ~2^31 ops). */
+struct gwaoi_mgr;
+int gwaoi_debug_set_next_seq(struct gwaoi_mgr* mgr, uint32_t next_seq);
+/* Test hook: cell size = D / cells_per_dist for grids built from now on (default 2). */
+int gwaoi_debug_set_cells_per_dist(struct gwaoi_mgr* mgr, float cells_per_dist);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GWAOI_TOOLS_H */

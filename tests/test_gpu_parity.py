@@ -1,0 +1,265 @@
+"""GPU parity tests: libgwaoi (hand-written HIP, gfx950) against the CPU oracles, through the C ABI.
+
+Bar: bit-exact. Every tick's event list must equal the oracle's canonical event list element for
+element (same pairs, same kinds, same order), and the exported relation must equal the oracle's
+neighbour sets. Oracle (i) is the go-aoi XZListAOIManager restatement; oracle (ii) (stateful grid
+model, cross-checked against (i) in test_oracle.py) is used where (i) is too slow (1M entities).
+Parity against go-aoi itself is UNPINNED (module absent here; DESIGN.md "Oracle").
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import aoi_harness as H  # noqa: E402
+from golden import make_golden as G  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def po(oracle_lib):
+    return oracle_lib
+
+
+def engine(case, **kw):
+    from goworld_amd.engine import Engine
+    return Engine(case["dist"], capacity=case["cap"], bounds=case.get("bounds"), **kw)
+
+
+def assert_same(a, b, what):
+    assert np.array_equal(a, b), what + ": " + H.fmt_diff(a, b)
+
+
+def run_against_oracle(po, case, check_relation_every=1, eng=None, oracle="xz", cells_per_dist=None):
+    eng = eng or engine(case)
+    if cells_per_dist:
+        eng.debug_set_cells_per_dist(cells_per_dist)
+    if oracle == "xz":
+        orc = po.XZListOracle(case["dist"], case["cap"])
+    else:
+        orc = po.GridOracle(case["dist"], case["cap"], case.get("bounds") or (-1000, -1000, 1000, 1000))
+    for t, ops in enumerate(case["ticks"]):
+        want = H.oracle_tick(orc, ops)
+        got = H.gpu_tick(eng, ops)
+        assert_same(got, want, f"{case['name']} tick {t}")
+        if check_relation_every and t % check_relation_every == 0:
+            rg, ro = eng.relation(), orc.relation()
+            assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1]), f"relation tick {t}"
+    return eng, orc
+
+
+@pytest.mark.parametrize("path", G.fixture_paths(), ids=lambda p: os.path.basename(p))
+def test_golden_fixtures(gpu, path):
+    case = G.load(path)
+    eng = engine(case)
+    for t, ops in enumerate(case["ticks"]):
+        got = H.gpu_tick(eng, ops)
+        assert_same(got, case["events"][t], f"{case['name']} tick {t}")
+    rp, cols = eng.relation()
+    assert np.array_equal(rp, case["rel"][0]) and np.array_equal(cols, case["rel"][1])
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_op_mixes(gpu, po, seed):
+    case = H.case_random_ops(seed=1000 + seed, n=[64, 300, 1000, 2000][seed % 4], nticks=10,
+                             ops_per_tick=[40, 400, 800, 3000][seed % 4], world=[100.0, 300.0, 1000.0][seed % 3],
+                             dist=[10.0, 50.0, 100.0][seed % 3], snap=seed % 2 == 0)
+    run_against_oracle(po, case, check_relation_every=3)
+
+
+@pytest.mark.parametrize("cpd", [0.5, 1.0, 3.0])
+def test_cell_size_does_not_change_events(gpu, po, cpd):
+    case = H.case_random_ops(seed=7, n=500, nticks=6, ops_per_tick=600, world=300.0, dist=40.0)
+    run_against_oracle(po, case, check_relation_every=2, cells_per_dist=cpd)
+
+
+def test_auto_extent_regrid(gpu, po):
+    """No extent hint: the manager starts from Space.GetSpaceRange's +-1000 and regrids as entities
+    appear far outside it (clamped edge cells in between) — events must not change."""
+    case = H.case_random_ops(seed=9, n=400, nticks=8, ops_per_tick=300, world=20000.0, dist=100.0, snap=False)
+    case["bounds"] = None
+    run_against_oracle(po, case, check_relation_every=2)
+
+
+def test_config1_walk_100_ticks(gpu, po):
+    """N=10,000, L=3,500, D=100, seed 0x5EED0001, 100 ticks, against the
+    go-aoi list restatement tick by tick."""
+    case = H.case_walk(0x5EED0001, 10000, 3500.0, 101, workload=po)
+    eng, orc = run_against_oracle(po, case, check_relation_every=25)
+    assert eng.count()[0] == 10000
+
+
+def test_device_staged_moves_and_generator(gpu, po):
+    """Inputs resident in HBM (the bench path): the device generator is bit-identical to the host
+    one, and device-staged ticks give the same events as host-staged ones."""
+    from goworld_amd.engine import DeviceBuffer, wl_init, wl_iota, wl_step
+    n, L, seed = 20000, 5000.0, 0x5EED0042
+    bx, bz, bs = DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(4 * n)
+    wl_init(0, bx.ptr, bz.ptr, n, seed, L)
+    wl_iota(0, bs.ptr, n)
+    hx, hz = po.workload_init(seed, n, L)
+    assert np.array_equal(bx.download(np.float32, n), hx) and np.array_equal(bz.download(np.float32, n), hz)
+    from goworld_amd.engine import Engine
+    a = Engine(100.0, n, bounds=(0, 0, L, L))
+    b = Engine(100.0, n, bounds=(0, 0, L, L))
+    for i in range(n):
+        a.enter(i, float(hx[i]), float(hz[i]))
+    for i in range(n):
+        b.enter(i, float(hx[i]), float(hz[i]))
+    assert_same(a.tick(), b.tick(), "enter tick")
+    for t in range(1, 6):
+        wl_step(0, bx.ptr, bz.ptr, bx.ptr, bz.ptr, n, seed, t, L, 1.0)
+        po.workload_step(seed, t, hx, hz, L, 1.0)
+        assert np.array_equal(bx.download(np.float32, n), hx)
+        a.stage_moves(np.arange(n, dtype=np.uint32), hx, hz)
+        b.stage_moves_device(bs.ptr, bx.ptr, bz.ptr, n)
+        assert_same(b.tick(), a.tick(), f"tick {t}")
+
+
+def test_multi_space_batching(gpu, po):
+    """Several independent Spaces (different D) in one manager: events equal those of one oracle per
+    Space, in global op order; no pair ever crosses Spaces."""
+    from goworld_amd.engine import Engine
+    rng = np.random.default_rng(3)
+    dists = [25.0, 50.0, 100.0, 200.0]
+    per = 400
+    ns = len(dists)
+    cap = ns * per
+    eng = Engine(capacity=cap, spaces=[(d, (0.0, 0.0, 1000.0, 1000.0)) for d in dists])
+    orcs = [po.XZListOracle(d, cap) for d in dists]
+    space_of = np.repeat(np.arange(ns), per)
+    pos = rng.uniform(0, 1000, (cap, 2)).astype(np.float32)
+    order = rng.permutation(cap)
+    for t in range(6):
+        want = []
+        if t == 0:
+            for s in order:
+                eng.enter(int(s), float(pos[s, 0]), float(pos[s, 1]), space=int(space_of[s]))
+                o = orcs[space_of[s]]
+                o.enter(int(s), float(pos[s, 0]), float(pos[s, 1]))
+                ev = o.take_events()
+                if len(ev):
+                    want.append(ev[np.argsort(ev[:, 1], kind="stable")])
+        else:
+            pos = (pos + rng.uniform(-5, 5, pos.shape)).astype(np.float32)
+            mv = rng.permutation(cap)[: cap // 2]
+            eng.stage_moves(mv.astype(np.uint32), pos[mv, 0], pos[mv, 1])
+            for s in mv:
+                o = orcs[space_of[s]]
+                o.moved(int(s), float(pos[s, 0]), float(pos[s, 1]))
+                ev = o.take_events()
+                if len(ev):
+                    want.append(ev[np.argsort(ev[:, 1], kind="stable")])
+        want = np.concatenate(want) if want else np.zeros((0, 2), np.uint32)
+        got = eng.tick()
+        assert_same(got, want, f"multispace tick {t}")
+        sm = got[:, 0]
+        so = got[:, 1] & 0x7FFFFFFF
+        assert np.all(space_of[sm] == space_of[so])
+
+
+def test_seq_renormalisation(gpu, po):
+    """The per-entity op sequence numbers are rank-compressed before they would overflow; events must
+    be unaffected across the renormalisation."""
+    case = H.case_random_ops(seed=21, n=300, nticks=12, ops_per_tick=250, world=200.0, dist=30.0)
+    from goworld_amd.engine import Engine
+    eng = Engine(case["dist"], capacity=case["cap"])
+    orc = po.XZListOracle(case["dist"], case["cap"])
+    for t, ops in enumerate(case["ticks"]):
+        if t == 4:
+            eng.debug_set_next_seq(0x7ff00000 - 700)
+        want = H.oracle_tick(orc, ops)
+        assert_same(H.gpu_tick(eng, ops), want, f"tick {t}")
+    rg, ro = eng.relation(), orc.relation()
+    assert np.array_equal(rg[1], ro[1])
+
+
+def test_misuse_is_reported(gpu):
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine, wl_iota
+    eng = Engine(100.0, 64)
+    eng.enter(1, 0.0, 0.0)
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng.enter(1, 5.0, 5.0)
+    assert e.value.code == _lib.GWAOI_ERR_STATE
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng.moved(2, 0.0, 0.0)
+    assert e.value.code == _lib.GWAOI_ERR_STATE
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng.leave(3)
+    assert e.value.code == _lib.GWAOI_ERR_STATE
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng.moved(64, 0.0, 0.0)
+    assert e.value.code == _lib.GWAOI_ERR_INVALID
+    eng.tick()
+    # device-staged batch naming an absent slot is caught on the device
+    bs = DeviceBuffer(4 * 4)
+    bs.upload(np.asarray([1, 5, 1, 1], np.uint32))
+    bx = DeviceBuffer(16)
+    bx.upload(np.zeros(4, np.float32))
+    eng.stage_moves_device(bs.ptr, bx.ptr, bx.ptr, 2)
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng.tick()
+    assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK
+    # duplicate slot in a device-staged batch
+    eng2 = Engine(100.0, 64)
+    eng2.enter(1, 0.0, 0.0)
+    eng2.tick()
+    eng2.stage_moves_device(bs.ptr + 8, bx.ptr, bx.ptr, 2)
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng2.tick()
+    assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK
+
+
+def test_empty_and_tiny(gpu, po):
+    from goworld_amd.engine import Engine
+    eng = Engine(100.0, 4)
+    assert len(eng.tick()) == 0  # nothing staged
+    eng.enter(0, 1.0, 1.0)
+    assert len(eng.tick()) == 0  # alone
+    eng.enter(1, 1.0, 1.0)
+    ev = eng.tick()
+    assert ev.tolist() == [[1, 0 | H.EV_ENTER]]
+    eng.leave(0)
+    eng.leave(1)
+    ev = eng.tick()
+    assert ev.tolist() == [[0, 1]]  # 1 was 0's neighbour; when 1 leaves it has none
+    rp, cols = eng.relation()
+    assert len(cols) == 0 and eng.count()[0] == 0
+    # re-enter the same slots, same tick as a move of the other (forces a sub-pass)
+    eng.enter(0, 0.0, 0.0)
+    eng.enter(1, 100.0, 100.0)
+    eng.moved(0, -0.5, -0.5)  # second op on slot 0: flushes [enter 0, enter 1] first
+    ev = eng.tick()
+    assert ev.tolist() == [[1, 0 | H.EV_ENTER], [0, 1]]
+    assert eng.last.n_subticks == 2
+
+
+@pytest.mark.slow
+def test_config2_full_size_two_ticks(gpu, po):
+    """SURVEY.md §8(d) config 2 at full size: N=1,000,000, L=35,000, D=100, seed 0x5EED0002; the
+    bulk enter tick and two all-moving ticks against oracle (ii)."""
+    from goworld_amd.engine import Engine
+    n, L, seed = 1_000_000, 35000.0, 0x5EED0002
+    x, z = po.workload_init(seed, n, L)
+    eng = Engine(100.0, n, bounds=(0, 0, L, L))
+    orc = po.GridOracle(100.0, n, (0, 0, L, L))
+    slots = np.arange(n, dtype=np.uint32)
+    orc.bulk_enter(slots, x, z)  # events suppressed on the oracle side: compare relation instead
+    eng_ops = [(H.ENTER, i, float(x[i]), float(z[i])) for i in range(n)]
+    ev0 = H.gpu_tick(eng, eng_ops)
+    rg, ro = eng.relation(), orc.relation()
+    assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1])
+    assert len(ev0) == len(ro[1]) // 2  # one ENTER per pair, raised by the later Enter
+    for t in (1, 2):
+        po.workload_step(seed, t, x, z, L, 1.0)
+        orc.moved_batch(slots, x, z)
+        ev = orc.take_events()
+        want = ev[np.lexsort((ev[:, 1], ev[:, 0]))]  # rank == slot
+        eng.stage_moves(slots, x, z)
+        got = eng.tick()
+        assert_same(got, want, f"1M tick {t}")
+        assert len(got) > 10000
