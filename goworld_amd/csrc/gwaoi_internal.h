@@ -58,6 +58,7 @@ struct ApplyArgs {
   uint32_t* old_side;        // side array of the old grid
   const uint32_t* old_gidx;  // slot -> entry index in the old grid
   uint32_t* ctr;
+  uint32_t* rank_tail;        // rank_cnt[n_ops], zeroed (the scan's total slot)
 };
 
 struct BinArgs {
@@ -113,10 +114,17 @@ void launch_bin_scatter(const BinArgs& a, hipStream_t st);
 void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st);
 uint32_t scan_part_words(uint32_t n);
 void launch_sweep(const SweepArgs& a, hipStream_t st);
-void launch_sweep_leaves(const SweepArgs& a, hipStream_t st);
-void launch_place(const uint4* ev_tmp, const uint32_t* ctr, uint32_t ev_cap, const uint32_t* rank_off,
-                  uint2* ev_out, hipStream_t st);
-void launch_slice_sort(const uint32_t* rank_off, uint32_t n_ops, uint2* ev_out, hipStream_t st);
+// Event ordering runs without a host round trip: each step checks on the device that the sweep's
+// event count fit both buffers (else it does nothing and the host re-runs after growing them).
+struct EvGuard {
+  const uint32_t* ctr;
+  uint32_t tmp_cap;
+  uint64_t keep;     // events already in ev_out from earlier passes of this tick
+  uint64_t out_cap;
+};
+void launch_place(const uint4* ev_tmp, const EvGuard& g, const uint32_t* rank_off, uint2* ev_out, hipStream_t st);
+void launch_slice_sort(const uint32_t* rank_off, uint32_t n_ops, const EvGuard& g, uint2* ev_out, hipStream_t st);
+void launch_copy_out(const uint2* ev_out, const EvGuard& g, uint2* host_mapped, hipStream_t st);
 void launch_relation(const RelArgs& a, hipStream_t st);
 void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, hipStream_t st);
 void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st);

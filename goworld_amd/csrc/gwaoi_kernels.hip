@@ -113,6 +113,7 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   if (i >= a.n_ops) return;
   const uint32_t s = a.op_slot[i];
   const uint32_t q = a.base + i;
+  if (i == 0) *a.rank_tail = 0u;
   const uint8_t kind = a.op_kind ? a.op_kind[i] : (uint8_t)OP_MOVE;
   if (a.check) {
     if (s >= a.cap) {
@@ -279,18 +280,36 @@ void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Sweep: one thread per mover.
-__device__ __forceinline__ void emit(const SweepArgs& a, uint32_t rank, uint32_t mover, uint32_t other,
-                                     bool enter) {
-  const uint32_t idx = atomicAdd(&a.ctr[CTR_EVENTS], 1u);
-  const uint32_t local = atomicAdd(&a.rank_cnt[rank], 1u);
-  if (enter) atomicAdd(&a.ctr[CTR_ENTER], 1u);
-  if (idx < a.ev_cap) a.ev_tmp[idx] = make_uint4(rank, local, mover, other | (enter ? 0x80000000u : 0u));
+// Sweep: one thread per mover. Events are rare (~0.3 per mover per tick) but a single global counter
+// hit by every event serialises at the memory side, so each block stages its events in LDS and
+// reserves its output range with ONE global atomic; a mover's events are numbered in a register
+// (one thread per mover), and its count is stored once, without atomics.
+constexpr int kEvLds = 1024;  // events staged per block (16 KiB); overflow goes straight to global
+
+struct EvQueue {
+  uint4 ev[kEvLds];
+  uint32_t n;
+  uint32_t enter;
+  uint32_t base;
+};
+
+__device__ __forceinline__ void emit(const SweepArgs& a, EvQueue& q, uint32_t rank, uint32_t local,
+                                     uint32_t mover, uint32_t other, bool enter) {
+  const uint4 rec = make_uint4(rank, local, mover, other | (enter ? 0x80000000u : 0u));
+  const uint32_t li = atomicAdd(&q.n, 1u);
+  if (li < (uint32_t)kEvLds) {
+    q.ev[li] = rec;
+  } else {
+    const uint32_t gi = atomicAdd(&a.ctr[CTR_EVENTS], 1u);
+    if (gi < a.ev_cap) a.ev_tmp[gi] = rec;
+  }
+  if (enter) atomicAdd(&q.enter, 1u);
 }
 
-// valid1: m is present after its op (not a Leave); (mx1, mz1) its new position.
-__device__ __forceinline__ void sweep_mover(const SweepArgs& a, uint32_t sm, uint32_t q, bool valid1,
-                                            float mx1, float mz1) {
+// valid1: m is present after its op (not a Leave); (mx1, mz1) its new position. Returns the number
+// of events m raised.
+__device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, EvQueue& eq, uint32_t sm, uint32_t q,
+                                                bool valid1, float mx1, float mz1) {
   const uint32_t sp = a.space_of[sm];
   const uint32_t q0 = a.old_seq[sm];
   const bool valid0 = q0 != 0;
@@ -301,6 +320,7 @@ __device__ __forceinline__ void sweep_mover(const SweepArgs& a, uint32_t sm, uin
   const uint32_t rank = q - a.base;
   const Bounds b1 = {mx1 - D, mx1 + D, mz1 - D, mz1 + D};
   const Bounds b0 = {mx0 - D, mx0 + D, mz0 - D, mz0 + D};
+  uint32_t local = 0;
 
   // (A) old grid: candidates o at their start-of-pass position that have not acted yet in this pass
   //     (no op, or a later op). before = in(L, F) at the start of the pass; after = in(m_new, o_old).
@@ -317,7 +337,7 @@ __device__ __forceinline__ void sweep_mover(const SweepArgs& a, uint32_t sm, uin
       bool before = false;
       if (valid0) before = (e.w > q0) ? inbox(ox, oz, D, mx0, mz0) : b0.has(ox, oz);
       const bool after = valid1 && b1.has(ox, oz);
-      if (before != after) emit(a, rank, sm, e.z, after);
+      if (before != after) emit(a, eq, rank, local++, sm, e.z, after);
     });
   }
   // (B) new grid: candidates o that acted earlier in this pass and are present after it.
@@ -331,59 +351,76 @@ __device__ __forceinline__ void sweep_mover(const SweepArgs& a, uint32_t sm, uin
       const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
       const bool before = valid0 && inbox(ox, oz, D, mx0, mz0);
       const bool after = valid1 && b1.has(ox, oz);
-      if (before != after) emit(a, rank, sm, e.z, after);
+      if (before != after) emit(a, eq, rank, local++, sm, e.z, after);
     });
+  }
+  return local;
+}
+
+// Threads [0, n_new): new-grid entries (movers present after the pass are those whose seq belongs
+// to this pass). Threads [n_new, n_new + n_leaves): Leave ops (absent after the pass).
+__global__ void __launch_bounds__(kBlock) k_sweep(SweepArgs a) {
+  __shared__ EvQueue eq;
+  if (threadIdx.x == 0) {
+    eq.n = 0;
+    eq.enter = 0;
+  }
+  __syncthreads();
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t < a.n_new) {
+    const uint4 e = a.ng.ent[t];
+    if (e.w >= a.base) a.rank_cnt[e.w - a.base] = sweep_mover(a, eq, e.z, e.w, true, __uint_as_float(e.x),
+                                                             __uint_as_float(e.y));
+  } else if (t < a.n_new + a.n_leaves) {
+    const uint32_t i = a.leave_ops[t - a.n_new];
+    a.rank_cnt[i] = sweep_mover(a, eq, a.op_slot[i], a.base + i, false, 0.0f, 0.0f);
+  }
+  __syncthreads();
+  const uint32_t nq = min(eq.n, (uint32_t)kEvLds);
+  if (threadIdx.x == 0) {
+    eq.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+    if (eq.enter) atomicAdd(&a.ctr[CTR_ENTER], eq.enter);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
+    const uint32_t gi = eq.base + i;
+    if (gi < a.ev_cap) a.ev_tmp[gi] = eq.ev[i];
   }
 }
 
-// Movers that are present after the pass: every new-grid entry whose seq belongs to this pass.
-__global__ void __launch_bounds__(kBlock) k_sweep(SweepArgs a) {
-  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= a.n_new) return;
-  const uint4 e = a.ng.ent[j];
-  if (e.w < a.base) return;  // did not act in this pass
-  sweep_mover(a, e.z, e.w, true, __uint_as_float(e.x), __uint_as_float(e.y));
-}
-
-// Leave ops (absent after the pass, so not in the new grid).
-__global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  if (t >= a.n_leaves) return;
-  const uint32_t i = a.leave_ops[t];
-  sweep_mover(a, a.op_slot[i], a.base + i, false, 0.0f, 0.0f);
-}
-
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
-  if (!a.n_new) return;
-  hipLaunchKernelGGL(k_sweep, dim3((a.n_new + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
-}
-void launch_sweep_leaves(const SweepArgs& a, hipStream_t st) {
-  if (!a.n_leaves) return;
-  hipLaunchKernelGGL(k_sweep_leaves, dim3((a.n_leaves + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+  const uint32_t n = a.n_new + a.n_leaves;
+  if (!n) return;
+  hipLaunchKernelGGL(k_sweep, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
 }
 
 // ---------------------------------------------------------------------------------------------
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each
 // rank's slice sorted by other|kind (LEAVE = bit31 clear sorts first).
-__global__ void __launch_bounds__(kBlock) k_place(const uint4* __restrict__ ev_tmp, const uint32_t* ctr,
-                                                  uint32_t ev_cap, const uint32_t* __restrict__ rank_off,
-                                                  uint2* __restrict__ ev_out) {
-  const uint32_t n = min(ctr[CTR_EVENTS], ev_cap);
+__device__ __forceinline__ bool ev_fits(const EvGuard& g, uint32_t* n) {
+  *n = g.ctr[CTR_EVENTS];
+  return *n <= g.tmp_cap && g.keep + *n <= g.out_cap;
+}
+
+__global__ void __launch_bounds__(kBlock) k_place(const uint4* __restrict__ ev_tmp, EvGuard g,
+                                                  const uint32_t* __restrict__ rank_off, uint2* __restrict__ ev_out) {
+  uint32_t n;
+  if (!ev_fits(g, &n)) return;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     const uint4 e = ev_tmp[i];
     ev_out[rank_off[e.x] + e.y] = make_uint2(e.z, e.w);
   }
 }
 
-void launch_place(const uint4* ev_tmp, const uint32_t* ctr, uint32_t ev_cap, const uint32_t* rank_off,
-                  uint2* ev_out, hipStream_t st) {
-  hipLaunchKernelGGL(k_place, dim3(1024), dim3(kBlock), 0, st, ev_tmp, ctr, ev_cap, rank_off, ev_out);
+void launch_place(const uint4* ev_tmp, const EvGuard& g, const uint32_t* rank_off, uint2* ev_out, hipStream_t st) {
+  hipLaunchKernelGGL(k_place, dim3(1024), dim3(kBlock), 0, st, ev_tmp, g, rank_off, ev_out);
 }
 
 __global__ void __launch_bounds__(kBlock) k_slice_sort(const uint32_t* __restrict__ rank_off, uint32_t n_ops,
-                                                       uint2* __restrict__ ev) {
+                                                       EvGuard g, uint2* __restrict__ ev) {
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-  if (r >= n_ops) return;
+  uint32_t n;
+  if (r >= n_ops || !ev_fits(g, &n)) return;
   const uint32_t b = rank_off[r], e = rank_off[r + 1];
   for (uint32_t i = b + 1; i < e; ++i) {
     const uint2 v = ev[i];
@@ -396,10 +433,22 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(const uint32_t* __restric
   }
 }
 
-void launch_slice_sort(const uint32_t* rank_off, uint32_t n_ops, uint2* ev_out, hipStream_t st) {
+void launch_slice_sort(const uint32_t* rank_off, uint32_t n_ops, const EvGuard& g, uint2* ev_out, hipStream_t st) {
   if (!n_ops) return;
-  hipLaunchKernelGGL(k_slice_sort, dim3((n_ops + kBlock - 1) / kBlock), dim3(kBlock), 0, st, rank_off, n_ops,
+  hipLaunchKernelGGL(k_slice_sort, dim3((n_ops + kBlock - 1) / kBlock), dim3(kBlock), 0, st, rank_off, n_ops, g,
                      ev_out);
+}
+
+// Deliver the ordered events to mapped pinned host memory (GPU-initiated PCIe writes), so the host
+// needs no second round trip to learn the count before a copy.
+__global__ void __launch_bounds__(kBlock) k_copy_out(const uint2* __restrict__ ev, EvGuard g, uint2* host) {
+  uint32_t n;
+  if (!ev_fits(g, &n)) return;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) host[i] = ev[i];
+}
+
+void launch_copy_out(const uint2* ev_out, const EvGuard& g, uint2* host_mapped, hipStream_t st) {
+  hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, ev_out, g, host_mapped);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -147,7 +147,8 @@ struct gwaoi_mgr {
   // events
   uint4* ev_tmp = nullptr;
   uint2* ev_out = nullptr;   // device, accumulated over the passes of one tick
-  gwaoi_event* h_ev = nullptr;  // pinned, accumulated over the passes of one tick
+  gwaoi_event* h_ev = nullptr;  // pinned + mapped, accumulated over the passes of one tick
+  uint2* d_hev = nullptr;       // device alias of h_ev (the copy-out kernel writes it over PCIe)
   uint64_t ev_cap = 0;       // capacity of ev_out / h_ev
   uint32_t tmp_cap = 0;      // capacity of ev_tmp
   uint64_t tick_events = 0, tick_enter = 0;  // accumulated over the passes since the last tick
@@ -251,10 +252,14 @@ int ensure_events(gwaoi_mgr* m, uint64_t need_out, uint32_t need_tmp, uint64_t k
     uint2* nd = nullptr;
     gwaoi_event* nh = nullptr;
     RCHK(dalloc(&nd, nc));
-    int r = halloc(&nh, nc);
-    if (r) {
+    hipError_t he = hipHostMalloc((void**)&nh, nc * sizeof(gwaoi_event), hipHostMallocMapped | hipHostMallocCoherent);
+    void* dh = nullptr;
+    if (he == hipSuccess) he = hipHostGetDevicePointer(&dh, nh, 0);
+    if (he != hipSuccess) {
+      set_err("mapped host event buffer (%llu events): %s", (unsigned long long)nc, hipGetErrorString(he));
       hipFree(nd);
-      return r;
+      if (nh) hipHostFree(nh);
+      return GWAOI_ERR_NOMEM;
     }
     if (keep) {
       HIPCHK(hipMemcpyAsync(nd, m->ev_out, keep * sizeof(uint2), hipMemcpyDeviceToDevice, m->stream));
@@ -265,6 +270,7 @@ int ensure_events(gwaoi_mgr* m, uint64_t need_out, uint32_t need_tmp, uint64_t k
     if (m->h_ev) hipHostFree(m->h_ev);
     m->ev_out = nd;
     m->h_ev = nh;
+    m->d_hev = (uint2*)dh;
     m->ev_cap = nc;
   }
   return GWAOI_OK;
@@ -387,6 +393,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   a.old_side = m->grid[og].side;
   a.old_gidx = m->grid[og].gidx;
   a.ctr = m->ctr;
+  a.rank_tail = m->rank_cnt + n_ops;
   gw::launch_apply(a, st);
   HIPCHK(hipGetLastError());
   if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
@@ -398,9 +405,11 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   const uint64_t keep = m->tick_events;
   // events: expected count is small; grow and re-run the (pure) sweep on overflow
   for (int attempt = 0;; ++attempt) {
-    HIPCHK(hipMemsetAsync(m->rank_cnt, 0, (size_t)(n_ops + 1) * sizeof(uint32_t), st));
-    HIPCHK(hipMemsetAsync(m->ctr, 0, 1 * sizeof(uint32_t), st));           // CTR_EVENTS
-    HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
+    if (attempt) {  // re-run after growing the event buffers: reset what the sweep accumulates
+      HIPCHK(hipMemsetAsync(m->rank_cnt + n_ops, 0, sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
+    }
     gw::SweepArgs s;
     s.og = {m->grid[og].ent, m->grid[og].cs, m->grid[og].side, m->grid[og].d_geom};
     s.ng = {m->grid[ng].ent, m->grid[ng].cs, m->grid[ng].side, m->grid[ng].d_geom};
@@ -418,10 +427,17 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.rank_cnt = m->rank_cnt;
     s.ctr = m->ctr;
     gw::launch_sweep(s, st);
-    gw::launch_sweep_leaves(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
+    // canonical order; every step is guarded on the device against a buffer overflow, so the host
+    // synchronises once, at the end of the pass
     gw::launch_scan(m->rank_cnt, n_ops + 1, m->part, st);
+    const gw::EvGuard g = {m->ctr, m->tmp_cap, keep, m->ev_cap};
+    gw::launch_place(m->ev_tmp, g, m->rank_cnt, m->ev_out + keep, st);
+    gw::launch_slice_sort(m->rank_cnt, n_ops, g, m->ev_out + keep, st);
+    if (copy_events) gw::launch_copy_out(m->ev_out + keep, g, m->d_hev + keep, st);
+    HIPCHK(hipGetLastError());
+    if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
     HIPCHK(hipMemcpyAsync(m->h_ctr, m->ctr, gw::CTR_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (m->h_ctr[gw::CTR_ERR]) {
@@ -438,14 +454,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       set_err("event buffer overflow persisted");
       return GWAOI_ERR_NOMEM;
     }
-    uint2* out = m->ev_out + keep;
-    gw::launch_place(m->ev_tmp, m->ctr, m->tmp_cap, m->rank_cnt, out, st);
-    gw::launch_slice_sort(m->rank_cnt, n_ops, out, st);
-    HIPCHK(hipGetLastError());
-    if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
-    if (copy_events && nev)
-      HIPCHK(hipMemcpyAsync(m->h_ev + keep, out, (size_t)nev * sizeof(uint2), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
     m->tick_events += nev;
     m->tick_enter += m->h_ctr[gw::CTR_ENTER];
     if (m->timing) {
