@@ -107,6 +107,7 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cells-per-dist", type=float, default=None)
+    ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -162,6 +163,8 @@ def main():
     eng = Engine(D, capacity=n, device=dev, bounds=(0.0, 0.0, L, L))
     if args.cells_per_dist:
         eng.debug_set_cells_per_dist(args.cells_per_dist)
+    if not args.sweep_lds:
+        eng.debug_set_sweep_lds(False)
     x0 = snap.download(np.float32, n, 0)
     z0 = snap.download(np.float32, n, 4 * n)
     eng.stage_enters(np.arange(n, dtype=np.uint32), x0, z0)

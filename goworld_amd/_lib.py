@@ -32,7 +32,7 @@ ABI_SYMBOLS = (
 TOOL_SYMBOLS = (
     "gwaoi_device_count", "gwaoi_dev_malloc", "gwaoi_dev_free", "gwaoi_dev_htod", "gwaoi_dev_dtoh",
     "gwaoi_dev_sync", "gwaoi_wl_init", "gwaoi_wl_step", "gwaoi_wl_iota", "gwaoi_debug_set_next_seq",
-    "gwaoi_debug_set_cells_per_dist",
+    "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_sweep_lds",
 )
 
 
@@ -126,6 +126,7 @@ def load(path: str = SO_PATH):
         "gwaoi_wl_iota": ([ctypes.c_int, vp, u32], ctypes.c_int),
         "gwaoi_debug_set_next_seq": ([vp, u32], ctypes.c_int),
         "gwaoi_debug_set_cells_per_dist": ([vp, f32], ctypes.c_int),
+        "gwaoi_debug_set_sweep_lds": ([vp, ctypes.c_int], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -14,26 +14,35 @@ enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2 };
 enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u };
 
 // Counters block in device memory (one 64-B line).
-enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_N = 16 };
+enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_N = 16 };
 
-// Cell geometry of one Space inside one grid snapshot. A grid is a counting sort of every present
-// entity by cell key = base + cz * ncx + cx; the cells of one row of one Space are contiguous, so a
-// query box is (rows) x (one contiguous segment per row).
+// Cells are grouped in square tiles of kTile x kTile cells; cell keys are tile-major,
+//   key = base + (tz * ntx + tx) * 256 + lz * 16 + lx   (cx = 16 tx + lx, cz = 16 tz + lz),
+// so a tile's entities are contiguous (the unit of work and of LDS staging in the sweep) and a cell
+// row inside a tile is contiguous.
+constexpr int kTile = 16;
+constexpr int kTileCells = kTile * kTile;
+
+// Cell geometry of one Space inside one grid snapshot.
 struct Geom {
-  float x0, z0;   // origin of cell (0,0)
-  float inv_c;    // 1 / cell side
-  float D;        // AOI distance of the Space (manager-wide per Space, as NewXZListAOIManager)
-  int32_t ncx, ncz;
-  uint32_t base;  // first cell key of this Space
+  float x0, z0;       // origin of cell (0,0)
+  float inv_c;        // 1 / cell side
+  float D;            // AOI distance of the Space (manager-wide per Space, as NewXZListAOIManager)
+  int32_t ncx, ncz;   // cells per axis (multiples of kTile)
+  int32_t ntx, ntz;   // tiles per axis
+  uint32_t base;      // first cell key of this Space
+  uint32_t tile_base; // first tile index of this Space (base / 256)
+  int32_t reach;      // halo (cells) staged around a tile in the sweep
   uint32_t pad;
 };
 
 // One grid snapshot: all present entities sorted by cell. ent[j] = {x bits, z bits, slot, seq}.
 struct GridView {
   const uint4* ent;
-  const uint32_t* cs;    // cell_start[ncells + 1]
-  const uint32_t* side;  // side[j] = op seq of entry j's slot this pass (old-grid role), else stale
-  const Geom* geom;      // [nspaces]
+  const uint32_t* cs;          // cell_start[ncells + 1]
+  const uint32_t* side;        // side[j] = op seq of entry j's slot this pass (old-grid role), else stale
+  const Geom* geom;            // [nspaces]
+  const uint32_t* tile_space;  // [ntiles] tile -> space
 };
 
 struct ApplyArgs {
@@ -75,9 +84,15 @@ struct BinArgs {
   uint32_t* gidx;
 };
 
+// A unit of sweep work: up to kUnit consecutive new-grid entries of one tile.
+constexpr int kUnit = 512;
+
 struct SweepArgs {
   GridView og;  // old grid: state at the start of the pass
   GridView ng;  // new grid: state at the end of the pass
+  const uint4* units;  // {space, tile, e0, e1}; count in ctr[CTR_UNITS]
+  uint32_t max_units;  // blocks [0, max_units) take units, the rest take Leave ops
+  int use_lds;         // 0: every unit on the global-memory path (A/B and fallback)
   const float* old_x;
   const float* old_z;
   const uint32_t* old_seq;
@@ -113,7 +128,10 @@ void launch_bin_scatter(const BinArgs& a, hipStream_t st);
 // part: scratch of scan_part_words(n) words.
 void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st);
 uint32_t scan_part_words(uint32_t n);
+void launch_units(const GridView& ng, uint32_t ntiles, uint4* units, uint32_t* ctr, hipStream_t st);
 void launch_sweep(const SweepArgs& a, hipStream_t st);
+size_t sweep_lds_bytes();
+void sweep_init();  // once per process (dynamic LDS limit of the sweep)
 // Event ordering runs without a host round trip: each step checks on the device that the sweep's
 // event count fit both buffers (else it does nothing and the host re-runs after growing them).
 struct EvGuard {

@@ -64,11 +64,14 @@ __device__ __forceinline__ CellBox qbox(const Geom& g, float cx, float cz) {
   return b;
 }
 
-// Visit the entries of the cells covered by the union of box A (if va) and box B (if vb), each
-// entry once: one or two contiguous segments per cell row.
-template <class F>
-__device__ __forceinline__ void for_each_entry(const Geom& g, const uint32_t* __restrict__ cs, bool va,
-                                               CellBox A, bool vb, CellBox B, F&& f) {
+__device__ __forceinline__ uint32_t cell_key(const Geom& g, int cx, int cz) {
+  return g.base + ((uint32_t)((cz >> 4) * g.ntx + (cx >> 4)) << 8) + (uint32_t)(((cz & 15) << 4) | (cx & 15));
+}
+
+// Row intervals of the union of box A (if va) and box B (if vb): one or two column intervals per
+// row, so every cell is visited once.
+template <class RowF>
+__device__ __forceinline__ void for_each_row_interval(bool va, CellBox A, bool vb, CellBox B, RowF&& rf) {
   int r0 = va ? A.z0 : B.z0, r1 = va ? A.z1 : B.z1;
   if (va && vb) {
     r0 = min(A.z0, B.z0);
@@ -77,31 +80,37 @@ __device__ __forceinline__ void for_each_entry(const Geom& g, const uint32_t* __
   for (int r = r0; r <= r1; ++r) {
     const bool ia = va && r >= A.z0 && r <= A.z1;
     const bool ib = vb && r >= B.z0 && r <= B.z1;
-    int s0, s1, t0 = 0, t1 = -1;
     if (ia && ib) {
       if (B.x0 <= A.x1 + 1 && A.x0 <= B.x1 + 1) {
-        s0 = min(A.x0, B.x0);
-        s1 = max(A.x1, B.x1);
+        rf(r, min(A.x0, B.x0), max(A.x1, B.x1));
       } else {
-        s0 = A.x0;
-        s1 = A.x1;
-        t0 = B.x0;
-        t1 = B.x1;
+        rf(r, A.x0, A.x1);
+        rf(r, B.x0, B.x1);
       }
     } else if (ia) {
-      s0 = A.x0;
-      s1 = A.x1;
+      rf(r, A.x0, A.x1);
     } else if (ib) {
-      s0 = B.x0;
-      s1 = B.x1;
-    } else {
-      continue;
+      rf(r, B.x0, B.x1);
     }
-    const uint32_t row = g.base + (uint32_t)r * (uint32_t)g.ncx;
-    for (uint32_t j = cs[row + s0], e = cs[row + s1 + 1]; j < e; ++j) f(j);
-    if (t1 >= t0)
-      for (uint32_t j = cs[row + t0], e = cs[row + t1 + 1]; j < e; ++j) f(j);
   }
+}
+
+// Global-memory path: entries of row r, columns [c0, c1]: one contiguous segment per tile crossed.
+template <class F>
+__device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t* __restrict__ cs, int r, int c0,
+                                                   int c1, F&& f) {
+  const uint32_t rowbase = g.base + ((uint32_t)((r >> 4) * g.ntx) << 8) + (uint32_t)((r & 15) << 4);
+  for (int tx = c0 >> 4; tx <= (c1 >> 4); ++tx) {
+    const int lo = max(c0, tx << 4), hi = min(c1, (tx << 4) + 15);
+    const uint32_t k = rowbase + ((uint32_t)tx << 8) + (uint32_t)(lo & 15);
+    for (uint32_t j = cs[k], e = cs[k + (uint32_t)(hi - lo) + 1]; j < e; ++j) f(j);
+  }
+}
+
+template <class F>
+__device__ __forceinline__ void for_each_entry(const Geom& g, const uint32_t* __restrict__ cs, bool va,
+                                               CellBox A, bool vb, CellBox B, F&& f) {
+  for_each_row_interval(va, A, vb, B, [&](int r, int c0, int c1) { row_entries_global(g, cs, r, c0, c1, f); });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -158,8 +167,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_count(BinArgs a) {
   const uint32_t q = a.seq[s];
   if (!q) return;
   const Geom g = a.geom[a.space_of[s]];
-  const uint32_t key = g.base + (uint32_t)cellc(a.pos_z[s], g.z0, g.inv_c, g.ncz) * (uint32_t)g.ncx +
-                       (uint32_t)cellc(a.pos_x[s], g.x0, g.inv_c, g.ncx);
+  const uint32_t key = cell_key(g, cellc(a.pos_x[s], g.x0, g.inv_c, g.ncx), cellc(a.pos_z[s], g.z0, g.inv_c, g.ncz));
   a.key_of[s] = key;
   a.local_of[s] = atomicAdd(&a.cs[key], 1u);
 }
@@ -280,118 +288,322 @@ void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Sweep: one thread per mover. Events are rare (~0.3 per mover per tick) but a single global counter
-// hit by every event serialises at the memory side, so each block stages its events in LDS and
-// reserves its output range with ONE global atomic; a mover's events are numbered in a register
-// (one thread per mover), and its count is stored once, without atomics.
-constexpr int kEvLds = 1024;  // events staged per block (16 KiB); overflow goes straight to global
+// Work units: every tile's new-grid entries, split evenly into chunks of at most kUnit. Appended
+// with one atomic per wave (unit order is irrelevant: events are ordered canonically later).
+__global__ void __launch_bounds__(kBlock) k_units(GridView ng, uint32_t ntiles, uint4* __restrict__ units,
+                                                  uint32_t* ctr) {
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  uint32_t start = 0, cnt = 0;
+  if (t < ntiles) {
+    start = ng.cs[t << 8];
+    cnt = ng.cs[(t + 1) << 8] - start;
+  }
+  const uint32_t nu = (cnt + kUnit - 1) / kUnit;
+  const uint32_t incl = wave_incl_scan(nu);
+  const uint32_t tot = __shfl(incl, 63, 64);
+  uint32_t wbase = 0;
+  if ((threadIdx.x & 63) == 63 && tot) wbase = atomicAdd(&ctr[CTR_UNITS], tot);
+  wbase = __shfl(wbase, 63, 64);
+  if (!nu) return;
+  const uint32_t chunk = (cnt + nu - 1) / nu;
+  const uint32_t sp = ng.tile_space[t];
+  uint32_t u = wbase + incl - nu;
+  for (uint32_t k = 0; k < nu; ++k, ++u) {
+    const uint32_t e0 = start + k * chunk;
+    units[u] = make_uint4(sp, t, e0, min(e0 + chunk, start + cnt));
+  }
+}
 
-struct EvQueue {
-  uint4 ev[kEvLds];
-  uint32_t n;
-  uint32_t enter;
-  uint32_t base;
+void launch_units(const GridView& ng, uint32_t ntiles, uint4* units, uint32_t* ctr, hipStream_t st) {
+  hipLaunchKernelGGL(k_units, dim3((ntiles + kBlock - 1) / kBlock), dim3(kBlock), 0, st, ng, ntiles, units, ctr);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sweep. One block (kUnit = 512 threads) per unit of up to 512 new-grid entries of one tile; one
+// thread per mover. The block stages, for BOTH grids, every entry of the unit's tile rows plus a
+// halo of `reach` cells into LDS (cell starts, entries, and the old grid's side stamps), laid out
+// row by row so that any row interval of the region is one contiguous LDS range. Each mover then
+// walks its candidates in LDS. Movers whose query boxes leave the region (teleports), units whose
+// region does not fit, and Leave ops take the global-memory path; both paths evaluate the same
+// predicates.
+//
+// Events are rare (~0.3 per mover per tick), but one global counter hit by every event serialises
+// at the memory side, so each block stages its events in LDS and reserves its output range with ONE
+// global atomic; a mover's events are numbered in a register (one thread per mover) and its count is
+// stored once, without atomics.
+constexpr int kSweepBlock = kUnit;
+constexpr int kEvLds = 512;      // events staged per block before spilling to global atomics
+constexpr int kRegCells = 1024;  // max cells in a staged region
+constexpr int kCap = 1536;       // max entries staged per grid
+
+struct SweepSmem {  // dynamic LDS, carved by hand (16-B aligned offsets)
+  uint32_t n, enter, base, flags;
+  uint32_t ws[16];                 // block-scan scratch
+  union {
+    uint4 ev[kEvLds];           // event queue (after staging)
+    uint32_t gs[2][kRegCells];  // global start of each region cell (during staging)
+  } u;
+  uint32_t lcs[2][kRegCells + 4];  // LDS start of each region cell (+ total)
+  uint4 ent[2][kCap];
+  uint32_t side[kCap];
 };
 
-__device__ __forceinline__ void emit(const SweepArgs& a, EvQueue& q, uint32_t rank, uint32_t local,
+size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
+
+__device__ __forceinline__ void emit(const SweepArgs& a, SweepSmem& sm, uint32_t rank, uint32_t local,
                                      uint32_t mover, uint32_t other, bool enter) {
   const uint4 rec = make_uint4(rank, local, mover, other | (enter ? 0x80000000u : 0u));
-  const uint32_t li = atomicAdd(&q.n, 1u);
+  const uint32_t li = atomicAdd(&sm.n, 1u);
   if (li < (uint32_t)kEvLds) {
-    q.ev[li] = rec;
+    sm.u.ev[li] = rec;
   } else {
     const uint32_t gi = atomicAdd(&a.ctr[CTR_EVENTS], 1u);
     if (gi < a.ev_cap) a.ev_tmp[gi] = rec;
   }
-  if (enter) atomicAdd(&q.enter, 1u);
+  if (enter) atomicAdd(&sm.enter, 1u);
 }
 
-// valid1: m is present after its op (not a Leave); (mx1, mz1) its new position. Returns the number
-// of events m raised.
-__device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, EvQueue& eq, uint32_t sm, uint32_t q,
-                                                bool valid1, float mx1, float mz1) {
-  const uint32_t sp = a.space_of[sm];
-  const uint32_t q0 = a.old_seq[sm];
-  const bool valid0 = q0 != 0;
-  const float mx0 = a.old_x[sm], mz0 = a.old_z[sm];
-  const Geom go = a.og.geom[sp];
-  const Geom gn = a.ng.geom[sp];
-  const float D = go.D;
-  const uint32_t rank = q - a.base;
-  const Bounds b1 = {mx1 - D, mx1 + D, mz1 - D, mz1 + D};
-  const Bounds b0 = {mx0 - D, mx0 + D, mz0 - D, mz0 + D};
-  uint32_t local = 0;
+struct Mover {
+  uint32_t sm, q, q0, rank;
+  bool valid0, valid1;
+  float mx0, mz0, mx1, mz1, D;
+};
 
-  // (A) old grid: candidates o at their start-of-pass position that have not acted yet in this pass
-  //     (no op, or a later op). before = in(L, F) at the start of the pass; after = in(m_new, o_old).
-  {
-    const CellBox A0 = qbox(go, mx0, mz0), A1 = qbox(go, mx1, mz1);
-    const uint4* __restrict__ ent = a.og.ent;
-    const uint32_t* __restrict__ side = a.og.side;
-    for_each_entry(go, a.og.cs, valid0, A0, valid1, A1, [&](uint32_t j) {
-      const uint4 e = ent[j];
-      if (e.z == sm) return;
-      const uint32_t qo = side[j];
-      if (qo >= a.base && qo < q) return;  // o acted earlier in this pass: handled in (B)
-      const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
-      bool before = false;
-      if (valid0) before = (e.w > q0) ? inbox(ox, oz, D, mx0, mz0) : b0.has(ox, oz);
-      const bool after = valid1 && b1.has(ox, oz);
-      if (before != after) emit(a, eq, rank, local++, sm, e.z, after);
-    });
-  }
-  // (B) new grid: candidates o that acted earlier in this pass and are present after it.
-  //     before = in(o_new, m_old) (o's op set the pair); after = in(m_new, o_new).
-  {
-    const CellBox B0 = qbox(gn, mx0, mz0), B1 = qbox(gn, mx1, mz1);
-    const uint4* __restrict__ ent = a.ng.ent;
-    for_each_entry(gn, a.ng.cs, valid0, B0, valid1, B1, [&](uint32_t j) {
-      const uint4 e = ent[j];
-      if (!(e.w >= a.base && e.w < q)) return;
-      const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
-      const bool before = valid0 && inbox(ox, oz, D, mx0, mz0);
-      const bool after = valid1 && b1.has(ox, oz);
-      if (before != after) emit(a, eq, rank, local++, sm, e.z, after);
-    });
-  }
+__device__ __forceinline__ Mover make_mover(const SweepArgs& a, uint32_t sm, uint32_t q, bool valid1, float mx1,
+                                            float mz1, float D) {
+  Mover m;
+  m.sm = sm;
+  m.q = q;
+  m.q0 = a.old_seq[sm];
+  m.rank = q - a.base;
+  m.valid0 = m.q0 != 0;
+  m.valid1 = valid1;
+  m.mx0 = a.old_x[sm];
+  m.mz0 = a.old_z[sm];
+  m.mx1 = mx1;
+  m.mz1 = mz1;
+  m.D = D;
+  return m;
+}
+
+// The per-mover evaluation, over candidate iterators of the old grid (callback(entry, side)) and
+// of the new grid (callback(entry)).
+//  (A) old grid: o at its start-of-pass position, skipped if it acted earlier in this pass;
+//      before = in(L, F) over the start-of-pass state, after = in(m_new, o_old).
+//  (B) new grid: only o that acted earlier in this pass (and are present after it);
+//      before = in(o_new, m_old), after = in(m_new, o_new).
+template <class ForOld, class ForNew>
+__device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, SweepSmem& smem, const Mover& m,
+                                                ForOld&& for_old, ForNew&& for_new) {
+  const float D = m.D;
+  const Bounds b1 = {m.mx1 - D, m.mx1 + D, m.mz1 - D, m.mz1 + D};
+  const Bounds b0 = {m.mx0 - D, m.mx0 + D, m.mz0 - D, m.mz0 + D};
+  const uint32_t base = a.base;
+  uint32_t local = 0;
+  for_old([&](const uint4 e, uint32_t qo) {
+    if (e.z == m.sm) return;
+    if (qo >= base && qo < m.q) return;  // o acted earlier in this pass: handled in (B)
+    const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
+    bool before = false;
+    if (m.valid0) before = (e.w > m.q0) ? inbox(ox, oz, D, m.mx0, m.mz0) : b0.has(ox, oz);
+    const bool after = m.valid1 && b1.has(ox, oz);
+    if (before != after) emit(a, smem, m.rank, local++, m.sm, e.z, after);
+  });
+  for_new([&](const uint4 e) {
+    if (!(e.w >= base && e.w < m.q)) return;
+    const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
+    const bool before = m.valid0 && inbox(ox, oz, D, m.mx0, m.mz0);
+    const bool after = m.valid1 && b1.has(ox, oz);
+    if (before != after) emit(a, smem, m.rank, local++, m.sm, e.z, after);
+  });
   return local;
 }
 
-// Threads [0, n_new): new-grid entries (movers present after the pass are those whose seq belongs
-// to this pass). Threads [n_new, n_new + n_leaves): Leave ops (absent after the pass).
-__global__ void __launch_bounds__(kBlock) k_sweep(SweepArgs a) {
-  __shared__ EvQueue eq;
+__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, SweepSmem& smem, const Mover& m,
+                                                 const Geom& go, const Geom& gn) {
+  const CellBox A0 = qbox(go, m.mx0, m.mz0), A1 = qbox(go, m.mx1, m.mz1);
+  const CellBox B0 = qbox(gn, m.mx0, m.mz0), B1 = qbox(gn, m.mx1, m.mz1);
+  return sweep_mover(
+      a, smem, m,
+      [&](auto&& f) {
+        for_each_entry(go, a.og.cs, m.valid0, A0, m.valid1, A1, [&](uint32_t j) { f(a.og.ent[j], a.og.side[j]); });
+      },
+      [&](auto&& f) {
+        for_each_entry(gn, a.ng.cs, m.valid0, B0, m.valid1, B1, [&](uint32_t j) { f(a.ng.ent[j]); });
+      });
+}
+
+struct Region {
+  int zr0, zr1, xr0, xr1, ncols, ncells;
+  __device__ __forceinline__ bool holds(const CellBox& b) const {
+    return b.z0 >= zr0 && b.z1 <= zr1 && b.x0 >= xr0 && b.x1 <= xr1;
+  }
+};
+
+__device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& smem, const Mover& m, const Region& R,
+                                              const Geom& g) {
+  const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
+  auto rows = [&](const uint32_t* lcs, auto&& f) {
+    for_each_row_interval(m.valid0, A0, m.valid1, A1, [&](int r, int c0, int c1) {
+      const int b = (r - R.zr0) * R.ncols - R.xr0;
+      for (uint32_t j = lcs[b + c0], e = lcs[b + c1 + 1]; j < e; ++j) f(j);
+    });
+  };
+  return sweep_mover(
+      a, smem, m, [&](auto&& f) { rows(smem.lcs[0], [&](uint32_t j) { f(smem.ent[0][j], smem.side[j]); }); },
+      [&](auto&& f) { rows(smem.lcs[1], [&](uint32_t j) { f(smem.ent[1][j]); }); });
+}
+
+// exclusive scan of v over a kSweepBlock-thread block; *total = block sum (LDS scratch `ws`)
+__device__ __forceinline__ uint32_t block_excl_scan_512(uint32_t v, uint32_t* ws, uint32_t* total) {
+  constexpr int NW = kSweepBlock / 64;
+  const uint32_t inc = wave_incl_scan(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const uint32_t x = ws[k];
+    pre += k < w ? x : 0u;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc - v;
+}
+
+// Stage the region of grid `gi` (0 = old, 1 = new). Returns the staged entry count (block-uniform);
+// a count > kCap means "does not fit" and nothing was copied.
+__device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, const Region& R, SweepSmem& smem,
+                                          int gi, uint32_t* ws) {
+  uint32_t* gs = smem.u.gs[gi];
+  uint32_t* lcs = smem.lcs[gi];
+  // two region cells per thread (kRegCells = 2 * kSweepBlock)
+  const int c0 = 2 * threadIdx.x;
+  uint32_t n0 = 0, n1 = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int c = c0 + k;
+    if (c < R.ncells) {
+      const int rr = c / R.ncols, cc = c - rr * R.ncols;
+      const uint32_t key = cell_key(g, R.xr0 + cc, R.zr0 + rr);
+      const uint32_t s0 = gv.cs[key], s1 = gv.cs[key + 1];
+      gs[c] = s0;
+      (k ? n1 : n0) = s1 - s0;
+    }
+  }
+  uint32_t total;
+  const uint32_t pre = block_excl_scan_512(n0 + n1, ws, &total);
+  if (c0 < R.ncells) lcs[c0] = pre;
+  if (c0 + 1 < R.ncells) lcs[c0 + 1] = pre + n0;
+  if (threadIdx.x == 0) lcs[R.ncells] = total;
+  if (total > (uint32_t)kCap) return total;
+  __syncthreads();
+  for (int c = threadIdx.x; c < R.ncells; c += kSweepBlock) {
+    const uint32_t d = lcs[c], n = lcs[c + 1] - d, s = gs[c];
+    for (uint32_t k = 0; k < n; ++k) {
+      smem.ent[gi][d + k] = gv.ent[s + k];
+      if (gi == 0) smem.side[d + k] = gv.side[s + k];
+    }
+  }
+  return total;
+}
+
+__device__ __forceinline__ bool same_geom(const Geom& a, const Geom& b) {
+  return a.x0 == b.x0 && a.z0 == b.z0 && a.inv_c == b.inv_c && a.ncx == b.ncx && a.ncz == b.ncz && a.base == b.base;
+}
+
+__global__ void __launch_bounds__(kSweepBlock) k_sweep(SweepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  SweepSmem& smem = *reinterpret_cast<SweepSmem*>(smem_raw);
+  uint32_t* ws = smem.ws;
+
+  if (blockIdx.x < a.max_units) {
+    if (blockIdx.x >= a.ctr[CTR_UNITS]) return;  // block-uniform: no barrier reached
+    const uint4 u = a.units[blockIdx.x];
+    const Geom gn = a.ng.geom[u.x];
+    const Geom go = a.og.geom[u.x];
+    // region: the unit's cell rows and its tile's columns, plus `reach` cells around
+    bool lds = a.use_lds && gn.reach > 0 && same_geom(go, gn);
+    Region R;
+    if (lds) {
+      const uint32_t tl = u.y - gn.tile_base;
+      const int tz = (int)(tl / (uint32_t)gn.ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)gn.ntx);
+      const int rf = cellc(__uint_as_float(a.ng.ent[u.z].y), gn.z0, gn.inv_c, gn.ncz);
+      const int rl = cellc(__uint_as_float(a.ng.ent[u.w - 1].y), gn.z0, gn.inv_c, gn.ncz);
+      R.zr0 = max(0, rf - gn.reach);
+      R.zr1 = min(gn.ncz - 1, rl + gn.reach);
+      R.xr0 = max(0, tx * kTile - gn.reach);
+      R.xr1 = min(gn.ncx - 1, tx * kTile + kTile - 1 + gn.reach);
+      R.ncols = R.xr1 - R.xr0 + 1;
+      R.ncells = (R.zr1 - R.zr0 + 1) * R.ncols;
+      lds = R.ncells <= kRegCells;
+    }
+    if (lds) {
+      const uint32_t n_old = stage(a.og, go, R, smem, 0, ws);
+      __syncthreads();
+      const uint32_t n_new = stage(a.ng, gn, R, smem, 1, ws);
+      lds = n_old <= (uint32_t)kCap && n_new <= (uint32_t)kCap;  // block-uniform
+    }
+    __syncthreads();  // staging done; the gs scratch becomes the event queue
+    if (threadIdx.x == 0) {
+      smem.n = 0;
+      smem.enter = 0;
+    }
+    __syncthreads();
+    const uint32_t j = u.z + threadIdx.x;
+    if (j < u.w) {
+      const uint4 e = a.ng.ent[j];
+      if (e.w >= a.base) {  // acted in this pass
+        const Mover m = make_mover(a, e.z, e.w, true, __uint_as_float(e.x), __uint_as_float(e.y), gn.D);
+        uint32_t cnt;
+        if (lds && R.holds(qbox(gn, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(gn, m.mx0, m.mz0))))
+          cnt = sweep_lds(a, smem, m, R, gn);
+        else
+          cnt = sweep_global(a, smem, m, go, gn);
+        a.rank_cnt[m.rank] = cnt;
+      }
+    }
+  } else {
+    if (threadIdx.x == 0) {
+      smem.n = 0;
+      smem.enter = 0;
+    }
+    __syncthreads();
+    const uint32_t t = (blockIdx.x - a.max_units) * kSweepBlock + threadIdx.x;
+    if (t < a.n_leaves) {
+      const uint32_t i = a.leave_ops[t];
+      const uint32_t sm = a.op_slot[i];
+      const uint32_t sp = a.space_of[sm];
+      const Geom go = a.og.geom[sp], gn = a.ng.geom[sp];
+      const Mover m = make_mover(a, sm, a.base + i, false, 0.0f, 0.0f, go.D);
+      a.rank_cnt[i] = sweep_global(a, smem, m, go, gn);
+    }
+  }
+  // flush the block's events with one global atomic
+  __syncthreads();
+  const uint32_t nq = min(smem.n, (uint32_t)kEvLds);
   if (threadIdx.x == 0) {
-    eq.n = 0;
-    eq.enter = 0;
+    smem.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+    if (smem.enter) atomicAdd(&a.ctr[CTR_ENTER], smem.enter);
   }
   __syncthreads();
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  if (t < a.n_new) {
-    const uint4 e = a.ng.ent[t];
-    if (e.w >= a.base) a.rank_cnt[e.w - a.base] = sweep_mover(a, eq, e.z, e.w, true, __uint_as_float(e.x),
-                                                             __uint_as_float(e.y));
-  } else if (t < a.n_new + a.n_leaves) {
-    const uint32_t i = a.leave_ops[t - a.n_new];
-    a.rank_cnt[i] = sweep_mover(a, eq, a.op_slot[i], a.base + i, false, 0.0f, 0.0f);
-  }
-  __syncthreads();
-  const uint32_t nq = min(eq.n, (uint32_t)kEvLds);
-  if (threadIdx.x == 0) {
-    eq.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
-    if (eq.enter) atomicAdd(&a.ctr[CTR_ENTER], eq.enter);
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
-    const uint32_t gi = eq.base + i;
-    if (gi < a.ev_cap) a.ev_tmp[gi] = eq.ev[i];
+  for (uint32_t i = threadIdx.x; i < nq; i += kSweepBlock) {
+    const uint32_t gi = smem.base + i;
+    if (gi < a.ev_cap) a.ev_tmp[gi] = smem.u.ev[i];
   }
 }
 
+void sweep_init() {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)sizeof(SweepSmem));
+}
+
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
-  const uint32_t n = a.n_new + a.n_leaves;
-  if (!n) return;
-  hipLaunchKernelGGL(k_sweep, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+  const uint32_t nb = a.max_units + (a.n_leaves + kSweepBlock - 1) / kSweepBlock;
+  if (!nb) return;
+  hipLaunchKernelGGL(k_sweep, dim3(nb), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
 }
 
 // ---------------------------------------------------------------------------------------------

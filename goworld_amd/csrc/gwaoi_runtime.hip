@@ -89,8 +89,10 @@ struct Grid {
   uint32_t* side = nullptr;
   uint32_t* gidx = nullptr;
   gw::Geom* d_geom = nullptr;
+  uint32_t* d_tile_space = nullptr;  // tile -> space
   std::vector<gw::Geom> h_geom;  // what d_geom holds
   uint32_t ncells = 0;
+  uint32_t ntiles = 0;
 };
 
 }  // namespace
@@ -140,6 +142,9 @@ struct gwaoi_mgr {
   int cur = 0;  // grid holding the current state
   uint32_t next_seq = 1;
   uint32_t* rank_cnt = nullptr;  // [cap + 1]
+  uint4* units = nullptr;        // sweep work units
+  uint32_t max_units = 0;        // capacity of units
+  int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
   uint32_t* part = nullptr;
   uint32_t part_words = 0;
   uint32_t* ctr = nullptr;       // [CTR_N]
@@ -189,7 +194,7 @@ void space_extent(const SpaceHost& sh, float* x0, float* z0, float* x1, float* z
 
 void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
   out.resize(m->nspaces);
-  const uint64_t share = std::max<uint64_t>(16, m->max_cells / std::max<uint32_t>(1, m->nspaces));
+  const uint64_t share = std::max<uint64_t>(gw::kTileCells, m->max_cells / std::max<uint32_t>(1, m->nspaces));
   uint32_t base = 0;
   for (uint32_t s = 0; s < m->nspaces; ++s) {
     SpaceHost& sh = m->spaces[s];
@@ -199,26 +204,40 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
     if (!std::isfinite(z0) || !std::isfinite(z1) || !(z1 > z0)) { z0 = -1000.f; z1 = 1000.f; }
     double c = (double)sh.desc.dist / (double)m->cells_per_dist;
     if (!(c > 0)) c = 1.0;
-    auto dims = [&](double cc, int64_t* nx, int64_t* nz) {
-      *nx = (int64_t)(((double)x1 - x0) / cc) + 1;
-      *nz = (int64_t)(((double)z1 - z0) / cc) + 1;
+    // tiles of kTile x kTile cells; cell counts padded to whole tiles
+    auto dims = [&](double cc, int64_t* tx, int64_t* tz) {
+      const int64_t nx = (int64_t)(((double)x1 - x0) / cc) + 1, nz = (int64_t)(((double)z1 - z0) / cc) + 1;
+      *tx = (nx + gw::kTile - 1) / gw::kTile;
+      *tz = (nz + gw::kTile - 1) / gw::kTile;
     };
-    int64_t nx, nz;
-    dims(c, &nx, &nz);
-    while ((uint64_t)(nx * nz) > share || nx > (1 << 22) || nz > (1 << 22)) {
+    int64_t tx, tz;
+    dims(c, &tx, &tz);
+    while ((uint64_t)(tx * tz) * gw::kTileCells > share || tx * gw::kTile > (1 << 22) || tz * gw::kTile > (1 << 22)) {
       c *= 1.25;
-      dims(c, &nx, &nz);
+      dims(c, &tx, &tz);
     }
     gw::Geom g;
     g.x0 = x0;
     g.z0 = z0;
     g.inv_c = (float)(1.0 / c);
     g.D = sh.desc.dist;
-    g.ncx = (int32_t)nx;
-    g.ncz = (int32_t)nz;
+    g.ncx = (int32_t)(tx * gw::kTile);
+    g.ncz = (int32_t)(tz * gw::kTile);
+    g.ntx = (int32_t)tx;
+    g.ntz = (int32_t)tz;
     g.base = base;
+    g.tile_base = base / gw::kTileCells;
+    // halo for the sweep's LDS staging: a query box spans (D + margin) / c cells on each side of the
+    // mover's cell, +1 for a mover whose old position is in the neighbouring cell; larger moves take
+    // the global path. Region = (16 + 2 reach)^2 cells must fit the kernel's region budget.
+    const double maxc = std::max({std::fabs((double)x0), std::fabs((double)x1), std::fabs((double)z0),
+                                  std::fabs((double)z1)});
+    const double span = ((double)sh.desc.dist * (1.0 + 1e-5) + (maxc + sh.desc.dist) * 1e-6) / c;
+    int reach = (int)std::ceil(span) + 1;
+    if ((gw::kTile + 2 * reach) * (gw::kTile + 2 * reach) > 1024) reach = 0;  // LDS path off for this Space
+    g.reach = reach;
     g.pad = 0;
-    base += (uint32_t)(nx * nz);
+    base += (uint32_t)(tx * tz) * gw::kTileCells;
     sh.gx0 = x0;
     sh.gz0 = z0;
     sh.gx1 = x1;
@@ -232,6 +251,8 @@ uint32_t total_cells(const std::vector<gw::Geom>& g) {
   for (auto& x : g) t += (uint32_t)(x.ncx * x.ncz);
   return t;
 }
+
+uint32_t total_tiles(const std::vector<gw::Geom>& g) { return total_cells(g) / gw::kTileCells; }
 
 bool same_geom(const std::vector<gw::Geom>& a, const std::vector<gw::Geom>& b) {
   return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(gw::Geom)) == 0;
@@ -280,8 +301,13 @@ int upload_geom(gwaoi_mgr* m, Grid& g, const std::vector<gw::Geom>& geo) {
   if (same_geom(g.h_geom, geo)) return GWAOI_OK;
   g.h_geom = geo;
   g.ncells = total_cells(geo);
-  HIPCHK(hipMemcpyAsync(g.d_geom, g.h_geom.data(), geo.size() * sizeof(gw::Geom), hipMemcpyHostToDevice,
-                        m->stream));
+  g.ntiles = total_tiles(geo);
+  std::vector<uint32_t> ts(g.ntiles);
+  for (uint32_t s = 0; s < geo.size(); ++s)
+    for (uint32_t t = 0; t < (uint32_t)(geo[s].ntx * geo[s].ntz); ++t) ts[geo[s].tile_base + t] = s;
+  HIPCHK(hipStreamSynchronize(m->stream));  // the staging vectors below are pageable
+  HIPCHK(hipMemcpy(g.d_geom, g.h_geom.data(), geo.size() * sizeof(gw::Geom), hipMemcpyHostToDevice));
+  if (g.ntiles) HIPCHK(hipMemcpy(g.d_tile_space, ts.data(), g.ntiles * sizeof(uint32_t), hipMemcpyHostToDevice));
   return GWAOI_OK;
 }
 
@@ -399,6 +425,11 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
 
   RCHK(build_grid(m, ng));
+  {
+    const Grid& G = m->grid[ng];
+    gw::launch_units({G.ent, G.cs, G.side, G.d_geom, G.d_tile_space}, G.ntiles, m->units, m->ctr, st);
+    HIPCHK(hipGetLastError());
+  }
   if (m->timing) HIPCHK(hipEventRecord(m->tev[2], st));
 
   const uint32_t n_new = dev ? m->n_present_dev : m->n_present;
@@ -411,8 +442,11 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
     }
     gw::SweepArgs s;
-    s.og = {m->grid[og].ent, m->grid[og].cs, m->grid[og].side, m->grid[og].d_geom};
-    s.ng = {m->grid[ng].ent, m->grid[ng].cs, m->grid[ng].side, m->grid[ng].d_geom};
+    s.og = {m->grid[og].ent, m->grid[og].cs, m->grid[og].side, m->grid[og].d_geom, m->grid[og].d_tile_space};
+    s.ng = {m->grid[ng].ent, m->grid[ng].cs, m->grid[ng].side, m->grid[ng].d_geom, m->grid[ng].d_tile_space};
+    s.units = m->units;
+    s.max_units = std::min<uint32_t>(m->max_units, m->grid[ng].ntiles + n_new / gw::kUnit + 1);
+    s.use_lds = m->sweep_lds;
     s.old_x = m->old_x;
     s.old_z = m->old_z;
     s.old_seq = m->old_seq;
@@ -545,12 +579,12 @@ void free_all(gwaoi_mgr* m) {
   if (m->stream) hipStreamSynchronize(m->stream);
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->stamp,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_op_x, m->d_op_z,
-                   m->d_op_kind, m->rank_cnt, m->part, m->ctr, m->ev_tmp, m->ev_out};
+                   m->d_op_kind, m->rank_cnt, m->part, m->ctr, m->ev_tmp, m->ev_out, m->units};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
-    void* gp[] = {g.ent, g.cs, g.side, g.gidx, g.d_geom};
+    void* gp[] = {g.ent, g.cs, g.side, g.gidx, g.d_geom, g.d_tile_space};
     for (void* p : gp)
       if (p) hipFree(p);
   }
@@ -597,7 +631,8 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     sh.desc = spaces[s];
     sh.auto_extent = !(spaces[s].max_x > spaces[s].min_x && spaces[s].max_z > spaces[s].min_z);
   }
-  m->max_cells = (uint32_t)std::min<uint64_t>(0x7fffffffu, std::max<uint64_t>(4096, 2ull * capacity) + 16ull * nspaces);
+  m->max_cells = (uint32_t)std::min<uint64_t>(0x7fff0000u, std::max<uint64_t>(4096, 2ull * capacity) +
+                                                             (uint64_t)gw::kTileCells * nspaces);
   m->h_present.assign(capacity, 0);
   m->h_space_of.assign(capacity, 0);
   m->h_stamp.assign(capacity, 0);
@@ -646,6 +681,14 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     chk(dalloc(&g.side, C));
     chk(dalloc(&g.gidx, C));
     chk(dalloc(&g.d_geom, nspaces));
+    chk(dalloc(&g.d_tile_space, (size_t)m->max_cells / gw::kTileCells + 1));
+  }
+  m->max_units = m->max_cells / gw::kTileCells + capacity / gw::kUnit + 2;
+  chk(dalloc(&m->units, m->max_units));
+  static bool sweep_ready = false;
+  if (!sweep_ready) {
+    gw::sweep_init();
+    sweep_ready = true;
   }
   if (r == GWAOI_OK) r = ensure_events(m, std::max<uint64_t>(1u << 16, C / 2), (uint32_t)std::max<uint64_t>(1u << 16, C / 2), 0);
   for (auto& e : m->tev)
@@ -870,7 +913,7 @@ int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint6
   uint32_t* d_rp = nullptr;
   RCHK(dalloc(&d_rp, (size_t)m->cap + 1));
   gw::RelArgs a;
-  a.g = {g.ent, g.cs, g.side, g.d_geom};
+  a.g = {g.ent, g.cs, g.side, g.d_geom, g.d_tile_space};
   a.pos_x = m->pos_x;
   a.pos_z = m->pos_z;
   a.seq = m->seq;
@@ -1014,6 +1057,12 @@ int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
     return GWAOI_ERR_INVALID;
   }
   m->next_seq = next_seq;
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
+  RCHK(check_mgr(m));
+  m->sweep_lds = enable ? 1 : 0;
   return GWAOI_OK;
 }
 

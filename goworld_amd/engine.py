@@ -160,6 +160,9 @@ class Engine:
     def debug_set_next_seq(self, v: int):
         check(self._L.gwaoi_debug_set_next_seq(self._h, v))
 
+    def debug_set_sweep_lds(self, on: bool):
+        check(self._L.gwaoi_debug_set_sweep_lds(self._h, 1 if on else 0))
+
     def debug_set_cells_per_dist(self, v: float):
         check(self._L.gwaoi_debug_set_cells_per_dist(self._h, v))
 

@@ -32,6 +32,8 @@ int gwaoi_wl_iota(int device, uint32_t* d, uint32_t n);
  * otherwise runs every ~2^31 ops). */
 struct gwaoi_mgr;
 int gwaoi_debug_set_next_seq(struct gwaoi_mgr* mgr, uint32_t next_seq);
+/* Test hook: 0 = the sweep reads candidates from global memory only (A/B of the LDS-staged path). */
+int gwaoi_debug_set_sweep_lds(struct gwaoi_mgr* mgr, int enable);
 /* Test hook: cell size = D / cells_per_dist for grids built from now on (default 2). */
 int gwaoi_debug_set_cells_per_dist(struct gwaoi_mgr* mgr, float cells_per_dist);
 

@@ -33,10 +33,13 @@ def assert_same(a, b, what):
     assert np.array_equal(a, b), what + ": " + H.fmt_diff(a, b)
 
 
-def run_against_oracle(po, case, check_relation_every=1, eng=None, oracle="xz", cells_per_dist=None):
+def run_against_oracle(po, case, check_relation_every=1, eng=None, oracle="xz", cells_per_dist=None,
+                       sweep_lds=True):
     eng = eng or engine(case)
     if cells_per_dist:
         eng.debug_set_cells_per_dist(cells_per_dist)
+    if not sweep_lds:
+        eng.debug_set_sweep_lds(False)
     if oracle == "xz":
         orc = po.XZListOracle(case["dist"], case["cap"])
     else:
@@ -70,7 +73,25 @@ def test_random_op_mixes(gpu, po, seed):
     run_against_oracle(po, case, check_relation_every=3)
 
 
-@pytest.mark.parametrize("cpd", [0.5, 1.0, 3.0])
+@pytest.mark.parametrize("seed", range(3))
+def test_global_sweep_path(gpu, po, seed):
+    """The global-memory sweep path (taken by teleports, oversized regions and Leave ops) on its own."""
+    case = H.case_random_ops(seed=300 + seed, n=800, nticks=8, ops_per_tick=900, world=400.0, dist=60.0)
+    run_against_oracle(po, case, check_relation_every=4, sweep_lds=False)
+
+
+def test_lds_and_global_sweep_agree_walk(gpu, po):
+    """Config-1 style walk: LDS-staged and global sweep paths give identical events."""
+    from goworld_amd.engine import Engine
+    case = H.case_walk(0x5EED0007, 20000, 5000.0, 12, workload=po)
+    a = Engine(case["dist"], capacity=case["cap"], bounds=case["bounds"])
+    b = Engine(case["dist"], capacity=case["cap"], bounds=case["bounds"])
+    b.debug_set_sweep_lds(False)
+    for t, ops in enumerate(case["ticks"]):
+        assert_same(H.gpu_tick(a, ops), H.gpu_tick(b, ops), f"tick {t}")
+
+
+@pytest.mark.parametrize("cpd", [0.5, 1.0, 3.0, 4.0])
 def test_cell_size_does_not_change_events(gpu, po, cpd):
     case = H.case_random_ops(seed=7, n=500, nticks=6, ops_per_tick=600, world=300.0, dist=40.0)
     run_against_oracle(po, case, check_relation_every=2, cells_per_dist=cpd)
