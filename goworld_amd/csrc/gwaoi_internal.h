@@ -54,7 +54,6 @@ struct ApplyArgs {
   uint32_t n_ops;
   uint32_t base;             // seq of op 0; op i gets seq base + i
   uint32_t cap;
-  uint32_t batch;            // pass id, for duplicate detection of device-staged batches
   int check;                 // validate (device-staged)
   float* pos_x;
   float* pos_z;
@@ -63,7 +62,6 @@ struct ApplyArgs {
   float* old_x;
   float* old_z;
   uint32_t* old_seq;
-  uint32_t* stamp;
   uint32_t* old_side;        // side array of the old grid
   const uint32_t* old_gidx;  // slot -> entry index in the old grid
   uint32_t* ctr;
@@ -140,9 +138,23 @@ struct EvGuard {
   uint64_t keep;     // events already in ev_out from earlier passes of this tick
   uint64_t out_cap;
 };
-void launch_place(const uint4* ev_tmp, const EvGuard& g, const uint32_t* rank_off, uint2* ev_out, hipStream_t st);
-void launch_slice_sort(const uint32_t* rank_off, uint32_t n_ops, const EvGuard& g, uint2* ev_out, hipStream_t st);
-void launch_copy_out(const uint2* ev_out, const EvGuard& g, uint2* host_mapped, hipStream_t st);
+struct OrderArgs {
+  EvGuard g;
+  const uint4* ev_tmp;
+  const uint32_t* rank_off;  // exclusive scan of per-op event counts, [n_ops + 1]
+  uint2* ev_out;             // this pass's slice of the output (offset by g.keep)
+  uint2* host_out;           // mapped pinned host slice, or null (events stay in HBM)
+  uint32_t n_ops;
+  uint32_t* zero_cs;         // cell counts of the grid the next pass builds
+  uint32_t zero_n;
+  uint32_t* ctr_next;        // the next pass's counter block
+  const uint32_t* op_slot;   // device-staged batch check
+  const uint32_t* seq;
+  uint32_t base, cap;
+  int check_ops;
+};
+// k_place (+ zeroing side jobs) -> k_slice_sort (+ batch check) -> k_copy_out (if host_out)
+void launch_order(const OrderArgs& o, hipStream_t st);
 void launch_relation(const RelArgs& a, hipStream_t st);
 void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, hipStream_t st);
 void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st);

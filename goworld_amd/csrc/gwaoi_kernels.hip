@@ -115,8 +115,9 @@ __device__ __forceinline__ void for_each_entry(const Geom& g, const uint32_t* __
 
 // ---------------------------------------------------------------------------------------------
 // apply: one thread per op. Records each mover's start-of-pass state, stamps its old-grid entry
-// with the op's seq, and writes the new state. Slots of one pass are distinct (host guarantees it;
-// device-staged batches are checked here).
+// with the op's seq, and writes the new state. Slots of one pass are distinct (the host guarantees
+// it for host-staged ops; for device-staged batches k_slice_sort checks afterwards that every op's
+// slot carries that op's seq — a duplicate leaves one of two ops without it).
 __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= a.n_ops) return;
@@ -124,15 +125,9 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   const uint32_t q = a.base + i;
   if (i == 0) *a.rank_tail = 0u;
   const uint8_t kind = a.op_kind ? a.op_kind[i] : (uint8_t)OP_MOVE;
-  if (a.check) {
-    if (s >= a.cap) {
-      atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SLOT);
-      return;
-    }
-    if (atomicExch(&a.stamp[s], a.batch) == a.batch) {
-      atomicOr(&a.ctr[CTR_ERR], ERR_DUP_SLOT);
-      return;
-    }
+  if (a.check && s >= a.cap) {
+    atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SLOT);
+    return;
   }
   const uint32_t q0 = a.seq[s];
   if (a.check && q0 == 0) {
@@ -608,32 +603,39 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
 
 // ---------------------------------------------------------------------------------------------
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each
-// rank's slice sorted by other|kind (LEAVE = bit31 clear sorts first).
+// rank's slice sorted by other|kind (LEAVE = bit31 clear sorts first). Every step checks on the
+// device that the sweep's events fit the buffers (else it writes nothing; the host grows them and
+// re-runs), so the host synchronises once per pass. Two side jobs ride along: k_place zeroes the
+// cell counts of the grid the NEXT pass builds and the next pass's counter block; k_slice_sort
+// validates device-staged batches (every op's slot must carry that op's seq).
 __device__ __forceinline__ bool ev_fits(const EvGuard& g, uint32_t* n) {
   *n = g.ctr[CTR_EVENTS];
   return *n <= g.tmp_cap && g.keep + *n <= g.out_cap;
 }
 
-__global__ void __launch_bounds__(kBlock) k_place(const uint4* __restrict__ ev_tmp, EvGuard g,
-                                                  const uint32_t* __restrict__ rank_off, uint2* __restrict__ ev_out) {
+__global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
+  const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
+  for (uint32_t i = tid; i < o.zero_n; i += nth) o.zero_cs[i] = 0u;
+  if (tid < CTR_N) o.ctr_next[tid] = 0u;
   uint32_t n;
-  if (!ev_fits(g, &n)) return;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
-    const uint4 e = ev_tmp[i];
-    ev_out[rank_off[e.x] + e.y] = make_uint2(e.z, e.w);
+  if (!ev_fits(o.g, &n)) return;
+  for (uint32_t i = tid; i < n; i += nth) {
+    const uint4 e = o.ev_tmp[i];
+    o.ev_out[o.rank_off[e.x] + e.y] = make_uint2(e.z, e.w);
   }
 }
 
-void launch_place(const uint4* ev_tmp, const EvGuard& g, const uint32_t* rank_off, uint2* ev_out, hipStream_t st) {
-  hipLaunchKernelGGL(k_place, dim3(1024), dim3(kBlock), 0, st, ev_tmp, g, rank_off, ev_out);
-}
-
-__global__ void __launch_bounds__(kBlock) k_slice_sort(const uint32_t* __restrict__ rank_off, uint32_t n_ops,
-                                                       EvGuard g, uint2* __restrict__ ev) {
+__global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+  if (r >= o.n_ops) return;
+  if (o.check_ops) {
+    const uint32_t s = o.op_slot[r];
+    if (s < o.cap && o.seq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
+  }
   uint32_t n;
-  if (r >= n_ops || !ev_fits(g, &n)) return;
-  const uint32_t b = rank_off[r], e = rank_off[r + 1];
+  if (!ev_fits(o.g, &n)) return;
+  const uint32_t b = o.rank_off[r], e = o.rank_off[r + 1];
+  uint2* ev = o.ev_out;
   for (uint32_t i = b + 1; i < e; ++i) {
     const uint2 v = ev[i];
     uint32_t k = i;
@@ -645,22 +647,19 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(const uint32_t* __restric
   }
 }
 
-void launch_slice_sort(const uint32_t* rank_off, uint32_t n_ops, const EvGuard& g, uint2* ev_out, hipStream_t st) {
-  if (!n_ops) return;
-  hipLaunchKernelGGL(k_slice_sort, dim3((n_ops + kBlock - 1) / kBlock), dim3(kBlock), 0, st, rank_off, n_ops, g,
-                     ev_out);
-}
-
 // Deliver the ordered events to mapped pinned host memory (GPU-initiated PCIe writes), so the host
 // needs no second round trip to learn the count before a copy.
-__global__ void __launch_bounds__(kBlock) k_copy_out(const uint2* __restrict__ ev, EvGuard g, uint2* host) {
+__global__ void __launch_bounds__(kBlock) k_copy_out(OrderArgs o) {
   uint32_t n;
-  if (!ev_fits(g, &n)) return;
-  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) host[i] = ev[i];
+  if (!ev_fits(o.g, &n)) return;
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) o.host_out[i] = o.ev_out[i];
 }
 
-void launch_copy_out(const uint2* ev_out, const EvGuard& g, uint2* host_mapped, hipStream_t st) {
-  hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, ev_out, g, host_mapped);
+void launch_order(const OrderArgs& o, hipStream_t st) {
+  hipLaunchKernelGGL(k_place, dim3(1024), dim3(kBlock), 0, st, o);
+  if (o.n_ops)
+    hipLaunchKernelGGL(k_slice_sort, dim3((o.n_ops + kBlock - 1) / kBlock), dim3(kBlock), 0, st, o);
+  if (o.host_out) hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, o);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -93,6 +93,7 @@ struct Grid {
   std::vector<gw::Geom> h_geom;  // what d_geom holds
   uint32_t ncells = 0;
   uint32_t ntiles = 0;
+  uint32_t cs_zeroed = 0;  // leading cs words known to be zero (zeroed by the previous pass's k_place)
 };
 
 }  // namespace
@@ -133,7 +134,7 @@ struct gwaoi_mgr {
 
   // ---- device state ----
   float *pos_x = nullptr, *pos_z = nullptr, *old_x = nullptr, *old_z = nullptr;
-  uint32_t *seq = nullptr, *space_of = nullptr, *old_seq = nullptr, *stamp = nullptr;
+  uint32_t *seq = nullptr, *space_of = nullptr, *old_seq = nullptr;
   uint32_t *key_of = nullptr, *local_of = nullptr;
   uint32_t *d_op_slot = nullptr, *d_op_space = nullptr, *d_leaves = nullptr;
   float *d_op_x = nullptr, *d_op_z = nullptr;
@@ -147,7 +148,9 @@ struct gwaoi_mgr {
   int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
   uint32_t* part = nullptr;
   uint32_t part_words = 0;
-  uint32_t* ctr = nullptr;       // [CTR_N]
+  uint32_t* ctr_buf = nullptr;   // [2][CTR_N]: pass P uses half P&1 and zeroes the other (k_place)
+  uint32_t* ctr = nullptr;       // current half
+  int ctr_sel = 0;
   uint32_t* h_ctr = nullptr;     // pinned
   // events
   uint4* ev_tmp = nullptr;
@@ -314,7 +317,8 @@ int upload_geom(gwaoi_mgr* m, Grid& g, const std::vector<gw::Geom>& geo) {
 // Build grid `gi` from the per-slot state (pos, seq, space_of).
 int build_grid(gwaoi_mgr* m, int gi) {
   Grid& g = m->grid[gi];
-  HIPCHK(hipMemsetAsync(g.cs, 0, (size_t)(g.ncells + 1) * sizeof(uint32_t), m->stream));
+  if (g.cs_zeroed < g.ncells + 1) HIPCHK(hipMemsetAsync(g.cs, 0, (size_t)(g.ncells + 1) * sizeof(uint32_t), m->stream));
+  g.cs_zeroed = 0;
   gw::BinArgs b;
   b.pos_x = m->pos_x;
   b.pos_z = m->pos_z;
@@ -395,8 +399,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     if (m->n_leaves)
       HIPCHK(hipMemcpyAsync(m->d_leaves, m->h_leaves, m->n_leaves * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
-  HIPCHK(hipMemsetAsync(m->ctr, 0, gw::CTR_N * sizeof(uint32_t), st));
-
   gw::ApplyArgs a;
   a.op_slot = dev ? m->dv_slot : m->d_op_slot;
   a.op_x = dev ? m->dv_x : m->d_op_x;
@@ -406,7 +408,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   a.n_ops = n_ops;
   a.base = base;
   a.cap = m->cap;
-  a.batch = m->pass_id;
   a.check = dev ? 1 : 0;
   a.pos_x = m->pos_x;
   a.pos_z = m->pos_z;
@@ -415,7 +416,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   a.old_x = m->old_x;
   a.old_z = m->old_z;
   a.old_seq = m->old_seq;
-  a.stamp = m->stamp;
   a.old_side = m->grid[og].side;
   a.old_gidx = m->grid[og].gidx;
   a.ctr = m->ctr;
@@ -466,10 +466,22 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     // canonical order; every step is guarded on the device against a buffer overflow, so the host
     // synchronises once, at the end of the pass
     gw::launch_scan(m->rank_cnt, n_ops + 1, m->part, st);
-    const gw::EvGuard g = {m->ctr, m->tmp_cap, keep, m->ev_cap};
-    gw::launch_place(m->ev_tmp, g, m->rank_cnt, m->ev_out + keep, st);
-    gw::launch_slice_sort(m->rank_cnt, n_ops, g, m->ev_out + keep, st);
-    if (copy_events) gw::launch_copy_out(m->ev_out + keep, g, m->d_hev + keep, st);
+    gw::OrderArgs o;
+    o.g = {m->ctr, m->tmp_cap, keep, m->ev_cap};
+    o.ev_tmp = m->ev_tmp;
+    o.rank_off = m->rank_cnt;
+    o.ev_out = m->ev_out + keep;
+    o.host_out = copy_events ? m->d_hev + keep : nullptr;
+    o.n_ops = n_ops;
+    o.zero_cs = m->grid[og].cs;  // the grid the next pass builds into
+    o.zero_n = m->grid[og].ncells + 1;
+    o.ctr_next = m->ctr_buf + (m->ctr_sel ^ 1) * gw::CTR_N;
+    o.op_slot = a.op_slot;
+    o.seq = m->seq;
+    o.base = base;
+    o.cap = m->cap;
+    o.check_ops = dev ? 1 : 0;
+    gw::launch_order(o, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
     HIPCHK(hipMemcpyAsync(m->h_ctr, m->ctr, gw::CTR_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -509,6 +521,9 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     break;
   }
   m->cur = ng;
+  m->grid[og].cs_zeroed = m->grid[og].ncells + 1;
+  m->ctr_sel ^= 1;
+  m->ctr = m->ctr_buf + m->ctr_sel * gw::CTR_N;
   m->tick_passes++;
   m->tick_ops += n_ops;
   m->n_ops = 0;
@@ -577,9 +592,9 @@ void stage(gwaoi_mgr* m, uint32_t slot, uint8_t kind, float x, float z, uint32_t
 void free_all(gwaoi_mgr* m) {
   hipSetDevice(m->device);
   if (m->stream) hipStreamSynchronize(m->stream);
-  void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->stamp,
+  void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_op_x, m->d_op_z,
-                   m->d_op_kind, m->rank_cnt, m->part, m->ctr, m->ev_tmp, m->ev_out, m->units};
+                   m->d_op_kind, m->rank_cnt, m->part, m->ctr_buf, m->ev_tmp, m->ev_out, m->units};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
@@ -654,7 +669,6 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->seq, C));
   chk(dalloc(&m->space_of, C));
   chk(dalloc(&m->old_seq, C));
-  chk(dalloc(&m->stamp, C));
   chk(dalloc(&m->key_of, C));
   chk(dalloc(&m->local_of, C));
   chk(dalloc(&m->d_op_slot, C));
@@ -666,7 +680,8 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->rank_cnt, C + 1));
   m->part_words = gw::scan_part_words(std::max<uint32_t>(m->max_cells, capacity) + 1);
   chk(dalloc(&m->part, m->part_words));
-  chk(dalloc(&m->ctr, gw::CTR_N));
+  chk(dalloc(&m->ctr_buf, 2 * gw::CTR_N));
+  m->ctr = m->ctr_buf;
   chk(halloc(&m->h_ctr, gw::CTR_N));
   chk(halloc(&m->h_op_slot, C));
   chk(halloc(&m->h_op_x, C));
@@ -704,11 +719,11 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
         r = GWAOI_ERR_HIP;
       }
     };
+    z(m->ctr_buf, 2 * gw::CTR_N * 4);
     z(m->pos_x, C * 4);
     z(m->pos_z, C * 4);
     z(m->seq, C * 4);
     z(m->space_of, C * 4);
-    z(m->stamp, C * 4);
     for (int gi = 0; gi < 2; ++gi) {
       z(m->grid[gi].side, C * 4);
       z(m->grid[gi].gidx, C * 4);
