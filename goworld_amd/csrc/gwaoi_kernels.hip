@@ -615,10 +615,12 @@ __device__ __forceinline__ bool ev_fits(const EvGuard& g, uint32_t* n) {
 
 __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
   const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
+  uint32_t n;
+  // An overflowing pass is re-run from the sweep, which still reads the old grid: side jobs only
+  // once the pass is final.
+  if (!ev_fits(o.g, &n)) return;
   for (uint32_t i = tid; i < o.zero_n; i += nth) o.zero_cs[i] = 0u;
   if (tid < CTR_N) o.ctr_next[tid] = 0u;
-  uint32_t n;
-  if (!ev_fits(o.g, &n)) return;
   for (uint32_t i = tid; i < n; i += nth) {
     const uint4 e = o.ev_tmp[i];
     o.ev_out[o.rank_off[e.x] + e.y] = make_uint2(e.z, e.w);
