@@ -163,8 +163,8 @@ def main():
     eng = Engine(D, capacity=n, device=dev, bounds=(0.0, 0.0, L, L))
     if args.cells_per_dist:
         eng.debug_set_cells_per_dist(args.cells_per_dist)
-    if not args.sweep_lds:
-        eng.debug_set_sweep_lds(False)
+    if args.sweep_lds != 1:
+        eng._L.gwaoi_debug_set_sweep_lds(eng.handle, args.sweep_lds)
     x0 = snap.download(np.float32, n, 0)
     z0 = snap.download(np.float32, n, 4 * n)
     eng.stage_enters(np.arange(n, dtype=np.uint32), x0, z0)

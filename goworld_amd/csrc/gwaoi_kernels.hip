@@ -345,7 +345,8 @@ struct SweepSmem {  // dynamic LDS, carved by hand (16-B aligned offsets)
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
 
-__device__ __forceinline__ void emit(const SweepArgs& a, SweepSmem& sm, uint32_t rank, uint32_t local,
+template <class Q>
+__device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, uint32_t local,
                                      uint32_t mover, uint32_t other, bool enter) {
   const uint4 rec = make_uint4(rank, local, mover, other | (enter ? 0x80000000u : 0u));
   const uint32_t li = atomicAdd(&sm.n, 1u);
@@ -387,8 +388,8 @@ __device__ __forceinline__ Mover make_mover(const SweepArgs& a, uint32_t sm, uin
 //      before = in(L, F) over the start-of-pass state, after = in(m_new, o_old).
 //  (B) new grid: only o that acted earlier in this pass (and are present after it);
 //      before = in(o_new, m_old), after = in(m_new, o_new).
-template <class ForOld, class ForNew>
-__device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, SweepSmem& smem, const Mover& m,
+template <class Q, class ForOld, class ForNew>
+__device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, Q& smem, const Mover& m,
                                                 ForOld&& for_old, ForNew&& for_new) {
   const float D = m.D;
   const Bounds b1 = {m.mx1 - D, m.mx1 + D, m.mz1 - D, m.mz1 + D};
@@ -414,7 +415,8 @@ __device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, SweepSmem& s
   return local;
 }
 
-__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, SweepSmem& smem, const Mover& m,
+template <class Q>
+__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& smem, const Mover& m,
                                                  const Geom& go, const Geom& gn) {
   const CellBox A0 = qbox(go, m.mx0, m.mz0), A1 = qbox(go, m.mx1, m.mz1);
   const CellBox B0 = qbox(gn, m.mx0, m.mz0), B1 = qbox(gn, m.mx1, m.mz1);
@@ -548,7 +550,9 @@ __global__ void __launch_bounds__(kSweepBlock) k_sweep(SweepArgs a) {
     }
     __syncthreads();
     const uint32_t j = u.z + threadIdx.x;
-    if (j < u.w) {
+    if (a.use_lds == 2) {  // ablation (timing only): staging without the candidate walk
+      if (j < u.w && a.ng.ent[j].w >= a.base) a.rank_cnt[a.ng.ent[j].w - a.base] = 0;
+    } else if (j < u.w) {
       const uint4 e = a.ng.ent[j];
       if (e.w >= a.base) {  // acted in this pass
         const Mover m = make_mover(a, e.z, e.w, true, __uint_as_float(e.x), __uint_as_float(e.y), gn.D);
@@ -595,7 +599,58 @@ void sweep_init() {
                             (int)sizeof(SweepSmem));
 }
 
+// Flat variant (use_lds == 0): one thread per new-grid entry in key (tile-major) order, 256-thread
+// blocks and only the event queue in LDS, i.e. full occupancy; candidates come through L1/L2.
+struct FlatQ {
+  uint32_t n, enter, base, flags;
+  union {
+    uint4 ev[kEvLds];
+  } u;
+};
+
+__global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
+  __shared__ FlatQ q;
+  if (threadIdx.x == 0) {
+    q.n = 0;
+    q.enter = 0;
+  }
+  __syncthreads();
+  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+  if (t < a.n_new) {
+    const uint4 e = a.ng.ent[t];
+    if (e.w >= a.base) {
+      const uint32_t sp = a.space_of[e.z];
+      const Geom go = a.og.geom[sp], gn = a.ng.geom[sp];
+      const Mover m = make_mover(a, e.z, e.w, true, __uint_as_float(e.x), __uint_as_float(e.y), gn.D);
+      a.rank_cnt[m.rank] = sweep_global(a, q, m, go, gn);
+    }
+  } else if (t < a.n_new + a.n_leaves) {
+    const uint32_t i = a.leave_ops[t - a.n_new];
+    const uint32_t sm = a.op_slot[i];
+    const uint32_t sp = a.space_of[sm];
+    const Geom go = a.og.geom[sp], gn = a.ng.geom[sp];
+    const Mover m = make_mover(a, sm, a.base + i, false, 0.0f, 0.0f, go.D);
+    a.rank_cnt[i] = sweep_global(a, q, m, go, gn);
+  }
+  __syncthreads();
+  const uint32_t nq = min(q.n, (uint32_t)kEvLds);
+  if (threadIdx.x == 0) {
+    q.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+    if (q.enter) atomicAdd(&a.ctr[CTR_ENTER], q.enter);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
+    const uint32_t gi = q.base + i;
+    if (gi < a.ev_cap) a.ev_tmp[gi] = q.u.ev[i];
+  }
+}
+
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
+  if (a.use_lds == 0) {
+    const uint32_t n = a.n_new + a.n_leaves;
+    if (n) hipLaunchKernelGGL(k_sweep_flat, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+    return;
+  }
   const uint32_t nb = a.max_units + (a.n_leaves + kSweepBlock - 1) / kSweepBlock;
   if (!nb) return;
   hipLaunchKernelGGL(k_sweep, dim3(nb), dim3(kSweepBlock), sizeof(SweepSmem), st, a);

@@ -1077,7 +1077,7 @@ int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
 
 int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
   RCHK(check_mgr(m));
-  m->sweep_lds = enable ? 1 : 0;
+  m->sweep_lds = enable < 0 ? 0 : (enable > 2 ? 1 : enable);
   return GWAOI_OK;
 }
 
