@@ -17,11 +17,13 @@ enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u };
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_N = 16 };
 
 // Cells are grouped in square tiles of kTile x kTile cells; cell keys are tile-major,
-//   key = base + (tz * ntx + tx) * 256 + lz * 16 + lx   (cx = 16 tx + lx, cz = 16 tz + lz),
+//   key = base + (tz * ntx + tx) * 1024 + lz * 32 + lx   (cx = 32 tx + lx, cz = 32 tz + lz),
 // so a tile's entities are contiguous (the unit of work and of LDS staging in the sweep) and a cell
 // row inside a tile is contiguous.
-constexpr int kTile = 16;
-constexpr int kTileCells = kTile * kTile;
+constexpr int kTileShift = 5;
+constexpr int kTile = 1 << kTileShift;       // 32
+constexpr int kTileCellShift = 2 * kTileShift;
+constexpr int kTileCells = kTile * kTile;    // 1024
 
 // Cell geometry of one Space inside one grid snapshot.
 struct Geom {
@@ -31,7 +33,7 @@ struct Geom {
   int32_t ncx, ncz;   // cells per axis (multiples of kTile)
   int32_t ntx, ntz;   // tiles per axis
   uint32_t base;      // first cell key of this Space
-  uint32_t tile_base; // first tile index of this Space (base / 256)
+  uint32_t tile_base; // first tile index of this Space (base / kTileCells)
   int32_t reach;      // halo (cells) staged around a tile in the sweep
   uint32_t pad;
 };
@@ -82,15 +84,11 @@ struct BinArgs {
   uint32_t* gidx;
 };
 
-// A unit of sweep work: up to kUnit consecutive new-grid entries of one tile.
-constexpr int kUnit = 512;
-
 struct SweepArgs {
   GridView og;  // old grid: state at the start of the pass
   GridView ng;  // new grid: state at the end of the pass
-  const uint4* units;  // {space, tile, e0, e1}; count in ctr[CTR_UNITS]
-  uint32_t max_units;  // blocks [0, max_units) take units, the rest take Leave ops
-  int use_lds;         // 0: every unit on the global-memory path (A/B and fallback)
+  uint32_t ntiles;     // tiles of the new grid: blocks [0, ntiles) take one tile each, the rest Leave ops
+  int use_lds;         // 1: LDS-staged sweep; 0: flat global-memory sweep (A/B); 2: staging only (timing)
   const float* old_x;
   const float* old_z;
   const uint32_t* old_seq;
@@ -126,7 +124,6 @@ void launch_bin_scatter(const BinArgs& a, hipStream_t st);
 // part: scratch of scan_part_words(n) words.
 void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st);
 uint32_t scan_part_words(uint32_t n);
-void launch_units(const GridView& ng, uint32_t ntiles, uint4* units, uint32_t* ctr, hipStream_t st);
 void launch_sweep(const SweepArgs& a, hipStream_t st);
 size_t sweep_lds_bytes();
 void sweep_init();  // once per process (dynamic LDS limit of the sweep)

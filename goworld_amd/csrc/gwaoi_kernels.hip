@@ -65,7 +65,8 @@ __device__ __forceinline__ CellBox qbox(const Geom& g, float cx, float cz) {
 }
 
 __device__ __forceinline__ uint32_t cell_key(const Geom& g, int cx, int cz) {
-  return g.base + ((uint32_t)((cz >> 4) * g.ntx + (cx >> 4)) << 8) + (uint32_t)(((cz & 15) << 4) | (cx & 15));
+  return g.base + ((uint32_t)((cz >> kTileShift) * g.ntx + (cx >> kTileShift)) << kTileCellShift) +
+         (uint32_t)(((cz & (kTile - 1)) << kTileShift) | (cx & (kTile - 1)));
 }
 
 // Row intervals of the union of box A (if va) and box B (if vb): one or two column intervals per
@@ -99,10 +100,12 @@ __device__ __forceinline__ void for_each_row_interval(bool va, CellBox A, bool v
 template <class F>
 __device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t* __restrict__ cs, int r, int c0,
                                                    int c1, F&& f) {
-  const uint32_t rowbase = g.base + ((uint32_t)((r >> 4) * g.ntx) << 8) + (uint32_t)((r & 15) << 4);
-  for (int tx = c0 >> 4; tx <= (c1 >> 4); ++tx) {
-    const int lo = max(c0, tx << 4), hi = min(c1, (tx << 4) + 15);
-    const uint32_t k = rowbase + ((uint32_t)tx << 8) + (uint32_t)(lo & 15);
+  if (c0 > c1) return;
+  const uint32_t rowbase = g.base + ((uint32_t)((r >> kTileShift) * g.ntx) << kTileCellShift) +
+                           (uint32_t)((r & (kTile - 1)) << kTileShift);
+  for (int tx = c0 >> kTileShift; tx <= (c1 >> kTileShift); ++tx) {
+    const int lo = max(c0, tx << kTileShift), hi = min(c1, (tx << kTileShift) + kTile - 1);
+    const uint32_t k = rowbase + ((uint32_t)tx << kTileCellShift) + (uint32_t)(lo & (kTile - 1));
     for (uint32_t j = cs[k], e = cs[k + (uint32_t)(hi - lo) + 1]; j < e; ++j) f(j);
   }
 }
@@ -283,62 +286,37 @@ void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Work units: every tile's new-grid entries, split evenly into chunks of at most kUnit. Appended
-// with one atomic per wave (unit order is irrelevant: events are ordered canonically later).
-__global__ void __launch_bounds__(kBlock) k_units(GridView ng, uint32_t ntiles, uint4* __restrict__ units,
-                                                  uint32_t* ctr) {
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  uint32_t start = 0, cnt = 0;
-  if (t < ntiles) {
-    start = ng.cs[t << 8];
-    cnt = ng.cs[(t + 1) << 8] - start;
-  }
-  const uint32_t nu = (cnt + kUnit - 1) / kUnit;
-  const uint32_t incl = wave_incl_scan(nu);
-  const uint32_t tot = __shfl(incl, 63, 64);
-  uint32_t wbase = 0;
-  if ((threadIdx.x & 63) == 63 && tot) wbase = atomicAdd(&ctr[CTR_UNITS], tot);
-  wbase = __shfl(wbase, 63, 64);
-  if (!nu) return;
-  const uint32_t chunk = (cnt + nu - 1) / nu;
-  const uint32_t sp = ng.tile_space[t];
-  uint32_t u = wbase + incl - nu;
-  for (uint32_t k = 0; k < nu; ++k, ++u) {
-    const uint32_t e0 = start + k * chunk;
-    units[u] = make_uint4(sp, t, e0, min(e0 + chunk, start + cnt));
-  }
-}
-
-void launch_units(const GridView& ng, uint32_t ntiles, uint4* units, uint32_t* ctr, hipStream_t st) {
-  hipLaunchKernelGGL(k_units, dim3((ntiles + kBlock - 1) / kBlock), dim3(kBlock), 0, st, ng, ntiles, units, ctr);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Sweep. One block (kUnit = 512 threads) per unit of up to 512 new-grid entries of one tile; one
-// thread per mover. The block stages, for BOTH grids, every entry of the unit's tile rows plus a
-// halo of `reach` cells into LDS (cell starts, entries, and the old grid's side stamps), laid out
-// row by row so that any row interval of the region is one contiguous LDS range. Each mover then
-// walks its candidates in LDS. Movers whose query boxes leave the region (teleports), units whose
-// region does not fit, and Leave ops take the global-memory path; both paths evaluate the same
-// predicates.
+// Sweep. One 512-thread block per tile of the new grid (kTile x kTile cells); the block loops over
+// the tile's movers, one thread per mover. The block first stages, for BOTH grids, every entry of
+// the tile plus a halo of `reach` cells into LDS (entries, the old grid's side stamps, and a cell
+// start table), laid out row by row so that any row interval of the region is one contiguous LDS
+// range; each mover then walks its candidates in LDS. Movers whose query boxes leave the region
+// (teleports), tiles whose region does not fit, and Leave ops take the global-memory path; both
+// paths evaluate the same predicates.
+//
+// Ring walk: for a Moved op, a candidate strictly inside BOTH the old and the new box (shrunk by a
+// margin far above float32 rounding) is inside from every perspective before and after, so it
+// cannot raise an event. Cells whose every point is that deep (cell index strictly between the
+// cells of the shrunken bounds; cellc is monotone, clamping included) are skipped: only the ring of
+// border cells is read. Enter and Leave ops walk their whole box.
 //
 // Events are rare (~0.3 per mover per tick), but one global counter hit by every event serialises
 // at the memory side, so each block stages its events in LDS and reserves its output range with ONE
 // global atomic; a mover's events are numbered in a register (one thread per mover) and its count is
 // stored once, without atomics.
-constexpr int kSweepBlock = kUnit;
-constexpr int kEvLds = 512;      // events staged per block before spilling to global atomics
-constexpr int kRegCells = 1024;  // max cells in a staged region
-constexpr int kCap = 1536;       // max entries staged per grid
+constexpr int kSweepBlock = 512;
+constexpr int kEvLds = 256;       // events staged per block before spilling to global atomics
+constexpr int kRegCells = 2304;   // max cells of a staged region (48 x 48)
+constexpr int kCap = 1088;        // max entries staged per grid
+constexpr int kMaxRows = 48;
+constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
-struct SweepSmem {  // dynamic LDS, carved by hand (16-B aligned offsets)
+struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint32_t n, enter, base, flags;
-  uint32_t ws[16];                 // block-scan scratch
-  union {
-    uint4 ev[kEvLds];           // event queue (after staging)
-    uint32_t gs[2][kRegCells];  // global start of each region cell (during staging)
-  } u;
-  uint32_t lcs[2][kRegCells + 4];  // LDS start of each region cell (+ total)
+  uint32_t ws[16];                  // block-scan scratch
+  uint32_t gsp[2][kMaxRows * 3];    // global start of each (region row, tile part)
+  uint4 ev[kEvLds];                 // event queue
+  uint16_t lcs[2][kRegCells + 8];   // LDS start of each region cell (+ total)
   uint4 ent[2][kCap];
   uint32_t side[kCap];
 };
@@ -346,12 +324,12 @@ struct SweepSmem {  // dynamic LDS, carved by hand (16-B aligned offsets)
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
 
 template <class Q>
-__device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, uint32_t local,
-                                     uint32_t mover, uint32_t other, bool enter) {
+__device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, uint32_t local, uint32_t mover,
+                                     uint32_t other, bool enter) {
   const uint4 rec = make_uint4(rank, local, mover, other | (enter ? 0x80000000u : 0u));
   const uint32_t li = atomicAdd(&sm.n, 1u);
   if (li < (uint32_t)kEvLds) {
-    sm.u.ev[li] = rec;
+    sm.ev[li] = rec;
   } else {
     const uint32_t gi = atomicAdd(&a.ctr[CTR_EVENTS], 1u);
     if (gi < a.ev_cap) a.ev_tmp[gi] = rec;
@@ -382,77 +360,104 @@ __device__ __forceinline__ Mover make_mover(const SweepArgs& a, uint32_t sm, uin
   return m;
 }
 
-// The per-mover evaluation, over candidate iterators of the old grid (callback(entry, side)) and
-// of the new grid (callback(entry)).
+// The cells a mover must read, as column intervals per row: the union of its old and new query
+// boxes, minus (for a move whose boxes overlap) the cells deep inside both boxes.
+template <class RowF>
+__device__ __forceinline__ void walk_cells(const Mover& m, const Geom& g, RowF&& rowf) {
+  const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
+  if (!(m.valid0 && m.valid1)) {
+    for_each_row_interval(m.valid0, A0, m.valid1, A1, rowf);
+    return;
+  }
+  const int x0 = min(A0.x0, A1.x0), x1 = max(A0.x1, A1.x1);
+  const int z0 = min(A0.z0, A1.z0), z1 = max(A0.z1, A1.z1);
+  if (x1 - x0 > (A1.x1 - A1.x0) + 2 || z1 - z0 > (A1.z1 - A1.z0) + 2) {  // far apart: two boxes
+    for_each_row_interval(true, A0, true, A1, rowf);
+    return;
+  }
+  const float D = g.D;
+  const float ex = (fmaxf(fabsf(m.mx0), fabsf(m.mx1)) + D) * kInner;
+  const float ez = (fmaxf(fabsf(m.mz0), fabsf(m.mz1)) + D) * kInner;
+  const int ix0 = cellc((fmaxf(m.mx0, m.mx1) - D) + ex, g.x0, g.inv_c, g.ncx) + 1;
+  const int ix1 = cellc((fminf(m.mx0, m.mx1) + D) - ex, g.x0, g.inv_c, g.ncx) - 1;
+  const int iz0 = cellc((fmaxf(m.mz0, m.mz1) - D) + ez, g.z0, g.inv_c, g.ncz) + 1;
+  const int iz1 = cellc((fminf(m.mz0, m.mz1) + D) - ez, g.z0, g.inv_c, g.ncz) - 1;
+  const bool ring = ix0 <= ix1;
+  for (int r = z0; r <= z1; ++r) {
+    if (ring && r >= iz0 && r <= iz1) {
+      rowf(r, x0, ix0 - 1);
+      rowf(r, ix1 + 1, x1);
+    } else {
+      rowf(r, x0, x1);
+    }
+  }
+}
+
+// The per-mover evaluation over the candidates of a cell walk; `cand_old(j)` / `cand_new(j)`
+// read entry j of the old / new grid through the caller's accessor.
 //  (A) old grid: o at its start-of-pass position, skipped if it acted earlier in this pass;
 //      before = in(L, F) over the start-of-pass state, after = in(m_new, o_old).
 //  (B) new grid: only o that acted earlier in this pass (and are present after it);
 //      before = in(o_new, m_old), after = in(m_new, o_new).
-template <class Q, class ForOld, class ForNew>
-__device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, Q& smem, const Mover& m,
-                                                ForOld&& for_old, ForNew&& for_new) {
+template <class Q, class Rows>
+__device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, Q& q, const Mover& m, Rows&& rows) {
   const float D = m.D;
   const Bounds b1 = {m.mx1 - D, m.mx1 + D, m.mz1 - D, m.mz1 + D};
   const Bounds b0 = {m.mx0 - D, m.mx0 + D, m.mz0 - D, m.mz0 + D};
-  const uint32_t base = a.base;
+  const uint32_t rq = m.q - a.base;  // o acted earlier in this pass <=> (seq_o - base) < rq
   uint32_t local = 0;
-  for_old([&](const uint4 e, uint32_t qo) {
-    if (e.z == m.sm) return;
-    if (qo >= base && qo < m.q) return;  // o acted earlier in this pass: handled in (B)
-    const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
-    bool before = false;
-    if (m.valid0) before = (e.w > m.q0) ? inbox(ox, oz, D, m.mx0, m.mz0) : b0.has(ox, oz);
-    const bool after = m.valid1 && b1.has(ox, oz);
-    if (before != after) emit(a, smem, m.rank, local++, m.sm, e.z, after);
-  });
-  for_new([&](const uint4 e) {
-    if (!(e.w >= base && e.w < m.q)) return;
-    const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
-    const bool before = m.valid0 && inbox(ox, oz, D, m.mx0, m.mz0);
-    const bool after = m.valid1 && b1.has(ox, oz);
-    if (before != after) emit(a, smem, m.rank, local++, m.sm, e.z, after);
-  });
+  rows(
+      [&](const uint4 e, uint32_t qo) {  // old grid
+        if (e.z == m.sm || qo - a.base < rq) return;
+        const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
+        const bool before = m.valid0 && ((e.w > m.q0) ? inbox(ox, oz, D, m.mx0, m.mz0) : b0.has(ox, oz));
+        const bool after = m.valid1 && b1.has(ox, oz);
+        if (before != after) emit(a, q, m.rank, local++, m.sm, e.z, after);
+      },
+      [&](const uint4 e) {  // new grid
+        if (!(e.w - a.base < rq)) return;
+        const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
+        const bool before = m.valid0 && inbox(ox, oz, D, m.mx0, m.mz0);
+        const bool after = m.valid1 && b1.has(ox, oz);
+        if (before != after) emit(a, q, m.rank, local++, m.sm, e.z, after);
+      });
   return local;
 }
 
 template <class Q>
-__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& smem, const Mover& m,
-                                                 const Geom& go, const Geom& gn) {
-  const CellBox A0 = qbox(go, m.mx0, m.mz0), A1 = qbox(go, m.mx1, m.mz1);
-  const CellBox B0 = qbox(gn, m.mx0, m.mz0), B1 = qbox(gn, m.mx1, m.mz1);
-  return sweep_mover(
-      a, smem, m,
-      [&](auto&& f) {
-        for_each_entry(go, a.og.cs, m.valid0, A0, m.valid1, A1, [&](uint32_t j) { f(a.og.ent[j], a.og.side[j]); });
-      },
-      [&](auto&& f) {
-        for_each_entry(gn, a.ng.cs, m.valid0, B0, m.valid1, B1, [&](uint32_t j) { f(a.ng.ent[j]); });
-      });
+__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& q, const Mover& m, const Geom& go,
+                                                 const Geom& gn) {
+  return sweep_mover(a, q, m, [&](auto&& fo, auto&& fn) {
+    walk_cells(m, go, [&](int r, int c0, int c1) {
+      row_entries_global(go, a.og.cs, r, c0, c1, [&](uint32_t j) { fo(a.og.ent[j], a.og.side[j]); });
+    });
+    walk_cells(m, gn, [&](int r, int c0, int c1) {
+      row_entries_global(gn, a.ng.cs, r, c0, c1, [&](uint32_t j) { fn(a.ng.ent[j]); });
+    });
+  });
 }
 
 struct Region {
-  int zr0, zr1, xr0, xr1, ncols, ncells;
+  int zr0, zr1, xr0, xr1, ncols, nrows, ncells;
   __device__ __forceinline__ bool holds(const CellBox& b) const {
     return b.z0 >= zr0 && b.z1 <= zr1 && b.x0 >= xr0 && b.x1 <= xr1;
   }
 };
 
-__device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& smem, const Mover& m, const Region& R,
+__device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Region& R,
                                               const Geom& g) {
-  const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
-  auto rows = [&](const uint32_t* lcs, auto&& f) {
-    for_each_row_interval(m.valid0, A0, m.valid1, A1, [&](int r, int c0, int c1) {
+  return sweep_mover(a, sm, m, [&](auto&& fo, auto&& fn) {
+    walk_cells(m, g, [&](int r, int c0, int c1) {
+      if (c0 > c1) return;
       const int b = (r - R.zr0) * R.ncols - R.xr0;
-      for (uint32_t j = lcs[b + c0], e = lcs[b + c1 + 1]; j < e; ++j) f(j);
+      for (uint32_t j = sm.lcs[0][b + c0], e = sm.lcs[0][b + c1 + 1]; j < e; ++j) fo(sm.ent[0][j], sm.side[j]);
+      for (uint32_t j = sm.lcs[1][b + c0], e = sm.lcs[1][b + c1 + 1]; j < e; ++j) fn(sm.ent[1][j]);
     });
-  };
-  return sweep_mover(
-      a, smem, m, [&](auto&& f) { rows(smem.lcs[0], [&](uint32_t j) { f(smem.ent[0][j], smem.side[j]); }); },
-      [&](auto&& f) { rows(smem.lcs[1], [&](uint32_t j) { f(smem.ent[1][j]); }); });
+  });
 }
 
 // exclusive scan of v over a kSweepBlock-thread block; *total = block sum (LDS scratch `ws`)
-__device__ __forceinline__ uint32_t block_excl_scan_512(uint32_t v, uint32_t* ws, uint32_t* total) {
+__device__ __forceinline__ uint32_t block_excl_scan_big(uint32_t v, uint32_t* ws, uint32_t* total) {
   constexpr int NW = kSweepBlock / 64;
   const uint32_t inc = wave_incl_scan(v);
   const int w = threadIdx.x >> 6;
@@ -470,39 +475,64 @@ __device__ __forceinline__ uint32_t block_excl_scan_512(uint32_t v, uint32_t* ws
   return pre + inc - v;
 }
 
-// Stage the region of grid `gi` (0 = old, 1 = new). Returns the staged entry count (block-uniform);
-// a count > kCap means "does not fit" and nothing was copied.
-__device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, const Region& R, SweepSmem& smem,
-                                          int gi, uint32_t* ws) {
-  uint32_t* gs = smem.u.gs[gi];
-  uint32_t* lcs = smem.lcs[gi];
-  // two region cells per thread (kRegCells = 2 * kSweepBlock)
-  const int c0 = 2 * threadIdx.x;
-  uint32_t n0 = 0, n1 = 0;
+constexpr int kCellsPerThread = (kRegCells + kSweepBlock - 1) / kSweepBlock;
+
+// Stage the region of grid `gi` (0 = old, 1 = new): per-cell counts from the cell starts, a block
+// scan into the LDS cell-start table, then a flat copy (thread per entry: region row by binary
+// search, tile part by two compares, one 16-B load). Returns the staged count (block-uniform); a
+// count > kCap means "does not fit" and nothing was copied.
+__device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, const Region& R, SweepSmem& sm, int gi) {
+  uint16_t* lcs = sm.lcs[gi];
+  uint32_t* gsp = sm.gsp[gi];
+  const int pt0 = R.xr0 >> kTileShift;  // tile column of the region's first column
+  uint32_t n[kCellsPerThread];
+  uint32_t sum = 0;
+  const int c0 = threadIdx.x * kCellsPerThread;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kCellsPerThread; ++k) {
     const int c = c0 + k;
+    n[k] = 0;
     if (c < R.ncells) {
-      const int rr = c / R.ncols, cc = c - rr * R.ncols;
-      const uint32_t key = cell_key(g, R.xr0 + cc, R.zr0 + rr);
-      const uint32_t s0 = gv.cs[key], s1 = gv.cs[key + 1];
-      gs[c] = s0;
-      (k ? n1 : n0) = s1 - s0;
+      const int rr = c / R.ncols, col = R.xr0 + (c - rr * R.ncols);
+      const uint32_t key = cell_key(g, col, R.zr0 + rr);
+      const uint32_t s0 = gv.cs[key];
+      n[k] = gv.cs[key + 1] - s0;
+      if (col == R.xr0 || (col & (kTile - 1)) == 0) gsp[rr * 3 + ((col >> kTileShift) - pt0)] = s0;
     }
+    sum += n[k];
   }
   uint32_t total;
-  const uint32_t pre = block_excl_scan_512(n0 + n1, ws, &total);
-  if (c0 < R.ncells) lcs[c0] = pre;
-  if (c0 + 1 < R.ncells) lcs[c0 + 1] = pre + n0;
-  if (threadIdx.x == 0) lcs[R.ncells] = total;
+  uint32_t pre = block_excl_scan_big(sum, sm.ws, &total);
   if (total > (uint32_t)kCap) return total;
+#pragma unroll
+  for (int k = 0; k < kCellsPerThread; ++k) {
+    if (c0 + k < R.ncells) lcs[c0 + k] = (uint16_t)pre;
+    pre += n[k];
+  }
+  if (threadIdx.x == 0) lcs[R.ncells] = (uint16_t)total;
   __syncthreads();
-  for (int c = threadIdx.x; c < R.ncells; c += kSweepBlock) {
-    const uint32_t d = lcs[c], n = lcs[c + 1] - d, s = gs[c];
-    for (uint32_t k = 0; k < n; ++k) {
-      smem.ent[gi][d + k] = gv.ent[s + k];
-      if (gi == 0) smem.side[d + k] = gv.side[s + k];
+  for (uint32_t i = threadIdx.x; i < total; i += kSweepBlock) {
+    int lo = 0, hi = R.nrows;  // find rr with lcs[rr * ncols] <= i < lcs[(rr + 1) * ncols]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (lcs[mid * R.ncols] <= i) lo = mid;
+      else hi = mid;
     }
+    const int rb = lo * R.ncols;
+    // tile parts of the row start at region columns 0, then each multiple of kTile
+    const int p1c = ((pt0 + 1) << kTileShift) - R.xr0, p2c = p1c + kTile;
+    int p = 0, pc = 0;
+    if (p1c < R.ncols && lcs[rb + p1c] <= i) {
+      p = 1;
+      pc = p1c;
+      if (p2c < R.ncols && lcs[rb + p2c] <= i) {
+        p = 2;
+        pc = p2c;
+      }
+    }
+    const uint32_t src = gsp[lo * 3 + p] + (i - lcs[rb + pc]);
+    sm.ent[gi][i] = gv.ent[src];
+    if (gi == 0) sm.side[i] = gv.side[src];
   }
   return total;
 }
@@ -511,86 +541,83 @@ __device__ __forceinline__ bool same_geom(const Geom& a, const Geom& b) {
   return a.x0 == b.x0 && a.z0 == b.z0 && a.inv_c == b.inv_c && a.ncx == b.ncx && a.ncz == b.ncz && a.base == b.base;
 }
 
-__global__ void __launch_bounds__(kSweepBlock) k_sweep(SweepArgs a) {
+__global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  SweepSmem& smem = *reinterpret_cast<SweepSmem*>(smem_raw);
-  uint32_t* ws = smem.ws;
-
-  if (blockIdx.x < a.max_units) {
-    if (blockIdx.x >= a.ctr[CTR_UNITS]) return;  // block-uniform: no barrier reached
-    const uint4 u = a.units[blockIdx.x];
-    const Geom gn = a.ng.geom[u.x];
-    const Geom go = a.og.geom[u.x];
-    // region: the unit's cell rows and its tile's columns, plus `reach` cells around
+  SweepSmem& sm = *reinterpret_cast<SweepSmem*>(smem_raw);
+  if (threadIdx.x == 0) {
+    sm.n = 0;
+    sm.enter = 0;
+  }
+  if (blockIdx.x < a.ntiles) {
+    const uint32_t t = blockIdx.x;
+    const uint32_t e0 = a.ng.cs[t << kTileCellShift], e1 = a.ng.cs[(t + 1) << kTileCellShift];
+    // does the tile hold a mover of this pass? (block-uniform exit otherwise)
+    bool mine = false;
+    for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = a.ng.ent[j].w >= a.base;
+    if (!__syncthreads_or(mine)) return;
+    const uint32_t sp = a.ng.tile_space[t];
+    const Geom gn = a.ng.geom[sp];
+    const Geom go = a.og.geom[sp];
     bool lds = a.use_lds && gn.reach > 0 && same_geom(go, gn);
     Region R;
     if (lds) {
-      const uint32_t tl = u.y - gn.tile_base;
+      const uint32_t tl = t - gn.tile_base;
       const int tz = (int)(tl / (uint32_t)gn.ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)gn.ntx);
-      const int rf = cellc(__uint_as_float(a.ng.ent[u.z].y), gn.z0, gn.inv_c, gn.ncz);
-      const int rl = cellc(__uint_as_float(a.ng.ent[u.w - 1].y), gn.z0, gn.inv_c, gn.ncz);
-      R.zr0 = max(0, rf - gn.reach);
-      R.zr1 = min(gn.ncz - 1, rl + gn.reach);
+      R.zr0 = max(0, tz * kTile - gn.reach);
+      R.zr1 = min(gn.ncz - 1, tz * kTile + kTile - 1 + gn.reach);
       R.xr0 = max(0, tx * kTile - gn.reach);
       R.xr1 = min(gn.ncx - 1, tx * kTile + kTile - 1 + gn.reach);
       R.ncols = R.xr1 - R.xr0 + 1;
-      R.ncells = (R.zr1 - R.zr0 + 1) * R.ncols;
-      lds = R.ncells <= kRegCells;
+      R.nrows = R.zr1 - R.zr0 + 1;
+      R.ncells = R.nrows * R.ncols;
+      lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= kTile + 2 * kTile;
     }
     if (lds) {
-      const uint32_t n_old = stage(a.og, go, R, smem, 0, ws);
+      const uint32_t n_old = stage(a.og, go, R, sm, 0);
       __syncthreads();
-      const uint32_t n_new = stage(a.ng, gn, R, smem, 1, ws);
+      const uint32_t n_new = stage(a.ng, gn, R, sm, 1);
       lds = n_old <= (uint32_t)kCap && n_new <= (uint32_t)kCap;  // block-uniform
+      __syncthreads();
     }
-    __syncthreads();  // staging done; the gs scratch becomes the event queue
-    if (threadIdx.x == 0) {
-      smem.n = 0;
-      smem.enter = 0;
-    }
-    __syncthreads();
-    const uint32_t j = u.z + threadIdx.x;
     if (a.use_lds == 2) {  // ablation (timing only): staging without the candidate walk
-      if (j < u.w && a.ng.ent[j].w >= a.base) a.rank_cnt[a.ng.ent[j].w - a.base] = 0;
-    } else if (j < u.w) {
-      const uint4 e = a.ng.ent[j];
-      if (e.w >= a.base) {  // acted in this pass
+      for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock)
+        if (a.ng.ent[j].w >= a.base) a.rank_cnt[a.ng.ent[j].w - a.base] = 0;
+    } else {
+      for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
+        const uint4 e = a.ng.ent[j];
+        if (e.w < a.base) continue;  // did not act in this pass
         const Mover m = make_mover(a, e.z, e.w, true, __uint_as_float(e.x), __uint_as_float(e.y), gn.D);
         uint32_t cnt;
         if (lds && R.holds(qbox(gn, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(gn, m.mx0, m.mz0))))
-          cnt = sweep_lds(a, smem, m, R, gn);
+          cnt = sweep_lds(a, sm, m, R, gn);
         else
-          cnt = sweep_global(a, smem, m, go, gn);
+          cnt = sweep_global(a, sm, m, go, gn);
         a.rank_cnt[m.rank] = cnt;
       }
     }
   } else {
-    if (threadIdx.x == 0) {
-      smem.n = 0;
-      smem.enter = 0;
-    }
     __syncthreads();
-    const uint32_t t = (blockIdx.x - a.max_units) * kSweepBlock + threadIdx.x;
+    const uint32_t t = (blockIdx.x - a.ntiles) * kSweepBlock + threadIdx.x;
     if (t < a.n_leaves) {
       const uint32_t i = a.leave_ops[t];
-      const uint32_t sm = a.op_slot[i];
-      const uint32_t sp = a.space_of[sm];
+      const uint32_t smv = a.op_slot[i];
+      const uint32_t sp = a.space_of[smv];
       const Geom go = a.og.geom[sp], gn = a.ng.geom[sp];
-      const Mover m = make_mover(a, sm, a.base + i, false, 0.0f, 0.0f, go.D);
-      a.rank_cnt[i] = sweep_global(a, smem, m, go, gn);
+      const Mover m = make_mover(a, smv, a.base + i, false, 0.0f, 0.0f, go.D);
+      a.rank_cnt[i] = sweep_global(a, sm, m, go, gn);
     }
   }
   // flush the block's events with one global atomic
   __syncthreads();
-  const uint32_t nq = min(smem.n, (uint32_t)kEvLds);
+  const uint32_t nq = min(sm.n, (uint32_t)kEvLds);
   if (threadIdx.x == 0) {
-    smem.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
-    if (smem.enter) atomicAdd(&a.ctr[CTR_ENTER], smem.enter);
+    sm.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+    if (sm.enter) atomicAdd(&a.ctr[CTR_ENTER], sm.enter);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nq; i += kSweepBlock) {
-    const uint32_t gi = smem.base + i;
-    if (gi < a.ev_cap) a.ev_tmp[gi] = smem.u.ev[i];
+    const uint32_t gi = sm.base + i;
+    if (gi < a.ev_cap) a.ev_tmp[gi] = sm.ev[i];
   }
 }
 
@@ -603,9 +630,7 @@ void sweep_init() {
 // blocks and only the event queue in LDS, i.e. full occupancy; candidates come through L1/L2.
 struct FlatQ {
   uint32_t n, enter, base, flags;
-  union {
-    uint4 ev[kEvLds];
-  } u;
+  uint4 ev[kEvLds];
 };
 
 __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
@@ -626,10 +651,10 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
     }
   } else if (t < a.n_new + a.n_leaves) {
     const uint32_t i = a.leave_ops[t - a.n_new];
-    const uint32_t sm = a.op_slot[i];
-    const uint32_t sp = a.space_of[sm];
+    const uint32_t smv = a.op_slot[i];
+    const uint32_t sp = a.space_of[smv];
     const Geom go = a.og.geom[sp], gn = a.ng.geom[sp];
-    const Mover m = make_mover(a, sm, a.base + i, false, 0.0f, 0.0f, go.D);
+    const Mover m = make_mover(a, smv, a.base + i, false, 0.0f, 0.0f, go.D);
     a.rank_cnt[i] = sweep_global(a, q, m, go, gn);
   }
   __syncthreads();
@@ -641,7 +666,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
     const uint32_t gi = q.base + i;
-    if (gi < a.ev_cap) a.ev_tmp[gi] = q.u.ev[i];
+    if (gi < a.ev_cap) a.ev_tmp[gi] = q.ev[i];
   }
 }
 
@@ -651,7 +676,7 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
     if (n) hipLaunchKernelGGL(k_sweep_flat, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
     return;
   }
-  const uint32_t nb = a.max_units + (a.n_leaves + kSweepBlock - 1) / kSweepBlock;
+  const uint32_t nb = a.ntiles + (a.n_leaves + kSweepBlock - 1) / kSweepBlock;
   if (!nb) return;
   hipLaunchKernelGGL(k_sweep, dim3(nb), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
 }

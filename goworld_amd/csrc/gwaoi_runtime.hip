@@ -105,7 +105,7 @@ struct gwaoi_mgr {
   uint32_t cap = 0;
   uint32_t nspaces = 0;
   std::vector<SpaceHost> spaces;
-  float cells_per_dist = 2.0f;
+  float cells_per_dist = 4.0f;
   uint32_t max_cells = 0;
   bool broken = false;
 
@@ -143,8 +143,6 @@ struct gwaoi_mgr {
   int cur = 0;  // grid holding the current state
   uint32_t next_seq = 1;
   uint32_t* rank_cnt = nullptr;  // [cap + 1]
-  uint4* units = nullptr;        // sweep work units
-  uint32_t max_units = 0;        // capacity of units
   int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
   uint32_t* part = nullptr;
   uint32_t part_words = 0;
@@ -237,7 +235,7 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
                                   std::fabs((double)z1)});
     const double span = ((double)sh.desc.dist * (1.0 + 1e-5) + (maxc + sh.desc.dist) * 1e-6) / c;
     int reach = (int)std::ceil(span) + 1;
-    if ((gw::kTile + 2 * reach) * (gw::kTile + 2 * reach) > 1024) reach = 0;  // LDS path off for this Space
+    if ((gw::kTile + 2 * reach) * (gw::kTile + 2 * reach) > 2304) reach = 0;  // LDS path off for this Space
     g.reach = reach;
     g.pad = 0;
     base += (uint32_t)(tx * tz) * gw::kTileCells;
@@ -425,11 +423,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
 
   RCHK(build_grid(m, ng));
-  {
-    const Grid& G = m->grid[ng];
-    gw::launch_units({G.ent, G.cs, G.side, G.d_geom, G.d_tile_space}, G.ntiles, m->units, m->ctr, st);
-    HIPCHK(hipGetLastError());
-  }
   if (m->timing) HIPCHK(hipEventRecord(m->tev[2], st));
 
   const uint32_t n_new = dev ? m->n_present_dev : m->n_present;
@@ -444,8 +437,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     gw::SweepArgs s;
     s.og = {m->grid[og].ent, m->grid[og].cs, m->grid[og].side, m->grid[og].d_geom, m->grid[og].d_tile_space};
     s.ng = {m->grid[ng].ent, m->grid[ng].cs, m->grid[ng].side, m->grid[ng].d_geom, m->grid[ng].d_tile_space};
-    s.units = m->units;
-    s.max_units = std::min<uint32_t>(m->max_units, m->grid[ng].ntiles + n_new / gw::kUnit + 1);
+    s.ntiles = m->grid[ng].ntiles;
     s.use_lds = m->sweep_lds;
     s.old_x = m->old_x;
     s.old_z = m->old_z;
@@ -594,7 +586,7 @@ void free_all(gwaoi_mgr* m) {
   if (m->stream) hipStreamSynchronize(m->stream);
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_op_x, m->d_op_z,
-                   m->d_op_kind, m->rank_cnt, m->part, m->ctr_buf, m->ev_tmp, m->ev_out, m->units};
+                   m->d_op_kind, m->rank_cnt, m->part, m->ctr_buf, m->ev_tmp, m->ev_out};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
@@ -698,8 +690,6 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     chk(dalloc(&g.d_geom, nspaces));
     chk(dalloc(&g.d_tile_space, (size_t)m->max_cells / gw::kTileCells + 1));
   }
-  m->max_units = m->max_cells / gw::kTileCells + capacity / gw::kUnit + 2;
-  chk(dalloc(&m->units, m->max_units));
   static bool sweep_ready = false;
   if (!sweep_ready) {
     gw::sweep_init();
