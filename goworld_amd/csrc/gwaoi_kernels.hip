@@ -317,8 +317,8 @@ struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint32_t gsp[2][kMaxRows * 3];    // global start of each (region row, tile part)
   uint4 ev[kEvLds];                 // event queue
   uint16_t lcs[2][kRegCells + 8];   // LDS start of each region cell (+ total)
-  uint4 ent[2][kCap];
-  uint32_t side[kCap];
+  uint4 ent[2][kCap];  // old grid: {x, z, seq0, side}; new grid: {x, z, slot, seq}
+  uint32_t slot_old[kCap];
 };
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
@@ -444,16 +444,55 @@ struct Region {
   }
 };
 
+// LDS walk, written out for the hot loop: one 16-B LDS read per candidate, branch-free predicates,
+// a branch only where an event is raised (rare), two candidates per iteration.
+//  old-grid record {x, z, seq0, side}: skip o if (side - base) <= rank, i.e. o acted earlier in this
+//  pass or o is m itself (m's own old entry carries m's op seq); the slot is read only on emit.
+//  new-grid record {x, z, slot, seq}: o counts only if (seq - base) < rank (acted earlier).
 __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Region& R,
                                               const Geom& g) {
-  return sweep_mover(a, sm, m, [&](auto&& fo, auto&& fn) {
-    walk_cells(m, g, [&](int r, int c0, int c1) {
-      if (c0 > c1) return;
-      const int b = (r - R.zr0) * R.ncols - R.xr0;
-      for (uint32_t j = sm.lcs[0][b + c0], e = sm.lcs[0][b + c1 + 1]; j < e; ++j) fo(sm.ent[0][j], sm.side[j]);
-      for (uint32_t j = sm.lcs[1][b + c0], e = sm.lcs[1][b + c1 + 1]; j < e; ++j) fn(sm.ent[1][j]);
-    });
+  const float D = m.D;
+  const Bounds b1 = {m.mx1 - D, m.mx1 + D, m.mz1 - D, m.mz1 + D};
+  const Bounds b0 = {m.mx0 - D, m.mx0 + D, m.mz0 - D, m.mz0 + D};
+  const uint32_t base = a.base, rank = m.rank, q0 = m.q0;
+  const bool v0 = m.valid0, v1 = m.valid1;
+  const float mx0 = m.mx0, mz0 = m.mz0;
+  uint32_t local = 0;
+  auto old_ev = [&](const uint4 c, uint32_t j) {
+    const float ox = __uint_as_float(c.x), oz = __uint_as_float(c.y);
+    const bool in_o = inbox(ox, oz, D, mx0, mz0);  // o's perspective (o acted last)
+    const bool in_m = b0.has(ox, oz);             // m's perspective
+    const bool before = v0 && ((c.z > q0) ? in_o : in_m);
+    const bool after = v1 && b1.has(ox, oz);
+    if ((c.w - base) > rank && before != after) emit(a, sm, rank, local++, m.sm, sm.slot_old[j], after);
+  };
+  auto new_ev = [&](const uint4 c) {
+    const float ox = __uint_as_float(c.x), oz = __uint_as_float(c.y);
+    const bool before = v0 && inbox(ox, oz, D, mx0, mz0);
+    const bool after = v1 && b1.has(ox, oz);
+    if ((c.w - base) < rank && before != after) emit(a, sm, rank, local++, m.sm, c.z, after);
+  };
+  walk_cells(m, g, [&](int r, int c0, int c1) {
+    if (c0 > c1) return;
+    const int b = (r - R.zr0) * R.ncols - R.xr0;
+    uint32_t j = sm.lcs[0][b + c0];
+    const uint32_t e = sm.lcs[0][b + c1 + 1];
+    uint32_t k = sm.lcs[1][b + c0];
+    const uint32_t f = sm.lcs[1][b + c1 + 1];
+    for (; j + 1 < e; j += 2) {
+      const uint4 c0v = sm.ent[0][j], c1v = sm.ent[0][j + 1];
+      old_ev(c0v, j);
+      old_ev(c1v, j + 1);
+    }
+    if (j < e) old_ev(sm.ent[0][j], j);
+    for (; k + 1 < f; k += 2) {
+      const uint4 c0v = sm.ent[1][k], c1v = sm.ent[1][k + 1];
+      new_ev(c0v);
+      new_ev(c1v);
+    }
+    if (k < f) new_ev(sm.ent[1][k]);
   });
+  return local;
 }
 
 // exclusive scan of v over a kSweepBlock-thread block; *total = block sum (LDS scratch `ws`)
@@ -531,8 +570,13 @@ __device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, con
       }
     }
     const uint32_t src = gsp[lo * 3 + p] + (i - lcs[rb + pc]);
-    sm.ent[gi][i] = gv.ent[src];
-    if (gi == 0) sm.side[i] = gv.side[src];
+    const uint4 e = gv.ent[src];
+    if (gi == 0) {
+      sm.ent[0][i] = make_uint4(e.x, e.y, e.w, gv.side[src]);
+      sm.slot_old[i] = e.z;
+    } else {
+      sm.ent[1][i] = e;
+    }
   }
   return total;
 }
