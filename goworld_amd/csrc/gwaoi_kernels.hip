@@ -360,36 +360,84 @@ __device__ __forceinline__ Mover make_mover(const SweepArgs& a, uint32_t sm, uin
   return m;
 }
 
-// The cells a mover must read, as column intervals per row: the union of its old and new query
-// boxes, minus (for a move whose boxes overlap) the cells deep inside both boxes.
-template <class RowF>
-__device__ __forceinline__ void walk_cells(const Mover& m, const Geom& g, RowF&& rowf) {
+// The cells a mover must read: rows z0..z1 of the union of its old and new query boxes, and in each
+// row at most two column intervals — the two boxes' intervals (merged when they touch), or, for a
+// move whose boxes overlap, the two ring pieces left and right of the cells deep inside both boxes.
+// The walk runs over rows RELATIVE to each lane's own window with a wave-uniform trip count, and
+// always visits segment A then segment B (possibly empty), so lanes of a wave that sit in
+// different cell rows still follow the same control flow.
+struct Walk {
+  int z0, z1;          // rows
+  int ax0, ax1, az0, az1;  // box A columns / rows (old box, or the union for a ring walk)
+  int bx0, bx1, bz0, bz1;  // box B (new box); for a ring walk: inner rows bz0..bz1, inner cols bx0..bx1
+  bool ring;
+};
+
+__device__ __forceinline__ Walk make_walk(const Mover& m, const Geom& g) {
   const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
-  if (!(m.valid0 && m.valid1)) {
-    for_each_row_interval(m.valid0, A0, m.valid1, A1, rowf);
-    return;
-  }
-  const int x0 = min(A0.x0, A1.x0), x1 = max(A0.x1, A1.x1);
-  const int z0 = min(A0.z0, A1.z0), z1 = max(A0.z1, A1.z1);
-  if (x1 - x0 > (A1.x1 - A1.x0) + 2 || z1 - z0 > (A1.z1 - A1.z0) + 2) {  // far apart: two boxes
-    for_each_row_interval(true, A0, true, A1, rowf);
-    return;
-  }
-  const float D = g.D;
-  const float ex = (fmaxf(fabsf(m.mx0), fabsf(m.mx1)) + D) * kInner;
-  const float ez = (fmaxf(fabsf(m.mz0), fabsf(m.mz1)) + D) * kInner;
-  const int ix0 = cellc((fmaxf(m.mx0, m.mx1) - D) + ex, g.x0, g.inv_c, g.ncx) + 1;
-  const int ix1 = cellc((fminf(m.mx0, m.mx1) + D) - ex, g.x0, g.inv_c, g.ncx) - 1;
-  const int iz0 = cellc((fmaxf(m.mz0, m.mz1) - D) + ez, g.z0, g.inv_c, g.ncz) + 1;
-  const int iz1 = cellc((fminf(m.mz0, m.mz1) + D) - ez, g.z0, g.inv_c, g.ncz) - 1;
-  const bool ring = ix0 <= ix1;
-  for (int r = z0; r <= z1; ++r) {
-    if (ring && r >= iz0 && r <= iz1) {
-      rowf(r, x0, ix0 - 1);
-      rowf(r, ix1 + 1, x1);
-    } else {
-      rowf(r, x0, x1);
+  Walk w;
+  w.ring = false;
+  if (m.valid0 && m.valid1) {
+    const int x0 = min(A0.x0, A1.x0), x1 = max(A0.x1, A1.x1);
+    const int z0 = min(A0.z0, A1.z0), z1 = max(A0.z1, A1.z1);
+    if (x1 - x0 <= (A1.x1 - A1.x0) + 2 && z1 - z0 <= (A1.z1 - A1.z0) + 2) {
+      const float D = g.D;
+      const float ex = (fmaxf(fabsf(m.mx0), fabsf(m.mx1)) + D) * kInner;
+      const float ez = (fmaxf(fabsf(m.mz0), fabsf(m.mz1)) + D) * kInner;
+      w.ring = true;
+      w.z0 = w.az0 = z0;
+      w.z1 = w.az1 = z1;
+      w.ax0 = x0;
+      w.ax1 = x1;
+      w.bx0 = cellc((fmaxf(m.mx0, m.mx1) - D) + ex, g.x0, g.inv_c, g.ncx) + 1;
+      w.bx1 = cellc((fminf(m.mx0, m.mx1) + D) - ex, g.x0, g.inv_c, g.ncx) - 1;
+      w.bz0 = cellc((fmaxf(m.mz0, m.mz1) - D) + ez, g.z0, g.inv_c, g.ncz) + 1;
+      w.bz1 = cellc((fminf(m.mz0, m.mz1) + D) - ez, g.z0, g.inv_c, g.ncz) - 1;
+      if (w.bx0 > w.bx1) w.bz0 = 1, w.bz1 = 0;  // no inner cells: full rows
+      return w;
     }
+  }
+  const CellBox A = m.valid0 ? A0 : A1, B = m.valid1 ? A1 : A0;
+  w.ax0 = A.x0, w.ax1 = A.x1, w.az0 = A.z0, w.az1 = A.z1;
+  w.bx0 = B.x0, w.bx1 = B.x1, w.bz0 = B.z0, w.bz1 = B.z1;
+  w.z0 = min(A.z0, B.z0);
+  w.z1 = max(A.z1, B.z1);
+  return w;
+}
+
+// The two column segments of row r (empty segment: c0 > c1).
+__device__ __forceinline__ void walk_row(const Walk& w, int r, int& a0, int& a1, int& b0, int& b1) {
+  a0 = 1, a1 = 0, b0 = 1, b1 = 0;
+  if (r < w.z0 || r > w.z1) return;
+  if (w.ring) {
+    if (r >= w.bz0 && r <= w.bz1) {
+      a0 = w.ax0, a1 = w.bx0 - 1, b0 = w.bx1 + 1, b1 = w.ax1;
+    } else {
+      a0 = w.ax0, a1 = w.ax1;
+    }
+    return;
+  }
+  const bool ia = r >= w.az0 && r <= w.az1, ib = r >= w.bz0 && r <= w.bz1;
+  if (ia) a0 = w.ax0, a1 = w.ax1;
+  if (ib) b0 = w.bx0, b1 = w.bx1;
+  if (ia && ib && w.bx0 <= w.ax1 + 1 && w.ax0 <= w.bx1 + 1) {  // touching: one merged interval
+    a0 = min(w.ax0, w.bx0);
+    a1 = max(w.ax1, w.bx1);
+    b0 = 1, b1 = 0;
+  }
+}
+
+// segf(r, c0, c1) for each non-empty segment, rows relative to the lane's window.
+template <class SegF>
+__device__ __forceinline__ void walk_cells(const Mover& m, const Geom& g, SegF&& segf) {
+  const Walk w = make_walk(m, g);
+  const int h = w.z1 - w.z0;
+  for (int rel = 0; __any(rel <= h); ++rel) {  // vote over the ACTIVE lanes: wave-uniform trip count
+    const int r = w.z0 + rel;
+    int a0, a1, b0, b1;
+    walk_row(w, r, a0, a1, b0, b1);
+    segf(r, a0, a1);
+    segf(r, b0, b1);
   }
 }
 
