@@ -506,18 +506,27 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
   const bool v0 = m.valid0, v1 = m.valid1;
   const float mx0 = m.mx0, mz0 = m.mz0;
   uint32_t local = 0;
+  // Predicates in VALU arithmetic: lo <= p <= hi  <=>  min(p - lo, hi - p) >= 0, exactly (the sign
+  // of a binary32 difference of finite values is the sign of the exact difference when subnormals
+  // are kept; x - x = +0). An invalid side is forced to -1 (false).
+  const float sel0 = v0 ? 1.0f : -1.0f, sel1 = v1 ? 1.0f : -1.0f;
+  auto margin = [](float px, float pz, float lx, float hx, float lz, float hz) {
+    return fminf(fminf(px - lx, hx - px), fminf(pz - lz, hz - pz));
+  };
   auto old_ev = [&](const uint4 c, uint32_t j) {
     const float ox = __uint_as_float(c.x), oz = __uint_as_float(c.y);
-    const bool in_o = inbox(ox, oz, D, mx0, mz0);  // o's perspective (o acted last)
-    const bool in_m = b0.has(ox, oz);             // m's perspective
-    const bool before = v0 && ((c.z > q0) ? in_o : in_m);
-    const bool after = v1 && b1.has(ox, oz);
+    const float am = margin(ox, oz, b0.lx, b0.hx, b0.lz, b0.hz);                 // m's perspective
+    const float ao = margin(mx0, mz0, ox - D, ox + D, oz - D, oz + D);           // o's perspective
+    const float bf = fminf(sel0, (c.z > q0) ? ao : am);                          // o acted last?
+    const float af = fminf(sel1, margin(ox, oz, b1.lx, b1.hx, b1.lz, b1.hz));
+    const bool before = bf >= 0.0f, after = af >= 0.0f;
     if ((c.w - base) > rank && before != after) emit(a, sm, rank, local++, m.sm, sm.slot_old[j], after);
   };
   auto new_ev = [&](const uint4 c) {
     const float ox = __uint_as_float(c.x), oz = __uint_as_float(c.y);
-    const bool before = v0 && inbox(ox, oz, D, mx0, mz0);
-    const bool after = v1 && b1.has(ox, oz);
+    const float bf = fminf(sel0, margin(mx0, mz0, ox - D, ox + D, oz - D, oz + D));
+    const float af = fminf(sel1, margin(ox, oz, b1.lx, b1.hx, b1.lz, b1.hz));
+    const bool before = bf >= 0.0f, after = af >= 0.0f;
     if ((c.w - base) < rank && before != after) emit(a, sm, rank, local++, m.sm, c.z, after);
   };
   walk_cells(m, g, [&](int r, int c0, int c1) {
