@@ -38,11 +38,18 @@ struct Geom {
   uint32_t pad;
 };
 
-// One grid snapshot: all present entities sorted by cell. ent[j] = {x bits, z bits, slot, seq}.
+// The pass's grid: every record sorted by cell key (counting sort). Per slot: a MAIN record at its
+// end-of-pass cell (if present at the end) and a GHOST record at its start-of-pass cell (if present
+// at the start and that cell differs, or it left in this pass).
+//   ra[j] = {x_bin bits, z_bin bits, slot | flags, opq}   (binned position; opq = op seq of this pass)
+//   rb[j] = {x_start bits, z_start bits, seq_start, seq_end}
+enum : uint32_t { REC_GHOST = 0x80000000u, REC_HASG = 0x40000000u, REC_SLOT = 0x3fffffffu };
+constexpr uint32_t kNoKey = 0xffffffffu;
+
 struct GridView {
-  const uint4* ent;
+  const uint4* ra;
+  const uint4* rb;
   const uint32_t* cs;          // cell_start[ncells + 1]
-  const uint32_t* side;        // side[j] = op seq of entry j's slot this pass (old-grid role), else stale
   const Geom* geom;            // [nspaces]
   const uint32_t* tile_space;  // [ntiles] tile -> space
 };
@@ -64,10 +71,9 @@ struct ApplyArgs {
   float* old_x;
   float* old_z;
   uint32_t* old_seq;
-  uint32_t* old_side;        // side array of the old grid
-  const uint32_t* old_gidx;  // slot -> entry index in the old grid
+  uint32_t* opq;             // op seq of this pass (stale for slots without an op)
   uint32_t* ctr;
-  uint32_t* rank_tail;        // rank_cnt[n_ops], zeroed (the scan's total slot)
+  uint32_t* rank_tail;       // rank_cnt[n_ops], zeroed (the scan's total slot)
 };
 
 struct BinArgs {
@@ -75,26 +81,32 @@ struct BinArgs {
   const float* pos_z;
   const uint32_t* seq;
   const uint32_t* space_of;
-  const Geom* geom;
-  uint32_t cap;
-  uint32_t* key_of;
-  uint32_t* local_of;
-  uint32_t* cs;      // counts, then (after scan) cell_start
-  uint4* ent;
-  uint32_t* gidx;
-};
-
-struct SweepArgs {
-  GridView og;  // old grid: state at the start of the pass
-  GridView ng;  // new grid: state at the end of the pass
-  uint32_t ntiles;     // tiles of the new grid: blocks [0, ntiles) take one tile each, the rest Leave ops
-  int use_lds;         // 1: LDS-staged sweep; 0: flat global-memory sweep (A/B); 2: staging only (timing)
   const float* old_x;
   const float* old_z;
   const uint32_t* old_seq;
+  const uint32_t* opq;
+  uint32_t base, n_ops;
+  const Geom* geom;
+  uint32_t cap;
+  uint32_t* key_of;    // [2 cap]: main / ghost key per slot (kNoKey = none)
+  uint32_t* local_of;  // [2 cap]
+  uint32_t* cs;        // counts, then (after scan) cell_start
+  uint4* ra;
+  uint4* rb;
+};
+
+struct SweepArgs {
+  GridView g;
+  const float* old_x;  // start-of-pass state of Leave ops' slots
+  const float* old_z;
+  const uint32_t* old_seq;
   const uint32_t* space_of;
-  uint32_t base;    // seq of op 0 of this pass
-  uint32_t n_new;   // entries in the new grid
+  uint32_t base;       // seq of op 0 of this pass
+  uint32_t n_ops;
+  uint32_t n_rec;      // upper bound on records in the grid (flat variant grid size)
+  uint32_t ncells;     // cells of the grid (cs[ncells] = record count)
+  uint32_t ntiles;     // tiles of the grid: blocks [0, ntiles) take one tile each, the rest Leave ops
+  int use_lds;         // 1: LDS-staged sweep; 0: flat global-memory sweep (A/B); 2: staging only (timing)
   const uint32_t* op_slot;    // for the leave path
   const uint32_t* leave_ops;  // op indices of OP_LEAVE ops
   uint32_t n_leaves;

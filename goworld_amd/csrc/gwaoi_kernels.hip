@@ -12,8 +12,13 @@
 //   before(m,o) = state just before m's op:  in(o_new, m_old) if o acted earlier in this pass,
 //                                            else in(L, F) over the start-of-pass state,
 //   after(m,o)  = in(m_new, o at that time) (o_new if o acted earlier, else o_old),
-// and emits ENTER/LEAVE(m,o) where they differ. Old-pass positions come from the old grid (the
-// previous pass's new grid), new ones from the new grid; both are cell-sorted snapshots.
+// and emits ENTER/LEAVE(m,o) where they differ.
+//
+// One cell-sorted grid per pass holds, for every entity, a record binned at its END-of-pass cell
+// carrying both its start- and end-of-pass state; an entity whose start cell differs (or that left)
+// also gets a "ghost" record at its start cell. Every candidate is then met once, in the cell of
+// the position that matters for the pair (start position if it has not acted yet, end position
+// if it has).
 //
 // Float semantics: every bound is one binary32 add/sub (built with -ffp-contract=off, denormals
 // preserved), compared inclusively — bit-exact with Go float32 arithmetic.
@@ -43,13 +48,6 @@ __device__ __forceinline__ bool inbox(float cx, float cz, float D, float px, flo
   return px >= lx && px <= hx && pz >= lz && pz <= hz;
 }
 
-struct Bounds {
-  float lx, hx, lz, hz;
-  __device__ __forceinline__ bool has(float px, float pz) const {
-    return px >= lx && px <= hx && pz >= lz && pz <= hz;
-  }
-};
-
 struct CellBox {
   int x0, x1, z0, z1;
 };
@@ -69,34 +67,11 @@ __device__ __forceinline__ uint32_t cell_key(const Geom& g, int cx, int cz) {
          (uint32_t)(((cz & (kTile - 1)) << kTileShift) | (cx & (kTile - 1)));
 }
 
-// Row intervals of the union of box A (if va) and box B (if vb): one or two column intervals per
-// row, so every cell is visited once.
-template <class RowF>
-__device__ __forceinline__ void for_each_row_interval(bool va, CellBox A, bool vb, CellBox B, RowF&& rf) {
-  int r0 = va ? A.z0 : B.z0, r1 = va ? A.z1 : B.z1;
-  if (va && vb) {
-    r0 = min(A.z0, B.z0);
-    r1 = max(A.z1, B.z1);
-  }
-  for (int r = r0; r <= r1; ++r) {
-    const bool ia = va && r >= A.z0 && r <= A.z1;
-    const bool ib = vb && r >= B.z0 && r <= B.z1;
-    if (ia && ib) {
-      if (B.x0 <= A.x1 + 1 && A.x0 <= B.x1 + 1) {
-        rf(r, min(A.x0, B.x0), max(A.x1, B.x1));
-      } else {
-        rf(r, A.x0, A.x1);
-        rf(r, B.x0, B.x1);
-      }
-    } else if (ia) {
-      rf(r, A.x0, A.x1);
-    } else if (ib) {
-      rf(r, B.x0, B.x1);
-    }
-  }
+__device__ __forceinline__ uint32_t cell_key_of(const Geom& g, float x, float z) {
+  return cell_key(g, cellc(x, g.x0, g.inv_c, g.ncx), cellc(z, g.z0, g.inv_c, g.ncz));
 }
 
-// Global-memory path: entries of row r, columns [c0, c1]: one contiguous segment per tile crossed.
+// Global-memory path: records of row r, columns [c0, c1]: one contiguous segment per tile crossed.
 template <class F>
 __device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t* __restrict__ cs, int r, int c0,
                                                    int c1, F&& f) {
@@ -110,17 +85,11 @@ __device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t
   }
 }
 
-template <class F>
-__device__ __forceinline__ void for_each_entry(const Geom& g, const uint32_t* __restrict__ cs, bool va,
-                                               CellBox A, bool vb, CellBox B, F&& f) {
-  for_each_row_interval(va, A, vb, B, [&](int r, int c0, int c1) { row_entries_global(g, cs, r, c0, c1, f); });
-}
-
 // ---------------------------------------------------------------------------------------------
-// apply: one thread per op. Records each mover's start-of-pass state, stamps its old-grid entry
-// with the op's seq, and writes the new state. Slots of one pass are distinct (the host guarantees
-// it for host-staged ops; for device-staged batches k_slice_sort checks afterwards that every op's
-// slot carries that op's seq — a duplicate leaves one of two ops without it).
+// apply: one thread per op. Records the slot's start-of-pass state and this pass's op seq, then
+// writes the end-of-pass state. Slots of one pass are distinct (the host guarantees it for
+// host-staged ops; for device-staged batches k_slice_sort checks afterwards that every op's slot
+// carries that op's seq — a duplicate leaves one of two ops without it).
 __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= a.n_ops) return;
@@ -140,7 +109,7 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   a.old_x[s] = a.pos_x[s];
   a.old_z[s] = a.pos_z[s];
   a.old_seq[s] = q0;
-  if (q0) a.old_side[a.old_gidx[s]] = q;
+  a.opq[s] = q;
   if (kind == OP_LEAVE) {
     a.seq[s] = 0;
   } else {
@@ -157,27 +126,71 @@ void launch_apply(const ApplyArgs& a, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Counting sort of present entities by cell key: count (atomics give each entity its rank inside
-// its cell), exclusive scan of the counts, scatter.
+// The pass's grid: counting sort of records by cell key. Per slot: a main record at its end cell
+// (if present at the end) and a ghost record at its start cell (if present at the start and its
+// start cell differs, or it left). Count (atomics rank records inside a cell), scan, scatter.
+//   ra = {x_bin, z_bin, slot | flags, opq}     rb = {x_start, z_start, seq_start, seq_end}
+struct SlotState {
+  bool acted, p_start, p_end;
+  float x0, z0, x1, z1;
+  uint32_t q0, q1, oq;
+};
+
+__device__ __forceinline__ SlotState slot_state(const BinArgs& a, uint32_t s) {
+  SlotState t;
+  t.oq = a.opq[s];
+  t.acted = (t.oq - a.base) < a.n_ops;
+  t.q1 = a.seq[s];
+  t.p_end = t.q1 != 0;
+  t.x1 = a.pos_x[s];
+  t.z1 = a.pos_z[s];
+  if (t.acted) {
+    t.q0 = a.old_seq[s];
+    t.x0 = a.old_x[s];
+    t.z0 = a.old_z[s];
+  } else {
+    t.q0 = t.q1;
+    t.x0 = t.x1;
+    t.z0 = t.z1;
+  }
+  t.p_start = t.q0 != 0;
+  return t;
+}
+
 __global__ void __launch_bounds__(kBlock) k_bin_count(BinArgs a) {
   const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
   if (s >= a.cap) return;
-  const uint32_t q = a.seq[s];
-  if (!q) return;
-  const Geom g = a.geom[a.space_of[s]];
-  const uint32_t key = cell_key(g, cellc(a.pos_x[s], g.x0, g.inv_c, g.ncx), cellc(a.pos_z[s], g.z0, g.inv_c, g.ncz));
-  a.key_of[s] = key;
-  a.local_of[s] = atomicAdd(&a.cs[key], 1u);
+  const SlotState t = slot_state(a, s);
+  uint32_t k1 = kNoKey, k0 = kNoKey;
+  if (t.p_end || t.p_start) {
+    const Geom g = a.geom[a.space_of[s]];
+    if (t.p_end) k1 = cell_key_of(g, t.x1, t.z1);
+    if (t.p_start) k0 = cell_key_of(g, t.x0, t.z0);
+    if (k0 == k1) k0 = kNoKey;  // no ghost: the main record's cell is the start cell
+    if (k1 != kNoKey) a.local_of[2 * s] = atomicAdd(&a.cs[k1], 1u);
+    if (k0 != kNoKey) a.local_of[2 * s + 1] = atomicAdd(&a.cs[k0], 1u);
+  }
+  a.key_of[2 * s] = k1;
+  a.key_of[2 * s + 1] = k0;
 }
 
 __global__ void __launch_bounds__(kBlock) k_bin_scatter(BinArgs a) {
   const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
   if (s >= a.cap) return;
-  const uint32_t q = a.seq[s];
-  if (!q) return;
-  const uint32_t j = a.cs[a.key_of[s]] + a.local_of[s];
-  a.ent[j] = make_uint4(__float_as_uint(a.pos_x[s]), __float_as_uint(a.pos_z[s]), s, q);
-  a.gidx[s] = j;
+  const uint32_t k1 = a.key_of[2 * s], k0 = a.key_of[2 * s + 1];
+  if (k1 == kNoKey && k0 == kNoKey) return;
+  const SlotState t = slot_state(a, s);
+  const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
+  if (k1 != kNoKey) {
+    const uint32_t j = a.cs[k1] + a.local_of[2 * s];
+    a.ra[j] = make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq);
+    a.rb[j] = rb;
+  }
+  if (k0 != kNoKey) {
+    const uint32_t j = a.cs[k0] + a.local_of[2 * s + 1];
+    a.ra[j] = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq);
+    a.rb[j] = rb;
+  }
 }
 
 void launch_bin_count(const BinArgs& a, hipStream_t st) {
@@ -286,13 +299,12 @@ void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Sweep. One 512-thread block per tile of the new grid (kTile x kTile cells); the block loops over
-// the tile's movers, one thread per mover. The block first stages, for BOTH grids, every entry of
-// the tile plus a halo of `reach` cells into LDS (entries, the old grid's side stamps, and a cell
-// start table), laid out row by row so that any row interval of the region is one contiguous LDS
-// range; each mover then walks its candidates in LDS. Movers whose query boxes leave the region
-// (teleports), tiles whose region does not fit, and Leave ops take the global-memory path; both
-// paths evaluate the same predicates.
+// Sweep. One 512-thread block per tile of the pass's grid (kTile x kTile cells); the block loops
+// over the tile's movers, one thread per mover. The block first stages every record of the tile
+// plus a halo of `reach` cells into LDS (both record halves and a cell start table), laid out row by
+// row so that any row interval of the region is one contiguous LDS range; each mover then walks its
+// candidates in LDS. Movers whose query boxes leave the region (teleports), tiles whose region does
+// not fit, and Leave ops take the global-memory path; both paths evaluate the same predicates.
 //
 // Ring walk: for a Moved op, a candidate strictly inside BOTH the old and the new box (shrunk by a
 // margin far above float32 rounding) is inside from every perspective before and after, so it
@@ -307,18 +319,18 @@ void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st) {
 constexpr int kSweepBlock = 512;
 constexpr int kEvLds = 256;       // events staged per block before spilling to global atomics
 constexpr int kRegCells = 2304;   // max cells of a staged region (48 x 48)
-constexpr int kCap = 1088;        // max entries staged per grid
+constexpr int kCap = 1280;        // max records staged
 constexpr int kMaxRows = 48;
 constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
 struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint32_t n, enter, base, flags;
-  uint32_t ws[16];                  // block-scan scratch
-  uint32_t gsp[2][kMaxRows * 3];    // global start of each (region row, tile part)
-  uint4 ev[kEvLds];                 // event queue
-  uint16_t lcs[2][kRegCells + 8];   // LDS start of each region cell (+ total)
-  uint4 ent[2][kCap];  // old grid: {x, z, seq0, side}; new grid: {x, z, slot, seq}
-  uint32_t slot_old[kCap];
+  uint32_t ws[16];              // block-scan scratch
+  uint32_t gsp[kMaxRows * 3];   // global start of each (region row, tile part)
+  uint4 ev[kEvLds];             // event queue
+  uint16_t lcs[kRegCells + 8];  // LDS start of each region cell (+ total)
+  uint4 ra[kCap];
+  uint4 rb[kCap];
 };
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
@@ -338,27 +350,10 @@ __device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, u
 }
 
 struct Mover {
-  uint32_t sm, q, q0, rank;
+  uint32_t slot, q, q0, rank;
   bool valid0, valid1;
   float mx0, mz0, mx1, mz1, D;
 };
-
-__device__ __forceinline__ Mover make_mover(const SweepArgs& a, uint32_t sm, uint32_t q, bool valid1, float mx1,
-                                            float mz1, float D) {
-  Mover m;
-  m.sm = sm;
-  m.q = q;
-  m.q0 = a.old_seq[sm];
-  m.rank = q - a.base;
-  m.valid0 = m.q0 != 0;
-  m.valid1 = valid1;
-  m.mx0 = a.old_x[sm];
-  m.mz0 = a.old_z[sm];
-  m.mx1 = mx1;
-  m.mz1 = mz1;
-  m.D = D;
-  return m;
-}
 
 // The cells a mover must read: rows z0..z1 of the union of its old and new query boxes, and in each
 // row at most two column intervals — the two boxes' intervals (merged when they touch), or, for a
@@ -367,9 +362,9 @@ __device__ __forceinline__ Mover make_mover(const SweepArgs& a, uint32_t sm, uin
 // always visits segment A then segment B (possibly empty), so lanes of a wave that sit in
 // different cell rows still follow the same control flow.
 struct Walk {
-  int z0, z1;          // rows
-  int ax0, ax1, az0, az1;  // box A columns / rows (old box, or the union for a ring walk)
-  int bx0, bx1, bz0, bz1;  // box B (new box); for a ring walk: inner rows bz0..bz1, inner cols bx0..bx1
+  int z0, z1;
+  int ax0, ax1, az0, az1;  // box A (old box, or the union for a ring walk)
+  int bx0, bx1, bz0, bz1;  // box B (new box); for a ring walk: the inner rows / columns
   bool ring;
 };
 
@@ -427,7 +422,7 @@ __device__ __forceinline__ void walk_row(const Walk& w, int r, int& a0, int& a1,
   }
 }
 
-// segf(r, c0, c1) for each non-empty segment, rows relative to the lane's window.
+// segf(r, c0, c1) for each segment (possibly empty), rows relative to the lane's window.
 template <class SegF>
 __device__ __forceinline__ void walk_cells(const Mover& m, const Geom& g, SegF&& segf) {
   const Walk w = make_walk(m, g);
@@ -441,48 +436,68 @@ __device__ __forceinline__ void walk_cells(const Mover& m, const Geom& g, SegF&&
   }
 }
 
-// The per-mover evaluation over the candidates of a cell walk; `cand_old(j)` / `cand_new(j)`
-// read entry j of the old / new grid through the caller's accessor.
-//  (A) old grid: o at its start-of-pass position, skipped if it acted earlier in this pass;
-//      before = in(L, F) over the start-of-pass state, after = in(m_new, o_old).
-//  (B) new grid: only o that acted earlier in this pass (and are present after it);
-//      before = in(o_new, m_old), after = in(m_new, o_new).
-template <class Q, class Rows>
-__device__ __forceinline__ uint32_t sweep_mover(const SweepArgs& a, Q& q, const Mover& m, Rows&& rows) {
+// The pair logic for one candidate record (ra, rb) of the pass's grid, evaluated for mover m.
+//   acted earlier in this pass (opq in [base, q)): o is met at its END position (main record);
+//     before = in(o_new, m_old), after = in(m_new, o_new).
+//   otherwise: o is met at its START position (ghost record, or the main record when the start cell
+//     is the same and o was present at the start); before = in(L, F) over the start-of-pass state
+//     (o's perspective iff o's start seq > m's), after = in(m_new, o_start).
+// Predicates are VALU arithmetic: lo <= p <= hi  <=>  min(p - lo, hi - p) >= 0, exactly (the sign
+// of a binary32 difference of finite values is the sign of the exact difference when subnormals are
+// kept; x - x = +0). A side that does not exist (m absent before / after) is forced to -1 (false).
+struct Judge {
+  float lx0, hx0, lz0, hz0;  // m's old box
+  float lx1, hx1, lz1, hz1;  // m's new box
+  float mx0, mz0, D, sel0, sel1;
+  uint32_t base, rank, q, q0;
+};
+
+__device__ __forceinline__ Judge make_judge(const Mover& m, uint32_t base) {
+  Judge j;
   const float D = m.D;
-  const Bounds b1 = {m.mx1 - D, m.mx1 + D, m.mz1 - D, m.mz1 + D};
-  const Bounds b0 = {m.mx0 - D, m.mx0 + D, m.mz0 - D, m.mz0 + D};
-  const uint32_t rq = m.q - a.base;  // o acted earlier in this pass <=> (seq_o - base) < rq
-  uint32_t local = 0;
-  rows(
-      [&](const uint4 e, uint32_t qo) {  // old grid
-        if (e.z == m.sm || qo - a.base < rq) return;
-        const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
-        const bool before = m.valid0 && ((e.w > m.q0) ? inbox(ox, oz, D, m.mx0, m.mz0) : b0.has(ox, oz));
-        const bool after = m.valid1 && b1.has(ox, oz);
-        if (before != after) emit(a, q, m.rank, local++, m.sm, e.z, after);
-      },
-      [&](const uint4 e) {  // new grid
-        if (!(e.w - a.base < rq)) return;
-        const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
-        const bool before = m.valid0 && inbox(ox, oz, D, m.mx0, m.mz0);
-        const bool after = m.valid1 && b1.has(ox, oz);
-        if (before != after) emit(a, q, m.rank, local++, m.sm, e.z, after);
-      });
-  return local;
+  j.lx0 = m.mx0 - D, j.hx0 = m.mx0 + D, j.lz0 = m.mz0 - D, j.hz0 = m.mz0 + D;
+  j.lx1 = m.mx1 - D, j.hx1 = m.mx1 + D, j.lz1 = m.mz1 - D, j.hz1 = m.mz1 + D;
+  j.mx0 = m.mx0, j.mz0 = m.mz0, j.D = D;
+  j.sel0 = m.valid0 ? 1.0f : -1.0f;
+  j.sel1 = m.valid1 ? 1.0f : -1.0f;
+  j.base = base, j.rank = m.rank, j.q = m.q, j.q0 = m.q0;
+  return j;
+}
+
+__device__ __forceinline__ float margin(float px, float pz, float lx, float hx, float lz, float hz) {
+  return fminf(fminf(px - lx, hx - px), fminf(pz - lz, hz - pz));
+}
+
+// 0: no event; otherwise 1 = LEAVE, 2 = ENTER
+__device__ __forceinline__ int judge(const Judge& J, const uint4 ra, const uint4 rb) {
+  const uint32_t opq = ra.w;
+  const bool ae = (opq - J.base) < J.rank;  // acted earlier in this pass
+  const bool ghost = (ra.z & REC_GHOST) != 0, hasg = (ra.z & REC_HASG) != 0;
+  const uint32_t seq0 = rb.z;
+  const bool valid = (opq != J.q) && (ghost ? !ae : (ae || (!hasg && seq0 != 0)));
+  const float px = ae ? __uint_as_float(ra.x) : __uint_as_float(rb.x);
+  const float pz = ae ? __uint_as_float(ra.y) : __uint_as_float(rb.y);
+  const float D = J.D;
+  const float am = margin(px, pz, J.lx0, J.hx0, J.lz0, J.hz0);          // m's perspective
+  const float ao = margin(J.mx0, J.mz0, px - D, px + D, pz - D, pz + D);  // o's perspective
+  const float bf = fminf(J.sel0, (ae || seq0 > J.q0) ? ao : am);
+  const float af = fminf(J.sel1, margin(px, pz, J.lx1, J.hx1, J.lz1, J.hz1));
+  const bool before = bf >= 0.0f, after = af >= 0.0f;
+  return (valid && before != after) ? (after ? 2 : 1) : 0;
 }
 
 template <class Q>
-__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& q, const Mover& m, const Geom& go,
-                                                 const Geom& gn) {
-  return sweep_mover(a, q, m, [&](auto&& fo, auto&& fn) {
-    walk_cells(m, go, [&](int r, int c0, int c1) {
-      row_entries_global(go, a.og.cs, r, c0, c1, [&](uint32_t j) { fo(a.og.ent[j], a.og.side[j]); });
-    });
-    walk_cells(m, gn, [&](int r, int c0, int c1) {
-      row_entries_global(gn, a.ng.cs, r, c0, c1, [&](uint32_t j) { fn(a.ng.ent[j]); });
+__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& q, const Mover& m, const Geom& g) {
+  const Judge J = make_judge(m, a.base);
+  uint32_t local = 0;
+  walk_cells(m, g, [&](int r, int c0, int c1) {
+    row_entries_global(g, a.g.cs, r, c0, c1, [&](uint32_t j) {
+      const uint4 ra = a.g.ra[j];
+      const int ev = judge(J, ra, a.g.rb[j]);
+      if (ev) emit(a, q, m.rank, local++, m.slot, ra.z & REC_SLOT, ev == 2);
     });
   });
+  return local;
 }
 
 struct Region {
@@ -492,62 +507,25 @@ struct Region {
   }
 };
 
-// LDS walk, written out for the hot loop: one 16-B LDS read per candidate, branch-free predicates,
-// a branch only where an event is raised (rare), two candidates per iteration.
-//  old-grid record {x, z, seq0, side}: skip o if (side - base) <= rank, i.e. o acted earlier in this
-//  pass or o is m itself (m's own old entry carries m's op seq); the slot is read only on emit.
-//  new-grid record {x, z, slot, seq}: o counts only if (seq - base) < rank (acted earlier).
 __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Region& R,
                                               const Geom& g) {
-  const float D = m.D;
-  const Bounds b1 = {m.mx1 - D, m.mx1 + D, m.mz1 - D, m.mz1 + D};
-  const Bounds b0 = {m.mx0 - D, m.mx0 + D, m.mz0 - D, m.mz0 + D};
-  const uint32_t base = a.base, rank = m.rank, q0 = m.q0;
-  const bool v0 = m.valid0, v1 = m.valid1;
-  const float mx0 = m.mx0, mz0 = m.mz0;
+  const Judge J = make_judge(m, a.base);
   uint32_t local = 0;
-  // Predicates in VALU arithmetic: lo <= p <= hi  <=>  min(p - lo, hi - p) >= 0, exactly (the sign
-  // of a binary32 difference of finite values is the sign of the exact difference when subnormals
-  // are kept; x - x = +0). An invalid side is forced to -1 (false).
-  const float sel0 = v0 ? 1.0f : -1.0f, sel1 = v1 ? 1.0f : -1.0f;
-  auto margin = [](float px, float pz, float lx, float hx, float lz, float hz) {
-    return fminf(fminf(px - lx, hx - px), fminf(pz - lz, hz - pz));
-  };
-  auto old_ev = [&](const uint4 c, uint32_t j) {
-    const float ox = __uint_as_float(c.x), oz = __uint_as_float(c.y);
-    const float am = margin(ox, oz, b0.lx, b0.hx, b0.lz, b0.hz);                 // m's perspective
-    const float ao = margin(mx0, mz0, ox - D, ox + D, oz - D, oz + D);           // o's perspective
-    const float bf = fminf(sel0, (c.z > q0) ? ao : am);                          // o acted last?
-    const float af = fminf(sel1, margin(ox, oz, b1.lx, b1.hx, b1.lz, b1.hz));
-    const bool before = bf >= 0.0f, after = af >= 0.0f;
-    if ((c.w - base) > rank && before != after) emit(a, sm, rank, local++, m.sm, sm.slot_old[j], after);
-  };
-  auto new_ev = [&](const uint4 c) {
-    const float ox = __uint_as_float(c.x), oz = __uint_as_float(c.y);
-    const float bf = fminf(sel0, margin(mx0, mz0, ox - D, ox + D, oz - D, oz + D));
-    const float af = fminf(sel1, margin(ox, oz, b1.lx, b1.hx, b1.lz, b1.hz));
-    const bool before = bf >= 0.0f, after = af >= 0.0f;
-    if ((c.w - base) < rank && before != after) emit(a, sm, rank, local++, m.sm, c.z, after);
-  };
   walk_cells(m, g, [&](int r, int c0, int c1) {
-    if (c0 > c1) return;
     const int b = (r - R.zr0) * R.ncols - R.xr0;
-    uint32_t j = sm.lcs[0][b + c0];
-    const uint32_t e = sm.lcs[0][b + c1 + 1];
-    uint32_t k = sm.lcs[1][b + c0];
-    const uint32_t f = sm.lcs[1][b + c1 + 1];
-    for (; j + 1 < e; j += 2) {
-      const uint4 c0v = sm.ent[0][j], c1v = sm.ent[0][j + 1];
-      old_ev(c0v, j);
-      old_ev(c1v, j + 1);
+    uint32_t j = sm.lcs[b + c0];
+    const uint32_t e = (c0 <= c1) ? (uint32_t)sm.lcs[b + c1 + 1] : j;
+    for (; j + 1 < e; j += 2) {  // two candidates per iteration: both LDS reads in flight
+      const uint4 ra0 = sm.ra[j], rb0 = sm.rb[j], ra1 = sm.ra[j + 1], rb1 = sm.rb[j + 1];
+      const int e0 = judge(J, ra0, rb0), e1 = judge(J, ra1, rb1);
+      if (e0) emit(a, sm, m.rank, local++, m.slot, ra0.z & REC_SLOT, e0 == 2);
+      if (e1) emit(a, sm, m.rank, local++, m.slot, ra1.z & REC_SLOT, e1 == 2);
     }
-    if (j < e) old_ev(sm.ent[0][j], j);
-    for (; k + 1 < f; k += 2) {
-      const uint4 c0v = sm.ent[1][k], c1v = sm.ent[1][k + 1];
-      new_ev(c0v);
-      new_ev(c1v);
+    if (j < e) {
+      const uint4 ra0 = sm.ra[j];
+      const int e0 = judge(J, ra0, sm.rb[j]);
+      if (e0) emit(a, sm, m.rank, local++, m.slot, ra0.z & REC_SLOT, e0 == 2);
     }
-    if (k < f) new_ev(sm.ent[1][k]);
   });
   return local;
 }
@@ -573,13 +551,11 @@ __device__ __forceinline__ uint32_t block_excl_scan_big(uint32_t v, uint32_t* ws
 
 constexpr int kCellsPerThread = (kRegCells + kSweepBlock - 1) / kSweepBlock;
 
-// Stage the region of grid `gi` (0 = old, 1 = new): per-cell counts from the cell starts, a block
-// scan into the LDS cell-start table, then a flat copy (thread per entry: region row by binary
-// search, tile part by two compares, one 16-B load). Returns the staged count (block-uniform); a
-// count > kCap means "does not fit" and nothing was copied.
-__device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, const Region& R, SweepSmem& sm, int gi) {
-  uint16_t* lcs = sm.lcs[gi];
-  uint32_t* gsp = sm.gsp[gi];
+// Stage the region: per-cell counts from the cell starts, a block scan into the LDS cell-start
+// table, then a flat copy (thread per record: region row by binary search, tile part by two
+// compares, two 16-B loads). Returns the staged count (block-uniform); a count > kCap means "does
+// not fit" and nothing was copied.
+__device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, const Region& R, SweepSmem& sm) {
   const int pt0 = R.xr0 >> kTileShift;  // tile column of the region's first column
   uint32_t n[kCellsPerThread];
   uint32_t sum = 0;
@@ -593,7 +569,7 @@ __device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, con
       const uint32_t key = cell_key(g, col, R.zr0 + rr);
       const uint32_t s0 = gv.cs[key];
       n[k] = gv.cs[key + 1] - s0;
-      if (col == R.xr0 || (col & (kTile - 1)) == 0) gsp[rr * 3 + ((col >> kTileShift) - pt0)] = s0;
+      if (col == R.xr0 || (col & (kTile - 1)) == 0) sm.gsp[rr * 3 + ((col >> kTileShift) - pt0)] = s0;
     }
     sum += n[k];
   }
@@ -602,44 +578,72 @@ __device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, con
   if (total > (uint32_t)kCap) return total;
 #pragma unroll
   for (int k = 0; k < kCellsPerThread; ++k) {
-    if (c0 + k < R.ncells) lcs[c0 + k] = (uint16_t)pre;
+    if (c0 + k < R.ncells) sm.lcs[c0 + k] = (uint16_t)pre;
     pre += n[k];
   }
-  if (threadIdx.x == 0) lcs[R.ncells] = (uint16_t)total;
+  if (threadIdx.x == 0) sm.lcs[R.ncells] = (uint16_t)total;
   __syncthreads();
+  const int p1c = ((pt0 + 1) << kTileShift) - R.xr0, p2c = p1c + kTile;
   for (uint32_t i = threadIdx.x; i < total; i += kSweepBlock) {
     int lo = 0, hi = R.nrows;  // find rr with lcs[rr * ncols] <= i < lcs[(rr + 1) * ncols]
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
-      if (lcs[mid * R.ncols] <= i) lo = mid;
+      if (sm.lcs[mid * R.ncols] <= i) lo = mid;
       else hi = mid;
     }
     const int rb = lo * R.ncols;
-    // tile parts of the row start at region columns 0, then each multiple of kTile
-    const int p1c = ((pt0 + 1) << kTileShift) - R.xr0, p2c = p1c + kTile;
+    // tile parts of the row start at region column 0, then at each multiple of kTile
     int p = 0, pc = 0;
-    if (p1c < R.ncols && lcs[rb + p1c] <= i) {
+    if (p1c < R.ncols && sm.lcs[rb + p1c] <= i) {
       p = 1;
       pc = p1c;
-      if (p2c < R.ncols && lcs[rb + p2c] <= i) {
+      if (p2c < R.ncols && sm.lcs[rb + p2c] <= i) {
         p = 2;
         pc = p2c;
       }
     }
-    const uint32_t src = gsp[lo * 3 + p] + (i - lcs[rb + pc]);
-    const uint4 e = gv.ent[src];
-    if (gi == 0) {
-      sm.ent[0][i] = make_uint4(e.x, e.y, e.w, gv.side[src]);
-      sm.slot_old[i] = e.z;
-    } else {
-      sm.ent[1][i] = e;
-    }
+    const uint32_t src = sm.gsp[lo * 3 + p] + (i - sm.lcs[rb + pc]);
+    sm.ra[i] = gv.ra[src];
+    sm.rb[i] = gv.rb[src];
   }
   return total;
 }
 
-__device__ __forceinline__ bool same_geom(const Geom& a, const Geom& b) {
-  return a.x0 == b.x0 && a.z0 == b.z0 && a.inv_c == b.inv_c && a.ncx == b.ncx && a.ncz == b.ncz && a.base == b.base;
+__device__ __forceinline__ Mover mover_of(const uint4 ra, const uint4 rb, uint32_t base, float D) {
+  Mover m;
+  m.slot = ra.z & REC_SLOT;
+  m.q = ra.w;
+  m.q0 = rb.z;
+  m.rank = m.q - base;
+  m.valid0 = m.q0 != 0;
+  m.valid1 = true;
+  m.mx0 = __uint_as_float(rb.x);
+  m.mz0 = __uint_as_float(rb.y);
+  m.mx1 = __uint_as_float(ra.x);
+  m.mz1 = __uint_as_float(ra.y);
+  m.D = D;
+  return m;
+}
+
+// a Leave op's mover, from the slot's start-of-pass state recorded by k_apply
+__device__ __forceinline__ Mover leaver(const SweepArgs& a, uint32_t i, float D) {
+  Mover m;
+  m.slot = a.op_slot[i];
+  m.q = a.base + i;
+  m.q0 = a.old_seq[m.slot];
+  m.rank = i;
+  m.valid0 = m.q0 != 0;
+  m.valid1 = false;
+  m.mx0 = a.old_x[m.slot];
+  m.mz0 = a.old_z[m.slot];
+  m.mx1 = m.mx0;
+  m.mz1 = m.mz0;
+  m.D = D;
+  return m;
+}
+
+__device__ __forceinline__ bool is_mover(const uint4 ra, uint32_t base, uint32_t n_ops) {
+  return !(ra.z & REC_GHOST) && (ra.w - base) < n_ops;
 }
 
 __global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
@@ -651,48 +655,46 @@ __global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
   }
   if (blockIdx.x < a.ntiles) {
     const uint32_t t = blockIdx.x;
-    const uint32_t e0 = a.ng.cs[t << kTileCellShift], e1 = a.ng.cs[(t + 1) << kTileCellShift];
+    const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
     // does the tile hold a mover of this pass? (block-uniform exit otherwise)
     bool mine = false;
-    for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = a.ng.ent[j].w >= a.base;
+    for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_mover(a.g.ra[j], a.base, a.n_ops);
     if (!__syncthreads_or(mine)) return;
-    const uint32_t sp = a.ng.tile_space[t];
-    const Geom gn = a.ng.geom[sp];
-    const Geom go = a.og.geom[sp];
-    bool lds = a.use_lds && gn.reach > 0 && same_geom(go, gn);
+    const uint32_t sp = a.g.tile_space[t];
+    const Geom g = a.g.geom[sp];
+    bool lds = a.use_lds && g.reach > 0;
     Region R;
     if (lds) {
-      const uint32_t tl = t - gn.tile_base;
-      const int tz = (int)(tl / (uint32_t)gn.ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)gn.ntx);
-      R.zr0 = max(0, tz * kTile - gn.reach);
-      R.zr1 = min(gn.ncz - 1, tz * kTile + kTile - 1 + gn.reach);
-      R.xr0 = max(0, tx * kTile - gn.reach);
-      R.xr1 = min(gn.ncx - 1, tx * kTile + kTile - 1 + gn.reach);
+      const uint32_t tl = t - g.tile_base;
+      const int tz = (int)(tl / (uint32_t)g.ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)g.ntx);
+      R.zr0 = max(0, tz * kTile - g.reach);
+      R.zr1 = min(g.ncz - 1, tz * kTile + kTile - 1 + g.reach);
+      R.xr0 = max(0, tx * kTile - g.reach);
+      R.xr1 = min(g.ncx - 1, tx * kTile + kTile - 1 + g.reach);
       R.ncols = R.xr1 - R.xr0 + 1;
       R.nrows = R.zr1 - R.zr0 + 1;
       R.ncells = R.nrows * R.ncols;
-      lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= kTile + 2 * kTile;
+      lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= 3 * kTile;
     }
     if (lds) {
-      const uint32_t n_old = stage(a.og, go, R, sm, 0);
-      __syncthreads();
-      const uint32_t n_new = stage(a.ng, gn, R, sm, 1);
-      lds = n_old <= (uint32_t)kCap && n_new <= (uint32_t)kCap;  // block-uniform
+      lds = stage(a.g, g, R, sm) <= (uint32_t)kCap;  // block-uniform
       __syncthreads();
     }
     if (a.use_lds == 2) {  // ablation (timing only): staging without the candidate walk
-      for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock)
-        if (a.ng.ent[j].w >= a.base) a.rank_cnt[a.ng.ent[j].w - a.base] = 0;
+      for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
+        const uint4 ra = a.g.ra[j];
+        if (is_mover(ra, a.base, a.n_ops)) a.rank_cnt[ra.w - a.base] = 0;
+      }
     } else {
       for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
-        const uint4 e = a.ng.ent[j];
-        if (e.w < a.base) continue;  // did not act in this pass
-        const Mover m = make_mover(a, e.z, e.w, true, __uint_as_float(e.x), __uint_as_float(e.y), gn.D);
+        const uint4 ra = a.g.ra[j];
+        if (!is_mover(ra, a.base, a.n_ops)) continue;
+        const Mover m = mover_of(ra, a.g.rb[j], a.base, g.D);
         uint32_t cnt;
-        if (lds && R.holds(qbox(gn, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(gn, m.mx0, m.mz0))))
-          cnt = sweep_lds(a, sm, m, R, gn);
+        if (lds && R.holds(qbox(g, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(g, m.mx0, m.mz0))))
+          cnt = sweep_lds(a, sm, m, R, g);
         else
-          cnt = sweep_global(a, sm, m, go, gn);
+          cnt = sweep_global(a, sm, m, g);
         a.rank_cnt[m.rank] = cnt;
       }
     }
@@ -701,11 +703,9 @@ __global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
     const uint32_t t = (blockIdx.x - a.ntiles) * kSweepBlock + threadIdx.x;
     if (t < a.n_leaves) {
       const uint32_t i = a.leave_ops[t];
-      const uint32_t smv = a.op_slot[i];
-      const uint32_t sp = a.space_of[smv];
-      const Geom go = a.og.geom[sp], gn = a.ng.geom[sp];
-      const Mover m = make_mover(a, smv, a.base + i, false, 0.0f, 0.0f, go.D);
-      a.rank_cnt[i] = sweep_global(a, sm, m, go, gn);
+      const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
+      const Mover m = leaver(a, i, g.D);
+      a.rank_cnt[i] = sweep_global(a, sm, m, g);
     }
   }
   // flush the block's events with one global atomic
@@ -727,8 +727,8 @@ void sweep_init() {
                             (int)sizeof(SweepSmem));
 }
 
-// Flat variant (use_lds == 0): one thread per new-grid entry in key (tile-major) order, 256-thread
-// blocks and only the event queue in LDS, i.e. full occupancy; candidates come through L1/L2.
+// Flat variant (use_lds == 0): one thread per record in key (tile-major) order, 256-thread blocks
+// and only the event queue in LDS, i.e. full occupancy; candidates come through L1/L2.
 struct FlatQ {
   uint32_t n, enter, base, flags;
   uint4 ev[kEvLds];
@@ -742,21 +742,20 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
   }
   __syncthreads();
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  if (t < a.n_new) {
-    const uint4 e = a.ng.ent[t];
-    if (e.w >= a.base) {
-      const uint32_t sp = a.space_of[e.z];
-      const Geom go = a.og.geom[sp], gn = a.ng.geom[sp];
-      const Mover m = make_mover(a, e.z, e.w, true, __uint_as_float(e.x), __uint_as_float(e.y), gn.D);
-      a.rank_cnt[m.rank] = sweep_global(a, q, m, go, gn);
+  const uint32_t n_rec = a.g.cs[a.ncells];
+  if (t < n_rec) {
+    const uint4 ra = a.g.ra[t];
+    if (is_mover(ra, a.base, a.n_ops)) {
+      const uint32_t slot = ra.z & REC_SLOT;
+      const Geom g = a.g.geom[a.space_of[slot]];
+      const Mover m = mover_of(ra, a.g.rb[t], a.base, g.D);
+      a.rank_cnt[m.rank] = sweep_global(a, q, m, g);
     }
-  } else if (t < a.n_new + a.n_leaves) {
-    const uint32_t i = a.leave_ops[t - a.n_new];
-    const uint32_t smv = a.op_slot[i];
-    const uint32_t sp = a.space_of[smv];
-    const Geom go = a.og.geom[sp], gn = a.ng.geom[sp];
-    const Mover m = make_mover(a, smv, a.base + i, false, 0.0f, 0.0f, go.D);
-    a.rank_cnt[i] = sweep_global(a, q, m, go, gn);
+  } else if (t >= a.n_rec && t < a.n_rec + a.n_leaves) {
+    const uint32_t i = a.leave_ops[t - a.n_rec];
+    const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
+    const Mover m = leaver(a, i, g.D);
+    a.rank_cnt[i] = sweep_global(a, q, m, g);
   }
   __syncthreads();
   const uint32_t nq = min(q.n, (uint32_t)kEvLds);
@@ -773,7 +772,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
 
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
   if (a.use_lds == 0) {
-    const uint32_t n = a.n_new + a.n_leaves;
+    const uint32_t n = a.n_rec + a.n_leaves;
     if (n) hipLaunchKernelGGL(k_sweep_flat, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
     return;
   }
@@ -782,7 +781,6 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_sweep, dim3(nb), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
 }
 
-// ---------------------------------------------------------------------------------------------
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each
 // rank's slice sorted by other|kind (LEAVE = bit31 clear sorts first). Every step checks on the
 // device that the sweep's events fit the buffers (else it writes nothing; the host grows them and
@@ -846,8 +844,8 @@ void launch_order(const OrderArgs& o, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Relation export: row s = {o : N(s,o)} = {o : in(L, F)}, L = later actor. Count pass (row_ptr null)
-// then fill pass; rows sorted afterwards.
+// Relation export: row s = {o : N(s,o)} = {o : in(L, F)}, L = later actor, over the END-of-pass
+// state (main records only). Count pass (row_ptr null) then fill pass; rows sorted afterwards.
 __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
   const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
   if (s >= a.cap) return;
@@ -859,20 +857,23 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
   const Geom g = a.g.geom[a.space_of[s]];
   const float sx = a.pos_x[s], sz = a.pos_z[s];
   const float D = g.D;
-  const Bounds bs = {sx - D, sx + D, sz - D, sz + D};
   const CellBox B = qbox(g, sx, sz);
   uint32_t n = 0;
   uint32_t w = a.row_ptr ? a.row_ptr[s] : 0u;
-  for_each_entry(g, a.g.cs, true, B, false, B, [&](uint32_t j) {
-    const uint4 e = a.g.ent[j];
-    if (e.z == s) return;
-    const float ox = __uint_as_float(e.x), oz = __uint_as_float(e.y);
-    const bool in = (e.w > qs) ? inbox(ox, oz, D, sx, sz) : bs.has(ox, oz);
-    if (in) {
-      if (a.row_ptr) a.cols[w++] = e.z;
-      ++n;
-    }
-  });
+  for (int r = B.z0; r <= B.z1; ++r) {
+    row_entries_global(g, a.g.cs, r, B.x0, B.x1, [&](uint32_t j) {
+      const uint4 ra = a.g.ra[j];
+      const uint32_t o = ra.z & REC_SLOT;
+      if ((ra.z & REC_GHOST) || o == s) return;
+      const uint32_t qo = a.g.rb[j].w;  // end-of-pass seq
+      const float ox = __uint_as_float(ra.x), oz = __uint_as_float(ra.y);
+      const bool in = (qo > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz);
+      if (in) {
+        if (a.row_ptr) a.cols[w++] = o;
+        ++n;
+      }
+    });
+  }
   if (!a.row_ptr) a.row_cnt[s] = n;
 }
 

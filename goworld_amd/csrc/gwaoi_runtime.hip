@@ -83,11 +83,10 @@ struct SpaceHost {
   float gx0, gz0, gx1, gz1;
 };
 
-struct Grid {
-  uint4* ent = nullptr;
+struct Grid {  // one pass's cell-sorted records (two buffers, alternating between passes)
+  uint4* ra = nullptr;
+  uint4* rb = nullptr;
   uint32_t* cs = nullptr;
-  uint32_t* side = nullptr;
-  uint32_t* gidx = nullptr;
   gw::Geom* d_geom = nullptr;
   uint32_t* d_tile_space = nullptr;  // tile -> space
   std::vector<gw::Geom> h_geom;  // what d_geom holds
@@ -134,7 +133,7 @@ struct gwaoi_mgr {
 
   // ---- device state ----
   float *pos_x = nullptr, *pos_z = nullptr, *old_x = nullptr, *old_z = nullptr;
-  uint32_t *seq = nullptr, *space_of = nullptr, *old_seq = nullptr;
+  uint32_t *seq = nullptr, *space_of = nullptr, *old_seq = nullptr, *opq = nullptr;
   uint32_t *key_of = nullptr, *local_of = nullptr;
   uint32_t *d_op_slot = nullptr, *d_op_space = nullptr, *d_leaves = nullptr;
   float *d_op_x = nullptr, *d_op_z = nullptr;
@@ -313,7 +312,9 @@ int upload_geom(gwaoi_mgr* m, Grid& g, const std::vector<gw::Geom>& geo) {
 }
 
 // Build grid `gi` from the per-slot state (pos, seq, space_of).
-int build_grid(gwaoi_mgr* m, int gi) {
+// Build grid `gi` for the pass whose ops have seqs [base, base + n_ops) (n_ops = 0: the current
+// state only, no ghosts).
+int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops) {
   Grid& g = m->grid[gi];
   if (g.cs_zeroed < g.ncells + 1) HIPCHK(hipMemsetAsync(g.cs, 0, (size_t)(g.ncells + 1) * sizeof(uint32_t), m->stream));
   g.cs_zeroed = 0;
@@ -322,13 +323,19 @@ int build_grid(gwaoi_mgr* m, int gi) {
   b.pos_z = m->pos_z;
   b.seq = m->seq;
   b.space_of = m->space_of;
+  b.old_x = m->old_x;
+  b.old_z = m->old_z;
+  b.old_seq = m->old_seq;
+  b.opq = m->opq;
+  b.base = base;
+  b.n_ops = n_ops;
   b.geom = g.d_geom;
   b.cap = m->cap;
   b.key_of = m->key_of;
   b.local_of = m->local_of;
   b.cs = g.cs;
-  b.ent = g.ent;
-  b.gidx = g.gidx;
+  b.ra = g.ra;
+  b.rb = g.rb;
   gw::launch_bin_count(b, m->stream);
   gw::launch_scan(g.cs, g.ncells + 1, m->part, m->stream);
   gw::launch_bin_scatter(b, m->stream);
@@ -348,9 +355,8 @@ int renormalise(gwaoi_mgr* m) {
   std::sort(v.begin(), v.end());
   for (size_t i = 0; i < v.size(); ++i) q[v[i].second] = (uint32_t)i + 1;
   HIPCHK(hipMemcpy(m->seq, q.data(), m->cap * sizeof(uint32_t), hipMemcpyHostToDevice));
-  for (int gi = 0; gi < 2; ++gi)
-    HIPCHK(hipMemsetAsync(m->grid[gi].side, 0, (size_t)m->cap * sizeof(uint32_t), m->stream));
-  RCHK(build_grid(m, m->cur));
+  HIPCHK(hipMemsetAsync(m->opq, 0, (size_t)m->cap * sizeof(uint32_t), m->stream));  // stale op seqs
+  RCHK(build_grid(m, m->cur, 0, 0));
   m->next_seq = (uint32_t)v.size() + 1;
   HIPCHK(hipStreamSynchronize(m->stream));
   return GWAOI_OK;
@@ -414,18 +420,18 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   a.old_x = m->old_x;
   a.old_z = m->old_z;
   a.old_seq = m->old_seq;
-  a.old_side = m->grid[og].side;
-  a.old_gidx = m->grid[og].gidx;
+  a.opq = m->opq;
   a.ctr = m->ctr;
   a.rank_tail = m->rank_cnt + n_ops;
   gw::launch_apply(a, st);
   HIPCHK(hipGetLastError());
   if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
 
-  RCHK(build_grid(m, ng));
+  RCHK(build_grid(m, ng, base, n_ops));
   if (m->timing) HIPCHK(hipEventRecord(m->tev[2], st));
 
   const uint32_t n_new = dev ? m->n_present_dev : m->n_present;
+  const uint32_t n_start = m->n_present_dev;  // present at the start of the pass
   const uint64_t keep = m->tick_events;
   // events: expected count is small; grow and re-run the (pure) sweep on overflow
   for (int attempt = 0;; ++attempt) {
@@ -435,16 +441,18 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
     }
     gw::SweepArgs s;
-    s.og = {m->grid[og].ent, m->grid[og].cs, m->grid[og].side, m->grid[og].d_geom, m->grid[og].d_tile_space};
-    s.ng = {m->grid[ng].ent, m->grid[ng].cs, m->grid[ng].side, m->grid[ng].d_geom, m->grid[ng].d_tile_space};
-    s.ntiles = m->grid[ng].ntiles;
+    const Grid& G = m->grid[ng];
+    s.g = {G.ra, G.rb, G.cs, G.d_geom, G.d_tile_space};
+    s.ntiles = G.ntiles;
+    s.ncells = G.ncells;
+    s.n_rec = n_start + n_new;  // upper bound on records (main + ghost)
     s.use_lds = m->sweep_lds;
     s.old_x = m->old_x;
     s.old_z = m->old_z;
     s.old_seq = m->old_seq;
     s.space_of = m->space_of;
     s.base = base;
-    s.n_new = n_new;
+    s.n_ops = n_ops;
     s.op_slot = a.op_slot;
     s.leave_ops = m->d_leaves;
     s.n_leaves = dev ? 0 : m->n_leaves;
@@ -584,14 +592,14 @@ void stage(gwaoi_mgr* m, uint32_t slot, uint8_t kind, float x, float z, uint32_t
 void free_all(gwaoi_mgr* m) {
   hipSetDevice(m->device);
   if (m->stream) hipStreamSynchronize(m->stream);
-  void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq,
+  void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->ctr_buf, m->ev_tmp, m->ev_out};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
-    void* gp[] = {g.ent, g.cs, g.side, g.gidx, g.d_geom, g.d_tile_space};
+    void* gp[] = {g.ra, g.rb, g.cs, g.d_geom, g.d_tile_space};
     for (void* p : gp)
       if (p) hipFree(p);
   }
@@ -661,8 +669,9 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->seq, C));
   chk(dalloc(&m->space_of, C));
   chk(dalloc(&m->old_seq, C));
-  chk(dalloc(&m->key_of, C));
-  chk(dalloc(&m->local_of, C));
+  chk(dalloc(&m->opq, C));
+  chk(dalloc(&m->key_of, 2 * C));
+  chk(dalloc(&m->local_of, 2 * C));
   chk(dalloc(&m->d_op_slot, C));
   chk(dalloc(&m->d_op_space, C));
   chk(dalloc(&m->d_leaves, C));
@@ -683,10 +692,9 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(halloc(&m->h_leaves, C));
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
-    chk(dalloc(&g.ent, C));
+    chk(dalloc(&g.ra, 2 * C));
+    chk(dalloc(&g.rb, 2 * C));
     chk(dalloc(&g.cs, (size_t)m->max_cells + 1));
-    chk(dalloc(&g.side, C));
-    chk(dalloc(&g.gidx, C));
     chk(dalloc(&g.d_geom, nspaces));
     chk(dalloc(&g.d_tile_space, (size_t)m->max_cells / gw::kTileCells + 1));
   }
@@ -711,12 +719,11 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     };
     z(m->ctr_buf, 2 * gw::CTR_N * 4);
     z(m->pos_x, C * 4);
+    z(m->opq, C * 4);
     z(m->pos_z, C * 4);
     z(m->seq, C * 4);
     z(m->space_of, C * 4);
     for (int gi = 0; gi < 2; ++gi) {
-      z(m->grid[gi].side, C * 4);
-      z(m->grid[gi].gidx, C * 4);
     }
     std::vector<gw::Geom> geo;
     compute_geometry(m, geo);
@@ -918,7 +925,7 @@ int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint6
   uint32_t* d_rp = nullptr;
   RCHK(dalloc(&d_rp, (size_t)m->cap + 1));
   gw::RelArgs a;
-  a.g = {g.ent, g.cs, g.side, g.d_geom, g.d_tile_space};
+  a.g = {g.ra, g.rb, g.cs, g.d_geom, g.d_tile_space};
   a.pos_x = m->pos_x;
   a.pos_z = m->pos_z;
   a.seq = m->seq;
