@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cells-per-dist", type=float, default=None)
     ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
+    ap.add_argument("--stamps", default=None, help="diagnostic GW_STAMPS build: dump the last sweep's per-block "
+                                                   "phase timestamps to this .npy file")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -201,6 +203,16 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     log(f"[rank {rank}] timed {K} ticks in {elapsed:.3f}s")
+
+    if rank == 0:
+        import ctypes
+        occ, ldsb = ctypes.c_int(0), ctypes.c_int(0)
+        if L_.gwaoi_debug_sweep_occupancy(dev, ctypes.byref(occ), ctypes.byref(ldsb)) == 0:
+            log(f"[rank 0] sweep: {occ.value} resident blocks per CU, {ldsb.value} B LDS per block")
+    if args.stamps and rank == 0:
+        buf = np.zeros(8 * 16384, dtype=np.uint64)
+        _lib.check(L_.gwaoi_debug_read_stamps(buf.ctypes.data, buf.nbytes))
+        np.save(args.stamps, buf.reshape(-1, 8))
 
     # ---- host-delivered latency (PCIe-inclusive; reported, never `value`) ----
     lat_host = []

@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(HERE, "libgwaoi.so")
+# GWAOI_LIB selects another build of the same library (A/B experiments: scripts/variants.py)
+SO_PATH = os.environ.get("GWAOI_LIB") or os.path.join(HERE, "libgwaoi.so")
 
 GWAOI_OK = 0
 GWAOI_ERR_INVALID = -1
@@ -32,7 +33,8 @@ ABI_SYMBOLS = (
 TOOL_SYMBOLS = (
     "gwaoi_device_count", "gwaoi_dev_malloc", "gwaoi_dev_free", "gwaoi_dev_htod", "gwaoi_dev_dtoh",
     "gwaoi_dev_sync", "gwaoi_wl_init", "gwaoi_wl_step", "gwaoi_wl_iota", "gwaoi_debug_set_next_seq",
-    "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_sweep_lds",
+    "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_sweep_lds", "gwaoi_debug_read_stamps",
+    "gwaoi_debug_sweep_occupancy",
 )
 
 
@@ -127,6 +129,9 @@ def load(path: str = SO_PATH):
         "gwaoi_debug_set_next_seq": ([vp, u32], ctypes.c_int),
         "gwaoi_debug_set_cells_per_dist": ([vp, f32], ctypes.c_int),
         "gwaoi_debug_set_sweep_lds": ([vp, ctypes.c_int], ctypes.c_int),
+        "gwaoi_debug_read_stamps": ([vp, ctypes.c_size_t], ctypes.c_int),
+        "gwaoi_debug_sweep_occupancy": ([ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
+                                        ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

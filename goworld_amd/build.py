@@ -36,22 +36,27 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    """Compile the library to `out`; `defines` (e.g. ["GW_SWEEP_BLOCK=512"]) builds an A/B variant."""
+    if not force and out == OUT and not _stale():
         return OUT
     cmd = [
         hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
         "-ffp-contract=off", "-fno-fast-math", "-fno-gpu-flush-denormals-to-zero",
+        # LDS event-queue atomics are one ds_add_rtn each; the wave-reduction rewrite the atomic
+        # optimizer wraps around every call costs more than it saves at ~1 event per 100 candidates
+        "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
         "-Wall", "-Wno-unused-result", "-Wno-unused-value",
         f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
+        *[f"-D{d}" for d in defines],
         *[os.path.join(CSRC, f) for f in SOURCES],
-        "-o", OUT + ".tmp",
+        "-o", out + ".tmp",
     ]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -24,6 +24,12 @@ constexpr int kTileShift = 5;
 constexpr int kTile = 1 << kTileShift;       // 32
 constexpr int kTileCellShift = 2 * kTileShift;
 constexpr int kTileCells = kTile * kTile;    // 1024
+// The sweep stages a tile plus a halo of `reach` cells in LDS; the region may hold at most this many
+// cells (a Space whose (kTile + 2 reach)^2 exceeds it takes the global-memory sweep path).
+#ifndef GW_REG_CELLS
+#define GW_REG_CELLS 2304
+#endif
+constexpr int kSweepRegCells = GW_REG_CELLS;  // 48 x 48
 
 // Cell geometry of one Space inside one grid snapshot.
 struct Geom {
@@ -139,6 +145,8 @@ uint32_t scan_part_words(uint32_t n);
 void launch_sweep(const SweepArgs& a, hipStream_t st);
 size_t sweep_lds_bytes();
 void sweep_init();  // once per process (dynamic LDS limit of the sweep)
+int read_stamps(void* host, size_t bytes);
+int sweep_occupancy(int* blocks);  // resident sweep blocks per CU (HIP occupancy API)  // GW_STAMPS diagnostic builds only (else -1)
 // Event ordering runs without a host round trip: each step checks on the device that the sweep's
 // event count fit both buffers (else it does nothing and the host re-runs after growing them).
 struct EvGuard {

@@ -299,27 +299,46 @@ void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Sweep. One 512-thread block per tile of the pass's grid (kTile x kTile cells); the block loops
-// over the tile's movers, one thread per mover. The block first stages every record of the tile
-// plus a halo of `reach` cells into LDS (both record halves and a cell start table), laid out row by
-// row so that any row interval of the region is one contiguous LDS range; each mover then walks its
-// candidates in LDS. Movers whose query boxes leave the region (teleports), tiles whose region does
-// not fit, and Leave ops take the global-memory path; both paths evaluate the same predicates.
+// Sweep. One block per tile of the pass's grid (kTile x kTile cells, ~520 entities at config-2
+// density); the block loops over the tile's movers, one thread per mover. The block first stages every
+// record of the tile plus a halo of `reach` cells into LDS (both record halves), with two cell-start
+// tables over the staged region: row-major (the records' own order, so a row interval of cells is one
+// contiguous LDS range) and column-major (through an index array, so a column interval of cells is one
+// contiguous range too). Each mover then walks its candidates in LDS. Movers whose query boxes leave
+// the region (teleports), tiles whose region does not fit, and Leave ops take the global-memory path;
+// every path evaluates the same predicates.
 //
 // Ring walk: for a Moved op, a candidate strictly inside BOTH the old and the new box (shrunk by a
 // margin far above float32 rounding) is inside from every perspective before and after, so it
 // cannot raise an event. Cells whose every point is that deep (cell index strictly between the
 // cells of the shrunken bounds; cellc is monotone, clamping included) are skipped: only the ring of
-// border cells is read. Enter and Leave ops walk their whole box.
+// border cells is read. For an ordinary move the ring is 1-2 full rows at the top and bottom of the
+// union box (row-major segments) and 1-2 columns left and right over the rows between them
+// (column-major segments): at most 8 contiguous LDS ranges, walked as ONE flat candidate stream per
+// lane, so the lanes of a wave stay converged for max-over-lanes(candidates) iterations instead of a
+// per-row loop whose trip count is the max over lanes row by row. Enter and Leave ops, and moves
+// whose ring is wider, walk the box row by row.
 //
 // Events are rare (~0.3 per mover per tick), but one global counter hit by every event serialises
 // at the memory side, so each block stages its events in LDS and reserves its output range with ONE
 // global atomic; a mover's events are numbered in a register (one thread per mover) and its count is
 // stored once, without atomics.
-constexpr int kSweepBlock = 512;
-constexpr int kEvLds = 256;       // events staged per block before spilling to global atomics
-constexpr int kRegCells = 2304;   // max cells of a staged region (48 x 48)
-constexpr int kCap = 1280;        // max records staged
+#ifndef GW_SWEEP_BLOCK
+#define GW_SWEEP_BLOCK 576
+#endif
+#ifndef GW_SWEEP_WAVES_PER_EU
+#define GW_SWEEP_WAVES_PER_EU 5
+#endif
+constexpr int kSweepBlock = GW_SWEEP_BLOCK;  // 9 waves: a config-2 tile holds ~520 movers (one round, rarely two)
+#ifndef GW_EV_LDS
+#define GW_EV_LDS 192
+#endif
+constexpr int kEvLds = GW_EV_LDS;      // events staged per block before spilling to global atomics
+constexpr int kRegCells = kSweepRegCells;  // max cells of a staged region (48 x 48)
+#ifndef GW_CAP
+#define GW_CAP 1200
+#endif
+constexpr int kCap = GW_CAP;  // max records staged (config 2: ~1030 +- 32 in a 44 x 44 region)
 constexpr int kMaxRows = 48;
 constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
@@ -328,16 +347,24 @@ struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint32_t ws[16];              // block-scan scratch
   uint32_t gsp[kMaxRows * 3];   // global start of each (region row, tile part)
   uint4 ev[kEvLds];             // event queue
-  uint16_t lcs[kRegCells + 8];  // LDS start of each region cell (+ total)
-  uint4 ra[kCap];
-  uint4 rb[kCap];
+  uint16_t lcs[kRegCells + 8];  // row-major: LDS start of each region cell (+ total)
+  uint16_t ccs[kRegCells + 8];  // column-major: start in cidx of each region cell (+ total)
+  uint16_t cidx[kCap];          // column-major order of the staged records (LDS record indices)
+  uint4 rp[kCap];      // staged record, LDS form: {x_start, z_start, x_end, z_end} (float bits)
+  uint4 rm[kCap];      // {r, lo, span, seq_start}: op rank (~0u: no op) and the validity window
+  uint32_t rslot[kCap];  // slot (read only when an event is emitted)
 };
+// two blocks per CU (160 KiB of LDS)
+static_assert(sizeof(SweepSmem) <= 163840 / 2, "sweep LDS budget: 2 blocks per CU");
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
 
+// Queue one event in the block's LDS queue (one LDS atomic; the file is built without the atomic
+// optimizer, so this is a single ds_add_rtn rather than a wave reduction around every call). Enter
+// events are counted in a register (`nent`) and added to the block total once per thread.
 template <class Q>
 __device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, uint32_t local, uint32_t mover,
-                                     uint32_t other, bool enter) {
+                                     uint32_t other, bool enter, uint32_t& nent) {
   const uint4 rec = make_uint4(rank, local, mover, other | (enter ? 0x80000000u : 0u));
   const uint32_t li = atomicAdd(&sm.n, 1u);
   if (li < (uint32_t)kEvLds) {
@@ -346,7 +373,7 @@ __device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, u
     const uint32_t gi = atomicAdd(&a.ctr[CTR_EVENTS], 1u);
     if (gi < a.ev_cap) a.ev_tmp[gi] = rec;
   }
-  if (enter) atomicAdd(&sm.enter, 1u);
+  nent += enter ? 1u : 0u;
 }
 
 struct Mover {
@@ -442,59 +469,99 @@ __device__ __forceinline__ void walk_cells(const Mover& m, const Geom& g, SegF&&
 //   otherwise: o is met at its START position (ghost record, or the main record when the start cell
 //     is the same and o was present at the start); before = in(L, F) over the start-of-pass state
 //     (o's perspective iff o's start seq > m's), after = in(m_new, o_start).
-// Predicates are VALU arithmetic: lo <= p <= hi  <=>  min(p - lo, hi - p) >= 0, exactly (the sign
-// of a binary32 difference of finite values is the sign of the exact difference when subnormals are
-// kept; x - x = +0). A side that does not exist (m absent before / after) is forced to -1 (false).
+// "before" is one box test whose centre and test point are selected per candidate (m's old box
+// around o, or o's box around m's old position), so both perspectives cost one set of compares.
+// Every bound is one binary32 add/sub and every comparison inclusive, exactly as go-aoi's
+// `lo <= p && p <= hi` on float32 (a NaN coordinate compares false, as in Go).
 struct Judge {
-  float lx0, hx0, lz0, hz0;  // m's old box
   float lx1, hx1, lz1, hz1;  // m's new box
-  float mx0, mz0, D, sel0, sel1;
+  float mx0, mz0, D;
+  bool v0, v1;               // m present before / after its op
   uint32_t base, rank, q, q0;
 };
 
 __device__ __forceinline__ Judge make_judge(const Mover& m, uint32_t base) {
   Judge j;
   const float D = m.D;
-  j.lx0 = m.mx0 - D, j.hx0 = m.mx0 + D, j.lz0 = m.mz0 - D, j.hz0 = m.mz0 + D;
   j.lx1 = m.mx1 - D, j.hx1 = m.mx1 + D, j.lz1 = m.mz1 - D, j.hz1 = m.mz1 + D;
   j.mx0 = m.mx0, j.mz0 = m.mz0, j.D = D;
-  j.sel0 = m.valid0 ? 1.0f : -1.0f;
-  j.sel1 = m.valid1 ? 1.0f : -1.0f;
+  j.v0 = m.valid0;
+  j.v1 = m.valid1;
   j.base = base, j.rank = m.rank, j.q = m.q, j.q0 = m.q0;
   return j;
-}
-
-__device__ __forceinline__ float margin(float px, float pz, float lx, float hx, float lz, float hz) {
-  return fminf(fminf(px - lx, hx - px), fminf(pz - lz, hz - pz));
 }
 
 // 0: no event; otherwise 1 = LEAVE, 2 = ENTER
 __device__ __forceinline__ int judge(const Judge& J, const uint4 ra, const uint4 rb) {
   const uint32_t opq = ra.w;
   const bool ae = (opq - J.base) < J.rank;  // acted earlier in this pass
-  const bool ghost = (ra.z & REC_GHOST) != 0, hasg = (ra.z & REC_HASG) != 0;
+  const bool ghost = ra.z >= REC_GHOST, hasg = (ra.z & REC_HASG) != 0;
   const uint32_t seq0 = rb.z;
-  const bool valid = (opq != J.q) && (ghost ? !ae : (ae || (!hasg && seq0 != 0)));
+  const bool valid = (opq != J.q) & (ghost ? !ae : (ae | (!hasg & (seq0 != 0u))));
   const float px = ae ? __uint_as_float(ra.x) : __uint_as_float(rb.x);
   const float pz = ae ? __uint_as_float(ra.y) : __uint_as_float(rb.y);
+  const bool useo = ae | (seq0 > J.q0);  // o's box (o acted last) or m's old box
+  const float cx = useo ? px : J.mx0, cz = useo ? pz : J.mz0;  // box centre
+  const float tx = useo ? J.mx0 : px, tz = useo ? J.mz0 : pz;  // point tested
   const float D = J.D;
-  const float am = margin(px, pz, J.lx0, J.hx0, J.lz0, J.hz0);          // m's perspective
-  const float ao = margin(J.mx0, J.mz0, px - D, px + D, pz - D, pz + D);  // o's perspective
-  const float bf = fminf(J.sel0, (ae || seq0 > J.q0) ? ao : am);
-  const float af = fminf(J.sel1, margin(px, pz, J.lx1, J.hx1, J.lz1, J.hz1));
-  const bool before = bf >= 0.0f, after = af >= 0.0f;
-  return (valid && before != after) ? (after ? 2 : 1) : 0;
+  const bool before = J.v0 & (tx >= cx - D) & (tx <= cx + D) & (tz >= cz - D) & (tz <= cz + D);
+  const bool after = J.v1 & (px >= J.lx1) & (px <= J.hx1) & (pz >= J.lz1) & (pz <= J.hz1);
+  return (valid & (before != after)) ? (after ? 2 : 1) : 0;
+}
+
+// The LDS form of a grid record, precomputing what judge() derives per candidate. With r = the
+// record's op rank in this pass (~0u if its entity has no op), the record is a valid candidate for
+// the mover of rank k iff (k - lo) < span (unsigned) and r != k:
+//   ghost (start cell; met only if not acted earlier):       k < r          lo = 0,     span = r
+//   main with a ghost (met only if acted earlier):            k > r          lo = r + 1, span = ~0u - r - 1
+//   main alone, absent at the start (entered in this pass):   k > r          (same)
+//   main alone, present at the start:                         k != r         lo = 0,     span = ~0u
+// which is judge()'s `valid` term case by case; positions: start always, end = the binned position
+// (for a ghost the binned position is its start, and a ghost is never used "acted earlier").
+__device__ __forceinline__ void lds_record(const uint4 ra, const uint4 rb, uint32_t base, uint32_t n_ops, uint4& rp,
+                                           uint4& rm, uint32_t& rslot) {
+  const uint32_t q = ra.w - base;
+  const uint32_t r = q < n_ops ? q : ~0u;
+  const bool ghost = ra.z >= REC_GHOST, hasg = (ra.z & REC_HASG) != 0;
+  uint32_t lo, span;
+  if (ghost) {
+    lo = 0u, span = r;
+  } else if (hasg || rb.z == 0u) {
+    lo = r + 1u, span = ~0u - r - 1u;
+  } else {
+    lo = 0u, span = ~0u;
+  }
+  rp = make_uint4(rb.x, rb.y, ra.x, ra.y);
+  rm = make_uint4(r, lo, span, rb.z);
+  rslot = ra.z & REC_SLOT;
+}
+
+// judge() on the LDS form
+__device__ __forceinline__ int judge_lds(const Judge& J, const uint4 rp, const uint4 rm) {
+  const uint32_t r = rm.x, seq0 = rm.w;
+  const bool ae = r < J.rank;  // acted earlier in this pass
+  const bool valid = ((J.rank - rm.y) < rm.z) & (r != J.rank);
+  const float px = __uint_as_float(ae ? rp.z : rp.x);
+  const float pz = __uint_as_float(ae ? rp.w : rp.y);
+  const bool useo = ae | (seq0 > J.q0);  // o's box (o acted last) or m's old box
+  const float cx = useo ? px : J.mx0, cz = useo ? pz : J.mz0;  // box centre
+  const float tx = useo ? J.mx0 : px, tz = useo ? J.mz0 : pz;  // point tested
+  const float D = J.D;
+  const bool before = J.v0 & (tx >= cx - D) & (tx <= cx + D) & (tz >= cz - D) & (tz <= cz + D);
+  const bool after = J.v1 & (px >= J.lx1) & (px <= J.hx1) & (pz >= J.lz1) & (pz <= J.hz1);
+  return (valid & (before != after)) ? (after ? 2 : 1) : 0;
 }
 
 template <class Q>
-__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& q, const Mover& m, const Geom& g) {
+__device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& q, const Mover& m, const Geom& g,
+                                                 uint32_t& nent) {
   const Judge J = make_judge(m, a.base);
   uint32_t local = 0;
   walk_cells(m, g, [&](int r, int c0, int c1) {
     row_entries_global(g, a.g.cs, r, c0, c1, [&](uint32_t j) {
       const uint4 ra = a.g.ra[j];
       const int ev = judge(J, ra, a.g.rb[j]);
-      if (ev) emit(a, q, m.rank, local++, m.slot, ra.z & REC_SLOT, ev == 2);
+      if (ev) emit(a, q, m.rank, local++, m.slot, ra.z & REC_SLOT, ev == 2, nent);
     });
   });
   return local;
@@ -507,24 +574,114 @@ struct Region {
   }
 };
 
+// The ring of an ordinary move as at most 8 contiguous LDS ranges in two streams: the row stream
+// (row-major: top rows z0, z0+1 and bottom rows z1, z1-1 over the union's columns) and the column
+// stream (column-major: columns x0, x0+1, x1, x1-1 over the inner rows bz0..bz1). Returns false when
+// the move has no such ring (no inner cells, or a ring side wider than 2 cells): the row walk handles
+// it.
+struct RingStream {
+  uint32_t p1, p2, p3;      // exclusive prefix of the 4 segment lengths (p0 = 0)
+  uint32_t d0, d1, d2, d3;  // d0 = start of segment 0; ds = offset(s) - offset(s-1), offset = start - p
+  uint32_t total;
+};
+
+__device__ __forceinline__ void make_stream(RingStream& S, const uint32_t st[4], const uint32_t en[4]) {
+  const uint32_t l0 = en[0] - st[0], l1 = en[1] - st[1], l2 = en[2] - st[2], l3 = en[3] - st[3];
+  S.p1 = l0;
+  S.p2 = l0 + l1;
+  S.p3 = l0 + l1 + l2;
+  S.total = S.p3 + l3;
+  const uint32_t o0 = st[0], o1 = st[1] - S.p1, o2 = st[2] - S.p2, o3 = st[3] - S.p3;
+  S.d0 = o0;
+  S.d1 = o1 - o0;
+  S.d2 = o2 - o1;
+  S.d3 = o3 - o2;
+}
+
+// index of candidate k of a stream: k + the offset of the segment holding k (value selects only: an
+// indexed pick from a register array would go through scratch)
+__device__ __forceinline__ uint32_t stream_at(const RingStream& S, uint32_t k) {
+  return k + S.d0 + (k >= S.p1 ? S.d1 : 0u) + (k >= S.p2 ? S.d2 : 0u) + (k >= S.p3 ? S.d3 : 0u);
+}
+
+__device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const SweepSmem& sm, RingStream& Rs,
+                                          RingStream& Cs) {
+  if (!w.ring || w.bz0 > w.bz1 || w.bx0 > w.bx1) return false;
+  if (w.bz0 - w.z0 > 2 || w.z1 - w.bz1 > 2 || w.bx0 - w.ax0 > 2 || w.ax1 - w.bx1 > 2) return false;
+  uint32_t st[4], en[4];
+  const int xa = w.ax0 - R.xr0, xb = w.ax1 - R.xr0 + 1;
+  auto row = [&](int slot, int r, bool on) {
+    const int b = (r - R.zr0) * R.ncols;
+    st[slot] = on ? sm.lcs[b + xa] : 0u;
+    en[slot] = on ? sm.lcs[b + xb] : 0u;
+  };
+  row(0, w.z0, true);
+  row(1, w.z1, true);
+  row(2, w.z0 + 1, w.z0 + 1 < w.bz0);
+  row(3, w.z1 - 1, w.z1 - 1 > w.bz1);
+  make_stream(Rs, st, en);
+  const int za = w.bz0 - R.zr0, zb = w.bz1 - R.zr0 + 1;
+  auto col = [&](int slot, int c, bool on) {
+    const int b = (c - R.xr0) * R.nrows;
+    st[slot] = on ? sm.ccs[b + za] : 0u;
+    en[slot] = on ? sm.ccs[b + zb] : 0u;
+  };
+  col(0, w.ax0, true);
+  col(1, w.ax1, true);
+  col(2, w.ax0 + 1, w.ax0 + 1 < w.bx0);
+  col(3, w.ax1 - 1, w.ax1 - 1 > w.bx1);
+  make_stream(Cs, st, en);
+  return true;
+}
+
 __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Region& R,
-                                              const Geom& g) {
+                                              const Geom& g, uint32_t& nent) {
   const Judge J = make_judge(m, a.base);
   uint32_t local = 0;
+  RingStream Rs, Cs;
+  if (ring_plan(make_walk(m, g), R, sm, Rs, Cs)) {
+    // row stream: LDS record indices directly
+    uint32_t k = 0;
+    for (; k + 1 < Rs.total; k += 2) {  // two candidates per iteration: both LDS reads in flight
+      const uint32_t j0 = stream_at(Rs, k), j1 = stream_at(Rs, k + 1);
+      const uint4 p0 = sm.rp[j0], q0 = sm.rm[j0], p1 = sm.rp[j1], q1 = sm.rm[j1];
+      const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
+      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
+      if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j1], e1 == 2, nent);
+    }
+    if (k < Rs.total) {
+      const uint32_t j0 = stream_at(Rs, k);
+      const int e0 = judge_lds(J, sm.rp[j0], sm.rm[j0]);
+      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
+    }
+    // column stream: through the column-major index
+    for (k = 0; k + 1 < Cs.total; k += 2) {
+      const uint32_t j0 = sm.cidx[stream_at(Cs, k)], j1 = sm.cidx[stream_at(Cs, k + 1)];
+      const uint4 p0 = sm.rp[j0], q0 = sm.rm[j0], p1 = sm.rp[j1], q1 = sm.rm[j1];
+      const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
+      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
+      if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j1], e1 == 2, nent);
+    }
+    if (k < Cs.total) {
+      const uint32_t j0 = sm.cidx[stream_at(Cs, k)];
+      const int e0 = judge_lds(J, sm.rp[j0], sm.rm[j0]);
+      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
+    }
+    return local;
+  }
   walk_cells(m, g, [&](int r, int c0, int c1) {
     const int b = (r - R.zr0) * R.ncols - R.xr0;
     uint32_t j = sm.lcs[b + c0];
     const uint32_t e = (c0 <= c1) ? (uint32_t)sm.lcs[b + c1 + 1] : j;
     for (; j + 1 < e; j += 2) {  // two candidates per iteration: both LDS reads in flight
-      const uint4 ra0 = sm.ra[j], rb0 = sm.rb[j], ra1 = sm.ra[j + 1], rb1 = sm.rb[j + 1];
-      const int e0 = judge(J, ra0, rb0), e1 = judge(J, ra1, rb1);
-      if (e0) emit(a, sm, m.rank, local++, m.slot, ra0.z & REC_SLOT, e0 == 2);
-      if (e1) emit(a, sm, m.rank, local++, m.slot, ra1.z & REC_SLOT, e1 == 2);
+      const uint4 p0 = sm.rp[j], q0 = sm.rm[j], p1 = sm.rp[j + 1], q1 = sm.rm[j + 1];
+      const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
+      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j], e0 == 2, nent);
+      if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j + 1], e1 == 2, nent);
     }
     if (j < e) {
-      const uint4 ra0 = sm.ra[j];
-      const int e0 = judge(J, ra0, sm.rb[j]);
-      if (e0) emit(a, sm, m.rank, local++, m.slot, ra0.z & REC_SLOT, e0 == 2);
+      const int e0 = judge_lds(J, sm.rp[j], sm.rm[j]);
+      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j], e0 == 2, nent);
     }
   });
   return local;
@@ -555,7 +712,8 @@ constexpr int kCellsPerThread = (kRegCells + kSweepBlock - 1) / kSweepBlock;
 // table, then a flat copy (thread per record: region row by binary search, tile part by two
 // compares, two 16-B loads). Returns the staged count (block-uniform); a count > kCap means "does
 // not fit" and nothing was copied.
-__device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, const Region& R, SweepSmem& sm) {
+__device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, const Region& R, SweepSmem& sm,
+                                          uint32_t base, uint32_t n_ops) {
   const int pt0 = R.xr0 >> kTileShift;  // tile column of the region's first column
   uint32_t n[kCellsPerThread];
   uint32_t sum = 0;
@@ -583,6 +741,34 @@ __device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, con
   }
   if (threadIdx.x == 0) sm.lcs[R.ncells] = (uint16_t)total;
   __syncthreads();
+  // column-major cell starts (cell counts from the row-major table) and the column-major index
+  // array: cell (rr, cc) is column-major cell cc * nrows + rr
+  {
+    uint32_t cn[kCellsPerThread], cl[kCellsPerThread];
+    uint32_t sum2 = 0;
+#pragma unroll
+    for (int k = 0; k < kCellsPerThread; ++k) {
+      const int cm = c0 + k;
+      cn[k] = 0;
+      cl[k] = 0;
+      if (cm < R.ncells) {
+        const int cc = cm / R.nrows, rr = cm - cc * R.nrows;
+        const int c = rr * R.ncols + cc;
+        cl[k] = sm.lcs[c];
+        cn[k] = sm.lcs[c + 1] - cl[k];
+      }
+      sum2 += cn[k];
+    }
+    uint32_t tot2;
+    uint32_t pre2 = block_excl_scan_big(sum2, sm.ws, &tot2);
+#pragma unroll
+    for (int k = 0; k < kCellsPerThread; ++k) {
+      if (c0 + k < R.ncells) sm.ccs[c0 + k] = (uint16_t)pre2;
+      for (uint32_t i = 0; i < cn[k]; ++i) sm.cidx[pre2 + i] = (uint16_t)(cl[k] + i);
+      pre2 += cn[k];
+    }
+    if (threadIdx.x == 0) sm.ccs[R.ncells] = (uint16_t)total;
+  }
   const int p1c = ((pt0 + 1) << kTileShift) - R.xr0, p2c = p1c + kTile;
   for (uint32_t i = threadIdx.x; i < total; i += kSweepBlock) {
     int lo = 0, hi = R.nrows;  // find rr with lcs[rr * ncols] <= i < lcs[(rr + 1) * ncols]
@@ -603,8 +789,7 @@ __device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, con
       }
     }
     const uint32_t src = sm.gsp[lo * 3 + p] + (i - sm.lcs[rb + pc]);
-    sm.ra[i] = gv.ra[src];
-    sm.rb[i] = gv.rb[src];
+    lds_record(gv.ra[src], gv.rb[src], base, n_ops, sm.rp[i], sm.rm[i], sm.rslot[i]);
   }
   return total;
 }
@@ -642,19 +827,54 @@ __device__ __forceinline__ Mover leaver(const SweepArgs& a, uint32_t i, float D)
   return m;
 }
 
+// Diagnostic build only (GW_STAMPS=1, scripts/variants.py): per-block timestamps of the sweep's
+// phases, read back with gwaoi_debug_read_stamps. The product build compiles none of this.
+#ifndef GW_STAMPS
+#define GW_STAMPS 0
+#endif
+#if GW_STAMPS
+constexpr int kStampWords = 8;
+__device__ unsigned long long gw_stamps[kStampWords * 16384];
+#define GW_STAMP(k, v)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 16384) gw_stamps[blockIdx.x * kStampWords + (k)] = (v); \
+  } while (0)
+#else
+#define GW_STAMP(k, v) \
+  do {                 \
+  } while (0)
+#endif
+
+// XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD
+// b % 8), each with its own L2. Give XCD x a contiguous run of tiles, visited in order, so the halo a
+// tile shares with its predecessor is still in that XCD's L2. A bijection on [0, n).
+#ifndef GW_XCD_REMAP
+#define GW_XCD_REMAP 1
+#endif
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
+  if (!GW_XCD_REMAP) return b;
+  const uint32_t x = b % kXcds, i = b / kXcds, per = n / kXcds, rem = n % kXcds;
+  return x * per + min(x, rem) + i;
+}
+
 __device__ __forceinline__ bool is_mover(const uint4 ra, uint32_t base, uint32_t n_ops) {
   return !(ra.z & REC_GHOST) && (ra.w - base) < n_ops;
 }
 
-__global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
+// 2 blocks x 9 waves per CU (LDS-bound) need 5 waves per SIMD: at most 96 VGPRs
+__global__ void __launch_bounds__(kSweepBlock) __attribute__((amdgpu_waves_per_eu(GW_SWEEP_WAVES_PER_EU)))
+k_sweep(SweepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   SweepSmem& sm = *reinterpret_cast<SweepSmem*>(smem_raw);
+  uint32_t nent = 0;  // enter events of this thread's movers
+  GW_STAMP(0, __builtin_amdgcn_s_memrealtime());
   if (threadIdx.x == 0) {
     sm.n = 0;
     sm.enter = 0;
   }
   if (blockIdx.x < a.ntiles) {
-    const uint32_t t = blockIdx.x;
+    const uint32_t t = xcd_tile(blockIdx.x, a.ntiles);
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
     // does the tile hold a mover of this pass? (block-uniform exit otherwise)
     bool mine = false;
@@ -677,8 +897,14 @@ __global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
       lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= 3 * kTile;
     }
     if (lds) {
-      lds = stage(a.g, g, R, sm) <= (uint32_t)kCap;  // block-uniform
+      GW_STAMP(1, __builtin_amdgcn_s_memrealtime());
+      const uint32_t nst = stage(a.g, g, R, sm, a.base, a.n_ops);
+      lds = nst <= (uint32_t)kCap;  // block-uniform
       __syncthreads();
+      GW_STAMP(2, __builtin_amdgcn_s_memrealtime());
+      GW_STAMP(5, nst);
+      GW_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                      ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32));
     }
     if (a.use_lds == 2) {  // ablation (timing only): staging without the candidate walk
       for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
@@ -692,9 +918,9 @@ __global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
         const Mover m = mover_of(ra, a.g.rb[j], a.base, g.D);
         uint32_t cnt;
         if (lds && R.holds(qbox(g, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(g, m.mx0, m.mz0))))
-          cnt = sweep_lds(a, sm, m, R, g);
+          cnt = sweep_lds(a, sm, m, R, g, nent);
         else
-          cnt = sweep_global(a, sm, m, g);
+          cnt = sweep_global(a, sm, m, g, nent);
         a.rank_cnt[m.rank] = cnt;
       }
     }
@@ -705,11 +931,14 @@ __global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
       const uint32_t i = a.leave_ops[t];
       const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
       const Mover m = leaver(a, i, g.D);
-      a.rank_cnt[i] = sweep_global(a, sm, m, g);
+      a.rank_cnt[i] = sweep_global(a, sm, m, g, nent);
     }
   }
   // flush the block's events with one global atomic
+  if (nent) atomicAdd(&sm.enter, nent);
+  GW_STAMP(7, __builtin_amdgcn_s_memrealtime());  // thread 0's walk done
   __syncthreads();
+  GW_STAMP(3, __builtin_amdgcn_s_memrealtime());
   const uint32_t nq = min(sm.n, (uint32_t)kEvLds);
   if (threadIdx.x == 0) {
     sm.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
@@ -720,6 +949,23 @@ __global__ void __launch_bounds__(kSweepBlock, 6) k_sweep(SweepArgs a) {
     const uint32_t gi = sm.base + i;
     if (gi < a.ev_cap) a.ev_tmp[gi] = sm.ev[i];
   }
+  GW_STAMP(4, __builtin_amdgcn_s_memrealtime());
+}
+
+int read_stamps(void* host, size_t bytes) {
+#if GW_STAMPS
+  if (bytes > sizeof(gw_stamps)) bytes = sizeof(gw_stamps);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gw_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+#else
+  (void)host;
+  (void)bytes;
+  return -1;
+#endif
+}
+
+int sweep_occupancy(int* blocks) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void*>(&k_sweep), kSweepBlock,
+                                                      sizeof(SweepSmem)) == hipSuccess ? 0 : -3;
 }
 
 void sweep_init() {
@@ -736,6 +982,7 @@ struct FlatQ {
 
 __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
   __shared__ FlatQ q;
+  uint32_t nent = 0;
   if (threadIdx.x == 0) {
     q.n = 0;
     q.enter = 0;
@@ -749,14 +996,15 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
       const uint32_t slot = ra.z & REC_SLOT;
       const Geom g = a.g.geom[a.space_of[slot]];
       const Mover m = mover_of(ra, a.g.rb[t], a.base, g.D);
-      a.rank_cnt[m.rank] = sweep_global(a, q, m, g);
+      a.rank_cnt[m.rank] = sweep_global(a, q, m, g, nent);
     }
   } else if (t >= a.n_rec && t < a.n_rec + a.n_leaves) {
     const uint32_t i = a.leave_ops[t - a.n_rec];
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
-    a.rank_cnt[i] = sweep_global(a, q, m, g);
+    a.rank_cnt[i] = sweep_global(a, q, m, g, nent);
   }
+  if (nent) atomicAdd(&q.enter, nent);
   __syncthreads();
   const uint32_t nq = min(q.n, (uint32_t)kEvLds);
   if (threadIdx.x == 0) {

@@ -46,6 +46,9 @@ void set_err(const char* fmt, ...) {
   } while (0)
 
 constexpr uint32_t kSeqLimit = 0x7ff00000u;  // renormalise seqs before they pass this
+#ifndef GW_CELLS_PER_SLOT
+#define GW_CELLS_PER_SLOT 2  // grid cell budget per slot of capacity (cells beyond it coarsen the grid)
+#endif
 
 template <class T>
 int dalloc(T** p, size_t n) {
@@ -229,12 +232,12 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
     g.tile_base = base / gw::kTileCells;
     // halo for the sweep's LDS staging: a query box spans (D + margin) / c cells on each side of the
     // mover's cell, +1 for a mover whose old position is in the neighbouring cell; larger moves take
-    // the global path. Region = (16 + 2 reach)^2 cells must fit the kernel's region budget.
+    // the global path. Region = (kTile + 2 reach)^2 cells must fit the kernel's region budget.
     const double maxc = std::max({std::fabs((double)x0), std::fabs((double)x1), std::fabs((double)z0),
                                   std::fabs((double)z1)});
     const double span = ((double)sh.desc.dist * (1.0 + 1e-5) + (maxc + sh.desc.dist) * 1e-6) / c;
     int reach = (int)std::ceil(span) + 1;
-    if ((gw::kTile + 2 * reach) * (gw::kTile + 2 * reach) > 2304) reach = 0;  // LDS path off for this Space
+    if ((gw::kTile + 2 * reach) * (gw::kTile + 2 * reach) > gw::kSweepRegCells) reach = 0;  // LDS path off for this Space
     g.reach = reach;
     g.pad = 0;
     base += (uint32_t)(tx * tz) * gw::kTileCells;
@@ -646,7 +649,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     sh.desc = spaces[s];
     sh.auto_extent = !(spaces[s].max_x > spaces[s].min_x && spaces[s].max_z > spaces[s].min_z);
   }
-  m->max_cells = (uint32_t)std::min<uint64_t>(0x7fff0000u, std::max<uint64_t>(4096, 2ull * capacity) +
+  m->max_cells = (uint32_t)std::min<uint64_t>(0x7fff0000u, std::max<uint64_t>(4096, (uint64_t)GW_CELLS_PER_SLOT * capacity) +
                                                              (uint64_t)gw::kTileCells * nspaces);
   m->h_present.assign(capacity, 0);
   m->h_space_of.assign(capacity, 0);
@@ -1076,6 +1079,25 @@ int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
   RCHK(check_mgr(m));
   m->sweep_lds = enable < 0 ? 0 : (enable > 2 ? 1 : enable);
   return GWAOI_OK;
+}
+
+int gwaoi_debug_sweep_occupancy(int device, int* blocks_per_cu, int* lds_bytes) {
+  if (!blocks_per_cu || !lds_bytes) return GWAOI_ERR_INVALID;
+  HIPCHK(hipSetDevice(device));
+  gw::sweep_init();
+  *lds_bytes = (int)gw::sweep_lds_bytes();
+  if (gw::sweep_occupancy(blocks_per_cu)) {
+    set_err("hipOccupancyMaxActiveBlocksPerMultiprocessor failed");
+    return GWAOI_ERR_HIP;
+  }
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_read_stamps(void* host, size_t bytes) {
+  if (!host) return GWAOI_ERR_INVALID;
+  const int r = gw::read_stamps(host, bytes);
+  if (r) set_err("debug_read_stamps: library not built with GW_STAMPS=1");
+  return r;
 }
 
 int gwaoi_debug_set_cells_per_dist(gwaoi_mgr* m, float cpd) {

@@ -34,8 +34,13 @@ struct gwaoi_mgr;
 int gwaoi_debug_set_next_seq(struct gwaoi_mgr* mgr, uint32_t next_seq);
 /* Test hook: 0 = the sweep reads candidates from global memory only (A/B of the LDS-staged path). */
 int gwaoi_debug_set_sweep_lds(struct gwaoi_mgr* mgr, int enable);
-/* Test hook: cell size = D / cells_per_dist for grids built from now on (default 2). */
+/* Test hook: cell size = D / cells_per_dist for grids built from now on (default 4). */
 int gwaoi_debug_set_cells_per_dist(struct gwaoi_mgr* mgr, float cells_per_dist);
+/* Diagnostic builds only (GW_STAMPS=1): per-block phase timestamps of the last sweep launch
+ * (8 x uint64 per block). Returns GWAOI_ERR_INVALID/-1 in a product build. */
+int gwaoi_debug_read_stamps(void* host, size_t bytes);
+/* Diagnostics: resident sweep workgroups per CU (HIP occupancy API) and the sweep's LDS bytes. */
+int gwaoi_debug_sweep_occupancy(int device, int* blocks_per_cu, int* lds_bytes);
 
 #ifdef __cplusplus
 }
