@@ -47,14 +47,18 @@ struct Geom {
 // The pass's grid: every record sorted by cell key (counting sort). Per slot: a MAIN record at its
 // end-of-pass cell (if present at the end) and a GHOST record at its start-of-pass cell (if present
 // at the start and that cell differs, or it left in this pass).
-//   ra[j] = {x_bin bits, z_bin bits, slot | flags, opq}   (binned position; opq = op seq of this pass)
-//   rb[j] = {x_start bits, z_start bits, seq_start, seq_end}
+//   rec[j].a = {x_bin bits, z_bin bits, slot | flags, opq}   (binned position; opq = op seq of this pass)
+//   rec[j].b = {x_start bits, z_start bits, seq_start, seq_end}
 enum : uint32_t { REC_GHOST = 0x80000000u, REC_HASG = 0x40000000u, REC_SLOT = 0x3fffffffu };
 constexpr uint32_t kNoKey = 0xffffffffu;
 
+struct Rec {  // one grid record, 32 B contiguous (one write per record, one 32-B read in the sweep)
+  uint4 a;
+  uint4 b;
+};
+
 struct GridView {
-  const uint4* ra;
-  const uint4* rb;
+  const Rec* rec;
   const uint32_t* cs;          // cell_start[ncells + 1]
   const Geom* geom;            // [nspaces]
   const uint32_t* tile_space;  // [ntiles] tile -> space
@@ -97,9 +101,17 @@ struct BinArgs {
   uint32_t* key_of;    // [2 cap]: main / ghost key per slot (kNoKey = none)
   uint32_t* local_of;  // [2 cap]
   uint32_t* cs;        // counts, then (after scan) cell_start
-  uint4* ra;
-  uint4* rb;
+  Rec* rec;
+  // tile-bucketed build (launch_bin_tiles): per-(tile, slot chunk) histogram, bucket buffers
+  uint32_t ntiles, nblk;
+  uint32_t* thist;            // [ntiles * nblk + 1]
+  const uint32_t* tile_space;  // tile -> space
+  Rec* trec;                  // records bucketed by tile (the other grid's buffer: unused this pass)
 };
+// Slots per block of the tile-bucketed build, and the largest tile count its LDS histogram holds
+// (larger grids use the cell-atomic build).
+constexpr uint32_t kBinChunk = 4096;
+constexpr uint32_t kMaxLdsTiles = 12288;
 
 struct SweepArgs {
   GridView g;
@@ -134,13 +146,20 @@ struct RelArgs {
   uint32_t* cols;
 };
 
+// Scan scratch (the chunk sums of launch_scan), owned by the stream's manager.
+struct ScanCtx {
+  uint32_t* status = nullptr;  // scan_part_words(max n) words
+};
+
 // ---- launchers (gwaoi_kernels.hip) ----
 void launch_apply(const ApplyArgs& a, hipStream_t st);
 void launch_bin_count(const BinArgs& a, hipStream_t st);
 void launch_bin_scatter(const BinArgs& a, hipStream_t st);
+// Tile-bucketed build: LDS tile histograms per slot chunk -> (scan thist) -> bucket scatter -> per-tile
+// LDS cell sort that writes the records and every cell start. part: scan scratch.
+void launch_bin_tiles(const BinArgs& a, ScanCtx& sc, hipStream_t st);
 // In-place exclusive scan of d[0..n); d[n-1] must be 0 on entry if the total is wanted there.
-// part: scratch of scan_part_words(n) words.
-void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st);
+void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st);
 uint32_t scan_part_words(uint32_t n);
 void launch_sweep(const SweepArgs& a, hipStream_t st);
 size_t sweep_lds_bytes();

@@ -183,13 +183,11 @@ __global__ void __launch_bounds__(kBlock) k_bin_scatter(BinArgs a) {
   const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
   if (k1 != kNoKey) {
     const uint32_t j = a.cs[k1] + a.local_of[2 * s];
-    a.ra[j] = make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq);
-    a.rb[j] = rb;
+    a.rec[j] = Rec{make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq), rb};
   }
   if (k0 != kNoKey) {
     const uint32_t j = a.cs[k0] + a.local_of[2 * s + 1];
-    a.ra[j] = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq);
-    a.rb[j] = rb;
+    a.rec[j] = Rec{make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq), rb};
   }
 }
 
@@ -201,10 +199,7 @@ void launch_bin_scatter(const BinArgs& a, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Exclusive scan (u32): per-block reduce, scan of block sums, block scan + offset. Wave64 prefix
-// sums by __shfl_up; 256-thread blocks, 16 items per thread.
-constexpr int kScanItems = 16;
-constexpr uint32_t kScanChunk = kBlock * kScanItems;
+// Exclusive scan (u32) building blocks: wave64 prefix sums by __shfl_up, block scan over 256 threads.
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;
@@ -234,69 +229,274 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total)
   return pre + inc - v;
 }
 
+// Two-kernel scan: k_scan_reduce writes each chunk's sum to part[]; k_scan_apply has every block sum
+// the part[] entries before its chunk itself (at most kScanMaxChunks plain loads from L2, one or a
+// few per thread) and scan its chunk. (A single-pass version that waits on published chunk
+// aggregates through agent-scope atomics measured 3-6x slower here.) IPT items per thread keep the
+// chunk count <= kScanMaxChunks up to 16.7M items.
+constexpr uint32_t kScanMaxChunks = 1024;
+
+template <int IPT>
+__device__ __forceinline__ void scan_load(const uint32_t* __restrict__ d, uint32_t n, uint32_t b0, uint32_t (&v)[IPT]) {
+  if (b0 + IPT <= n) {
+#pragma unroll
+    for (int k = 0; k < IPT; k += 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(d + b0 + k);
+      v[k] = q.x, v[k + 1] = q.y, v[k + 2] = q.z, v[k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) v[k] = (b0 + k < n) ? d[b0 + k] : 0u;
+  }
+}
+
+template <int IPT>
 __global__ void __launch_bounds__(kBlock) k_scan_reduce(const uint32_t* __restrict__ d, uint32_t n,
                                                         uint32_t* __restrict__ part) {
-  const uint32_t b0 = blockIdx.x * kScanChunk + threadIdx.x * kScanItems;
+  uint32_t v[IPT];
+  scan_load<IPT>(d, n, (blockIdx.x * kBlock + threadIdx.x) * IPT, v);
   uint32_t sum = 0;
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) sum += (b0 + k < n) ? d[b0 + k] : 0u;
+  for (int k = 0; k < IPT; ++k) sum += v[k];
   uint32_t tot;
   block_excl_scan(sum, &tot);
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-__global__ void __launch_bounds__(kBlock) k_scan_part(uint32_t* part, uint32_t nb) {
-  // single block; nb <= kScanChunk
-  const uint32_t b0 = threadIdx.x * kScanItems;
-  uint32_t v[kScanItems];
+template <int IPT>
+__global__ void __launch_bounds__(kBlock) k_scan_apply(uint32_t* __restrict__ d, uint32_t n,
+                                                       const uint32_t* __restrict__ part) {
+  uint32_t before = 0;
+  for (uint32_t p = threadIdx.x; p < blockIdx.x; p += kBlock) before += part[p];
+  const uint32_t b0 = (blockIdx.x * kBlock + threadIdx.x) * IPT;
+  uint32_t v[IPT];
+  scan_load<IPT>(d, n, b0, v);
   uint32_t sum = 0;
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    v[k] = (b0 + k < nb) ? part[b0 + k] : 0u;
-    sum += v[k];
-  }
-  uint32_t tot;
-  uint32_t pre = block_excl_scan(sum, &tot);
+  for (int k = 0; k < IPT; ++k) sum += v[k];
+  uint32_t tot_before, tot;
+  block_excl_scan(before, &tot_before);
+  uint32_t pre = block_excl_scan(sum, &tot) + tot_before;
+  if (b0 + IPT <= n) {
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    if (b0 + k < nb) part[b0 + k] = pre;
-    pre += v[k];
+    for (int k = 0; k < IPT; k += 4) {
+      uint4 q;
+      q.x = pre, pre += v[k];
+      q.y = pre, pre += v[k + 1];
+      q.z = pre, pre += v[k + 2];
+      q.w = pre, pre += v[k + 3];
+      *reinterpret_cast<uint4*>(d + b0 + k) = q;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      if (b0 + k < n) d[b0 + k] = pre;
+      pre += v[k];
+    }
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_scan_down(uint32_t* __restrict__ d, uint32_t n,
-                                                      const uint32_t* __restrict__ part) {
-  const uint32_t b0 = blockIdx.x * kScanChunk + threadIdx.x * kScanItems;
-  uint32_t v[kScanItems];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    v[k] = (b0 + k < n) ? d[b0 + k] : 0u;
-    sum += v[k];
-  }
-  uint32_t tot;
-  uint32_t pre = block_excl_scan(sum, &tot) + (part ? part[blockIdx.x] : 0u);
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    if (b0 + k < n) d[b0 + k] = pre;
-    pre += v[k];
-  }
+static uint32_t scan_ipt(uint32_t n) {
+  for (uint32_t ipt : {4u, 16u})
+    if ((n + kBlock * ipt - 1) / (kBlock * ipt) <= kScanMaxChunks) return ipt;
+  return 64u;
 }
 
-uint32_t scan_part_words(uint32_t n) { return (n + kScanChunk - 1) / kScanChunk + 1; }
+uint32_t scan_part_words(uint32_t n) {
+  const uint32_t ipt = scan_ipt(n);
+  return (n + kBlock * ipt - 1) / (kBlock * ipt) + 1;
+}
 
-void launch_scan(uint32_t* d, uint32_t n, uint32_t* part, hipStream_t st) {
+template <int IPT>
+static void scan_ipt_launch(ScanCtx& c, uint32_t* d, uint32_t n, uint32_t nb, hipStream_t st) {
+  if (nb > 1) hipLaunchKernelGGL(k_scan_reduce<IPT>, dim3(nb), dim3(kBlock), 0, st, (const uint32_t*)d, n, c.status);
+  hipLaunchKernelGGL(k_scan_apply<IPT>, dim3(nb), dim3(kBlock), 0, st, d, n, (const uint32_t*)c.status);
+}
+
+void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st) {
   if (!n) return;
-  const uint32_t nb = (n + kScanChunk - 1) / kScanChunk;
-  if (nb == 1) {
-    hipLaunchKernelGGL(k_scan_down, dim3(1), dim3(kBlock), 0, st, d, n, (const uint32_t*)nullptr);
-    return;
-  }
-  // nb <= kScanChunk: n <= 16.7M per level. Larger n would need a recursive level.
-  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kBlock), 0, st, (const uint32_t*)d, n, part);
-  hipLaunchKernelGGL(k_scan_part, dim3(1), dim3(kBlock), 0, st, part, nb);
-  hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(kBlock), 0, st, d, n, (const uint32_t*)part);
+  const uint32_t ipt = scan_ipt(n);
+  const uint32_t nb = (n + kBlock * ipt - 1) / (kBlock * ipt);
+  if (ipt == 4)
+    scan_ipt_launch<4>(c, d, n, nb, st);
+  else if (ipt == 16)
+    scan_ipt_launch<16>(c, d, n, nb, st);
+  else
+    scan_ipt_launch<64>(c, d, n, nb, st);
 }
+
+// ---- tile-bucketed build: no global atomics ------------------------------------------------------
+// (1) k_bin_tcount: block b takes slots [b * kBinChunk, (b + 1) * kBinChunk); each record's rank
+//     inside (block, tile) comes from an LDS atomic on the block's tile histogram, which is then
+//     stored as thist[tile * nblk + b]. (2) exclusive scan of thist: bucket offsets, tile-major.
+// (3) k_bin_tscatter: records to their (tile, block) bucket. (4) k_bin_tsort: one block per tile
+//     counts its records per cell (LDS), scans the 1024 counts, writes the tile's cell starts and
+//     places every record (LDS atomic rank within its cell). The cell of a record is recomputed from
+//     its binned position with the same cell_key_of as (1).
+constexpr int kBinThreads = 1024;  // 16 waves: one block per CU at 1M slots, latency hidden by width
+constexpr int kBinItems = kBinChunk / kBinThreads;
+
+__global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
+  extern __shared__ uint32_t th[];
+  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) th[i] = 0u;
+  __syncthreads();
+  const uint32_t s0 = blockIdx.x * kBinChunk;
+#pragma unroll
+  for (int k = 0; k < kBinItems; ++k) {
+    const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
+    if (s >= a.cap) break;
+    const SlotState t = slot_state(a, s);
+    uint32_t k1 = kNoKey, k0 = kNoKey;
+    if (t.p_end || t.p_start) {
+      const Geom g = a.geom[a.space_of[s]];
+      if (t.p_end) k1 = cell_key_of(g, t.x1, t.z1);
+      if (t.p_start) k0 = cell_key_of(g, t.x0, t.z0);
+      if (k0 == k1) k0 = kNoKey;
+      if (k1 != kNoKey) a.local_of[2 * s] = atomicAdd(&th[k1 >> kTileCellShift], 1u);
+      if (k0 != kNoKey) a.local_of[2 * s + 1] = atomicAdd(&th[k0 >> kTileCellShift], 1u);
+    }
+    a.key_of[2 * s] = k1;
+    a.key_of[2 * s + 1] = k0;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) a.thist[i * a.nblk + blockIdx.x] = th[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.thist[a.ntiles * a.nblk] = 0u;  // the scan's total slot
+}
+
+__global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
+  const uint32_t s0 = blockIdx.x * kBinChunk;
+#pragma unroll
+  for (int k = 0; k < kBinItems; ++k) {
+    const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
+    if (s >= a.cap) break;
+    const uint32_t k1 = a.key_of[2 * s], k0 = a.key_of[2 * s + 1];
+    if (k1 == kNoKey && k0 == kNoKey) continue;
+    const SlotState t = slot_state(a, s);
+    const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
+    if (k1 != kNoKey) {
+      const uint32_t j = a.thist[(k1 >> kTileCellShift) * a.nblk + blockIdx.x] + a.local_of[2 * s];
+      a.trec[j] = Rec{make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq),
+                      rb};
+    }
+    if (k0 != kNoKey) {
+      const uint32_t j = a.thist[(k0 >> kTileCellShift) * a.nblk + blockIdx.x] + a.local_of[2 * s + 1];
+      a.trec[j] = Rec{make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq), rb};
+    }
+  }
+}
+
+// Tiles of up to 4 * kBlock records (all of config 2's) keep their records in registers between the
+// count and the placement (one read); larger tiles stream them twice.
+// cell index inside its tile, with the Space's geometry fields read as scalars (a local Geom copy
+// here gets demoted to scratch/LDS by the compiler)
+struct TileMap {
+  float x0, z0, inv_c;
+  int ncx, ncz;
+};
+
+__device__ __forceinline__ TileMap tile_map(const Geom* __restrict__ gp) {
+  TileMap m;
+  m.x0 = gp->x0;
+  m.z0 = gp->z0;
+  m.inv_c = gp->inv_c;
+  m.ncx = gp->ncx;
+  m.ncz = gp->ncz;
+  return m;
+}
+
+__device__ __forceinline__ uint32_t tile_cell(const TileMap& m, float x, float z) {
+  const int cx = cellc(x, m.x0, m.inv_c, m.ncx), cz = cellc(z, m.z0, m.inv_c, m.ncz);
+  return (uint32_t)(((cz & (kTile - 1)) << kTileShift) | (cx & (kTile - 1)));
+}
+
+__global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
+  __shared__ uint32_t cnt[kTileCells];
+  __shared__ uint32_t ws[kBlock / 64];
+  const uint32_t t = blockIdx.x;
+  const uint32_t b = a.thist[t * a.nblk], e = a.thist[(t + 1) * a.nblk];
+  for (int c = threadIdx.x; c < kTileCells; c += kBlock) cnt[c] = 0u;
+  const TileMap g = tile_map(&a.geom[a.tile_space[t]]);
+  const bool small = e - b <= 4u * kBlock;
+  // small tiles: four records per thread held in registers (loads clamped into [b, e) instead of
+  // conditional, so the compiler keeps them in VGPRs)
+  const uint32_t j0 = b + threadIdx.x, j1 = j0 + kBlock, j2 = j1 + kBlock, j3 = j2 + kBlock;
+  const uint32_t last = e > b ? e - 1 : b;
+  const bool on0 = small && j0 < e, on1 = small && j1 < e, on2 = small && j2 < e, on3 = small && j3 < e;
+  uint4 a0, b0, a1, b1, a2, b2, a3, b3;
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+  if (small && e > b) {
+    a0 = a.trec[min(j0, last)].a, b0 = a.trec[min(j0, last)].b;
+    a1 = a.trec[min(j1, last)].a, b1 = a.trec[min(j1, last)].b;
+    a2 = a.trec[min(j2, last)].a, b2 = a.trec[min(j2, last)].b;
+    a3 = a.trec[min(j3, last)].a, b3 = a.trec[min(j3, last)].b;
+    c0 = tile_cell(g, __uint_as_float(a0.x), __uint_as_float(a0.y));
+    c1 = tile_cell(g, __uint_as_float(a1.x), __uint_as_float(a1.y));
+    c2 = tile_cell(g, __uint_as_float(a2.x), __uint_as_float(a2.y));
+    c3 = tile_cell(g, __uint_as_float(a3.x), __uint_as_float(a3.y));
+  }
+  __syncthreads();
+  if (small) {
+    if (on0) atomicAdd(&cnt[c0], 1u);
+    if (on1) atomicAdd(&cnt[c1], 1u);
+    if (on2) atomicAdd(&cnt[c2], 1u);
+    if (on3) atomicAdd(&cnt[c3], 1u);
+  } else {
+    for (uint32_t j = b + threadIdx.x; j < e; j += kBlock) {
+      const uint4 ra = a.trec[j].a;
+      atomicAdd(&cnt[tile_cell(g, __uint_as_float(ra.x), __uint_as_float(ra.y))], 1u);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the 1024 counts (4 per thread, consecutive)
+  constexpr int kPer = kTileCells / kBlock;
+  static_assert(kPer == 4, "one uint4 of counts per thread");
+  const uint4 cv = *reinterpret_cast<const uint4*>(&cnt[threadIdx.x * kPer]);
+  const uint32_t sum = cv.x + cv.y + cv.z + cv.w;
+  const uint32_t inc = wave_incl_scan(sum);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t pre = b + inc - sum;
+  for (int k = 0; k < w; ++k) pre += ws[k];
+  const uint4 cso = make_uint4(pre, pre + cv.x, pre + cv.x + cv.y, pre + cv.x + cv.y + cv.z);
+  *reinterpret_cast<uint4*>(&cnt[threadIdx.x * kPer]) = cso;
+  *reinterpret_cast<uint4*>(&a.cs[(t << kTileCellShift) + threadIdx.x * kPer]) = cso;
+  if (t + 1 == a.ntiles && threadIdx.x == 0) a.cs[a.ntiles << kTileCellShift] = e;
+  __syncthreads();
+  if (small) {
+    if (on0) {
+      Rec* o = &a.rec[atomicAdd(&cnt[c0], 1u)];
+      o->a = a0, o->b = b0;
+    }
+    if (on1) {
+      Rec* o = &a.rec[atomicAdd(&cnt[c1], 1u)];
+      o->a = a1, o->b = b1;
+    }
+    if (on2) {
+      Rec* o = &a.rec[atomicAdd(&cnt[c2], 1u)];
+      o->a = a2, o->b = b2;
+    }
+    if (on3) {
+      Rec* o = &a.rec[atomicAdd(&cnt[c3], 1u)];
+      o->a = a3, o->b = b3;
+    }
+  } else {
+    for (uint32_t j = b + threadIdx.x; j < e; j += kBlock) {
+      const uint4 ra = a.trec[j].a, rb = a.trec[j].b;
+      Rec* o = &a.rec[atomicAdd(&cnt[tile_cell(g, __uint_as_float(ra.x), __uint_as_float(ra.y))], 1u)];
+      o->a = ra, o->b = rb;
+    }
+  }
+}
+
+void launch_bin_tiles(const BinArgs& a, ScanCtx& sc, hipStream_t st) {
+  if (!a.ntiles) return;
+  hipLaunchKernelGGL(k_bin_tcount, dim3(a.nblk), dim3(kBinThreads), a.ntiles * sizeof(uint32_t), st, a);
+  launch_scan(sc, a.thist, a.ntiles * a.nblk + 1, st);
+  hipLaunchKernelGGL(k_bin_tscatter, dim3(a.nblk), dim3(kBinThreads), 0, st, a);
+  hipLaunchKernelGGL(k_bin_tsort, dim3(a.ntiles), dim3(kBlock), 0, st, a);
+}
+
 
 // ---------------------------------------------------------------------------------------------
 // Sweep. One block per tile of the pass's grid (kTile x kTile cells, ~520 entities at config-2
@@ -559,8 +759,8 @@ __device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& q, const
   uint32_t local = 0;
   walk_cells(m, g, [&](int r, int c0, int c1) {
     row_entries_global(g, a.g.cs, r, c0, c1, [&](uint32_t j) {
-      const uint4 ra = a.g.ra[j];
-      const int ev = judge(J, ra, a.g.rb[j]);
+      const uint4 ra = a.g.rec[j].a;
+      const int ev = judge(J, ra, a.g.rec[j].b);
       if (ev) emit(a, q, m.rank, local++, m.slot, ra.z & REC_SLOT, ev == 2, nent);
     });
   });
@@ -789,7 +989,10 @@ __device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, con
       }
     }
     const uint32_t src = sm.gsp[lo * 3 + p] + (i - sm.lcs[rb + pc]);
-    lds_record(gv.ra[src], gv.rb[src], base, n_ops, sm.rp[i], sm.rm[i], sm.rslot[i]);
+    {
+      const Rec r = gv.rec[src];
+      lds_record(r.a, r.b, base, n_ops, sm.rp[i], sm.rm[i], sm.rslot[i]);
+    }
   }
   return total;
 }
@@ -878,7 +1081,7 @@ k_sweep(SweepArgs a) {
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
     // does the tile hold a mover of this pass? (block-uniform exit otherwise)
     bool mine = false;
-    for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_mover(a.g.ra[j], a.base, a.n_ops);
+    for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_mover(a.g.rec[j].a, a.base, a.n_ops);
     if (!__syncthreads_or(mine)) return;
     const uint32_t sp = a.g.tile_space[t];
     const Geom g = a.g.geom[sp];
@@ -908,14 +1111,14 @@ k_sweep(SweepArgs a) {
     }
     if (a.use_lds == 2) {  // ablation (timing only): staging without the candidate walk
       for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
-        const uint4 ra = a.g.ra[j];
+        const uint4 ra = a.g.rec[j].a;
         if (is_mover(ra, a.base, a.n_ops)) a.rank_cnt[ra.w - a.base] = 0;
       }
     } else {
       for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
-        const uint4 ra = a.g.ra[j];
+        const uint4 ra = a.g.rec[j].a;
         if (!is_mover(ra, a.base, a.n_ops)) continue;
-        const Mover m = mover_of(ra, a.g.rb[j], a.base, g.D);
+        const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
         uint32_t cnt;
         if (lds && R.holds(qbox(g, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(g, m.mx0, m.mz0))))
           cnt = sweep_lds(a, sm, m, R, g, nent);
@@ -991,11 +1194,11 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t n_rec = a.g.cs[a.ncells];
   if (t < n_rec) {
-    const uint4 ra = a.g.ra[t];
+    const uint4 ra = a.g.rec[t].a;
     if (is_mover(ra, a.base, a.n_ops)) {
       const uint32_t slot = ra.z & REC_SLOT;
       const Geom g = a.g.geom[a.space_of[slot]];
-      const Mover m = mover_of(ra, a.g.rb[t], a.base, g.D);
+      const Mover m = mover_of(ra, a.g.rec[t].b, a.base, g.D);
       a.rank_cnt[m.rank] = sweep_global(a, q, m, g, nent);
     }
   } else if (t >= a.n_rec && t < a.n_rec + a.n_leaves) {
@@ -1110,10 +1313,10 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
   uint32_t w = a.row_ptr ? a.row_ptr[s] : 0u;
   for (int r = B.z0; r <= B.z1; ++r) {
     row_entries_global(g, a.g.cs, r, B.x0, B.x1, [&](uint32_t j) {
-      const uint4 ra = a.g.ra[j];
+      const uint4 ra = a.g.rec[j].a;
       const uint32_t o = ra.z & REC_SLOT;
       if ((ra.z & REC_GHOST) || o == s) return;
-      const uint32_t qo = a.g.rb[j].w;  // end-of-pass seq
+      const uint32_t qo = a.g.rec[j].b.w;  // end-of-pass seq
       const float ox = __uint_as_float(ra.x), oz = __uint_as_float(ra.y);
       const bool in = (qo > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz);
       if (in) {

@@ -87,8 +87,7 @@ struct SpaceHost {
 };
 
 struct Grid {  // one pass's cell-sorted records (two buffers, alternating between passes)
-  uint4* ra = nullptr;
-  uint4* rb = nullptr;
+  gw::Rec* rec = nullptr;
   uint32_t* cs = nullptr;
   gw::Geom* d_geom = nullptr;
   uint32_t* d_tile_space = nullptr;  // tile -> space
@@ -146,8 +145,11 @@ struct gwaoi_mgr {
   uint32_t next_seq = 1;
   uint32_t* rank_cnt = nullptr;  // [cap + 1]
   int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
-  uint32_t* part = nullptr;
+  uint32_t* part = nullptr;     // scan chunk sums
   uint32_t part_words = 0;
+  gw::ScanCtx scan;
+  uint32_t* thist = nullptr;     // tile-bucketed build: [max tiles * nblk + 1]
+  uint32_t nblk = 0;
   uint32_t* ctr_buf = nullptr;   // [2][CTR_N]: pass P uses half P&1 and zeroes the other (k_place)
   uint32_t* ctr = nullptr;       // current half
   int ctr_sel = 0;
@@ -314,12 +316,18 @@ int upload_geom(gwaoi_mgr* m, Grid& g, const std::vector<gw::Geom>& geo) {
   return GWAOI_OK;
 }
 
+// Grids of up to kMaxLdsTiles tiles are built tile-bucketed (no global atomics); larger ones by the
+// cell-atomic counting sort, which needs zeroed cell counts.
+bool tile_build(const Grid& g) { return g.ntiles <= gw::kMaxLdsTiles; }
+
 // Build grid `gi` from the per-slot state (pos, seq, space_of).
 // Build grid `gi` for the pass whose ops have seqs [base, base + n_ops) (n_ops = 0: the current
 // state only, no ghosts).
 int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops) {
   Grid& g = m->grid[gi];
-  if (g.cs_zeroed < g.ncells + 1) HIPCHK(hipMemsetAsync(g.cs, 0, (size_t)(g.ncells + 1) * sizeof(uint32_t), m->stream));
+  const bool tiles = tile_build(g);
+  if (!tiles && g.cs_zeroed < g.ncells + 1)
+    HIPCHK(hipMemsetAsync(g.cs, 0, (size_t)(g.ncells + 1) * sizeof(uint32_t), m->stream));
   g.cs_zeroed = 0;
   gw::BinArgs b;
   b.pos_x = m->pos_x;
@@ -337,11 +345,19 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops) {
   b.key_of = m->key_of;
   b.local_of = m->local_of;
   b.cs = g.cs;
-  b.ra = g.ra;
-  b.rb = g.rb;
-  gw::launch_bin_count(b, m->stream);
-  gw::launch_scan(g.cs, g.ncells + 1, m->part, m->stream);
-  gw::launch_bin_scatter(b, m->stream);
+  b.rec = g.rec;
+  b.ntiles = g.ntiles;
+  b.nblk = m->nblk;
+  b.thist = m->thist;
+  b.tile_space = g.d_tile_space;
+  b.trec = m->grid[gi ^ 1].rec;  // the other grid's records are not read by this pass
+  if (tiles) {
+    gw::launch_bin_tiles(b, m->scan, m->stream);
+  } else {
+    gw::launch_bin_count(b, m->stream);
+    gw::launch_scan(m->scan, g.cs, g.ncells + 1, m->stream);
+    gw::launch_bin_scatter(b, m->stream);
+  }
   HIPCHK(hipGetLastError());
   return GWAOI_OK;
 }
@@ -445,7 +461,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     }
     gw::SweepArgs s;
     const Grid& G = m->grid[ng];
-    s.g = {G.ra, G.rb, G.cs, G.d_geom, G.d_tile_space};
+    s.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
     s.ntiles = G.ntiles;
     s.ncells = G.ncells;
     s.n_rec = n_start + n_new;  // upper bound on records (main + ghost)
@@ -468,7 +484,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
     // canonical order; every step is guarded on the device against a buffer overflow, so the host
     // synchronises once, at the end of the pass
-    gw::launch_scan(m->rank_cnt, n_ops + 1, m->part, st);
+    gw::launch_scan(m->scan, m->rank_cnt, n_ops + 1, st);
     gw::OrderArgs o;
     o.g = {m->ctr, m->tmp_cap, keep, m->ev_cap};
     o.ev_tmp = m->ev_tmp;
@@ -476,8 +492,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     o.ev_out = m->ev_out + keep;
     o.host_out = copy_events ? m->d_hev + keep : nullptr;
     o.n_ops = n_ops;
-    o.zero_cs = m->grid[og].cs;  // the grid the next pass builds into
-    o.zero_n = m->grid[og].ncells + 1;
+    o.zero_cs = m->grid[og].cs;  // the grid the next pass builds into (cell-atomic build only)
+    o.zero_n = tile_build(m->grid[og]) ? 0u : m->grid[og].ncells + 1;
     o.ctr_next = m->ctr_buf + (m->ctr_sel ^ 1) * gw::CTR_N;
     o.op_slot = a.op_slot;
     o.seq = m->seq;
@@ -524,7 +540,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     break;
   }
   m->cur = ng;
-  m->grid[og].cs_zeroed = m->grid[og].ncells + 1;
+  m->grid[og].cs_zeroed = tile_build(m->grid[og]) ? 0u : m->grid[og].ncells + 1;
   m->ctr_sel ^= 1;
   m->ctr = m->ctr_buf + m->ctr_sel * gw::CTR_N;
   m->tick_passes++;
@@ -597,12 +613,12 @@ void free_all(gwaoi_mgr* m) {
   if (m->stream) hipStreamSynchronize(m->stream);
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_op_x, m->d_op_z,
-                   m->d_op_kind, m->rank_cnt, m->part, m->ctr_buf, m->ev_tmp, m->ev_out};
+                   m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
-    void* gp[] = {g.ra, g.rb, g.cs, g.d_geom, g.d_tile_space};
+    void* gp[] = {g.rec, g.cs, g.d_geom, g.d_tile_space};
     for (void* p : gp)
       if (p) hipFree(p);
   }
@@ -682,8 +698,15 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->d_op_z, C));
   chk(dalloc(&m->d_op_kind, C));
   chk(dalloc(&m->rank_cnt, C + 1));
-  m->part_words = gw::scan_part_words(std::max<uint32_t>(m->max_cells, capacity) + 1);
+  m->nblk = (capacity + gw::kBinChunk - 1) / gw::kBinChunk;
+  const uint64_t max_tiles = m->max_cells / gw::kTileCells + 1;
+  const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
+  chk(dalloc(&m->thist, thist_n));
+  // the scan has at most 1024 chunks up to 16.7M items (scan_ipt), more beyond
+  m->part_words = std::max<uint32_t>(1024 + 2, gw::scan_part_words((uint32_t)std::max<uint64_t>(
+                                                   {(uint64_t)m->max_cells, (uint64_t)capacity, thist_n}) + 1));
   chk(dalloc(&m->part, m->part_words));
+  m->scan.status = m->part;
   chk(dalloc(&m->ctr_buf, 2 * gw::CTR_N));
   m->ctr = m->ctr_buf;
   chk(halloc(&m->h_ctr, gw::CTR_N));
@@ -695,8 +718,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(halloc(&m->h_leaves, C));
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
-    chk(dalloc(&g.ra, 2 * C));
-    chk(dalloc(&g.rb, 2 * C));
+    chk(dalloc(&g.rec, 2 * C));
     chk(dalloc(&g.cs, (size_t)m->max_cells + 1));
     chk(dalloc(&g.d_geom, nspaces));
     chk(dalloc(&g.d_tile_space, (size_t)m->max_cells / gw::kTileCells + 1));
@@ -928,7 +950,7 @@ int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint6
   uint32_t* d_rp = nullptr;
   RCHK(dalloc(&d_rp, (size_t)m->cap + 1));
   gw::RelArgs a;
-  a.g = {g.ra, g.rb, g.cs, g.d_geom, g.d_tile_space};
+  a.g = {g.rec, g.cs, g.d_geom, g.d_tile_space};
   a.pos_x = m->pos_x;
   a.pos_z = m->pos_z;
   a.seq = m->seq;
@@ -939,7 +961,7 @@ int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint6
   a.cols = nullptr;
   hipError_t e = hipMemsetAsync(d_rp + m->cap, 0, sizeof(uint32_t), st);
   gw::launch_relation(a, st);
-  gw::launch_scan(d_rp, m->cap + 1, m->part, st);
+  gw::launch_scan(m->scan, d_rp, m->cap + 1, st);
   uint32_t total = 0;
   if (e == hipSuccess) e = hipMemcpyAsync(&total, d_rp + m->cap, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
