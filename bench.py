@@ -234,16 +234,17 @@ def main():
         ticks = max(1, st["ticks"])
         sweep_ms = st["ms_sweep"] / ticks
         ev_per_tick = st["events"] / ticks
-        # algorithmic bytes of ONE sweep launch (DESIGN.md "Kernels"): per mover its own new-grid
-        # entry 16 B + start-of-pass state (old x, z, seq, space) 16 B, the old-grid entry 16 B + side 4 B
-        # of every entity, per event 16 B staged; cell tables 2 x 4 B per cell.
-        cells = (int(L / (D / 2.0)) + 1) ** 2
-        b_sweep = 52.0 * n + 16.0 * ev_per_tick + 8.0 * cells
+        # algorithmic bytes of ONE sweep launch (DESIGN.md "Measurement"): every record of the pass's
+        # cell-sorted grid read once (32 B: binned + start state), every cell start once (4 B), the
+        # per-op event count written (4 B per mover), every event staged once (16 B).
+        rec_per_tick = st["grid_records"] / ticks
+        cells = st["grid_cells"] / ticks
+        b_sweep = 32.0 * rec_per_tick + 4.0 * cells + 4.0 * n + 16.0 * ev_per_tick
         achieved = b_sweep / (sweep_ms * 1e-3) / 1e9
         pmc = load_pmc_traffic()
         traffic = None
         if pmc and pmc.get("n") == n and "sweep_bytes_per_launch" in pmc:
-            traffic = pmc["sweep_bytes_per_launch"]
+            traffic = pmc["sweep_bytes_per_launch"] / (sweep_ms * 1e-3) / 1e9  # GB/s, same unit as achieved
         # SURVEY.md §8(d) whole-tick formula (assumes a CSR-state design; ours keeps no lists)
         b_survey = 24.0 * n + 4.0 * (2 * nnz) + 8.0 * ev_per_tick
         result = {
@@ -273,13 +274,17 @@ def main():
             "stage_ms": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_sweep (+k_sweep_leaves)",
+                "kernel": "k_sweep",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_bytes_per_launch": (pmc or {}).get("sweep_bytes_per_launch") if traffic else None,
                 "algorithmic_bytes_per_launch": b_sweep,
+                "grid_records_per_tick": rec_per_tick,
+                "grid_cells": cells,
+                "traffic_source": (pmc or {}).get("source"),
                 "avg_launch_ms": sweep_ms,
                 "survey_formula": {
                     "bytes_per_tick": b_survey,

@@ -74,6 +74,8 @@ class Stats(ctypes.Structure):
         ("ms_total", ctypes.c_double),
         ("sweep_movers", ctypes.c_uint64),
         ("events", ctypes.c_uint64),
+        ("grid_records", ctypes.c_uint64),
+        ("grid_cells", ctypes.c_uint64),
     ]
 
 

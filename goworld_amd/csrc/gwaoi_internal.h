@@ -14,7 +14,8 @@ enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2 };
 enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u };
 
 // Counters block in device memory (one 64-B line).
-enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_N = 16 };
+enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
+       CTR_N = 16 };
 
 // Cells are grouped in square tiles of kTile x kTile cells; cell keys are tile-major,
 //   key = base + (tz * ntx + tx) * 1024 + lz * 32 + lx   (cx = 32 tx + lx, cz = 32 tz + lz),
@@ -184,6 +185,7 @@ struct OrderArgs {
   uint32_t* zero_cs;         // cell counts of the grid the next pass builds
   uint32_t zero_n;
   uint32_t* ctr_next;        // the next pass's counter block
+  const uint32_t* grid_total;  // cs[ncells] of this pass's grid (record count, reported in the stats)
   const uint32_t* op_slot;   // device-staged batch check
   const uint32_t* seq;
   uint32_t base, cap;

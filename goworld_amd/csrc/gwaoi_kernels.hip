@@ -1251,6 +1251,7 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
   if (!ev_fits(o.g, &n)) return;
   for (uint32_t i = tid; i < o.zero_n; i += nth) o.zero_cs[i] = 0u;
   if (tid < CTR_N) o.ctr_next[tid] = 0u;
+  if (tid == 0) const_cast<uint32_t*>(o.g.ctr)[CTR_RECORDS] = *o.grid_total;
   for (uint32_t i = tid; i < n; i += nth) {
     const uint4 e = o.ev_tmp[i];
     o.ev_out[o.rank_off[e.x] + e.y] = make_uint2(e.z, e.w);

@@ -495,6 +495,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     o.zero_cs = m->grid[og].cs;  // the grid the next pass builds into (cell-atomic build only)
     o.zero_n = tile_build(m->grid[og]) ? 0u : m->grid[og].ncells + 1;
     o.ctr_next = m->ctr_buf + (m->ctr_sel ^ 1) * gw::CTR_N;
+    o.grid_total = m->grid[ng].cs + m->grid[ng].ncells;
     o.op_slot = a.op_slot;
     o.seq = m->seq;
     o.base = base;
@@ -536,6 +537,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       m->stats.ms_total += t04;
       m->stats.sweep_movers += n_ops;
       m->stats.events += nev;
+      m->stats.grid_records += m->h_ctr[gw::CTR_RECORDS];
+      m->stats.grid_cells += m->grid[ng].ncells;
     }
     break;
   }

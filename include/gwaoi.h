@@ -133,6 +133,8 @@ typedef struct {
   double ms_total;         /* first to last kernel of the pass */
   uint64_t sweep_movers;   /* movers processed by the sweep */
   uint64_t events;         /* events emitted */
+  uint64_t grid_records;   /* records of the passes' cell-sorted grids (main + ghost) */
+  uint64_t grid_cells;     /* cells of those grids */
 } gwaoi_stats;
 int gwaoi_set_timing(gwaoi_mgr* mgr, int enable);
 int gwaoi_get_stats(const gwaoi_mgr* mgr, gwaoi_stats* out);
