@@ -84,7 +84,7 @@ struct ApplyArgs {
   uint32_t* old_seq;
   uint32_t* opq;             // op seq of this pass (stale for slots without an op)
   uint32_t* ctr;
-  uint32_t* rank_tail;       // rank_cnt[n_ops], zeroed (the scan's total slot)
+  uint32_t* rank_cnt;        // [n_ops + 1]: zeroed here (the sweep stores non-zero counts; [n_ops] = scan total)
 };
 
 struct BinArgs {

@@ -95,7 +95,8 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   if (i >= a.n_ops) return;
   const uint32_t s = a.op_slot[i];
   const uint32_t q = a.base + i;
-  if (i == 0) *a.rank_tail = 0u;
+  if (i == 0) a.rank_cnt[a.n_ops] = 0u;
+  a.rank_cnt[i] = 0u;  // the sweep stores only non-zero event counts
   const uint8_t kind = a.op_kind ? a.op_kind[i] : (uint8_t)OP_MOVE;
   if (a.check && s >= a.cap) {
     atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SLOT);
@@ -352,11 +353,12 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
       if (t.p_end) k1 = cell_key_of(g, t.x1, t.z1);
       if (t.p_start) k0 = cell_key_of(g, t.x0, t.z0);
       if (k0 == k1) k0 = kNoKey;
-      if (k1 != kNoKey) a.local_of[2 * s] = atomicAdd(&th[k1 >> kTileCellShift], 1u);
-      if (k0 != kNoKey) a.local_of[2 * s + 1] = atomicAdd(&th[k0 >> kTileCellShift], 1u);
+      uint32_t l1 = 0, l0 = 0;
+      if (k1 != kNoKey) l1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
+      if (k0 != kNoKey) l0 = atomicAdd(&th[k0 >> kTileCellShift], 1u);
+      reinterpret_cast<uint2*>(a.local_of)[s] = make_uint2(l1, l0);
     }
-    a.key_of[2 * s] = k1;
-    a.key_of[2 * s + 1] = k0;
+    reinterpret_cast<uint2*>(a.key_of)[s] = make_uint2(k1, k0);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) a.thist[i * a.nblk + blockIdx.x] = th[i];
@@ -369,17 +371,19 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
   for (int k = 0; k < kBinItems; ++k) {
     const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
     if (s >= a.cap) break;
-    const uint32_t k1 = a.key_of[2 * s], k0 = a.key_of[2 * s + 1];
+    const uint2 kk = reinterpret_cast<const uint2*>(a.key_of)[s];
+    const uint32_t k1 = kk.x, k0 = kk.y;
     if (k1 == kNoKey && k0 == kNoKey) continue;
+    const uint2 ll = reinterpret_cast<const uint2*>(a.local_of)[s];
     const SlotState t = slot_state(a, s);
     const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
     if (k1 != kNoKey) {
-      const uint32_t j = a.thist[(k1 >> kTileCellShift) * a.nblk + blockIdx.x] + a.local_of[2 * s];
+      const uint32_t j = a.thist[(k1 >> kTileCellShift) * a.nblk + blockIdx.x] + ll.x;
       a.trec[j] = Rec{make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq),
                       rb};
     }
     if (k0 != kNoKey) {
-      const uint32_t j = a.thist[(k0 >> kTileCellShift) * a.nblk + blockIdx.x] + a.local_of[2 * s + 1];
+      const uint32_t j = a.thist[(k0 >> kTileCellShift) * a.nblk + blockIdx.x] + ll.y;
       a.trec[j] = Rec{make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq), rb};
     }
   }
@@ -1124,7 +1128,7 @@ k_sweep(SweepArgs a) {
           cnt = sweep_lds(a, sm, m, R, g, nent);
         else
           cnt = sweep_global(a, sm, m, g, nent);
-        a.rank_cnt[m.rank] = cnt;
+        if (cnt) a.rank_cnt[m.rank] = cnt;  // zeroed by k_apply (one coalesced pass instead of a scatter)
       }
     }
   } else {

@@ -441,7 +441,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   a.old_seq = m->old_seq;
   a.opq = m->opq;
   a.ctr = m->ctr;
-  a.rank_tail = m->rank_cnt + n_ops;
+  a.rank_cnt = m->rank_cnt;
   gw::launch_apply(a, st);
   HIPCHK(hipGetLastError());
   if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
@@ -455,7 +455,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   // events: expected count is small; grow and re-run the (pure) sweep on overflow
   for (int attempt = 0;; ++attempt) {
     if (attempt) {  // re-run after growing the event buffers: reset what the sweep accumulates
-      HIPCHK(hipMemsetAsync(m->rank_cnt + n_ops, 0, sizeof(uint32_t), st));
+      // the scan turned the counts into offsets, and the sweep stores non-zero counts only
+      HIPCHK(hipMemsetAsync(m->rank_cnt, 0, ((size_t)n_ops + 1) * sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
     }
