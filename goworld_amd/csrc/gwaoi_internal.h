@@ -8,10 +8,10 @@
 namespace gw {
 
 // Op kinds staged by the host (the reference's three AOIManager calls, Space.go:211/221, 243, 259).
-enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2 };
+enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2, OP_KIND = 3, OP_SILENT = 0x80 };
 
 // Device-side error bits (device-staged batches are validated on the GPU).
-enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u };
+enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u, ERR_PRESENT_SLOT = 8u };
 
 // Counters block in device memory (one 64-B line).
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
@@ -69,8 +69,9 @@ struct ApplyArgs {
   const uint32_t* op_slot;
   const float* op_x;
   const float* op_z;
-  const uint8_t* op_kind;    // null => all OP_MOVE (device-staged batch)
-  const uint32_t* op_space;  // space of OP_ENTER ops
+  const uint8_t* op_kind;    // null => all OP_MOVE (device-staged moves); may carry OP_SILENT
+  const uint32_t* op_space;  // space of OP_ENTER ops (null: Space 0)
+  uint32_t* leaves;          // device-staged mixed batch: Leave op indices are appended here
   uint32_t n_ops;
   uint32_t base;             // seq of op 0; op i gets seq base + i
   uint32_t cap;
@@ -127,8 +128,11 @@ struct SweepArgs {
   uint32_t ntiles;     // tiles of the grid: blocks [0, ntiles) take one tile each, the rest Leave ops
   int use_lds;         // 1: LDS-staged sweep; 0: flat global-memory sweep (A/B); 2: staging only (timing)
   const uint32_t* op_slot;    // for the leave path
+  const uint8_t* op_kind;     // per op (null: all moves); OP_SILENT movers are applied, not walked
   const uint32_t* leave_ops;  // op indices of OP_LEAVE ops
-  uint32_t n_leaves;
+  uint32_t n_leaves;          // host-staged: the count; device-staged mixed batch: see leaves_dev
+  const uint32_t* n_leaves_dev;  // non-null: the count is on the device (ctr[CTR_LEAVES])
+  uint32_t leave_blocks;      // blocks after the tiles that walk the Leave ops
   uint4* ev_tmp;    // {rank, local index within rank, mover, other|kind}
   uint32_t ev_cap;
   uint32_t* rank_cnt;
@@ -164,6 +168,7 @@ void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st);
 uint32_t scan_part_words(uint32_t n);
 void launch_sweep(const SweepArgs& a, hipStream_t st);
 size_t sweep_lds_bytes();
+uint32_t sweep_block();  // threads per sweep block
 void sweep_init();  // once per process (dynamic LDS limit of the sweep)
 int read_stamps(void* host, size_t bytes);
 int sweep_occupancy(int* blocks);  // resident sweep blocks per CU (HIP occupancy API)  // GW_STAMPS diagnostic builds only (else -1)
@@ -186,8 +191,8 @@ struct OrderArgs {
   uint32_t zero_n;
   uint32_t* ctr_next;        // the next pass's counter block
   const uint32_t* grid_total;  // cs[ncells] of this pass's grid (record count, reported in the stats)
-  const uint32_t* op_slot;   // device-staged batch check
-  const uint32_t* seq;
+  const uint32_t* op_slot;   // device-staged batch check: every op's slot carries that op's seq
+  const uint32_t* opq;
   uint32_t base, cap;
   int check_ops;
 };

@@ -90,23 +90,53 @@ __device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t
 // writes the end-of-pass state. Slots of one pass are distinct (the host guarantees it for
 // host-staged ops; for device-staged batches k_slice_sort checks afterwards that every op's slot
 // carries that op's seq — a duplicate leaves one of two ops without it).
+// lane-aggregated append: one atomic per wave for the lanes with `pred`; returns this lane's slot
+__device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if (!m) return 0u;
+  const int leader = __ffsll((long long)m) - 1;
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
 __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= a.n_ops) return;
-  const uint32_t s = a.op_slot[i];
+  const bool live = i < a.n_ops;
+  uint32_t s = 0, q0 = 0;
+  uint8_t kind = OP_MOVE;
+  bool ok = live;
+  if (live) {
+    s = a.op_slot[i];
+    kind = a.op_kind ? (uint8_t)(a.op_kind[i] & OP_KIND) : (uint8_t)OP_MOVE;
+    if (i == 0) a.rank_cnt[a.n_ops] = 0u;
+    a.rank_cnt[i] = 0u;  // the sweep stores only non-zero event counts
+    if (a.check && s >= a.cap) {
+      atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SLOT);
+      ok = false;
+    } else {
+      q0 = a.seq[s];
+      if (a.check && kind == OP_ENTER && q0 != 0) {
+        atomicOr(&a.ctr[CTR_ERR], ERR_PRESENT_SLOT);
+        ok = false;
+      } else if (a.check && kind != OP_ENTER && q0 == 0) {
+        atomicOr(&a.ctr[CTR_ERR], ERR_ABSENT_SLOT);
+        ok = false;
+      }
+    }
+  }
+  if (a.leaves) {  // device-staged mixed batch: Leave list and presence delta on the device (wave-uniform)
+    const bool lv = ok && kind == OP_LEAVE;
+    const uint32_t j = wave_append(&a.ctr[CTR_LEAVES], lv);
+    if (lv) a.leaves[j] = i;
+    const unsigned long long ent = __ballot(ok && kind == OP_ENTER), lea = __ballot(lv);
+    if ((threadIdx.x & 63) == 0 && (ent | lea))
+      atomicAdd(&a.ctr[CTR_PRESENT], (uint32_t)__popcll(ent) - (uint32_t)__popcll(lea));
+  }
+  if (!ok) return;
   const uint32_t q = a.base + i;
-  if (i == 0) a.rank_cnt[a.n_ops] = 0u;
-  a.rank_cnt[i] = 0u;  // the sweep stores only non-zero event counts
-  const uint8_t kind = a.op_kind ? a.op_kind[i] : (uint8_t)OP_MOVE;
-  if (a.check && s >= a.cap) {
-    atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SLOT);
-    return;
-  }
-  const uint32_t q0 = a.seq[s];
-  if (a.check && q0 == 0) {
-    atomicOr(&a.ctr[CTR_ERR], ERR_ABSENT_SLOT);
-    return;
-  }
   a.old_x[s] = a.pos_x[s];
   a.old_z[s] = a.pos_z[s];
   a.old_seq[s] = q0;
@@ -117,7 +147,7 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
     a.pos_x[s] = a.op_x[i];
     a.pos_z[s] = a.op_z[i];
     a.seq[s] = q;
-    if (kind == OP_ENTER) a.space_of[s] = a.op_space[i];
+    if (kind == OP_ENTER) a.space_of[s] = a.op_space ? a.op_space[i] : 0u;
   }
 }
 
@@ -562,6 +592,7 @@ struct SweepSmem {  // dynamic LDS (16-B aligned carve)
 static_assert(sizeof(SweepSmem) <= 163840 / 2, "sweep LDS budget: 2 blocks per CU");
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
+uint32_t sweep_block() { return kSweepBlock; }
 
 // Queue one event in the block's LDS queue (one LDS atomic; the file is built without the atomic
 // optimizer, so this is a single ds_add_rtn rather than a wave reduction around every call). Enter
@@ -1069,6 +1100,11 @@ __device__ __forceinline__ bool is_mover(const uint4 ra, uint32_t base, uint32_t
   return !(ra.z & REC_GHOST) && (ra.w - base) < n_ops;
 }
 
+// a mover whose events are reported (not an OP_SILENT halo copy)
+__device__ __forceinline__ bool is_walker(const SweepArgs& a, const uint4 ra) {
+  return is_mover(ra, a.base, a.n_ops) && !(a.op_kind && (a.op_kind[ra.w - a.base] & OP_SILENT));
+}
+
 // 2 blocks x 9 waves per CU (LDS-bound) need 5 waves per SIMD: at most 96 VGPRs
 __global__ void __launch_bounds__(kSweepBlock) __attribute__((amdgpu_waves_per_eu(GW_SWEEP_WAVES_PER_EU)))
 k_sweep(SweepArgs a) {
@@ -1085,7 +1121,7 @@ k_sweep(SweepArgs a) {
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
     // does the tile hold a mover of this pass? (block-uniform exit otherwise)
     bool mine = false;
-    for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_mover(a.g.rec[j].a, a.base, a.n_ops);
+    for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_walker(a, a.g.rec[j].a);
     if (!__syncthreads_or(mine)) return;
     const uint32_t sp = a.g.tile_space[t];
     const Geom g = a.g.geom[sp];
@@ -1121,7 +1157,7 @@ k_sweep(SweepArgs a) {
     } else {
       for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
         const uint4 ra = a.g.rec[j].a;
-        if (!is_mover(ra, a.base, a.n_ops)) continue;
+        if (!is_walker(a, ra)) continue;
         const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
         uint32_t cnt;
         if (lds && R.holds(qbox(g, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(g, m.mx0, m.mz0))))
@@ -1133,9 +1169,10 @@ k_sweep(SweepArgs a) {
     }
   } else {
     __syncthreads();
-    const uint32_t t = (blockIdx.x - a.ntiles) * kSweepBlock + threadIdx.x;
-    if (t < a.n_leaves) {
+    const uint32_t nl = a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves;
+    for (uint32_t t = (blockIdx.x - a.ntiles) * kSweepBlock + threadIdx.x; t < nl; t += a.leave_blocks * kSweepBlock) {
       const uint32_t i = a.leave_ops[t];
+      if (a.op_kind && (a.op_kind[i] & OP_SILENT)) continue;
       const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
       const Mover m = leaver(a, i, g.D);
       a.rank_cnt[i] = sweep_global(a, sm, m, g, nent);
@@ -1199,13 +1236,14 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
   const uint32_t n_rec = a.g.cs[a.ncells];
   if (t < n_rec) {
     const uint4 ra = a.g.rec[t].a;
-    if (is_mover(ra, a.base, a.n_ops)) {
+    if (is_walker(a, ra)) {
       const uint32_t slot = ra.z & REC_SLOT;
       const Geom g = a.g.geom[a.space_of[slot]];
       const Mover m = mover_of(ra, a.g.rec[t].b, a.base, g.D);
       a.rank_cnt[m.rank] = sweep_global(a, q, m, g, nent);
     }
-  } else if (t >= a.n_rec && t < a.n_rec + a.n_leaves) {
+  } else if (t >= a.n_rec && t < a.n_rec + (a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves) &&
+             !(a.op_kind && (a.op_kind[a.leave_ops[t - a.n_rec]] & OP_SILENT))) {
     const uint32_t i = a.leave_ops[t - a.n_rec];
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
@@ -1227,11 +1265,11 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
 
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
   if (a.use_lds == 0) {
-    const uint32_t n = a.n_rec + a.n_leaves;
+    const uint32_t n = a.n_rec + (a.n_leaves_dev ? a.n_ops : a.n_leaves);
     if (n) hipLaunchKernelGGL(k_sweep_flat, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
     return;
   }
-  const uint32_t nb = a.ntiles + (a.n_leaves + kSweepBlock - 1) / kSweepBlock;
+  const uint32_t nb = a.ntiles + a.leave_blocks;
   if (!nb) return;
   hipLaunchKernelGGL(k_sweep, dim3(nb), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
 }
@@ -1267,7 +1305,7 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
   if (r >= o.n_ops) return;
   if (o.check_ops) {
     const uint32_t s = o.op_slot[r];
-    if (s < o.cap && o.seq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
+    if (s < o.cap && o.opq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
   }
   uint32_t n;
   if (!ev_fits(o.g, &n)) return;

@@ -131,7 +131,9 @@ struct gwaoi_mgr {
   const uint32_t* dv_slot = nullptr;
   const float* dv_x = nullptr;
   const float* dv_z = nullptr;
+  const uint8_t* dv_kind = nullptr;  // mixed device batch (gwaoi_stage_ops_device), else null
   uint32_t dv_n = 0;
+  bool dev_managed = false;          // presence lives on the device only (mixed device batches)
 
   // ---- device state ----
   float *pos_x = nullptr, *pos_z = nullptr, *old_x = nullptr, *old_z = nullptr;
@@ -426,8 +428,10 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   a.op_slot = dev ? m->dv_slot : m->d_op_slot;
   a.op_x = dev ? m->dv_x : m->d_op_x;
   a.op_z = dev ? m->dv_z : m->d_op_z;
-  a.op_kind = dev ? nullptr : m->d_op_kind;
-  a.op_space = m->d_op_space;
+  const bool dev_mixed = dev && m->dv_kind;
+  a.op_kind = dev ? m->dv_kind : m->d_op_kind;
+  a.op_space = dev ? nullptr : m->d_op_space;
+  a.leaves = dev_mixed ? m->d_leaves : nullptr;
   a.n_ops = n_ops;
   a.base = base;
   a.cap = m->cap;
@@ -465,7 +469,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
     s.ntiles = G.ntiles;
     s.ncells = G.ncells;
-    s.n_rec = n_start + n_new;  // upper bound on records (main + ghost)
+    s.n_rec = dev_mixed ? n_start + n_ops : n_start + n_new;  // upper bound on records (main + ghost)
     s.use_lds = m->sweep_lds;
     s.old_x = m->old_x;
     s.old_z = m->old_z;
@@ -474,8 +478,12 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.base = base;
     s.n_ops = n_ops;
     s.op_slot = a.op_slot;
+    s.op_kind = a.op_kind;
     s.leave_ops = m->d_leaves;
     s.n_leaves = dev ? 0 : m->n_leaves;
+    s.n_leaves_dev = dev_mixed ? m->ctr + gw::CTR_LEAVES : nullptr;
+    s.leave_blocks = dev_mixed ? std::min<uint32_t>(256u, (n_ops + gw::sweep_block() - 1) / gw::sweep_block())
+                               : (s.n_leaves + gw::sweep_block() - 1) / gw::sweep_block();
     s.ev_tmp = m->ev_tmp;
     s.ev_cap = m->tmp_cap;
     s.rank_cnt = m->rank_cnt;
@@ -498,7 +506,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     o.ctr_next = m->ctr_buf + (m->ctr_sel ^ 1) * gw::CTR_N;
     o.grid_total = m->grid[ng].cs + m->grid[ng].ncells;
     o.op_slot = a.op_slot;
-    o.seq = m->seq;
+    o.opq = m->opq;
     o.base = base;
     o.cap = m->cap;
     o.check_ops = dev ? 1 : 0;
@@ -510,7 +518,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     if (m->h_ctr[gw::CTR_ERR]) {
       m->broken = true;
       set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
-              "capacity); the manager is unusable",
+              "capacity, 8=Enter of a present slot); the manager is unusable",
               m->h_ctr[gw::CTR_ERR]);
       return GWAOI_ERR_DEVICE_CHECK;
     }
@@ -555,7 +563,9 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->dv_slot = nullptr;
   m->dv_x = m->dv_z = nullptr;
   m->pass_id++;
+  if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
   m->n_present_dev = m->n_present;
+  m->dv_kind = nullptr;
   return GWAOI_OK;
 }
 
@@ -566,6 +576,15 @@ int check_mgr(const gwaoi_mgr* m) {
   }
   if (m->broken) {
     set_err("manager is unusable after a failed device-staged batch");
+    return GWAOI_ERR_STATE;
+  }
+  return GWAOI_OK;
+}
+
+int host_staging_ok(const gwaoi_mgr* m) {
+  if (m->dev_managed) {
+    set_err("this manager takes mixed device batches (gwaoi_stage_ops_device): its presence state is on the "
+            "device, host-staged Enter/Leave/Moved are not accepted");
     return GWAOI_ERR_STATE;
   }
   return GWAOI_OK;
@@ -812,6 +831,7 @@ int gwaoi_set_stream(gwaoi_mgr* m, void* s) {
 
 int gwaoi_enter_space(gwaoi_mgr* m, uint32_t space, uint32_t slot, float x, float z) {
   RCHK(check_mgr(m));
+  RCHK(host_staging_ok(m));
   if (slot >= m->cap || space >= m->nspaces) {
     set_err("enter: slot %u / space %u out of range", slot, space);
     return GWAOI_ERR_INVALID;
@@ -845,6 +865,7 @@ int gwaoi_stage_enters(gwaoi_mgr* m, uint32_t space, const uint32_t* slots, cons
 
 int gwaoi_leave(gwaoi_mgr* m, uint32_t slot) {
   RCHK(check_mgr(m));
+  RCHK(host_staging_ok(m));
   if (slot >= m->cap) {
     set_err("leave: slot %u out of range", slot);
     return GWAOI_ERR_INVALID;
@@ -863,6 +884,7 @@ int gwaoi_leave(gwaoi_mgr* m, uint32_t slot) {
 
 int gwaoi_moved(gwaoi_mgr* m, uint32_t slot, float x, float z) {
   RCHK(check_mgr(m));
+  RCHK(host_staging_ok(m));
   if (slot >= m->cap) {
     set_err("moved: slot %u out of range", slot);
     return GWAOI_ERR_INVALID;
@@ -904,6 +926,28 @@ int gwaoi_stage_moves_device(gwaoi_mgr* m, const uint32_t* d_slots, const float*
   m->dv_slot = d_slots;
   m->dv_x = d_x;
   m->dv_z = d_z;
+  m->dv_n = n;
+  return GWAOI_OK;
+}
+
+int gwaoi_stage_ops_device(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                           const uint8_t* d_kinds, uint32_t n) {
+  RCHK(check_mgr(m));
+  if (n && (!d_slots || !d_x || !d_z || !d_kinds)) {
+    set_err("stage_ops_device: null array");
+    return GWAOI_ERR_INVALID;
+  }
+  if (n > m->cap) {
+    set_err("stage_ops_device: %u ops > capacity %u", n, m->cap);
+    return GWAOI_ERR_INVALID;
+  }
+  RCHK(set_dev(m));
+  if (m->n_ops || m->dv_n) RCHK(run_pass(m, true));
+  m->dev_managed = true;
+  m->dv_slot = d_slots;
+  m->dv_x = d_x;
+  m->dv_z = d_z;
+  m->dv_kind = d_kinds;
   m->dv_n = n;
   return GWAOI_OK;
 }

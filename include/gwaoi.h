@@ -107,6 +107,21 @@ int gwaoi_stage_moves(gwaoi_mgr* mgr, const uint32_t* slots, const float* x, con
 int gwaoi_stage_moves_device(gwaoi_mgr* mgr, const uint32_t* d_slots, const float* d_x, const float* d_z,
                              uint32_t n);
 
+/* Mixed Enter/Leave/Moved batch from DEVICE arrays: kinds[i] is GWAOI_OP_MOVE, GWAOI_OP_ENTER (into
+ * Space 0) or GWAOI_OP_LEAVE, optionally | GWAOI_OP_SILENT: the op is applied (it changes the relation
+ * and is seen by every later op) but none of its own mover's events are emitted. SILENT is how a
+ * GPU holding a halo copy of an entity owned by another GPU applies that entity's op without
+ * reporting its events twice (X-strip partition, include/gwaoi_strips.h). Validated on the device
+ * (Enter of a present slot, Moved/Leave of an absent one, a slot twice -> GWAOI_ERR_DEVICE_CHECK).
+ * A manager that has taken a mixed device batch keeps its presence state on the device only: the
+ * host-staged calls above then return GWAOI_ERR_STATE. */
+#define GWAOI_OP_MOVE 0u
+#define GWAOI_OP_ENTER 1u
+#define GWAOI_OP_LEAVE 2u
+#define GWAOI_OP_SILENT 0x80u
+int gwaoi_stage_ops_device(gwaoi_mgr* mgr, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                           const uint8_t* d_kinds, uint32_t n);
+
 /* Apply every staged op; blocks until the events are on the host (or in device memory, see flags). */
 #define GWAOI_TICK_DEVICE_EVENTS 1u /* leave events in device memory (no D2H copy) */
 int gwaoi_tick(gwaoi_mgr* mgr, gwaoi_events* out);

@@ -284,3 +284,54 @@ def test_config2_full_size_two_ticks(gpu, po):
         got = eng.tick()
         assert_same(got, want, f"1M tick {t}")
         assert len(got) > 10000
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_device_mixed_ops_with_silent(gpu, po, seed):
+    """gwaoi_stage_ops_device: Enter/Leave/Moved from device arrays in one batch, some ops SILENT
+    (applied, their mover's events not reported). Expected: the oracle's events for the same call
+    sequence minus those raised by silent ops; the relation is unaffected by silence."""
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine
+    case = H.case_random_ops(seed=500 + seed, n=1500, nticks=8, ops_per_tick=1200, world=600.0, dist=60.0,
+                             dup=False)
+    rng = np.random.default_rng(seed)
+    eng = Engine(case["dist"], capacity=case["cap"])
+    orc = po.XZListOracle(case["dist"], case["cap"])
+    cap = case["cap"]
+    bs, bx, bz, bk = DeviceBuffer(4 * cap), DeviceBuffer(4 * cap), DeviceBuffer(4 * cap), DeviceBuffer(cap)
+    for t, ops in enumerate(case["ticks"]):
+        kinds = np.asarray([o[0] for o in ops], np.uint8)
+        silent = rng.random(len(ops)) < 0.3
+        bs.upload(np.asarray([o[1] for o in ops], np.uint32))
+        bx.upload(np.asarray([o[2] for o in ops], np.float32))
+        bz.upload(np.asarray([o[3] for o in ops], np.float32))
+        bk.upload(kinds | np.where(silent, _lib.GWAOI_OP_SILENT, 0).astype(np.uint8))
+        want = H.oracle_tick(orc, ops)
+        loud = {o[1] for o, sl in zip(ops, silent) if not sl}
+        want = want[np.isin(want[:, 0], list(loud))] if len(want) else want
+        eng.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, len(ops))
+        got = eng.tick()
+        assert_same(got, want, f"mixed tick {t}")
+    rg, ro = eng.relation(), orc.relation()
+    assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1])
+    with pytest.raises(_lib.GwaoiError) as e:  # host staging is refused once presence lives on the device
+        eng.moved(0, 0.0, 0.0)
+    assert e.value.code == _lib.GWAOI_ERR_STATE
+
+
+def test_device_mixed_ops_validation(gpu):
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine
+    eng = Engine(100.0, 16)
+    bs, bx, bk = DeviceBuffer(64), DeviceBuffer(64), DeviceBuffer(16)
+    bs.upload(np.asarray([1, 2], np.uint32))
+    bx.upload(np.zeros(2, np.float32))
+    bk.upload(np.asarray([_lib.GWAOI_OP_ENTER, _lib.GWAOI_OP_ENTER], np.uint8))
+    eng.stage_ops_device(bs.ptr, bx.ptr, bx.ptr, bk.ptr, 2)
+    assert eng.tick().tolist() == [[2, 1 | H.EV_ENTER]]
+    bk.upload(np.asarray([_lib.GWAOI_OP_ENTER], np.uint8))  # slot 1 is present: Enter is misuse
+    eng.stage_ops_device(bs.ptr, bx.ptr, bx.ptr, bk.ptr, 1)
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng.tick()
+    assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK
