@@ -40,6 +40,24 @@ TOOL_SYMBOLS = (
 )
 
 
+# include/gwaoi_strips.h (X-strip partition over several GPUs)
+STRIP_SYMBOLS = (
+    "gwaoi_strip_init_walk", "gwaoi_strip_walk", "gwaoi_strip_ingest", "gwaoi_strip_select",
+    "gwaoi_strip_absorb", "gwaoi_strip_emit", "gwaoi_strip_scratch_words",
+)
+
+
+class StripGeom(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint32),
+        ("xa", ctypes.c_float), ("xb", ctypes.c_float),
+        ("ra", ctypes.c_float), ("rb", ctypes.c_float),
+        ("left_hi", ctypes.c_float), ("right_lo", ctypes.c_float),
+        ("max_step", ctypes.c_float),
+        ("has_left", ctypes.c_int32), ("has_right", ctypes.c_int32),
+    ]
+
+
 class GwaoiError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"gwaoi error {code}: {msg}")
@@ -135,6 +153,13 @@ def load(path: str = SO_PATH):
         "gwaoi_debug_set_cells_per_dist": ([vp, f32], ctypes.c_int),
         "gwaoi_debug_set_sweep_lds": ([vp, ctypes.c_int], ctypes.c_int),
         "gwaoi_debug_read_stamps": ([vp, ctypes.c_size_t], ctypes.c_int),
+        "gwaoi_strip_init_walk": ([vp, vp, vp, vp, vp, u64, f32], ctypes.c_int),
+        "gwaoi_strip_walk": ([vp, vp, vp, vp, vp, vp, vp, u64, u64, f32, f32, vp], ctypes.c_int),
+        "gwaoi_strip_ingest": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),
+        "gwaoi_strip_select": ([vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp], ctypes.c_int),
+        "gwaoi_strip_absorb": ([vp, vp, vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_strip_emit": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "gwaoi_strip_scratch_words": ([u32], ctypes.c_size_t),
         "gwaoi_debug_sweep_occupancy": ([ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
                                         ctypes.c_int),
     }

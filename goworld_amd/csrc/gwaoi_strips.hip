@@ -1,0 +1,298 @@
+// gwaoi_strips.hip — per-GPU kernels of the X-strip partition (include/gwaoi_strips.h; host side in
+// goworld_amd/strips.py). State is indexed by global entity id; every pass is a flat, coalesced sweep
+// over the n ids or over a received record list. The id-ordered op list is a stream compaction
+// (block counts -> scan -> block-local scan and write), so the manager sees the global op order.
+#include <hip/hip_runtime.h>
+
+#include "gwaoi.h"
+#include "gwaoi_internal.h"
+#include "gwaoi_strips.h"
+#include "gwaoi_workload.h"
+
+namespace gw {
+namespace {
+
+constexpr int kSBlock = 256;
+constexpr int kSItems = 16;  // ids per thread in the compaction (one uint4 of flags)
+constexpr uint32_t kSChunk = kSBlock * kSItems;
+
+__device__ __forceinline__ bool in_range(float x, float lo, float hi) { return x >= lo && x < hi; }
+
+// one atomic per wave for the lanes with `pred`; returns this lane's slot
+__device__ __forceinline__ uint32_t wave_append_s(uint32_t* ctr, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if (!m) return 0u;
+  const int leader = __ffsll((long long)m) - 1;
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+__device__ __forceinline__ uint32_t block_scan_s(uint32_t v, uint32_t* total) {
+  __shared__ uint32_t ws[kSBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kSBlock / 64; ++k) {
+    pre += k < w ? ws[k] : 0u;
+    tot += ws[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc - v;
+}
+
+__global__ void __launch_bounds__(kSBlock) k_strip_init_walk(gwaoi_strip_geom g, uint8_t* flags, float* ex, float* ez,
+                                                             uint64_t seed, float L) {
+  const uint32_t i = blockIdx.x * kSBlock + threadIdx.x;
+  if (i >= g.n) return;
+  const float x = gww_init_coord(seed, g.n, i, 0, L), z = gww_init_coord(seed, g.n, i, 1, L);
+  uint8_t f = 0;
+  if (in_range(x, g.ra, g.rb)) {
+    f |= GWAOI_STRIP_END;
+    ex[i] = x;
+    ez[i] = z;
+  }
+  if (in_range(x, g.xa, g.xb)) f |= GWAOI_STRIP_OWNED;
+  flags[i] = f;
+}
+
+__global__ void __launch_bounds__(kSBlock) k_strip_walk(gwaoi_strip_geom g, uint8_t* flags, const float* sx,
+                                                        const float* sz, float* ex, float* ez, uint64_t seed,
+                                                        uint64_t tick, float L, float step, uint32_t* err) {
+  const uint32_t i = blockIdx.x * kSBlock + threadIdx.x;
+  if (i >= g.n) return;
+  const uint8_t f = flags[i];
+  if (!(f & GWAOI_STRIP_OWNED)) return;
+  const float x0 = sx[i];
+  const float x = gww_step_coord(x0, seed, tick, g.n, i, 0, L, step);
+  const float z = gww_step_coord(sz[i], seed, tick, g.n, i, 1, L, step);
+  if (!(fabsf(x - x0) <= g.max_step)) atomicOr(err, GWAOI_STRIP_ERR_STEP);
+  ex[i] = x;
+  ez[i] = z;
+  flags[i] = f | GWAOI_STRIP_END;
+}
+
+__global__ void __launch_bounds__(kSBlock) k_strip_ingest(gwaoi_strip_geom g, uint8_t* flags, const float* sx,
+                                                          float* ex, float* ez, const uint32_t* ids,
+                                                          const float* xs, const float* zs, uint32_t n,
+                                                          uint32_t* err) {
+  const uint32_t k = blockIdx.x * kSBlock + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t i = ids[k];
+  if (i >= g.n || !(flags[i] & GWAOI_STRIP_OWNED)) {
+    atomicOr(err, GWAOI_STRIP_ERR_NOT_OWNED);
+    return;
+  }
+  const float x = xs[k];
+  if (!(fabsf(x - sx[i]) <= g.max_step)) atomicOr(err, GWAOI_STRIP_ERR_STEP);
+  ex[i] = x;
+  ez[i] = zs[k];
+  flags[i] |= GWAOI_STRIP_END;
+}
+
+__global__ void __launch_bounds__(kSBlock) k_strip_select(gwaoi_strip_geom g, const uint8_t* flags, const float* sx,
+                                                          const float* ex, const float* ez, uint4* left,
+                                                          uint4* right, uint32_t cap, uint32_t* counts,
+                                                          uint32_t* err) {
+  const uint32_t i = blockIdx.x * kSBlock + threadIdx.x;
+  bool sl = false, sr = false;
+  float x1 = 0.f, z1 = 0.f;
+  if (i < g.n) {
+    const uint8_t f = flags[i];
+    if ((f & GWAOI_STRIP_OWNED) && (f & GWAOI_STRIP_END)) {
+      const float x0 = sx[i];
+      x1 = ex[i];
+      z1 = ez[i];
+      sl = g.has_left && (x0 < g.left_hi || x1 < g.left_hi);
+      sr = g.has_right && (x0 >= g.right_lo || x1 >= g.right_lo);
+    }
+  }
+  const uint4 rec = make_uint4(i, __float_as_uint(x1), __float_as_uint(z1), 0u);
+  const uint32_t pl = wave_append_s(&counts[0], sl);
+  const uint32_t pr = wave_append_s(&counts[1], sr);
+  if (sl) {
+    if (pl < cap) left[pl] = rec;
+    else atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
+  }
+  if (sr) {
+    if (pr < cap) right[pr] = rec;
+    else atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
+  }
+}
+
+__global__ void __launch_bounds__(kSBlock) k_strip_absorb(uint8_t* flags, float* ex, float* ez, const uint4* recs,
+                                                          uint32_t n) {
+  const uint32_t k = blockIdx.x * kSBlock + threadIdx.x;
+  if (k >= n) return;
+  const uint4 r = recs[k];
+  ex[r.x] = __uint_as_float(r.y);
+  ez[r.x] = __uint_as_float(r.z);
+  flags[r.x] |= GWAOI_STRIP_END;
+}
+
+// 16 flags of thread `t` of block `b` (ids b * kSChunk + t * 16 ...), zero beyond n
+__device__ __forceinline__ void load_flags16(const uint8_t* flags, uint32_t n, uint32_t i0, uint8_t (&f)[kSItems]) {
+  if (i0 + kSItems <= n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(flags + i0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < kSItems; ++k) f[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  } else {
+#pragma unroll
+    for (int k = 0; k < kSItems; ++k) f[k] = (i0 + k < n) ? flags[i0 + k] : (uint8_t)0;
+  }
+}
+
+__device__ __forceinline__ bool has_op(uint8_t f) { return (f & (GWAOI_STRIP_PRESENT | GWAOI_STRIP_END)) != 0; }
+
+__global__ void __launch_bounds__(kSBlock) k_strip_count(const uint8_t* flags, uint32_t n, uint32_t* blk) {
+  uint8_t f[kSItems];
+  load_flags16(flags, n, blockIdx.x * kSChunk + threadIdx.x * kSItems, f);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kSItems; ++k) c += has_op(f[k]) ? 1u : 0u;
+  uint32_t tot;
+  block_scan_s(c, &tot);
+  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kSBlock) k_strip_emit(gwaoi_strip_geom g, uint8_t* flags, float* sx, float* sz,
+                                                        const float* ex, const float* ez, const uint32_t* blk,
+                                                        uint32_t* ids, float* ox, float* oz, uint8_t* kinds) {
+  const uint32_t i0 = blockIdx.x * kSChunk + threadIdx.x * kSItems;
+  uint8_t f[kSItems];
+  load_flags16(flags, g.n, i0, f);
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kSItems; ++k) c += has_op(f[k]) ? 1u : 0u;
+  uint32_t tot;
+  uint32_t pos = blk[blockIdx.x] + block_scan_s(c, &tot);
+  uint8_t nf[kSItems];
+#pragma unroll
+  for (int k = 0; k < kSItems; ++k) {
+    const uint32_t i = i0 + k;
+    nf[k] = 0;
+    if (!has_op(f[k])) continue;
+    const bool p = f[k] & GWAOI_STRIP_PRESENT, e = f[k] & GWAOI_STRIP_END;
+    uint8_t kind = p ? (e ? GWAOI_OP_MOVE : GWAOI_OP_LEAVE) : GWAOI_OP_ENTER;
+    if (!(f[k] & GWAOI_STRIP_OWNED)) kind |= GWAOI_OP_SILENT;
+    float x = 0.f, z = 0.f;
+    if (e) {
+      x = ex[i];
+      z = ez[i];
+      sx[i] = x;
+      sz[i] = z;
+      nf[k] = GWAOI_STRIP_PRESENT | (in_range(x, g.xa, g.xb) ? GWAOI_STRIP_OWNED : 0);
+    }
+    ids[pos] = i;
+    ox[pos] = x;
+    oz[pos] = z;
+    kinds[pos] = kind;
+    ++pos;
+  }
+  if (i0 + kSItems <= g.n) {
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < kSItems; ++k) w[k >> 2] |= (uint32_t)nf[k] << (8 * (k & 3));
+    *reinterpret_cast<uint4*>(flags + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kSItems; ++k)
+      if (i0 + k < g.n) flags[i0 + k] = nf[k];
+  }
+}
+
+inline dim3 blocks_for(uint32_t n) { return dim3((n + kSBlock - 1) / kSBlock); }
+inline uint32_t emit_blocks(uint32_t n) { return (n + kSChunk - 1) / kSChunk; }
+
+}  // namespace
+}  // namespace gw
+
+extern "C" {
+
+int gwaoi_strip_init_walk(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* ex, float* ez, uint64_t seed,
+                          float L) {
+  if (!g || !flags || !ex || !ez) return GWAOI_ERR_INVALID;
+  if (g->n)
+    hipLaunchKernelGGL(gw::k_strip_init_walk, gw::blocks_for(g->n), dim3(gw::kSBlock), 0, (hipStream_t)stream, *g,
+                       flags, ex, ez, seed, L);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_walk(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, const float* sx, const float* sz,
+                     float* ex, float* ez, uint64_t seed, uint64_t tick, float L, float step, uint32_t* d_err) {
+  if (!g || !flags || !sx || !sz || !ex || !ez || !d_err) return GWAOI_ERR_INVALID;
+  if (g->n)
+    hipLaunchKernelGGL(gw::k_strip_walk, gw::blocks_for(g->n), dim3(gw::kSBlock), 0, (hipStream_t)stream, *g, flags,
+                       sx, sz, ex, ez, seed, tick, L, step, d_err);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_ingest(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, const float* sx, float* ex, float* ez,
+                       const uint32_t* d_ids, const float* d_x, const float* d_z, uint32_t n, uint32_t* d_err) {
+  if (!g || !flags || !sx || !ex || !ez || !d_err || (n && (!d_ids || !d_x || !d_z))) return GWAOI_ERR_INVALID;
+  if (n)
+    hipLaunchKernelGGL(gw::k_strip_ingest, gw::blocks_for(n), dim3(gw::kSBlock), 0, (hipStream_t)stream, *g, flags,
+                       sx, ex, ez, d_ids, d_x, d_z, n, d_err);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_select(void* stream, const gwaoi_strip_geom* g, const uint8_t* flags, const float* sx, const float* ex,
+                       const float* ez, uint32_t* d_left, uint32_t* d_right, uint32_t cap, uint32_t* d_counts,
+                       uint32_t* d_err) {
+  if (!g || !flags || !sx || !ex || !ez || !d_left || !d_right || !d_counts || !d_err) return GWAOI_ERR_INVALID;
+  if (hipMemsetAsync(d_counts, 0, 2 * sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return GWAOI_ERR_HIP;
+  if (g->n)
+    hipLaunchKernelGGL(gw::k_strip_select, gw::blocks_for(g->n), dim3(gw::kSBlock), 0, (hipStream_t)stream, *g, flags,
+                       sx, ex, ez, reinterpret_cast<uint4*>(d_left), reinterpret_cast<uint4*>(d_right), cap, d_counts,
+                       d_err);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_absorb(void* stream, uint8_t* flags, float* ex, float* ez, const uint32_t* d_recs, uint32_t n) {
+  if (!flags || !ex || !ez || (n && !d_recs)) return GWAOI_ERR_INVALID;
+  if (n)
+    hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n), dim3(gw::kSBlock), 0, (hipStream_t)stream, flags, ex, ez,
+                       reinterpret_cast<const uint4*>(d_recs), n);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+size_t gwaoi_strip_scratch_words(uint32_t n) {
+  const uint32_t nb = gw::emit_blocks(n);
+  return (size_t)nb + 1 + gw::scan_part_words(nb + 1) + 4;
+}
+
+int gwaoi_strip_emit(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* sx, float* sz, const float* ex,
+                     const float* ez, uint32_t* d_ids, float* d_x, float* d_z, uint8_t* d_kinds, uint32_t* d_scratch,
+                     uint32_t* d_n_ops) {
+  if (!g || !flags || !sx || !sz || !ex || !ez || !d_ids || !d_x || !d_z || !d_kinds || !d_scratch || !d_n_ops)
+    return GWAOI_ERR_INVALID;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t nb = gw::emit_blocks(g->n);
+  uint32_t* blk = d_scratch;  // [nb + 1]
+  gw::ScanCtx sc;
+  sc.status = d_scratch + nb + 1;
+  if (hipMemsetAsync(blk + nb, 0, sizeof(uint32_t), st) != hipSuccess) return GWAOI_ERR_HIP;
+  if (nb) {
+    hipLaunchKernelGGL(gw::k_strip_count, dim3(nb), dim3(gw::kSBlock), 0, st, flags, g->n, blk);
+    gw::launch_scan(sc, blk, nb + 1, st);
+    hipLaunchKernelGGL(gw::k_strip_emit, dim3(nb), dim3(gw::kSBlock), 0, st, *g, flags, sx, sz, ex, ez,
+                       (const uint32_t*)blk, d_ids, d_x, d_z, d_kinds);
+  }
+  if (hipMemcpyAsync(d_n_ops, blk + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return GWAOI_ERR_HIP;
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+}  // extern "C"

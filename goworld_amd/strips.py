@@ -1,0 +1,220 @@
+"""One Space partitioned into X-strips over several GPUs — host side of include/gwaoi_strips.h.
+
+SURVEY.md §8(e), config 4: a huge open world split into vertical strips, one per GPU (one process
+per GPU), halo copies of the entities near each strip edge exchanged every tick with the two
+neighbouring GPUs (torch.distributed point-to-point: RCCL over xGMI with the "nccl" backend, gloo in
+the CPU tests). The protocol and why it reproduces one manager's events exactly are in
+include/gwaoi_strips.h; in short, GPU r applies the op of every entity of its region in global id
+order, its owned entities loud and halo copies GWAOI_OP_SILENT, and reports the events of its owned
+movers only.
+
+torch is plumbing here (device buffers, the stream, the collectives); every per-entity step runs in
+libgwaoi's HIP kernels. A node is driven in two halves per tick so that several nodes can share one
+process (LoopbackExchange, the single-GPU tests) or run one per process (exchange_dist):
+    left, right = node.prepare(t)        # owned end positions + the records the neighbours need
+    left_in, right_in = <exchange>       # what the neighbours sent
+    events = node.finish(left_in, right_in)
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+from .engine import Engine
+
+f32 = np.float32
+
+
+class StripLayout:
+    """Equal-width strips over [0, L) in x; the halo covers D + the largest per-tick step."""
+
+    def __init__(self, world: int, L: float, dist: float, max_step: float, margin: Optional[float] = None):
+        self.world, self.L, self.dist, self.max_step = int(world), float(L), float(dist), float(max_step)
+        # query boxes are widened by (|c| + D) * 2^-20 before they become cell ranges; the halo keeps a
+        # margin far above that and above float rounding of the bounds
+        if margin is None:
+            margin = max(1.0, (self.L + self.dist) * 2.0 ** -16)
+        self.halo = float(f32(self.dist + self.max_step + margin))
+        if self.world > 1 and self.L / self.world <= 2 * self.halo + self.max_step:
+            raise ValueError(f"strips of width {self.L / self.world} are too narrow for a halo of {self.halo}")
+
+    def bounds(self, rank: int) -> Tuple[float, float]:
+        xa = -math.inf if rank == 0 else float(f32(rank * self.L / self.world))
+        xb = math.inf if rank == self.world - 1 else float(f32((rank + 1) * self.L / self.world))
+        return xa, xb
+
+    def owner_of(self, x: np.ndarray) -> np.ndarray:
+        """Strip index of each x (the same float32 comparisons as the kernels)."""
+        edges = np.asarray([self.bounds(r)[0] for r in range(1, self.world)], dtype=f32)
+        return np.searchsorted(edges, np.asarray(x, dtype=f32), side="right")
+
+    def geom(self, rank: int, n: int) -> _lib.StripGeom:
+        xa, xb = self.bounds(rank)
+        H = f32(self.halo)
+        g = _lib.StripGeom()
+        g.n = n
+        g.xa, g.xb = xa, xb
+        g.ra, g.rb = float(f32(f32(xa) - H)), float(f32(f32(xb) + H))
+        g.left_hi = float(f32(f32(xa) + H))   # the left neighbour's region ends at its xb + H = xa + H
+        g.right_lo = float(f32(f32(xb) - H))  # the right neighbour's region starts at xb - H
+        g.max_step = float(f32(self.max_step))
+        g.has_left = 1 if rank > 0 else 0
+        g.has_right = 1 if rank < self.world - 1 else 0
+        return g
+
+
+def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class StripNode:
+    """The strip of GPU `rank`: per-id state, the region's gwaoi manager, the per-tick kernels."""
+
+    def __init__(self, layout: StripLayout, rank: int, n: int, device: int = 0, seed: int = 0x5EED0004,
+                 halo_cap: Optional[int] = None):
+        self.layout, self.rank, self.n, self.seed = layout, int(rank), int(n), int(seed)
+        self.g = layout.geom(rank, n)
+        self.device = torch.device("cuda", device)
+        self._L = _lib.load()
+        dev = self.device
+        u8, i32, fl = torch.uint8, torch.int32, torch.float32
+        self.flags = torch.zeros(n, dtype=u8, device=dev)
+        self.sx, self.sz, self.ex, self.ez = (torch.zeros(n, dtype=fl, device=dev) for _ in range(4))
+        self.ids = torch.zeros(n, dtype=i32, device=dev)
+        self.ox, self.oz = torch.zeros(n, dtype=fl, device=dev), torch.zeros(n, dtype=fl, device=dev)
+        self.kinds = torch.zeros(n, dtype=u8, device=dev)
+        # the halo of one side holds ~ 2 H L density entities; keep room for several times that
+        cap = halo_cap or max(4096, int(8 * layout.halo * layout.L * n / (layout.L * layout.L)) + 4096)
+        self.cap = min(cap, n) if n else 1
+        self.left = torch.zeros((self.cap, 4), dtype=i32, device=dev)
+        self.right = torch.zeros((self.cap, 4), dtype=i32, device=dev)
+        self.counts = torch.zeros(4, dtype=i32, device=dev)  # [left, right, n_ops, err]
+        self.scratch = torch.zeros(int(self._L.gwaoi_strip_scratch_words(n)), dtype=i32, device=dev)
+        self.stream = torch.cuda.current_stream(dev)
+        lo = max(self.g.ra, 0.0)
+        hi = min(self.g.rb, layout.L)
+        self.eng = Engine(layout.dist, capacity=n, device=device, bounds=(lo, 0.0, hi, layout.L))
+        self.eng.set_stream(self.stream.cuda_stream)
+        self.tick_no = 0
+
+    # ---- raw kernel calls ----
+    def _s(self):
+        return ctypes.c_void_p(self.stream.cuda_stream)
+
+    def _g(self):
+        return ctypes.byref(self.g)
+
+    def _err(self):
+        return ctypes.c_void_p(self.counts.data_ptr() + 12)
+
+    def _emit_and_tick(self, host_events: bool):
+        L = self._L
+        check(L.gwaoi_strip_emit(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz), _ptr(self.ex),
+                                 _ptr(self.ez), _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds),
+                                 _ptr(self.scratch), ctypes.c_void_p(self.counts.data_ptr() + 8)))
+        c = self.counts.cpu()  # synchronises the stream
+        if int(c[3]):
+            raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, f"strip {self.rank}: protocol check failed (flags {int(c[3])})")
+        n_ops = int(c[2])
+        self.last_ops = n_ops
+        if n_ops:
+            self.eng.stage_ops_device(self.ids.data_ptr(), self.ox.data_ptr(), self.oz.data_ptr(),
+                                      self.kinds.data_ptr(), n_ops)
+        return self.eng.tick() if host_events else self.eng.tick_device()
+
+    # ---- protocol ----
+    def start(self, host_events: bool = False):
+        """Tick 0: every entity of the region enters (the seeded workload's initial placement)."""
+        check(self._L.gwaoi_strip_init_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
+                                            ctypes.c_uint64(self.seed), ctypes.c_float(self.layout.L)))
+        self.tick_no = 0
+        return self._emit_and_tick(host_events)
+
+    def prepare(self, t: int, step: float = 1.0, moves: Optional[Tuple[torch.Tensor, ...]] = None):
+        """End positions of the owned entities (the seeded walk's tick t, or `moves` = (ids, x, z)
+        device tensors) and the records each neighbour needs; returns (left, right) device tensors."""
+        L = self._L
+        if moves is None:
+            check(L.gwaoi_strip_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz),
+                                     _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed), ctypes.c_uint64(t),
+                                     ctypes.c_float(self.layout.L), ctypes.c_float(step), self._err()))
+        else:
+            ids, x, z = moves
+            check(L.gwaoi_strip_ingest(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
+                                       _ptr(self.ez), _ptr(ids), _ptr(x), _ptr(z), int(ids.numel()), self._err()))
+        check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
+                                   _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
+                                   ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+        c = self.counts.cpu()
+        if int(c[3]):
+            raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, f"strip {self.rank}: protocol check failed (flags {int(c[3])})")
+        self.tick_no = t
+        return self.left[: int(c[0])], self.right[: int(c[1])]
+
+    def finish(self, left_in: torch.Tensor, right_in: torch.Tensor, host_events: bool = False):
+        """Absorb the neighbours' records, run the tick; returns the manager's Events (device) or the
+        (n, 2) host array of the owned movers' events in canonical order."""
+        for recs in (left_in, right_in):
+            if recs is not None and recs.numel():
+                recs = recs.to(self.device).contiguous()
+                check(self._L.gwaoi_strip_absorb(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
+                                                 _ptr(recs), int(recs.shape[0])))
+        return self._emit_and_tick(host_events)
+
+    def close(self):
+        self.eng.close()
+
+
+class LoopbackExchange:
+    """Several strips in one process (tests, single-GPU runs): neighbour records handed over directly."""
+
+    @staticmethod
+    def exchange(outs: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> List[Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]]:
+        w = len(outs)
+        return [(outs[r - 1][1] if r > 0 else None, outs[r + 1][0] if r < w - 1 else None) for r in range(w)]
+
+
+def exchange_dist(left_out: torch.Tensor, right_out: torch.Tensor, rank: int, world: int,
+                  via_cpu: bool = False) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """Halo exchange with the two neighbouring ranks over torch.distributed (RCCL with "nccl").
+    Sizes first, then the records; every message carries at least one row so no transfer is empty.
+    via_cpu: stage through host memory (gloo, e.g. several ranks sharing one GPU in a test)."""
+    import torch.distributed as dist
+    dev = left_out.device
+    tdev = torch.device("cpu") if via_cpu else dev
+    peers = [p for p in (rank - 1, rank + 1) if 0 <= p < world]
+    out = {rank - 1: left_out, rank + 1: right_out}
+    sizes_out = {p: torch.tensor([out[p].shape[0]], dtype=torch.int64, device=tdev) for p in peers}
+    sizes_in = {p: torch.zeros(1, dtype=torch.int64, device=tdev) for p in peers}
+    ops = []
+    for p in peers:
+        ops.append(dist.P2POp(dist.isend, sizes_out[p], p))
+        ops.append(dist.P2POp(dist.irecv, sizes_in[p], p))
+    for r in dist.batch_isend_irecv(ops):
+        r.wait()
+    ops = []
+    recv = {}
+    for p in peers:
+        k = int(sizes_in[p].item())
+        recv[p] = torch.zeros((max(1, k), 4), dtype=torch.int32, device=tdev)
+        send = out[p].to(tdev)
+        if send.shape[0] == 0:
+            send = torch.zeros((1, 4), dtype=torch.int32, device=tdev)
+        ops.append(dist.P2POp(dist.isend, send.contiguous(), p))
+        ops.append(dist.P2POp(dist.irecv, recv[p], p))
+    for r in dist.batch_isend_irecv(ops):
+        r.wait()
+    res = []
+    for p in (rank - 1, rank + 1):
+        if p in recv:
+            k = int(sizes_in[p].item())
+            res.append(recv[p][:k].to(dev))
+        else:
+            res.append(None)
+    return res[0], res[1]

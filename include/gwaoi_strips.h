@@ -1,0 +1,86 @@
+/*
+ * gwaoi_strips.h — one Space partitioned into X-strips over several GPUs (SURVEY.md §8(e), config 4:
+ * a 16M-entity open world over the 8 GPUs of a node, halo rows exchanged over RCCL/xGMI).
+ *
+ * GPU r owns the entities whose START-of-tick x lies in its strip [xa, xb). Its REGION is the strip
+ * widened by a halo H = D + max_step + margin on each side: every entity that can share a box with
+ * an owned entity during the tick (either position, either perspective) has its start or end x in
+ * the region. GPU r runs one gwaoi manager (slot = global entity id) over the region and applies, in
+ * global id order, the op of every entity whose start or end x is in the region:
+ *     present at the start and at the end  -> Moved
+ *     end only (came into the region)      -> Enter
+ *     start only (left the region)         -> Leave
+ * owned entities loud, halo copies GWAOI_OP_SILENT. The local op order is the global op order, so the
+ * events of owned movers are exactly those of one manager running the whole world (each pair event
+ * is reported once, by the GPU that owns its mover). Entities that enter or leave the region are more
+ * than D away from every owned entity at both ends of the tick (H > D + max_step), so those ops raise
+ * no event for an owned mover. Ownership moves with the entity: next tick's owner is the strip of
+ * this tick's end x, which already holds the entity as a halo copy — no separate migration message.
+ *
+ * Per tick: (1) end positions of owned entities (gwaoi_strip_walk: the bench's seeded walk, or
+ * gwaoi_strip_ingest: external moves); (2) gwaoi_strip_select: owned entities with start or end x
+ * within the neighbours' regions -> two record lists; (3) the host exchanges them with the
+ * neighbours (torch.distributed send/recv = RCCL on xGMI); (4) gwaoi_strip_absorb the received lists;
+ * (5) gwaoi_strip_emit: the op list in id order + the state advance; (6) gwaoi_stage_ops_device +
+ * gwaoi_tick. Host side: goworld_amd/strips.py. All functions enqueue on `stream` (a hipStream_t;
+ * NULL = the null stream) and return at once; counts land in device memory.
+ *
+ * State arrays (device, length g->n): flags (uint8, GWAOI_STRIP_*), sx/sz start-of-tick positions,
+ * ex/ez end-of-tick positions. Exchange records are 4 x uint32: {id, x bits, z bits, 0}.
+ */
+#ifndef GWAOI_STRIPS_H
+#define GWAOI_STRIPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GWAOI_STRIP_PRESENT 1u /* in this GPU's manager at the start of the tick */
+#define GWAOI_STRIP_OWNED 2u   /* start-of-tick x in this GPU's strip */
+#define GWAOI_STRIP_END 4u     /* end-of-tick position known here this tick */
+
+#define GWAOI_STRIP_ERR_STEP 1u     /* an owned entity moved further than max_step in one tick */
+#define GWAOI_STRIP_ERR_NOT_OWNED 2u /* ingest named an entity this GPU does not own */
+#define GWAOI_STRIP_ERR_OVERFLOW 4u  /* a select list exceeded its capacity */
+
+typedef struct {
+  uint32_t n;       /* global entity count: ids 0..n-1 */
+  float xa, xb;     /* own strip: start-of-tick x in [xa, xb) = owned */
+  float ra, rb;     /* own region [ra, rb) = [xa - H, xb + H) (initial halo) */
+  float left_hi;    /* owned entity goes to the left neighbour if its start or end x < left_hi */
+  float right_lo;   /* ... to the right neighbour if its start or end x >= right_lo */
+  float max_step;   /* largest |x_end - x_start| of an owned entity the halo width covers */
+  int32_t has_left, has_right;
+} gwaoi_strip_geom;
+
+/* Tick 0 of the seeded workload (include/gwaoi_workload.h, all n ids): end position of every entity in
+ * the region, OWNED for the strip. The first gwaoi_strip_emit then yields the Enter pass. */
+int gwaoi_strip_init_walk(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* ex, float* ez,
+                          uint64_t seed, float L);
+/* End positions of the owned entities for tick `tick` of the seeded walk (bench workload). */
+int gwaoi_strip_walk(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, const float* sx, const float* sz,
+                     float* ex, float* ez, uint64_t seed, uint64_t tick, float L, float step, uint32_t* d_err);
+/* End positions of owned entities from external moves (ids, x, z in device memory). */
+int gwaoi_strip_ingest(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, const float* sx, float* ex, float* ez,
+                       const uint32_t* d_ids, const float* d_x, const float* d_z, uint32_t n, uint32_t* d_err);
+/* Owned entities to send: d_left / d_right receive up to `cap` records each; d_counts[0..1] their
+ * counts (zeroed here). */
+int gwaoi_strip_select(void* stream, const gwaoi_strip_geom* g, const uint8_t* flags, const float* sx,
+                       const float* ex, const float* ez, uint32_t* d_left, uint32_t* d_right, uint32_t cap,
+                       uint32_t* d_counts, uint32_t* d_err);
+/* Received records: end positions of halo entities. */
+int gwaoi_strip_absorb(void* stream, uint8_t* flags, float* ex, float* ez, const uint32_t* d_recs, uint32_t n);
+/* The tick's op list in id order (ids, x, z, kinds; *d_n_ops = count) and the state advance (flags,
+ * start positions) for the next tick. d_scratch: gwaoi_strip_scratch_words(n) words. */
+int gwaoi_strip_emit(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* sx, float* sz, const float* ex,
+                     const float* ez, uint32_t* d_ids, float* d_x, float* d_z, uint8_t* d_kinds, uint32_t* d_scratch,
+                     uint32_t* d_n_ops);
+size_t gwaoi_strip_scratch_words(uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GWAOI_STRIPS_H */
