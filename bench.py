@@ -1,14 +1,20 @@
 #!/usr/bin/env python3
 """bench.py — BASELINE.json metric: AOI entity-updates/sec + p99 tick latency at 1M entities.
 
-Workload: one Space per GPU, N = 1,000,000 entities, L = 35,000, D = 100,
-seeded random walk (include/gwaoi_workload.h), every entity moves once per tick in ascending slot
-order. A "step" is one tick: stage the N moves (device arrays, inputs resident in HBM) and run the
-AOI pipeline until the tick's events are complete in device memory and their count is on the host.
+Default workload: one Space per GPU, N = 1,000,000 entities, L = 35,000,
+D = 100, seeded random walk (include/gwaoi_workload.h), every entity moves once per tick in ascending
+slot order. A "step" is one tick: stage the N moves (device arrays, inputs resident in HBM) and run
+the AOI pipeline until the tick's events are complete in device memory and their count is on the host.
 
 Multi-GPU (torchrun, one process per GPU): every rank runs its own independent 1M-entity Space
 (seed + rank) — the path shards by Space with no data-path collective ("scaling": "weak"); the only
 collectives are the timing barrier and the max-over-ranks of the elapsed time.
+
+Other workloads (--workload; the JSON line names the one measured):
+  config3  512 Spaces x 2,000 entities per GPU in one manager (4,096 Spaces over 8 GPUs), L = 1,600
+  skew     config 5: 4 Spaces x 1M per GPU, D = 50/100/200/400, 10% of the entities in 64 hotspots
+  strips   config 4: ONE world of 2M entities per GPU (16M, L = 140,000 at 8 GPUs) cut into X-strips,
+           halo records exchanged with the neighbour GPUs every tick (torch.distributed = RCCL/xGMI)
 
 Prints ONE JSON line on rank 0. Also reports: p50/p99 tick latency with events left in HBM and with
 events delivered to host memory (PCIe-inclusive, never `value`), the sweep kernel's roofline, and
@@ -16,6 +22,7 @@ the CPU baseline (oracle (i), the go-aoi XZListAOIManager restatement, on a boun
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -24,6 +31,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "AOI entity-updates/sec (p99 tick latency reported alongside) at 1M entities per Space"
+DATA = "synthetic: seeded random walk of SURVEY.md §8(d) (include/gwaoi_workload.h), generated on device"
+DENSITY = 1_000_000 / 35000.0 ** 2  # entities per unit^2 of every config (config 4: 16M / 140,000^2)
 
 
 def log(*a):
@@ -88,64 +98,42 @@ def load_pmc_traffic():
         return None
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d
+            return json.load(f)
     except Exception:
         return None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--n", type=int, default=1_000_000)
-    ap.add_argument("--L", type=float, default=35000.0)
-    ap.add_argument("--dist", type=float, default=100.0)
-    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
-    ap.add_argument("--latency-ticks", type=int, default=200, help="extra ticks with events delivered to host")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cells-per-dist", type=float, default=None)
-    ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
-    ap.add_argument("--stamps", default=None, help="diagnostic GW_STAMPS build: dump the last sweep's per-block "
-                                                   "phase timestamps to this .npy file")
-    args = ap.parse_args()
+def spaces_workload(args, rank):
+    """(name, n_per, nspaces, dists, L, seed0, nhot, sigma) of a device-staged, all-moving workload."""
+    if args.workload == "config2":
+        return ("config 2: single Space of 1,000,000 entities per GPU, L=35,000, D=100, all moving each tick",
+                args.n, 1, [args.dist], args.L, args.seed + rank, 0, 0.0)
+    if args.workload == "config3":
+        k = args.spaces
+        return (f"config 3: {k} independent dungeon Spaces x 2,000 entities per GPU in one manager "
+                f"(4,096 Spaces over 8 GPUs), L=1,600 each, D=100",
+                2000, k, [100.0] * k, 1600.0, 0x5EED0003 + rank * k, 0, 0.0)
+    if args.workload == "skew":
+        # 10% of the entities in 64 Gaussian hotspots, sigma 55: peak density ~100x the mean
+        # (1,562 per hotspot / (2 pi 55^2) = 0.082 per unit^2 = 100 x 8.2e-4)
+        return ("config 5: skewed crowd, 4 Spaces x 1,000,000 per GPU (D = 50/100/200/400), L=35,000, 10% of the "
+                "entities in 64 Gaussian hotspots (sigma 55: peak density ~100x the mean)",
+                1_000_000, 4, [50.0, 100.0, 200.0, 400.0], 35000.0, 0x5EED0005 + rank * 4, 64, 55.0)
+    raise ValueError(args.workload)
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
 
-    import torch  # first: one HIP runtime per process (see goworld_amd/_lib.py)
-    import torch.distributed as dist
-    have_cuda = torch.cuda.is_available()
-    if world > 1:
-        backend = os.environ.get("GWAOI_DIST_BACKEND", "nccl" if have_cuda else "gloo")
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
-    elif have_cuda:
-        torch.cuda.set_device(local)
+def run_spaces(args, rank, world, dev, sync_all, allmax):
+    import ctypes
 
     import numpy as np
     from goworld_amd import _lib
-    from goworld_amd.engine import DeviceBuffer, Engine, wl_init, wl_iota, wl_step
+    from goworld_amd.engine import DeviceBuffer, Engine, wl_init_spaces, wl_iota, wl_step_spaces
 
-    dev = local
-    n, L, D = args.n, args.L, args.dist
-    seed = args.seed + rank
+    name, n_per, nsp, dists, L, seed0, nhot, sigma = spaces_workload(args, rank)
+    n = n_per * nsp
     W, K, H = args.warmup, args.steps, args.latency_ticks
     T = W + K + H + 1
     L_ = _lib.load()
-
-    def sync_all():
-        _lib.check(L_.gwaoi_dev_sync(dev))
-        if have_cuda:
-            torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
 
     # ---- untimed setup: positions for every tick generated on the device ----
     t_setup = time.perf_counter()
@@ -159,21 +147,24 @@ def main():
     def pz(t):
         return snap.ptr + (2 * t + 1) * 4 * n
 
-    wl_init(dev, px(0), pz(0), n, seed, L)
+    wl_init_spaces(dev, px(0), pz(0), n_per, nsp, seed0, L, nhot, sigma)
     for t in range(1, T):
-        wl_step(dev, px(t - 1), pz(t - 1), px(t), pz(t), n, seed, t, L, 1.0)
-    eng = Engine(D, capacity=n, device=dev, bounds=(0.0, 0.0, L, L))
+        wl_step_spaces(dev, px(t - 1), pz(t - 1), px(t), pz(t), n_per, nsp, seed0, t, L, 1.0)
+    eng = Engine(capacity=n, device=dev, spaces=[(d, (0.0, 0.0, L, L)) for d in dists])
     if args.cells_per_dist:
         eng.debug_set_cells_per_dist(args.cells_per_dist)
     if args.sweep_lds != 1:
         eng._L.gwaoi_debug_set_sweep_lds(eng.handle, args.sweep_lds)
     x0 = snap.download(np.float32, n, 0)
     z0 = snap.download(np.float32, n, 4 * n)
-    eng.stage_enters(np.arange(n, dtype=np.uint32), x0, z0)
+    for sp in range(nsp):
+        s = slice(sp * n_per, (sp + 1) * n_per)
+        eng.stage_enters(np.arange(sp * n_per, (sp + 1) * n_per, dtype=np.uint32), x0[s], z0[s], space=sp)
+    log(f"[rank {rank}] {n} entities staged ({time.perf_counter() - t_setup:.1f}s); running the Enter pass")
     ev0 = eng.tick_device()
     enter_pairs = int(ev0.count)
     del x0, z0
-    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s: {n} entities entered, {enter_pairs} pairs")
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s: {n} entities in {nsp} Spaces, {enter_pairs} pairs")
 
     def tick_dev(t):
         eng.stage_moves_device(slots.ptr, px(t), pz(t), n)
@@ -187,25 +178,18 @@ def main():
     eng.reset_stats()
     sync_all()
     lat = []
-    ev_total = 0
     t0 = time.perf_counter()
     for t in range(W + 1, W + K + 1):
         ts = time.perf_counter()
-        ev = tick_dev(t)
+        tick_dev(t)
         lat.append(time.perf_counter() - ts)
-        ev_total += int(ev.count)
     sync_all()
-    elapsed = time.perf_counter() - t0
+    elapsed = allmax(time.perf_counter() - t0)
     st = eng.stats()
     eng.set_timing(False)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
     log(f"[rank {rank}] timed {K} ticks in {elapsed:.3f}s")
 
     if rank == 0:
-        import ctypes
         occ, ldsb = ctypes.c_int(0), ctypes.c_int(0)
         if L_.gwaoi_debug_sweep_occupancy(dev, ctypes.byref(occ), ctypes.byref(ldsb)) == 0:
             log(f"[rank 0] sweep: {occ.value} resident blocks per CU, {ldsb.value} B LDS per block")
@@ -226,83 +210,230 @@ def main():
     rp, cols = eng.relation()
     nnz = int(len(cols))
     del rp, cols
+    eng.close()
+    if rank != 0:
+        return None
 
-    result = None
-    if rank == 0:
-        ms_step = elapsed / K * 1e3
-        value = n * K * world / elapsed
-        ticks = max(1, st["ticks"])
-        sweep_ms = st["ms_sweep"] / ticks
-        ev_per_tick = st["events"] / ticks
-        # algorithmic bytes of ONE sweep launch (DESIGN.md "Measurement"): every record of the pass's
-        # cell-sorted grid read once (32 B: binned + start state), every cell start once (4 B), the
-        # per-op event count written (4 B per mover), every event staged once (16 B).
-        rec_per_tick = st["grid_records"] / ticks
-        cells = st["grid_cells"] / ticks
-        b_sweep = 32.0 * rec_per_tick + 4.0 * cells + 4.0 * n + 16.0 * ev_per_tick
-        achieved = b_sweep / (sweep_ms * 1e-3) / 1e9
-        pmc = load_pmc_traffic()
-        traffic = None
-        if pmc and pmc.get("n") == n and "sweep_bytes_per_launch" in pmc:
-            traffic = pmc["sweep_bytes_per_launch"] / (sweep_ms * 1e-3) / 1e9  # GB/s, same unit as achieved
-        # SURVEY.md §8(d) whole-tick formula (assumes a CSR-state design; ours keeps no lists)
-        b_survey = 24.0 * n + 4.0 * (2 * nnz) + 8.0 * ev_per_tick
-        result = {
-            "metric": "AOI entity-updates/sec (p99 tick latency reported alongside) at 1M entities per Space",
-            "value": value,
-            "unit": "entity-updates/s",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": W,
-            "ms_per_step": ms_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic: seeded random walk of SURVEY.md §8(d) (include/gwaoi_workload.h), generated on device",
-            "config": {
-                "workload": "config 2: single Space of 1,000,000 entities per GPU, L=35,000, D=100, all moving each tick",
-                "entities_per_gpu": n, "world_L": L, "aoi_dist": D, "seed": hex(args.seed),
-                "parallelism": "independent Spaces, one per GPU, no data-path collective" if world > 1 else "1 GPU",
+    ms_step = elapsed / K * 1e3
+    ticks = max(1, st["ticks"])
+    sweep_ms = st["ms_sweep"] / ticks
+    ev_per_tick = st["events"] / ticks
+    # algorithmic bytes of ONE sweep launch (DESIGN.md "Measurement"): every record of the pass's
+    # cell-sorted grid read once (32 B: binned + start state), every cell start once (4 B), the
+    # per-op event count written (4 B per mover), every event staged once (16 B).
+    rec_per_tick = st["grid_records"] / ticks
+    cells = st["grid_cells"] / ticks
+    b_sweep = 32.0 * rec_per_tick + 4.0 * cells + 4.0 * n + 16.0 * ev_per_tick
+    achieved = b_sweep / (sweep_ms * 1e-3) / 1e9
+    pmc = load_pmc_traffic() if args.workload == "config2" else None
+    traffic = None
+    if pmc and pmc.get("n") == n and "sweep_bytes_per_launch" in pmc:
+        traffic = pmc["sweep_bytes_per_launch"] / (sweep_ms * 1e-3) / 1e9  # GB/s, same unit as achieved
+    # SURVEY.md §8(d) whole-tick formula (assumes a CSR-state design; ours keeps no lists)
+    b_survey = 24.0 * n + 4.0 * (2 * nnz) + 8.0 * ev_per_tick
+    return {
+        "metric": METRIC,
+        "value": n * K * world / elapsed,
+        "unit": "entity-updates/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": DATA,
+        "config": {
+            "workload": name,
+            "entities_per_gpu": n, "spaces_per_gpu": nsp, "world_L": L, "aoi_dist": dists if nsp > 1 else dists[0],
+            "seed": hex(seed0 - rank * (nsp if nsp > 1 else 1)),
+            "parallelism": "independent Spaces, one manager per GPU, no data-path collective" if world > 1 else "1 GPU",
+        },
+        "p50_tick_ms": percentile(lat, 50) * 1e3,
+        "p99_tick_ms": percentile(lat, 99) * 1e3,
+        "p50_tick_ms_host_events": percentile(lat_host, 50) * 1e3 if lat_host else None,
+        "p99_tick_ms_host_events": percentile(lat_host, 99) * 1e3 if lat_host else None,
+        "events_per_tick": ev_per_tick,
+        "relation_directed_entries": nnz,
+        "stage_ms": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_sweep",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "traffic_bytes_per_launch": (pmc or {}).get("sweep_bytes_per_launch") if traffic else None,
+            "algorithmic_bytes_per_launch": b_sweep,
+            "grid_records_per_tick": rec_per_tick,
+            "grid_cells": cells,
+            "traffic_source": (pmc or {}).get("source") if traffic else None,
+            "avg_launch_ms": sweep_ms,
+            "survey_formula": {
+                "bytes_per_tick": b_survey,
+                "achieved_GBps_over_tick": b_survey / (ms_step * 1e-3) / 1e9,
+                "frac": b_survey / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "note": "B_alg = 24N + 4(|S0|+|SB|) + 8|E| of SURVEY.md §8(d); counts CSR list traffic this "
+                        "design does not have (relation is recomputed from positions + op order)",
             },
-            "p50_tick_ms": percentile(lat, 50) * 1e3,
-            "p99_tick_ms": percentile(lat, 99) * 1e3,
-            "p50_tick_ms_host_events": percentile(lat_host, 50) * 1e3 if lat_host else None,
-            "p99_tick_ms_host_events": percentile(lat_host, 99) * 1e3 if lat_host else None,
-            "events_per_tick": ev_per_tick,
-            "relation_directed_entries": nnz,
-            "stage_ms": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "k_sweep",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_bytes_per_launch": (pmc or {}).get("sweep_bytes_per_launch") if traffic else None,
-                "algorithmic_bytes_per_launch": b_sweep,
-                "grid_records_per_tick": rec_per_tick,
-                "grid_cells": cells,
-                "traffic_source": (pmc or {}).get("source"),
-                "avg_launch_ms": sweep_ms,
-                "survey_formula": {
-                    "bytes_per_tick": b_survey,
-                    "achieved_GBps_over_tick": b_survey / (ms_step * 1e-3) / 1e9,
-                    "frac": b_survey / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "note": "B_alg = 24N + 4(|S0|+|SB|) + 8|E| of SURVEY.md §8(d); counts CSR list traffic this "
-                            "design does not have (relation is recomputed from positions + op order)",
-                },
-            },
-            "cpu_baseline": None,
-        }
-    # ---- CPU baseline (rank 0, N=1 only) ----
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        },
+        "cpu_baseline": None,
+    }
+
+
+def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
+    """config 4: one world of per_gpu * world entities (density of config 2) in X-strips, one per rank."""
+    import torch
+    from goworld_amd.strips import StripLayout, StripNode, exchange_dist
+
+    n = args.per_gpu * world
+    L = float(math.sqrt(n / DENSITY))
+    W, K = args.warmup, args.steps
+    lay = StripLayout(world, L, args.dist, 1.0)
+    t_setup = time.perf_counter()
+    nd = StripNode(lay, rank, n, device=dev, seed=args.seed_strips)
+    ev0 = nd.start()
+    log(f"[rank {rank}] strips setup {time.perf_counter() - t_setup:.1f}s: world {n} entities, L={L:.0f}, "
+        f"{nd.last_ops} in this region, {int(ev0.count)} owned enter pairs")
+
+    def tick(t):
+        lo, ro = nd.prepare(t)
+        if world > 1:
+            li, ri = exchange_dist(lo, ro, rank, world, via_cpu=via_cpu)
+        else:
+            li = ri = None
+        return nd.finish(li, ri), int(lo.shape[0] + ro.shape[0])
+
+    for t in range(1, W + 1):
+        tick(t)
+    nd.eng.set_timing(True)
+    nd.eng.reset_stats()
+    sync_all()
+    lat, sent, ops, evs = [], 0, 0, 0
+    t0 = time.perf_counter()
+    for t in range(W + 1, W + K + 1):
+        ts = time.perf_counter()
+        ev, k = tick(t)
+        lat.append(time.perf_counter() - ts)
+        sent += k
+        ops += nd.last_ops
+        evs += int(ev.count)
+    sync_all()
+    elapsed = allmax(time.perf_counter() - t0)
+    st = nd.eng.stats()
+    nd.close()
+    if world > 1:
+        import torch.distributed as dist
+        tot = torch.tensor([evs, sent], dtype=torch.float64, device="cpu" if via_cpu else torch.device("cuda", dev))
+        dist.all_reduce(tot)
+        evs, sent = float(tot[0]), float(tot[1])
+    if rank != 0:
+        return None
+    ticks = max(1, st["ticks"])
+    return {
+        "metric": METRIC,
+        "value": n * K / elapsed,
+        "unit": "entity-updates/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": DATA,
+        "config": {
+            "workload": f"config 4: one open world of {n} entities ({args.per_gpu} per GPU), L={L:.0f}, D={args.dist}, "
+                        f"X-strips over {world} GPU(s), halo {lay.halo:.1f} exchanged with the neighbours each tick",
+            "entities_total": n, "world_L": L, "aoi_dist": args.dist, "seed": hex(args.seed_strips),
+            "parallelism": f"{world} X-strips, halo exchange over torch.distributed "
+                           f"({'gloo via host' if via_cpu else 'RCCL/xGMI'})" if world > 1 else "1 GPU (one strip)",
+        },
+        "p50_tick_ms": percentile(lat, 50) * 1e3,
+        "p99_tick_ms": percentile(lat, 99) * 1e3,
+        "events_per_tick": evs / K,
+        "halo_records_per_tick": sent / K,
+        "rank0_ops_per_tick": ops / K,
+        "stage_ms_rank0": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", choices=["config2", "config3", "skew", "strips"], default="config2")
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--L", type=float, default=35000.0)
+    ap.add_argument("--dist", type=float, default=100.0)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
+    ap.add_argument("--spaces", type=int, default=512, help="config3: Spaces per GPU")
+    ap.add_argument("--per-gpu", type=int, default=2_000_000, help="strips: entities per GPU")
+    ap.add_argument("--seed-strips", type=lambda s: int(s, 0), default=0x5EED0004)
+    ap.add_argument("--latency-ticks", type=int, default=200, help="extra ticks with events delivered to host")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cells-per-dist", type=float, default=None)
+    ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
+    ap.add_argument("--stamps", default=None, help="diagnostic GW_STAMPS build: dump the last sweep's per-block "
+                                                   "phase timestamps to this .npy file")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+
+    import torch  # first: one HIP runtime per process (see goworld_amd/_lib.py)
+    import torch.distributed as dist
+    have_cuda = torch.cuda.is_available()
+    # one rank per GPU; more ranks than GPUs only for functional runs with gloo (ranks share a GPU)
+    ndev = torch.cuda.device_count() if have_cuda else 0
+    dev = local % ndev if ndev else local
+    backend = None
+    if world > 1:
+        backend = os.environ.get("GWAOI_DIST_BACKEND", "nccl" if have_cuda else "gloo")
+        if have_cuda:
+            torch.cuda.set_device(dev)
+        dist.init_process_group(backend=backend)
+    elif have_cuda:
+        torch.cuda.set_device(dev)
+
+    from goworld_amd import _lib
+    L_ = _lib.load()
+
+    def sync_all():
+        _lib.check(L_.gwaoi_dev_sync(dev))
+        if have_cuda:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    def allmax(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    if args.workload == "strips":
+        result = run_strips(args, rank, world, dev, sync_all, allmax, via_cpu=(backend == "gloo"))
+    else:
+        result = run_spaces(args, rank, world, dev, sync_all, allmax)
+
+    # ---- CPU baseline (rank 0, N=1, config 2 only) ----
+    if rank == 0 and world == 1 and args.workload == "config2" and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(n, L, D, args.seed, args.cpu_baseline_seconds)
+            result["cpu_baseline"] = cpu_baseline(args.n, args.L, args.dist, args.seed, args.cpu_baseline_seconds)
         except Exception as e:  # reported, never fatal to the GPU line
             result["cpu_baseline"] = {"error": repr(e)}
-    eng.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

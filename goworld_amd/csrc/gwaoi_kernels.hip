@@ -1419,6 +1419,46 @@ __global__ void __launch_bounds__(kBlock) k_iota(uint32_t* d, uint32_t n) {
   if (i < n) d[i] = i;
 }
 
+// several Spaces of n_per entities each (slot = space * n_per + i, seed of a Space = seed0 + space);
+// nhot > 0: the skewed crowd placement of config 5
+__global__ void __launch_bounds__(kBlock) k_wl_init_spaces(float* x, float* z, uint32_t n_per, uint32_t nspaces,
+                                                           uint64_t seed0, float L, uint32_t nhot, float sigma,
+                                                           uint32_t hot_every) {
+  const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= (uint64_t)n_per * nspaces) return;
+  const uint32_t sp = (uint32_t)(k / n_per), i = (uint32_t)(k - (uint64_t)sp * n_per);
+  x[k] = gww_skew_init_coord(seed0 + sp, n_per, i, 0, L, nhot, sigma, hot_every);
+  z[k] = gww_skew_init_coord(seed0 + sp, n_per, i, 1, L, nhot, sigma, hot_every);
+}
+
+__global__ void __launch_bounds__(kBlock) k_wl_step_spaces(const float* xp, const float* zp, float* xo, float* zo,
+                                                           uint32_t n_per, uint32_t nspaces, uint64_t seed0,
+                                                           uint64_t tick, float L, float s) {
+  const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= (uint64_t)n_per * nspaces) return;
+  const uint32_t sp = (uint32_t)(k / n_per), i = (uint32_t)(k - (uint64_t)sp * n_per);
+  const float x = gww_step_coord(xp[k], seed0 + sp, tick, n_per, i, 0, L, s);
+  const float z = gww_step_coord(zp[k], seed0 + sp, tick, n_per, i, 1, L, s);
+  xo[k] = x;
+  zo[k] = z;
+}
+
+void launch_wl_init_spaces(float* x, float* z, uint32_t n_per, uint32_t nspaces, uint64_t seed0, float L,
+                           uint32_t nhot, float sigma, uint32_t hot_every, hipStream_t st) {
+  const uint64_t n = (uint64_t)n_per * nspaces;
+  if (n)
+    hipLaunchKernelGGL(k_wl_init_spaces, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, x, z, n_per,
+                       nspaces, seed0, L, nhot, sigma, hot_every);
+}
+
+void launch_wl_step_spaces(const float* xp, const float* zp, float* xo, float* zo, uint32_t n_per, uint32_t nspaces,
+                           uint64_t seed0, uint64_t tick, float L, float s, hipStream_t st) {
+  const uint64_t n = (uint64_t)n_per * nspaces;
+  if (n)
+    hipLaunchKernelGGL(k_wl_step_spaces, dim3((uint32_t)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, xp, zp, xo,
+                       zo, n_per, nspaces, seed0, tick, L, s);
+}
+
 void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_wl_init, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, x, z, n, seed, L);
 }

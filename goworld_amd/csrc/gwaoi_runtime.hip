@@ -161,7 +161,8 @@ struct gwaoi_mgr {
   uint2* ev_out = nullptr;   // device, accumulated over the passes of one tick
   gwaoi_event* h_ev = nullptr;  // pinned + mapped, accumulated over the passes of one tick
   uint2* d_hev = nullptr;       // device alias of h_ev (the copy-out kernel writes it over PCIe)
-  uint64_t ev_cap = 0;       // capacity of ev_out / h_ev
+  uint64_t ev_cap = 0;       // capacity of ev_out
+  uint64_t hev_cap = 0;      // capacity of h_ev (0 until a pass delivers events to the host)
   uint32_t tmp_cap = 0;      // capacity of ev_tmp
   uint64_t tick_events = 0, tick_enter = 0;  // accumulated over the passes since the last tick
   uint32_t tick_passes = 0, tick_ops = 0;
@@ -267,7 +268,29 @@ bool same_geom(const std::vector<gw::Geom>& a, const std::vector<gw::Geom>& b) {
 
 // ------------------------------------------------------------------------------------------------
 
-int ensure_events(gwaoi_mgr* m, uint64_t need_out, uint32_t need_tmp, uint64_t keep) {
+// Event buffers: ev_tmp (sweep staging), ev_out (device, accumulated over a tick's passes) and the
+// mapped pinned host copy h_ev, allocated only once a pass delivers events to the host (a
+// device-events-only user never pins host memory). In copy mode the host capacity equals ev_cap.
+int ensure_host_events(gwaoi_mgr* m, uint64_t need, uint64_t keep) {
+  if (need <= m->hev_cap) return GWAOI_OK;
+  gwaoi_event* nh = nullptr;
+  hipError_t he = hipHostMalloc((void**)&nh, need * sizeof(gwaoi_event), hipHostMallocMapped | hipHostMallocCoherent);
+  void* dh = nullptr;
+  if (he == hipSuccess) he = hipHostGetDevicePointer(&dh, nh, 0);
+  if (he != hipSuccess) {
+    set_err("mapped host event buffer (%llu events): %s", (unsigned long long)need, hipGetErrorString(he));
+    if (nh) hipHostFree(nh);
+    return GWAOI_ERR_NOMEM;
+  }
+  if (keep && m->h_ev) std::memcpy(nh, m->h_ev, keep * sizeof(gwaoi_event));
+  if (m->h_ev) hipHostFree(m->h_ev);
+  m->h_ev = nh;
+  m->d_hev = (uint2*)dh;
+  m->hev_cap = need;
+  return GWAOI_OK;
+}
+
+int ensure_events(gwaoi_mgr* m, uint64_t need_out, uint32_t need_tmp, uint64_t keep, bool host) {
   if (need_tmp > m->tmp_cap) {
     uint32_t nc = std::max<uint32_t>(need_tmp, m->tmp_cap * 2);
     if (m->ev_tmp) hipFree(m->ev_tmp);
@@ -278,29 +301,16 @@ int ensure_events(gwaoi_mgr* m, uint64_t need_out, uint32_t need_tmp, uint64_t k
   if (need_out > m->ev_cap) {
     uint64_t nc = std::max<uint64_t>(need_out, m->ev_cap * 2);
     uint2* nd = nullptr;
-    gwaoi_event* nh = nullptr;
     RCHK(dalloc(&nd, nc));
-    hipError_t he = hipHostMalloc((void**)&nh, nc * sizeof(gwaoi_event), hipHostMallocMapped | hipHostMallocCoherent);
-    void* dh = nullptr;
-    if (he == hipSuccess) he = hipHostGetDevicePointer(&dh, nh, 0);
-    if (he != hipSuccess) {
-      set_err("mapped host event buffer (%llu events): %s", (unsigned long long)nc, hipGetErrorString(he));
-      hipFree(nd);
-      if (nh) hipHostFree(nh);
-      return GWAOI_ERR_NOMEM;
-    }
     if (keep) {
       HIPCHK(hipMemcpyAsync(nd, m->ev_out, keep * sizeof(uint2), hipMemcpyDeviceToDevice, m->stream));
-      std::memcpy(nh, m->h_ev, keep * sizeof(gwaoi_event));
       HIPCHK(hipStreamSynchronize(m->stream));
     }
     if (m->ev_out) hipFree(m->ev_out);
-    if (m->h_ev) hipHostFree(m->h_ev);
     m->ev_out = nd;
-    m->h_ev = nh;
-    m->d_hev = (uint2*)dh;
     m->ev_cap = nc;
   }
+  if (host) RCHK(ensure_host_events(m, m->ev_cap, keep));
   return GWAOI_OK;
 }
 
@@ -491,6 +501,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
+    if (copy_events) RCHK(ensure_host_events(m, m->ev_cap, keep));
     // canonical order; every step is guarded on the device against a buffer overflow, so the host
     // synchronises once, at the end of the pass
     gw::launch_scan(m->scan, m->rank_cnt, n_ops + 1, st);
@@ -524,7 +535,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     }
     const uint32_t nev = m->h_ctr[gw::CTR_EVENTS];
     if (nev > m->tmp_cap || keep + nev > m->ev_cap) {
-      RCHK(ensure_events(m, keep + nev, nev, keep));
+      RCHK(ensure_events(m, keep + nev, nev, keep, copy_events));
       if (attempt < 3) continue;
       set_err("event buffer overflow persisted");
       return GWAOI_ERR_NOMEM;
@@ -751,7 +762,8 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     gw::sweep_init();
     sweep_ready = true;
   }
-  if (r == GWAOI_OK) r = ensure_events(m, std::max<uint64_t>(1u << 16, C / 2), (uint32_t)std::max<uint64_t>(1u << 16, C / 2), 0);
+  if (r == GWAOI_OK)
+    r = ensure_events(m, std::max<uint64_t>(1u << 16, C / 2), (uint32_t)std::max<uint64_t>(1u << 16, C / 2), 0, false);
   for (auto& e : m->tev)
     if (r == GWAOI_OK && hipEventCreate(&e) != hipSuccess) {
       set_err("hipEventCreate failed");
@@ -1122,6 +1134,24 @@ int gwaoi_wl_step(int device, const float* d_xprev, const float* d_zprev, float*
                   uint64_t seed, uint64_t tick, float L, float s) {
   HIPCHK(hipSetDevice(device));
   gw::launch_wl_step(d_xprev, d_zprev, d_xout, d_zout, n, seed, tick, L, s, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return GWAOI_OK;
+}
+
+int gwaoi_wl_init_spaces(int device, float* d_x, float* d_z, uint32_t n_per, uint32_t nspaces, uint64_t seed0,
+                         float L, uint32_t nhot, float sigma, uint32_t hot_every) {
+  HIPCHK(hipSetDevice(device));
+  gw::launch_wl_init_spaces(d_x, d_z, n_per, nspaces, seed0, L, nhot, sigma, hot_every, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return GWAOI_OK;
+}
+
+int gwaoi_wl_step_spaces(int device, const float* d_xprev, const float* d_zprev, float* d_xout, float* d_zout,
+                         uint32_t n_per, uint32_t nspaces, uint64_t seed0, uint64_t tick, float L, float s) {
+  HIPCHK(hipSetDevice(device));
+  gw::launch_wl_step_spaces(d_xprev, d_zprev, d_xout, d_zout, n_per, nspaces, seed0, tick, L, s, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   return GWAOI_OK;

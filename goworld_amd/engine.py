@@ -220,3 +220,15 @@ def wl_step(device: int, d_xp: int, d_zp: int, d_xo: int, d_zo: int, n: int, see
 
 def wl_iota(device: int, d: int, n: int):
     check(_lib.load().gwaoi_wl_iota(device, ctypes.c_void_p(d), n))
+
+
+def wl_init_spaces(device: int, d_x: int, d_z: int, n_per: int, nspaces: int, seed0: int, L: float, nhot: int = 0,
+                   sigma: float = 0.0, hot_every: int = 10):
+    check(_lib.load().gwaoi_wl_init_spaces(device, ctypes.c_void_p(d_x), ctypes.c_void_p(d_z), n_per, nspaces, seed0,
+                                           L, nhot, sigma, hot_every))
+
+
+def wl_step_spaces(device: int, d_xp: int, d_zp: int, d_xo: int, d_zo: int, n_per: int, nspaces: int, seed0: int,
+                   tick: int, L: float, s: float = 1.0):
+    check(_lib.load().gwaoi_wl_step_spaces(device, ctypes.c_void_p(d_xp), ctypes.c_void_p(d_zp), ctypes.c_void_p(d_xo),
+                                           ctypes.c_void_p(d_zo), n_per, nspaces, seed0, tick, L, s))

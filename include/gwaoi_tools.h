@@ -27,6 +27,12 @@ int gwaoi_wl_init(int device, float* d_x, float* d_z, uint32_t n, uint64_t seed,
 int gwaoi_wl_step(int device, const float* d_xprev, const float* d_zprev, float* d_xout, float* d_zout,
                   uint32_t n, uint64_t seed, uint64_t tick, float L, float s);
 int gwaoi_wl_iota(int device, uint32_t* d, uint32_t n);
+/* nspaces Spaces of n_per entities (slot = space * n_per + i, Space seed = seed0 + space): placement
+ * (nhot > 0: config 5's skewed crowd, gww_skew_init_coord) and one walk step. */
+int gwaoi_wl_init_spaces(int device, float* d_x, float* d_z, uint32_t n_per, uint32_t nspaces, uint64_t seed0,
+                         float L, uint32_t nhot, float sigma, uint32_t hot_every);
+int gwaoi_wl_step_spaces(int device, const float* d_xprev, const float* d_zprev, float* d_xout, float* d_zout,
+                         uint32_t n_per, uint32_t nspaces, uint64_t seed0, uint64_t tick, float L, float s);
 
 /* Test hook: set the manager's next op sequence number (exercises the sequence renormalisation that
  * otherwise runs every ~2^31 ops). */

@@ -66,4 +66,20 @@ GWW_HD float gww_step_coord(float prev, uint64_t seed, uint64_t tick, uint64_t n
   return gww_reflect(prev + d, L);
 }
 
+/* Skewed crowd: one id in `hot_every` (id % hot_every == 1) sits around one
+ * of nhot hotspot centres (uniform in [L/8, 7L/8)^2) with an approximately Gaussian offset — the sum
+ * of four uniforms minus 2 (Irwin-Hall, std 1/sqrt(3)) times sigma*sqrt(3) — the others are uniform in
+ * [0,L)^2. Only binary32 add/mul, so host and device agree bit for bit (no libm transcendental whose
+ * last bit could differ). Reflected into [0, L) like the walk. Moves then use gww_step_coord. */
+GWW_HD float gww_skew_init_coord(uint64_t seed, uint64_t n, uint64_t id, uint32_t axis, float L, uint32_t nhot,
+                                 float sigma, uint32_t hot_every) {
+  if (nhot == 0u || hot_every == 0u || id % hot_every != 1u % hot_every) return gww_init_coord(seed, n, id, axis, L);
+  const uint32_t h = (uint32_t)(gww_splitmix64(seed ^ (0xC0FFEEull + id)) % nhot);
+  const float c = L * 0.125f + gww_u01(seed ^ 0x5A5A5A5Aull, 0, nhot, h, axis) * (L * 0.75f);
+  float s = 0.0f;
+  for (uint32_t k = 0; k < 4; ++k) s += gww_u01(seed, 1000003ull + k, n, id, axis);
+  const float v = c + (s - 2.0f) * (sigma * 1.7320508f);
+  return gww_reflect(v, L);
+}
+
 #endif /* GWAOI_WORKLOAD_H */

@@ -65,6 +65,8 @@ def lib():
         L.ow_init.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float, f32p, f32p]
         L.ow_step.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float,
                               ctypes.c_float, f32p, f32p]
+        L.ow_skew_init.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float, ctypes.c_uint32, ctypes.c_float,
+                                   ctypes.c_uint32, f32p, f32p]
         L.ow_u01.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                              ctypes.c_uint32]
         L.ow_u01.restype = ctypes.c_float
@@ -184,6 +186,14 @@ def workload_init(seed: int, n: int, L: float):
     x = np.zeros(n, dtype=np.float32)
     z = np.zeros(n, dtype=np.float32)
     lib().ow_init(seed, n, L, _f32(x)[1], _f32(z)[1])
+    return x, z
+
+
+def workload_skew_init(seed: int, n: int, L: float, nhot: int, sigma: float, hot_every: int = 10):
+    """config 5's skewed initial placement (gww_skew_init_coord)."""
+    x = np.zeros(n, dtype=np.float32)
+    z = np.zeros(n, dtype=np.float32)
+    lib().ow_skew_init(seed, n, L, nhot, sigma, hot_every, _f32(x)[1], _f32(z)[1])
     return x, z
 
 

@@ -24,3 +24,12 @@ void ow_step(uint64_t seed, uint64_t tick, uint32_t n, float L, float s, float* 
 float ow_u01(uint64_t seed, uint64_t tick, uint64_t n, uint64_t slot, uint32_t axis) {
   return gww_u01(seed, tick, n, slot, axis);
 }
+
+/* config 5 (skewed crowd) initial placement, host side */
+void ow_skew_init(uint64_t seed, uint32_t n, float L, uint32_t nhot, float sigma, uint32_t hot_every, float* x,
+                  float* z) {
+  for (uint32_t i = 0; i < n; ++i) {
+    x[i] = gww_skew_init_coord(seed, n, i, 0, L, nhot, sigma, hot_every);
+    z[i] = gww_skew_init_coord(seed, n, i, 1, L, nhot, sigma, hot_every);
+  }
+}
