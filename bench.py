@@ -269,6 +269,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "algorithmic_bytes_per_launch": b_sweep,
             "grid_records_per_tick": rec_per_tick,
             "grid_cells": cells,
+            "dense_movers_per_tick": st["dense_movers"] / ticks,
             "traffic_source": (pmc or {}).get("source") if traffic else None,
             "avg_launch_ms": sweep_ms,
             "survey_formula": {

@@ -97,6 +97,7 @@ class Stats(ctypes.Structure):
         ("events", ctypes.c_uint64),
         ("grid_records", ctypes.c_uint64),
         ("grid_cells", ctypes.c_uint64),
+        ("dense_movers", ctypes.c_uint64),
     ]
 
 

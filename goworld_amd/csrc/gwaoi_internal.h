@@ -15,7 +15,10 @@ enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u, ER
 
 // Counters block in device memory (one 64-B line).
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
-       CTR_N = 16 };
+       CTR_DENSE = 7, CTR_HOLES = 8, CTR_N = 16 };
+// CTR_EVENTS counts SLOTS of ev_tmp; k_sweep_dense reserves them in per-wave chunks and marks the
+// unused tail of its last chunk as holes (x == kEvHole), counted in CTR_HOLES. Events = slots - holes.
+constexpr uint32_t kEvHole = 0xFFFFFFFFu;
 
 // Cells are grouped in square tiles of kTile x kTile cells; cell keys are tile-major,
 //   key = base + (tz * ntx + tx) * 1024 + lz * 32 + lx   (cx = 32 tx + lx, cz = 32 tz + lz),
@@ -137,6 +140,8 @@ struct SweepArgs {
   uint32_t ev_cap;
   uint32_t* rank_cnt;
   uint32_t* ctr;
+  uint32_t* dense;      // grid indices of movers for k_sweep_dense (boxes beyond the tile's LDS region)
+  uint32_t dense_cap;
 };
 
 struct RelArgs {

@@ -605,7 +605,9 @@ __device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, u
   if (li < (uint32_t)kEvLds) {
     sm.ev[li] = rec;
   } else {
-    const uint32_t gi = atomicAdd(&a.ctr[CTR_EVENTS], 1u);
+    // queue full (crowded tiles): one global atomic per wave for the lanes that overflow together,
+    // not one per event on the single counter every block shares
+    const uint32_t gi = wave_append(&a.ctr[CTR_EVENTS], true);
     if (gi < a.ev_cap) a.ev_tmp[gi] = rec;
   }
   nent += enter ? 1u : 0u;
@@ -1160,10 +1162,19 @@ k_sweep(SweepArgs a) {
         if (!is_walker(a, ra)) continue;
         const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
         uint32_t cnt;
-        if (lds && R.holds(qbox(g, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(g, m.mx0, m.mz0))))
-          cnt = sweep_lds(a, sm, m, R, g, nent);
-        else
+        const bool in_lds = lds && R.holds(qbox(g, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(g, m.mx0, m.mz0)));
+        // movers whose boxes leave the staged region (teleports, a region over the LDS budget: dense
+        // crowds, large D) go to k_sweep_dense: one wave per mover, candidates 64 at a time
+        const uint32_t di = wave_append(&a.ctr[CTR_DENSE], !in_lds);
+        if (!in_lds) {
+          if (di < a.dense_cap) {
+            a.dense[di] = j;
+            continue;
+          }
           cnt = sweep_global(a, sm, m, g, nent);
+        } else {
+          cnt = sweep_lds(a, sm, m, R, g, nent);
+        }
         if (cnt) a.rank_cnt[m.rank] = cnt;  // zeroed by k_apply (one coalesced pass instead of a scatter)
       }
     }
@@ -1263,6 +1274,105 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
   }
 }
 
+// Dense movers: one WAVE per mover (grid-stride over the list k_sweep built). The walk is the same
+// row walk as sweep_global, but its cell ranges are collected one per lane, and the concatenated
+// candidate stream is judged 64 at a time (each lane finds its range by a binary search over the
+// lanes' inclusive prefix), so every 64 candidates cost one coalesced memory round trip whatever the
+// number of cells they come from. A mover's events are numbered by a ballot prefix on top of the
+// wave-uniform running count and written with one atomic per 64 candidates.
+constexpr int kDenseBlock = 256;
+constexpr int kDenseGrid = 1792;      // 7 waves per SIMD: every wave resident, so few chunk tails
+constexpr uint32_t kEvChunk = 128;    // event slots a wave reserves at a time (one returning atomic
+                                      // on the shared counter each: ~11 ns apiece when serialised)
+
+__global__ void __launch_bounds__(kDenseBlock) k_sweep_dense(SweepArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * kDenseBlock + threadIdx.x) >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
+  const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t nent = 0;
+  uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
+  for (uint32_t d = wave; d < nd; d += nwaves) {
+    const uint32_t j0 = a.dense[d];
+    const uint4 ma = a.g.rec[j0].a, mb = a.g.rec[j0].b;
+    const Geom g = a.g.geom[a.space_of[ma.z & REC_SLOT]];
+    const Mover m = mover_of(ma, mb, a.base, g.D);
+    const Judge J = make_judge(m, a.base);
+    uint32_t local = 0;      // wave-uniform
+    uint32_t pk = 0, pe = 0;  // this lane's cell-key range [pk, pe) (one tile part of one row segment)
+    int np = 0;               // parts collected (wave-uniform)
+    auto flush = [&]() {
+      // one round trip for every part's record range, then the candidates 64 at a time
+      uint32_t rs = 0, rl = 0;
+      if (lane < np) {
+        rs = a.g.cs[pk];
+        rl = a.g.cs[pe] - rs;
+      }
+      const uint32_t incl = wave_incl_scan(rl);
+      const uint32_t total = __shfl(incl, 63, 64);
+      for (uint32_t b = 0; b < total; b += 64) {
+        const uint32_t k = b + lane;
+        int lo = 0, hi = 63;  // first lane whose inclusive prefix exceeds k
+#pragma unroll
+        for (int st = 0; st < 6; ++st) {
+          const int mid = (lo + hi) >> 1;
+          if (__shfl(incl, mid, 64) > k) hi = mid;
+          else lo = mid + 1;
+        }
+        const uint32_t jj = __shfl(rs, lo, 64) + (k - (__shfl(incl, lo, 64) - __shfl(rl, lo, 64)));
+        int ev = 0;
+        uint32_t other = 0;
+        if (k < total) {
+          const uint4 ra = a.g.rec[jj].a;
+          ev = judge(J, ra, a.g.rec[jj].b);
+          other = ra.z & REC_SLOT;
+        }
+        const unsigned long long em = __ballot(ev != 0);
+        if (!em) continue;
+        const uint32_t cnt = (uint32_t)__popcll(em);
+        const uint32_t pre = (uint32_t)__popcll(em & below);
+        uint32_t gi = cur + pre;
+        if (cnt > left) {  // this chunk fills up: the rest goes to a fresh one
+          uint32_t nb = 0;
+          if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
+          nb = __shfl(nb, 0, 64);
+          if (pre >= left) gi = nb + (pre - left);
+          cur = nb + (cnt - left);
+          left = kEvChunk - (cnt - left);
+        } else {
+          cur += cnt;
+          left -= cnt;
+        }
+        if (ev) {
+          if (gi < a.ev_cap)
+            a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
+          nent += ev == 2 ? 1u : 0u;
+        }
+        local += cnt;
+      }
+      np = 0;
+    };
+    walk_cells(m, g, [&](int r, int c0, int c1) {
+      if (c0 > c1) return;
+      const uint32_t rowbase = g.base + ((uint32_t)((r >> kTileShift) * g.ntx) << kTileCellShift) +
+                               (uint32_t)((r & (kTile - 1)) << kTileShift);
+      for (int tx = c0 >> kTileShift; tx <= (c1 >> kTileShift); ++tx) {
+        const int lo = max(c0, tx << kTileShift), hi = min(c1, (tx << kTileShift) + kTile - 1);
+        const uint32_t kk = rowbase + ((uint32_t)tx << kTileCellShift) + (uint32_t)(lo & (kTile - 1));
+        if (lane == np) pk = kk, pe = kk + (uint32_t)(hi - lo) + 1;
+        if (++np == 64) flush();
+      }
+    });
+    if (np) flush();
+    if (lane == 0 && local) a.rank_cnt[m.rank] = local;
+  }
+  for (uint32_t i = lane; i < left; i += 64)
+    if (cur + i < a.ev_cap) a.ev_tmp[cur + i] = make_uint4(kEvHole, 0u, 0u, 0u);
+  if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
+  const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);  // one add per wave, not per lane
+  if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
+}
+
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
   if (a.use_lds == 0) {
     const uint32_t n = a.n_rec + (a.n_leaves_dev ? a.n_ops : a.n_leaves);
@@ -1272,6 +1382,8 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
   const uint32_t nb = a.ntiles + a.leave_blocks;
   if (!nb) return;
   hipLaunchKernelGGL(k_sweep, dim3(nb), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
+  // the dense list's length is on the device: a fixed grid that exits at once when it is empty
+  if (a.dense) hipLaunchKernelGGL(k_sweep_dense, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
 }
 
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each
@@ -1280,23 +1392,24 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
 // re-runs), so the host synchronises once per pass. Two side jobs ride along: k_place zeroes the
 // cell counts of the grid the NEXT pass builds and the next pass's counter block; k_slice_sort
 // validates device-staged batches (every op's slot must carry that op's seq).
-__device__ __forceinline__ bool ev_fits(const EvGuard& g, uint32_t* n) {
-  *n = g.ctr[CTR_EVENTS];
-  return *n <= g.tmp_cap && g.keep + *n <= g.out_cap;
+__device__ __forceinline__ bool ev_fits(const EvGuard& g, uint32_t* slots, uint32_t* n) {
+  *slots = g.ctr[CTR_EVENTS];
+  *n = *slots - g.ctr[CTR_HOLES];
+  return *slots <= g.tmp_cap && g.keep + *n <= g.out_cap;
 }
 
 __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
   const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
-  uint32_t n;
+  uint32_t slots, n;
   // An overflowing pass is re-run from the sweep, which still reads the old grid: side jobs only
   // once the pass is final.
-  if (!ev_fits(o.g, &n)) return;
+  if (!ev_fits(o.g, &slots, &n)) return;
   for (uint32_t i = tid; i < o.zero_n; i += nth) o.zero_cs[i] = 0u;
   if (tid < CTR_N) o.ctr_next[tid] = 0u;
   if (tid == 0) const_cast<uint32_t*>(o.g.ctr)[CTR_RECORDS] = *o.grid_total;
-  for (uint32_t i = tid; i < n; i += nth) {
+  for (uint32_t i = tid; i < slots; i += nth) {
     const uint4 e = o.ev_tmp[i];
-    o.ev_out[o.rank_off[e.x] + e.y] = make_uint2(e.z, e.w);
+    if (e.x != kEvHole) o.ev_out[o.rank_off[e.x] + e.y] = make_uint2(e.z, e.w);
   }
 }
 
@@ -1307,8 +1420,8 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
     const uint32_t s = o.op_slot[r];
     if (s < o.cap && o.opq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
   }
-  uint32_t n;
-  if (!ev_fits(o.g, &n)) return;
+  uint32_t slots, n;
+  if (!ev_fits(o.g, &slots, &n)) return;
   const uint32_t b = o.rank_off[r], e = o.rank_off[r + 1];
   uint2* ev = o.ev_out;
   for (uint32_t i = b + 1; i < e; ++i) {
@@ -1325,8 +1438,8 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
 // Deliver the ordered events to mapped pinned host memory (GPU-initiated PCIe writes), so the host
 // needs no second round trip to learn the count before a copy.
 __global__ void __launch_bounds__(kBlock) k_copy_out(OrderArgs o) {
-  uint32_t n;
-  if (!ev_fits(o.g, &n)) return;
+  uint32_t slots, n;
+  if (!ev_fits(o.g, &slots, &n)) return;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) o.host_out[i] = o.ev_out[i];
 }
 

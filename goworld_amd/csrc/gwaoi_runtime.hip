@@ -139,7 +139,7 @@ struct gwaoi_mgr {
   float *pos_x = nullptr, *pos_z = nullptr, *old_x = nullptr, *old_z = nullptr;
   uint32_t *seq = nullptr, *space_of = nullptr, *old_seq = nullptr, *opq = nullptr;
   uint32_t *key_of = nullptr, *local_of = nullptr;
-  uint32_t *d_op_slot = nullptr, *d_op_space = nullptr, *d_leaves = nullptr;
+  uint32_t *d_op_slot = nullptr, *d_op_space = nullptr, *d_leaves = nullptr, *d_dense = nullptr;
   float *d_op_x = nullptr, *d_op_z = nullptr;
   uint8_t* d_op_kind = nullptr;
   Grid grid[2];
@@ -473,6 +473,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemsetAsync(m->rank_cnt, 0, ((size_t)n_ops + 1) * sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_DENSE, 0, 2 * sizeof(uint32_t), st));  // + CTR_HOLES
     }
     gw::SweepArgs s;
     const Grid& G = m->grid[ng];
@@ -498,6 +499,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.ev_cap = m->tmp_cap;
     s.rank_cnt = m->rank_cnt;
     s.ctr = m->ctr;
+    s.dense = m->d_dense;
+    s.dense_cap = m->cap;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
@@ -533,9 +536,9 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
               m->h_ctr[gw::CTR_ERR]);
       return GWAOI_ERR_DEVICE_CHECK;
     }
-    const uint32_t nev = m->h_ctr[gw::CTR_EVENTS];
-    if (nev > m->tmp_cap || keep + nev > m->ev_cap) {
-      RCHK(ensure_events(m, keep + nev, nev, keep, copy_events));
+    const uint32_t slots = m->h_ctr[gw::CTR_EVENTS], nev = slots - m->h_ctr[gw::CTR_HOLES];
+    if (slots > m->tmp_cap || keep + nev > m->ev_cap) {
+      RCHK(ensure_events(m, keep + nev, slots, keep, copy_events));
       if (attempt < 3) continue;
       set_err("event buffer overflow persisted");
       return GWAOI_ERR_NOMEM;
@@ -559,6 +562,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       m->stats.events += nev;
       m->stats.grid_records += m->h_ctr[gw::CTR_RECORDS];
       m->stats.grid_cells += m->grid[ng].ncells;
+      m->stats.dense_movers += m->h_ctr[gw::CTR_DENSE];
     }
     break;
   }
@@ -646,7 +650,7 @@ void free_all(gwaoi_mgr* m) {
   hipSetDevice(m->device);
   if (m->stream) hipStreamSynchronize(m->stream);
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
-                   m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_op_x, m->d_op_z,
+                   m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out};
   for (void* p : dptrs)
     if (p) hipFree(p);
@@ -728,6 +732,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->d_op_slot, C));
   chk(dalloc(&m->d_op_space, C));
   chk(dalloc(&m->d_leaves, C));
+  chk(dalloc(&m->d_dense, C));
   chk(dalloc(&m->d_op_x, C));
   chk(dalloc(&m->d_op_z, C));
   chk(dalloc(&m->d_op_kind, C));

@@ -150,6 +150,7 @@ typedef struct {
   uint64_t events;         /* events emitted */
   uint64_t grid_records;   /* records of the passes' cell-sorted grids (main + ghost) */
   uint64_t grid_cells;     /* cells of those grids */
+  uint64_t dense_movers;   /* movers swept one wave each (boxes beyond their tile's LDS region) */
 } gwaoi_stats;
 int gwaoi_set_timing(gwaoi_mgr* mgr, int enable);
 int gwaoi_get_stats(const gwaoi_mgr* mgr, gwaoi_stats* out);

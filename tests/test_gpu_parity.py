@@ -286,6 +286,51 @@ def test_config2_full_size_two_ticks(gpu, po):
         assert len(got) > 10000
 
 
+def test_skewed_crowd_dense_path(gpu, po):
+    """Config 5 in miniature: a small-D Space with Gaussian hotspots (~100x the mean
+    density) and a large-D Space in one manager. Hotspot tiles and every D=400 tile exceed the sweep's
+    LDS region, so most movers take the wave-per-mover path (k_sweep_dense) with its chunked event
+    slots; relation after the enter tick and the last tick, events every tick, against oracle (ii)."""
+    from goworld_amd.engine import Engine
+    n, L = 60000, 8500.0  # the mean density of config 5 (1M in 35,000^2)
+    spaces = [(50.0, 0x5EED0050), (400.0, 0x5EED0400)]
+    eng = Engine(capacity=n * len(spaces), spaces=[(d, (0.0, 0.0, L, L)) for d, _ in spaces])
+    eng.set_timing(True)
+    pos, orcs = [], []
+    for k, (d, seed) in enumerate(spaces):
+        x, z = po.workload_skew_init(seed, n, L, 4, 55.0)
+        slots = np.arange(k * n, (k + 1) * n, dtype=np.uint32)
+        eng.stage_enters(slots, x, z, space=k)
+        o = po.GridOracle(d, n * len(spaces), (0, 0, L, L))
+        o.bulk_enter(slots, x, z)
+        pos.append((slots, x, z))
+        orcs.append(o)
+
+    def check_relation(what):
+        rg = eng.relation()
+        rel = [o.relation() for o in orcs]
+        rp = sum(r[0].astype(np.int64) for r in rel)
+        assert np.array_equal(rg[0], rp) and np.array_equal(rg[1], np.concatenate([r[1] for r in rel])), what
+
+    ev0 = eng.tick()
+    check_relation("enter tick")
+    assert len(ev0) > 1_000_000
+    for t in (1, 2, 3):
+        want = []
+        for (slots, x, z), (_, seed), o in zip(pos, spaces, orcs):
+            po.workload_step(seed, t, x, z, L, 1.0)
+            eng.stage_moves(slots, x, z)
+            o.moved_batch(slots, x, z)
+            want.append(o.take_events())
+        want = np.concatenate(want)
+        want = want[np.lexsort((want[:, 1], want[:, 0]))]  # rank == slot
+        assert_same(eng.tick(), want, f"skew tick {t}")
+        assert len(want) > 1000
+    check_relation("last tick")
+    st = eng.stats()
+    assert st["dense_movers"] > n  # the path under test was taken
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_device_mixed_ops_with_silent(gpu, po, seed):
     """gwaoi_stage_ops_device: Enter/Leave/Moved from device arrays in one batch, some ops SILENT
