@@ -1281,7 +1281,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
 // number of cells they come from. A mover's events are numbered by a ballot prefix on top of the
 // wave-uniform running count and written with one atomic per 64 candidates.
 constexpr int kDenseBlock = 256;
-constexpr int kDenseGrid = 1792;      // 7 waves per SIMD: every wave resident, so few chunk tails
+constexpr int kDenseGrid = 1536;      // 6 waves per SIMD (<= 80 VGPRs): every wave resident
 constexpr uint32_t kEvChunk = 128;    // event slots a wave reserves at a time (one returning atomic
                                       // on the shared counter each: ~11 ns apiece when serialised)
 
@@ -1352,18 +1352,39 @@ __global__ void __launch_bounds__(kDenseBlock) k_sweep_dense(SweepArgs a) {
       }
       np = 0;
     };
-    walk_cells(m, g, [&](int r, int c0, int c1) {
-      if (c0 > c1) return;
-      const uint32_t rowbase = g.base + ((uint32_t)((r >> kTileShift) * g.ntx) << kTileCellShift) +
-                               (uint32_t)((r & (kTile - 1)) << kTileShift);
-      for (int tx = c0 >> kTileShift; tx <= (c1 >> kTileShift); ++tx) {
-        const int lo = max(c0, tx << kTileShift), hi = min(c1, (tx << kTileShift) + kTile - 1);
-        const uint32_t kk = rowbase + ((uint32_t)tx << kTileCellShift) + (uint32_t)(lo & (kTile - 1));
-        if (lane == np) pk = kk, pe = kk + (uint32_t)(hi - lo) + 1;
-        if (++np == 64) flush();
+    // the walk, lane-parallel: lane = (row, segment) of 32 rows at a time; each segment splits into
+    // one part per tile it touches; part p is pulled by lane p % 64 (binary search over the prefix)
+    const Walk w = make_walk(m, g);
+    const int h = w.z1 - w.z0 + 1;
+    for (int rb = 0; rb < h; rb += 32) {
+      const int r = w.z0 + rb + (lane >> 1);
+      int a0, a1, b0, b1;
+      walk_row(w, rb + (lane >> 1) < h ? r : w.z1 + 1, a0, a1, b0, b1);
+      const int c0 = (lane & 1) ? b0 : a0, c1 = (lane & 1) ? b1 : a1;
+      const uint32_t nparts = c0 <= c1 ? (uint32_t)((c1 >> kTileShift) - (c0 >> kTileShift) + 1) : 0u;
+      const uint32_t pincl = wave_incl_scan(nparts);
+      const uint32_t T = __shfl(pincl, 63, 64);
+      for (uint32_t pb = 0; pb < T; pb += 64) {
+        const uint32_t p = pb + lane;
+        int lo = 0, hi = 63;
+#pragma unroll
+        for (int st = 0; st < 6; ++st) {
+          const int mid = (lo + hi) >> 1;
+          if (__shfl(pincl, mid, 64) > p) hi = mid;
+          else lo = mid + 1;
+        }
+        const int q = (int)(p - (__shfl(pincl, lo, 64) - __shfl(nparts, lo, 64)));
+        const int sc0 = __shfl(c0, lo, 64), sc1 = __shfl(c1, lo, 64), sr = __shfl(r, lo, 64);
+        const int tx = (sc0 >> kTileShift) + q;
+        const int plo = max(sc0, tx << kTileShift), phi = min(sc1, (tx << kTileShift) + kTile - 1);
+        pk = g.base + ((uint32_t)((sr >> kTileShift) * g.ntx) << kTileCellShift) +
+             (uint32_t)((sr & (kTile - 1)) << kTileShift) + ((uint32_t)tx << kTileCellShift) +
+             (uint32_t)(plo & (kTile - 1));
+        pe = pk + (uint32_t)(phi - plo) + 1;
+        np = (int)min(64u, T - pb);
+        flush();
       }
-    });
-    if (np) flush();
+    }
     if (lane == 0 && local) a.rank_cnt[m.rank] = local;
   }
   for (uint32_t i = lane; i < left; i += 64)
