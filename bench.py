@@ -104,21 +104,29 @@ def load_pmc_traffic():
 
 
 def spaces_workload(args, rank):
-    """(name, n_per, nspaces, dists, L, seed0, nhot, sigma) of a device-staged, all-moving workload."""
+    """(name, n_per, nspaces, dists, L, seed0, nhot, sigma, hot_every) of a device-staged, all-moving
+    workload."""
     if args.workload == "config2":
         return ("config 2: single Space of 1,000,000 entities per GPU, L=35,000, D=100, all moving each tick",
-                args.n, 1, [args.dist], args.L, args.seed + rank, 0, 0.0)
+                args.n, 1, [args.dist], args.L, args.seed + rank, 0, 0.0, 10)
     if args.workload == "config3":
         k = args.spaces
         return (f"config 3: {k} independent dungeon Spaces x 2,000 entities per GPU in one manager "
                 f"(4,096 Spaces over 8 GPUs), L=1,600 each, D=100",
-                2000, k, [100.0] * k, 1600.0, 0x5EED0003 + rank * k, 0, 0.0)
+                2000, k, [100.0] * k, 1600.0, 0x5EED0003 + rank * k, 0, 0.0, 10)
     if args.workload == "skew":
         # 10% of the entities in 64 Gaussian hotspots, sigma 55: peak density ~100x the mean
         # (1,562 per hotspot / (2 pi 55^2) = 0.082 per unit^2 = 100 x 8.2e-4)
         return ("config 5: skewed crowd, 4 Spaces x 1,000,000 per GPU (D = 50/100/200/400), L=35,000, 10% of the "
                 "entities in 64 Gaussian hotspots (sigma 55: peak density ~100x the mean)",
-                1_000_000, 4, [50.0, 100.0, 200.0, 400.0], 35000.0, 0x5EED0005 + rank * 4, 64, 55.0)
+                1_000_000, 4, [50.0, 100.0, 200.0, 400.0], 35000.0, 0x5EED0005 + rank * 4, 64, 55.0, 10)
+    if args.workload == "skew50":
+        # SURVEY.md 8(d) proportions: 50% of the entities in 64 hotspots per Space, sigma 123 for the same
+        # ~100x peak (7,812 per hotspot / (2 pi 123^2) = 0.082 per unit^2)
+        return ("config 5 (SURVEY proportions): skewed crowd, 4 Spaces x 1,000,000 per GPU (D = 50/100/200/400), "
+                "L=35,000, 50% of the entities in 64 Gaussian hotspots per Space (sigma 123: peak density ~100x "
+                "the mean)",
+                1_000_000, 4, [50.0, 100.0, 200.0, 400.0], 35000.0, 0x5EED0005 + rank * 4, 64, 123.0, 2)
     raise ValueError(args.workload)
 
 
@@ -129,7 +137,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     from goworld_amd import _lib
     from goworld_amd.engine import DeviceBuffer, Engine, wl_init_spaces, wl_iota, wl_step_spaces
 
-    name, n_per, nsp, dists, L, seed0, nhot, sigma = spaces_workload(args, rank)
+    name, n_per, nsp, dists, L, seed0, nhot, sigma, hot_every = spaces_workload(args, rank)
     n = n_per * nsp
     W, K, H = args.warmup, args.steps, args.latency_ticks
     T = W + K + H + 1
@@ -147,7 +155,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     def pz(t):
         return snap.ptr + (2 * t + 1) * 4 * n
 
-    wl_init_spaces(dev, px(0), pz(0), n_per, nsp, seed0, L, nhot, sigma)
+    wl_init_spaces(dev, px(0), pz(0), n_per, nsp, seed0, L, nhot, sigma, hot_every)
     for t in range(1, T):
         wl_step_spaces(dev, px(t - 1), pz(t - 1), px(t), pz(t), n_per, nsp, seed0, t, L, 1.0)
     eng = Engine(capacity=n, device=dev, spaces=[(d, (0.0, 0.0, L, L)) for d in dists])
@@ -155,16 +163,18 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         eng.debug_set_cells_per_dist(args.cells_per_dist)
     if args.sweep_lds != 1:
         eng._L.gwaoi_debug_set_sweep_lds(eng.handle, args.sweep_lds)
-    x0 = snap.download(np.float32, n, 0)
-    z0 = snap.download(np.float32, n, 4 * n)
-    for sp in range(nsp):
-        s = slice(sp * n_per, (sp + 1) * n_per)
-        eng.stage_enters(np.arange(sp * n_per, (sp + 1) * n_per, dtype=np.uint32), x0[s], z0[s], space=sp)
-    log(f"[rank {rank}] {n} entities staged ({time.perf_counter() - t_setup:.1f}s); running the Enter pass")
-    ev0 = eng.tick_device()
-    enter_pairs = int(ev0.count)
-    del x0, z0
-    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s: {n} entities in {nsp} Spaces, {enter_pairs} pairs")
+    # bulk restore (untimed): one device-staged pass of SILENT Enters into their Spaces; the relation
+    # is rebuilt without reporting its pairs (billions for config 5 in SURVEY proportions)
+    kinds = DeviceBuffer(n, dev)
+    kinds.upload(np.full(n, _lib.GWAOI_OP_ENTER | _lib.GWAOI_OP_SILENT, np.uint8))
+    spc = DeviceBuffer(4 * n, dev)
+    spc.upload(np.repeat(np.arange(nsp, dtype=np.uint32), n_per))
+    log(f"[rank {rank}] {n} entities generated ({time.perf_counter() - t_setup:.1f}s); running the Enter pass")
+    eng.stage_ops_device(slots.ptr, px(0), pz(0), kinds.ptr, n, spc.ptr)
+    eng.tick_device()
+    kinds.free()
+    spc.free()
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s: {eng.count()[0]} entities in {nsp} Spaces")
 
     def tick_dev(t):
         eng.stage_moves_device(slots.ptr, px(t), pz(t), n)
@@ -207,9 +217,11 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         lat_host.append(time.perf_counter() - ts)
 
     # relation size for the SURVEY §8(d) formula (directed entries |S|)
-    rp, cols = eng.relation()
-    nnz = int(len(cols))
-    del rp, cols
+    nnz = None
+    if args.workload in ("config2", "config3"):  # config 5's relation runs to billions of entries
+        rp, cols = eng.relation()
+        nnz = int(len(cols))
+        del rp, cols
     eng.close()
     if rank != 0:
         return None
@@ -230,7 +242,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     if pmc and pmc.get("n") == n and "sweep_bytes_per_launch" in pmc:
         traffic = pmc["sweep_bytes_per_launch"] / (sweep_ms * 1e-3) / 1e9  # GB/s, same unit as achieved
     # SURVEY.md §8(d) whole-tick formula (assumes a CSR-state design; ours keeps no lists)
-    b_survey = 24.0 * n + 4.0 * (2 * nnz) + 8.0 * ev_per_tick
+    b_survey = 24.0 * n + 4.0 * (2 * nnz) + 8.0 * ev_per_tick if nnz is not None else None
     return {
         "metric": METRIC,
         "value": n * K * world / elapsed,
@@ -272,7 +284,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "dense_movers_per_tick": st["dense_movers"] / ticks,
             "traffic_source": (pmc or {}).get("source") if traffic else None,
             "avg_launch_ms": sweep_ms,
-            "survey_formula": {
+            "survey_formula": None if b_survey is None else {
                 "bytes_per_tick": b_survey,
                 "achieved_GBps_over_tick": b_survey / (ms_step * 1e-3) / 1e9,
                 "frac": b_survey / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -369,7 +381,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=["config2", "config3", "skew", "strips"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "config3", "skew", "skew50", "strips"], default="config2")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--L", type=float, default=35000.0)
     ap.add_argument("--dist", type=float, default=100.0)

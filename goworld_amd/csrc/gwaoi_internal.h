@@ -11,7 +11,7 @@ namespace gw {
 enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2, OP_KIND = 3, OP_SILENT = 0x80 };
 
 // Device-side error bits (device-staged batches are validated on the GPU).
-enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u, ERR_PRESENT_SLOT = 8u };
+enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u, ERR_PRESENT_SLOT = 8u, ERR_BAD_SPACE = 16u };
 
 // Counters block in device memory (one 64-B line).
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
@@ -74,6 +74,7 @@ struct ApplyArgs {
   const float* op_z;
   const uint8_t* op_kind;    // null => all OP_MOVE (device-staged moves); may carry OP_SILENT
   const uint32_t* op_space;  // space of OP_ENTER ops (null: Space 0)
+  uint32_t nspaces;          // op_space values are checked against it (device-staged)
   uint32_t* leaves;          // device-staged mixed batch: Leave op indices are appended here
   uint32_t n_ops;
   uint32_t base;             // seq of op 0; op i gets seq base + i

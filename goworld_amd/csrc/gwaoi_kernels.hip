@@ -124,6 +124,9 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
       } else if (a.check && kind != OP_ENTER && q0 == 0) {
         atomicOr(&a.ctr[CTR_ERR], ERR_ABSENT_SLOT);
         ok = false;
+      } else if (a.check && kind == OP_ENTER && a.op_space && a.op_space[i] >= a.nspaces) {
+        atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SPACE);
+        ok = false;
       }
     }
   }

@@ -132,6 +132,7 @@ struct gwaoi_mgr {
   const float* dv_x = nullptr;
   const float* dv_z = nullptr;
   const uint8_t* dv_kind = nullptr;  // mixed device batch (gwaoi_stage_ops_device), else null
+  const uint32_t* dv_space = nullptr;  // Space of each device Enter (null: Space 0)
   uint32_t dv_n = 0;
   bool dev_managed = false;          // presence lives on the device only (mixed device batches)
 
@@ -440,7 +441,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   a.op_z = dev ? m->dv_z : m->d_op_z;
   const bool dev_mixed = dev && m->dv_kind;
   a.op_kind = dev ? m->dv_kind : m->d_op_kind;
-  a.op_space = dev ? nullptr : m->d_op_space;
+  a.op_space = dev ? m->dv_space : m->d_op_space;
+  a.nspaces = m->nspaces;
   a.leaves = dev_mixed ? m->d_leaves : nullptr;
   a.n_ops = n_ops;
   a.base = base;
@@ -532,7 +534,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     if (m->h_ctr[gw::CTR_ERR]) {
       m->broken = true;
       set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
-              "capacity, 8=Enter of a present slot); the manager is unusable",
+              "capacity, 8=Enter of a present slot, 16=Space id out of range); the manager is unusable",
               m->h_ctr[gw::CTR_ERR]);
       return GWAOI_ERR_DEVICE_CHECK;
     }
@@ -581,6 +583,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
   m->n_present_dev = m->n_present;
   m->dv_kind = nullptr;
+  m->dv_space = nullptr;
   return GWAOI_OK;
 }
 
@@ -949,6 +952,11 @@ int gwaoi_stage_moves_device(gwaoi_mgr* m, const uint32_t* d_slots, const float*
 
 int gwaoi_stage_ops_device(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,
                            const uint8_t* d_kinds, uint32_t n) {
+  return gwaoi_stage_ops_device_spaces(m, d_slots, d_x, d_z, d_kinds, nullptr, n);
+}
+
+int gwaoi_stage_ops_device_spaces(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                                  const uint8_t* d_kinds, const uint32_t* d_spaces, uint32_t n) {
   RCHK(check_mgr(m));
   if (n && (!d_slots || !d_x || !d_z || !d_kinds)) {
     set_err("stage_ops_device: null array");
@@ -965,6 +973,7 @@ int gwaoi_stage_ops_device(gwaoi_mgr* m, const uint32_t* d_slots, const float* d
   m->dv_x = d_x;
   m->dv_z = d_z;
   m->dv_kind = d_kinds;
+  m->dv_space = d_spaces;
   m->dv_n = n;
   return GWAOI_OK;
 }

@@ -121,6 +121,12 @@ int gwaoi_stage_moves_device(gwaoi_mgr* mgr, const uint32_t* d_slots, const floa
 #define GWAOI_OP_SILENT 0x80u
 int gwaoi_stage_ops_device(gwaoi_mgr* mgr, const uint32_t* d_slots, const float* d_x, const float* d_z,
                            const uint8_t* d_kinds, uint32_t n);
+/* The same with the Space of each Enter: d_spaces[i] (checked < the manager's Space count; a bad id
+ * fails the batch like the checks above). d_spaces may be null (every Enter into Space 0). This is
+ * the bulk restore of a multi-Space manager from HBM (one pass with S0 empty);
+ * with GWAOI_OP_SILENT on every op it rebuilds the relation without reporting the pairs. */
+int gwaoi_stage_ops_device_spaces(gwaoi_mgr* mgr, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                                  const uint8_t* d_kinds, const uint32_t* d_spaces, uint32_t n);
 
 /* Apply every staged op; blocks until the events are on the host (or in device memory, see flags). */
 #define GWAOI_TICK_DEVICE_EVENTS 1u /* leave events in device memory (no D2H copy) */

@@ -380,3 +380,57 @@ def test_device_mixed_ops_validation(gpu):
     with pytest.raises(_lib.GwaoiError) as e:
         eng.tick()
     assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK
+
+
+@pytest.mark.parametrize("silent", [False, True])
+def test_device_enters_into_spaces(gpu, po, silent):
+    """gwaoi_stage_ops_device_spaces: a device-staged bulk Enter into several Spaces (the bench's
+    restore pass). Loud: the events of one oracle per Space in op order; silent: none, and the same
+    relation either way. A Space id out of range fails the batch."""
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine
+    rng = np.random.default_rng(11)
+    dists, per = [30.0, 60.0, 120.0], 700
+    cap = per * len(dists)
+    eng = Engine(capacity=cap, spaces=[(d, (0.0, 0.0, 800.0, 800.0)) for d in dists])
+    orcs = [po.XZListOracle(d, cap) for d in dists]
+    order = rng.permutation(cap).astype(np.uint32)
+    space_of = (order % len(dists)).astype(np.uint32)
+    pos = rng.uniform(0, 800, (cap, 2)).astype(np.float32)
+    want = []
+    for s, sp in zip(order, space_of):
+        o = orcs[sp]
+        o.enter(int(s), float(pos[s, 0]), float(pos[s, 1]))
+        ev = o.take_events()
+        if len(ev):
+            want.append(ev[np.argsort(ev[:, 1], kind="stable")])
+    want = np.concatenate(want)
+    bs, bx, bz, bk, bp = (DeviceBuffer(4 * cap) for _ in range(5))
+    bs.upload(order)
+    bx.upload(np.ascontiguousarray(pos[order, 0]))
+    bz.upload(np.ascontiguousarray(pos[order, 1]))
+    bk.upload(np.full(cap, _lib.GWAOI_OP_ENTER | (_lib.GWAOI_OP_SILENT if silent else 0), np.uint8))
+    bp.upload(space_of)
+    eng.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, cap, bp.ptr)
+    got = eng.tick()
+    if silent:
+        assert len(got) == 0
+    else:
+        assert_same(got, want, "device enters into Spaces")
+    rg = eng.relation()
+    rel = [o.relation() for o in orcs]
+    assert np.array_equal(rg[0], sum(r[0].astype(np.int64) for r in rel))
+    # rows interleave Spaces: compare row by row
+    cols = [np.split(r[1], r[0][1:-1].astype(np.int64)) for r in rel]
+    gcols = np.split(rg[1], rg[0][1:-1].astype(np.int64))
+    for s in range(cap):
+        assert np.array_equal(gcols[s], cols[space_of[np.nonzero(order == s)[0][0]]][s]), f"row {s}"
+    assert eng.count()[0] == cap
+    bad = Engine(capacity=8, spaces=[(10.0, None), (20.0, None)])
+    bs.upload(np.asarray([0, 1], np.uint32))
+    bk.upload(np.asarray([_lib.GWAOI_OP_ENTER] * 2, np.uint8))
+    bp.upload(np.asarray([1, 2], np.uint32))  # Space 2 does not exist
+    bad.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, 2, bp.ptr)
+    with pytest.raises(_lib.GwaoiError) as e:
+        bad.tick()
+    assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK
