@@ -13,9 +13,12 @@ enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2, OP_KIND = 3, OP_SILENT
 // Device-side error bits (device-staged batches are validated on the GPU).
 enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u, ERR_PRESENT_SLOT = 8u, ERR_BAD_SPACE = 16u };
 
-// Counters block in device memory (one 64-B line).
+// Counters block in device memory.
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
-       CTR_DENSE = 7, CTR_HOLES = 8, CTR_N = 16 };
+       CTR_DENSE = 7, CTR_HOLES = 8,
+       CTR_TQ = 32,          // k_sweep's per-XCD tile queues (persistent blocks): queue q at CTR_TQ + q * CTR_QSTRIDE,
+       CTR_QSTRIDE = 32,     // one 128-B line each (a returning atomic serialises per line)
+       CTR_N = 32 + 8 * 32 };
 // CTR_EVENTS counts SLOTS of ev_tmp; k_sweep_dense reserves them in per-wave chunks and marks the
 // unused tail of its last chunk as holes (x == kEvHole), counted in CTR_HOLES. Events = slots - holes.
 constexpr uint32_t kEvHole = 0xFFFFFFFFu;

@@ -580,7 +580,8 @@ constexpr int kMaxRows = 48;
 constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
 struct SweepSmem {  // dynamic LDS (16-B aligned carve)
-  uint32_t n, enter, base, flags;
+  uint32_t n, enter, base, item;
+  uint32_t qk, pad0, pad1, pad2;  // qk: tile queues this block has found empty
   uint32_t ws[16];              // block-scan scratch
   uint32_t gsp[kMaxRows * 3];   // global start of each (region row, tile part)
   uint4 ev[kEvLds];             // event queue
@@ -1080,7 +1081,7 @@ constexpr int kStampWords = 8;
 __device__ unsigned long long gw_stamps[kStampWords * 16384];
 #define GW_STAMP(k, v)                                                              \
   do {                                                                              \
-    if (threadIdx.x == 0 && blockIdx.x < 16384) gw_stamps[blockIdx.x * kStampWords + (k)] = (v); \
+    if (threadIdx.x == 0 && sm.item < 16384) gw_stamps[sm.item * kStampWords + (k)] = (v); \
   } while (0)
 #else
 #define GW_STAMP(k, v) \
@@ -1091,15 +1092,10 @@ __device__ unsigned long long gw_stamps[kStampWords * 16384];
 // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD
 // b % 8), each with its own L2. Give XCD x a contiguous run of tiles, visited in order, so the halo a
 // tile shares with its predecessor is still in that XCD's L2. A bijection on [0, n).
-#ifndef GW_XCD_REMAP
-#define GW_XCD_REMAP 1
-#endif
 constexpr uint32_t kXcds = 8;
-__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t n) {
-  if (!GW_XCD_REMAP) return b;
-  const uint32_t x = b % kXcds, i = b / kXcds, per = n / kXcds, rem = n % kXcds;
-  return x * per + min(x, rem) + i;
-}
+#ifndef GW_SWEEP_PERSIST
+#define GW_SWEEP_PERSIST 0  // 1: persistent blocks over per-XCD tile queues (spills SGPRs today: 1 block per CU)
+#endif
 
 __device__ __forceinline__ bool is_mover(const uint4 ra, uint32_t base, uint32_t n_ops) {
   return !(ra.z & REC_GHOST) && (ra.w - base) < n_ops;
@@ -1110,24 +1106,17 @@ __device__ __forceinline__ bool is_walker(const SweepArgs& a, const uint4 ra) {
   return is_mover(ra, a.base, a.n_ops) && !(a.op_kind && (a.op_kind[ra.w - a.base] & OP_SILENT));
 }
 
-// 2 blocks x 9 waves per CU (LDS-bound) need 5 waves per SIMD: at most 96 VGPRs
-__global__ void __launch_bounds__(kSweepBlock) __attribute__((amdgpu_waves_per_eu(GW_SWEEP_WAVES_PER_EU)))
-k_sweep(SweepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  SweepSmem& sm = *reinterpret_cast<SweepSmem*>(smem_raw);
+// One work item of k_sweep: a tile (stage its region, walk its movers); the block's LDS event queue
+// is flushed with one global atomic at the end.
+__device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, const uint32_t item) {
   uint32_t nent = 0;  // enter events of this thread's movers
-  GW_STAMP(0, __builtin_amdgcn_s_memrealtime());
-  if (threadIdx.x == 0) {
-    sm.n = 0;
-    sm.enter = 0;
-  }
-  if (blockIdx.x < a.ntiles) {
-    const uint32_t t = xcd_tile(blockIdx.x, a.ntiles);
+  {
+    const uint32_t t = item;
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
     // does the tile hold a mover of this pass? (block-uniform exit otherwise)
     bool mine = false;
     for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_walker(a, a.g.rec[j].a);
-    if (!__syncthreads_or(mine)) return;
+    if (!__syncthreads_or(mine)) return;  // nothing queued: the caller's barrier follows
     const uint32_t sp = a.g.tile_space[t];
     const Geom g = a.g.geom[sp];
     bool lds = a.use_lds && g.reach > 0;
@@ -1181,16 +1170,6 @@ k_sweep(SweepArgs a) {
         if (cnt) a.rank_cnt[m.rank] = cnt;  // zeroed by k_apply (one coalesced pass instead of a scatter)
       }
     }
-  } else {
-    __syncthreads();
-    const uint32_t nl = a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves;
-    for (uint32_t t = (blockIdx.x - a.ntiles) * kSweepBlock + threadIdx.x; t < nl; t += a.leave_blocks * kSweepBlock) {
-      const uint32_t i = a.leave_ops[t];
-      if (a.op_kind && (a.op_kind[i] & OP_SILENT)) continue;
-      const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
-      const Mover m = leaver(a, i, g.D);
-      a.rank_cnt[i] = sweep_global(a, sm, m, g, nent);
-    }
   }
   // flush the block's events with one global atomic
   if (nent) atomicAdd(&sm.enter, nent);
@@ -1210,6 +1189,53 @@ k_sweep(SweepArgs a) {
   GW_STAMP(4, __builtin_amdgcn_s_memrealtime());
 }
 
+// 2 blocks x 9 waves per CU (LDS-bound) need 5 waves per SIMD: at most 96 VGPRs
+__global__ void __launch_bounds__(kSweepBlock) __attribute__((amdgpu_waves_per_eu(GW_SWEEP_WAVES_PER_EU)))
+k_sweep(SweepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  SweepSmem& sm = *reinterpret_cast<SweepSmem*>(smem_raw);
+  // Persistent blocks (2 per CU) pull tiles from per-XCD queues (queue x = the x-th contiguous
+  // eighth of the tiles, so neighbouring tiles, which share halo records, run on one XCD's L2; an
+  // XCD whose queue is empty steals from the next). Leaves run in k_sweep_leaves.
+#if !GW_SWEEP_PERSIST  // one block per item, tiles mapped XCD-aware by block index (A/B reference)
+  if (threadIdx.x == 0) {
+    const uint32_t xcd = blockIdx.x % kXcds;
+    const uint32_t per = a.ntiles / kXcds, rem = a.ntiles % kXcds;
+    const uint32_t b = blockIdx.x;
+    sm.item = xcd * per + min(xcd, rem) + b / kXcds;
+    sm.n = 0;
+    sm.enter = 0;
+  }
+  __syncthreads();
+  sweep_item(a, sm, __builtin_amdgcn_readfirstlane(sm.item));
+  return;
+#endif
+  if (threadIdx.x == 0) sm.qk = 0;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint32_t xcd = blockIdx.x % kXcds;
+      const uint32_t per = a.ntiles / kXcds, rem = a.ntiles % kXcds;
+      uint32_t item = ~0u, k = sm.qk;
+      for (; k < kXcds && item == ~0u; ++k) {
+        const uint32_t q = (xcd + k) % kXcds;
+        const uint32_t i = atomicAdd(&a.ctr[CTR_TQ + q * CTR_QSTRIDE], 1u);
+        if (i < per + (q < rem ? 1u : 0u)) item = q * per + min(q, rem) + i;
+      }
+      sm.qk = item == ~0u ? k : k - 1;
+      sm.item = item;
+      sm.n = 0;
+      sm.enter = 0;
+    }
+    __syncthreads();
+    // block-uniform: keep it (and the tile geometry derived from it) in scalar registers
+    const uint32_t item = __builtin_amdgcn_readfirstlane(sm.item);
+    if (item == ~0u) break;
+    GW_STAMP(0, __builtin_amdgcn_s_memrealtime());
+    sweep_item(a, sm, item);
+    __syncthreads();  // the next item reuses the LDS
+  }
+}
+
 int read_stamps(void* host, size_t bytes) {
 #if GW_STAMPS
   if (bytes > sizeof(gw_stamps)) bytes = sizeof(gw_stamps);
@@ -1226,9 +1252,21 @@ int sweep_occupancy(int* blocks) {
                                                       sizeof(SweepSmem)) == hipSuccess ? 0 : -3;
 }
 
+#if GW_SWEEP_PERSIST
+static uint32_t g_sweep_slots = 512;  // resident k_sweep blocks on the whole chip
+#else
+static uint32_t g_sweep_slots = ~0u;
+#endif
+
 void sweep_init() {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(SweepSmem));
+  int blocks = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(&k_sweep), kSweepBlock,
+                                                   sizeof(SweepSmem)) == hipSuccess &&
+      hipGetDevice(&dev) == hipSuccess &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && blocks > 0 && cus > 0)
+    g_sweep_slots = GW_SWEEP_PERSIST ? (uint32_t)(blocks * cus) : ~0u;
 }
 
 // Flat variant (use_lds == 0): one thread per record in key (tile-major) order, 256-thread blocks
@@ -1259,6 +1297,38 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
   } else if (t >= a.n_rec && t < a.n_rec + (a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves) &&
              !(a.op_kind && (a.op_kind[a.leave_ops[t - a.n_rec]] & OP_SILENT))) {
     const uint32_t i = a.leave_ops[t - a.n_rec];
+    const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
+    const Mover m = leaver(a, i, g.D);
+    a.rank_cnt[i] = sweep_global(a, q, m, g, nent);
+  }
+  if (nent) atomicAdd(&q.enter, nent);
+  __syncthreads();
+  const uint32_t nq = min(q.n, (uint32_t)kEvLds);
+  if (threadIdx.x == 0) {
+    q.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+    if (q.enter) atomicAdd(&a.ctr[CTR_ENTER], q.enter);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
+    const uint32_t gi = q.base + i;
+    if (gi < a.ev_cap) a.ev_tmp[gi] = q.ev[i];
+  }
+}
+
+// Leaves of a mixed device batch (or host-staged Leaves): each leaver's old neighbours through the
+// global-memory walk, one thread per leaver.
+__global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
+  __shared__ FlatQ q;
+  uint32_t nent = 0;
+  if (threadIdx.x == 0) {
+    q.n = 0;
+    q.enter = 0;
+  }
+  __syncthreads();
+  const uint32_t nl = a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves;
+  for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < nl; t += gridDim.x * kBlock) {
+    const uint32_t i = a.leave_ops[t];
+    if (a.op_kind && (a.op_kind[i] & OP_SILENT)) continue;
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
     a.rank_cnt[i] = sweep_global(a, q, m, g, nent);
@@ -1403,9 +1473,12 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
     if (n) hipLaunchKernelGGL(k_sweep_flat, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
     return;
   }
-  const uint32_t nb = a.ntiles + a.leave_blocks;
-  if (!nb) return;
-  hipLaunchKernelGGL(k_sweep, dim3(nb), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
+  // persistent: one block per resident slot, tiles pulled from the queues (CTR_TQ)
+  if (a.ntiles)
+    hipLaunchKernelGGL(k_sweep, dim3(std::min(a.ntiles, g_sweep_slots)), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
+  if (a.leave_blocks)
+    hipLaunchKernelGGL(k_sweep_leaves, dim3(a.leave_blocks * ((kSweepBlock + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       st, a);
   // the dense list's length is on the device: a fixed grid that exits at once when it is empty
   if (a.dense) hipLaunchKernelGGL(k_sweep_dense, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
 }

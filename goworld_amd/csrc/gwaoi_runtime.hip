@@ -476,6 +476,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_DENSE, 0, 2 * sizeof(uint32_t), st));  // + CTR_HOLES
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_TQ, 0, (gw::CTR_N - gw::CTR_TQ) * sizeof(uint32_t), st));
     }
     gw::SweepArgs s;
     const Grid& G = m->grid[ng];
