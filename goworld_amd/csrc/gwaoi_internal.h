@@ -19,6 +19,7 @@ enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 
        CTR_TQ = 32,          // k_sweep's per-XCD tile queues (persistent blocks): queue q at CTR_TQ + q * CTR_QSTRIDE,
        CTR_QSTRIDE = 32,     // one 128-B line each (a returning atomic serialises per line)
        CTR_N = 32 + 8 * 32 };
+constexpr int kPubWords = 16;  // counters [0, 16) are what the host reads after a pass
 // CTR_EVENTS counts SLOTS of ev_tmp; k_sweep_dense reserves them in per-wave chunks and marks the
 // unused tail of its last chunk as holes (x == kEvHole), counted in CTR_HOLES. Events = slots - holes.
 constexpr uint32_t kEvHole = 0xFFFFFFFFu;
@@ -207,6 +208,7 @@ struct OrderArgs {
 };
 // k_place (+ zeroing side jobs) -> k_slice_sort (+ batch check) -> k_copy_out (if host_out)
 void launch_order(const OrderArgs& o, hipStream_t st);
+void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_t st);
 void launch_relation(const RelArgs& a, hipStream_t st);
 void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, hipStream_t st);
 void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st);

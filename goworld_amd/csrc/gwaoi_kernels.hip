@@ -1547,6 +1547,20 @@ void launch_order(const OrderArgs& o, hipStream_t st) {
   if (o.host_out) hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, o);
 }
 
+// End-of-pass publication: the counters the host reads, then a sequence word, written by one thread
+// into mapped (coherent) host memory with system-scope stores; the host spins on the sequence word
+// instead of a DMA copy plus a stream synchronisation.
+__global__ void k_publish(const uint32_t* __restrict__ ctr, uint32_t* pub, uint32_t seq) {
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < kPubWords; ++i) __hip_atomic_store(&pub[i], ctr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  __hip_atomic_store(&pub[kPubWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_t st) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, ctr, pub, seq);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Relation export: row s = {o : N(s,o)} = {o : in(L, F)}, L = later actor, over the END-of-pass
 // state (main records only). Count pass (row_ptr null) then fill pass; rows sorted afterwards.

@@ -157,6 +157,13 @@ struct gwaoi_mgr {
   uint32_t* ctr = nullptr;       // current half
   int ctr_sel = 0;
   uint32_t* h_ctr = nullptr;     // pinned
+  uint32_t* h_pub = nullptr;     // mapped coherent host memory: [kPubWords] counters + sequence word
+  uint32_t* d_pub = nullptr;     // its device address
+  uint32_t pub_seq = 0;
+  struct {                       // the last timed pass, collected once its events are complete
+    bool pending = false;
+    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0;
+  } tpend;
   // events
   uint4* ev_tmp = nullptr;
   uint2* ev_out = nullptr;   // device, accumulated over the passes of one tick
@@ -401,6 +408,64 @@ void reset_tick(gwaoi_mgr* m) {
   m->tick_ops = 0;
 }
 
+// Stage times of the last timed pass into the stats (its hipEvents are complete or about to be).
+int collect_timing(gwaoi_mgr* m) {
+  if (!m->tpend.pending) return GWAOI_OK;
+  m->tpend.pending = false;
+  HIPCHK(hipEventSynchronize(m->tev[4]));
+  float t01, t12, t23, t34, t04;
+  HIPCHK(hipEventElapsedTime(&t01, m->tev[0], m->tev[1]));
+  HIPCHK(hipEventElapsedTime(&t12, m->tev[1], m->tev[2]));
+  HIPCHK(hipEventElapsedTime(&t23, m->tev[2], m->tev[3]));
+  HIPCHK(hipEventElapsedTime(&t34, m->tev[3], m->tev[4]));
+  HIPCHK(hipEventElapsedTime(&t04, m->tev[0], m->tev[4]));
+  m->stats.ticks++;
+  m->stats.ms_apply += t01;
+  m->stats.ms_grid += t12;
+  m->stats.ms_sweep += t23;
+  m->stats.ms_order += t34;
+  m->stats.ms_total += t04;
+  m->stats.sweep_movers += m->tpend.n_ops;
+  m->stats.events += m->tpend.nev;
+  m->stats.grid_records += m->tpend.records;
+  m->stats.grid_cells += m->tpend.ncells;
+  m->stats.dense_movers += m->tpend.dense;
+  return GWAOI_OK;
+}
+
+// End of a pass: the counters to h_ctr, every kernel of the pass complete. With the mapped
+// publication buffer, a one-thread kernel writes them there and the host spins on the sequence word
+// (polling the stream for errors now and then); host event delivery (GPU writes into mapped memory
+// by k_copy_out) keeps the stream synchronisation.
+int finish_pass(gwaoi_mgr* m, bool copy_events) {
+  hipStream_t st = m->stream;
+  if (!m->h_pub || copy_events) {
+    HIPCHK(hipMemcpyAsync(m->h_ctr, m->ctr, gw::CTR_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return GWAOI_OK;
+  }
+  const uint32_t seq = ++m->pub_seq ? m->pub_seq : ++m->pub_seq;  // never 0 (the initial value)
+  gw::launch_publish(m->ctr, m->d_pub, seq, st);
+  HIPCHK(hipGetLastError());
+  volatile uint32_t* flag = m->h_pub + gw::kPubWords;
+  for (uint64_t spin = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++spin) {
+    if ((spin & 0xFFFF) == 0) {
+      const hipError_t e = hipStreamQuery(st);
+      if (e == hipSuccess) {  // everything done: the flag must be visible now
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq) {
+          set_err("end-of-pass publication lost (flag %u, want %u)", *flag, seq);
+          return GWAOI_ERR_HIP;
+        }
+        break;
+      }
+      if (e != hipErrorNotReady) HIPCHK(e);
+    }
+    __builtin_ia32_pause();
+  }
+  std::memcpy(m->h_ctr, m->h_pub, gw::kPubWords * sizeof(uint32_t));
+  return GWAOI_OK;
+}
+
 // Run the device pipeline over the staged batch (host ops or the device batch). Events accumulate
 // (device buffer always, host buffer when copy_events) until the next gwaoi_tick returns them.
 int run_pass(gwaoi_mgr* m, bool copy_events) {
@@ -425,6 +490,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   }
   RCHK(upload_geom(m, m->grid[ng], geo));
 
+  RCHK(collect_timing(m));  // before the events are recorded again
   if (m->timing) HIPCHK(hipEventRecord(m->tev[0], st));
   if (!dev) {
     HIPCHK(hipMemcpyAsync(m->d_op_slot, m->h_op_slot, n_ops * sizeof(uint32_t), hipMemcpyHostToDevice, st));
@@ -530,8 +596,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     gw::launch_order(o, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
-    HIPCHK(hipMemcpyAsync(m->h_ctr, m->ctr, gw::CTR_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    RCHK(finish_pass(m, copy_events));
     if (m->h_ctr[gw::CTR_ERR]) {
       m->broken = true;
       set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
@@ -548,24 +613,13 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     }
     m->tick_events += nev;
     m->tick_enter += m->h_ctr[gw::CTR_ENTER];
-    if (m->timing) {
-      float t01, t12, t23, t34, t04;
-      HIPCHK(hipEventElapsedTime(&t01, m->tev[0], m->tev[1]));
-      HIPCHK(hipEventElapsedTime(&t12, m->tev[1], m->tev[2]));
-      HIPCHK(hipEventElapsedTime(&t23, m->tev[2], m->tev[3]));
-      HIPCHK(hipEventElapsedTime(&t34, m->tev[3], m->tev[4]));
-      HIPCHK(hipEventElapsedTime(&t04, m->tev[0], m->tev[4]));
-      m->stats.ticks++;
-      m->stats.ms_apply += t01;
-      m->stats.ms_grid += t12;
-      m->stats.ms_sweep += t23;
-      m->stats.ms_order += t34;
-      m->stats.ms_total += t04;
-      m->stats.sweep_movers += n_ops;
-      m->stats.events += nev;
-      m->stats.grid_records += m->h_ctr[gw::CTR_RECORDS];
-      m->stats.grid_cells += m->grid[ng].ncells;
-      m->stats.dense_movers += m->h_ctr[gw::CTR_DENSE];
+    if (m->timing) {  // read the hipEvents later (collect_timing): waiting on them here costs latency
+      m->tpend.pending = true;
+      m->tpend.n_ops = n_ops;
+      m->tpend.nev = nev;
+      m->tpend.records = m->h_ctr[gw::CTR_RECORDS];
+      m->tpend.ncells = m->grid[ng].ncells;
+      m->tpend.dense = m->h_ctr[gw::CTR_DENSE];
     }
     break;
   }
@@ -665,7 +719,7 @@ void free_all(gwaoi_mgr* m) {
       if (p) hipFree(p);
   }
   void* hptrs[] = {m->h_op_slot, m->h_op_x, m->h_op_z, m->h_op_kind, m->h_op_space, m->h_leaves, m->h_ctr,
-                   m->h_ev};
+                   m->h_ev, m->h_pub};
   for (void* p : hptrs)
     if (p) hipHostFree(p);
   for (auto& e : m->tev)
@@ -753,6 +807,19 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->ctr_buf, 2 * gw::CTR_N));
   m->ctr = m->ctr_buf;
   chk(halloc(&m->h_ctr, gw::CTR_N));
+  if (r == GWAOI_OK) {
+    void* dp = nullptr;
+    if (hipHostMalloc((void**)&m->h_pub, (gw::kPubWords + 1) * sizeof(uint32_t),
+                      hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+        hipHostGetDevicePointer(&dp, m->h_pub, 0) == hipSuccess) {
+      m->d_pub = (uint32_t*)dp;
+      std::memset(m->h_pub, 0, (gw::kPubWords + 1) * sizeof(uint32_t));
+    } else {  // the DMA-copy path below still works
+      (void)hipGetLastError();
+      if (m->h_pub) (void)hipHostFree(m->h_pub);
+      m->h_pub = nullptr;
+    }
+  }
   chk(halloc(&m->h_op_slot, C));
   chk(halloc(&m->h_op_x, C));
   chk(halloc(&m->h_op_z, C));
@@ -1076,18 +1143,25 @@ int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint6
 
 int gwaoi_set_timing(gwaoi_mgr* m, int enable) {
   if (!m) return GWAOI_ERR_INVALID;
+  RCHK(set_dev(m));
+  RCHK(collect_timing(m));
   m->timing = enable != 0;
   return GWAOI_OK;
 }
 
 int gwaoi_get_stats(const gwaoi_mgr* m, gwaoi_stats* out) {
   if (!m || !out) return GWAOI_ERR_INVALID;
+  gwaoi_mgr* mm = const_cast<gwaoi_mgr*>(m);  // the last timed pass is folded in on demand
+  RCHK(set_dev(mm));
+  RCHK(collect_timing(mm));
   *out = m->stats;
   return GWAOI_OK;
 }
 
 int gwaoi_reset_stats(gwaoi_mgr* m) {
   if (!m) return GWAOI_ERR_INVALID;
+  RCHK(set_dev(m));
+  RCHK(collect_timing(m));
   m->stats = gwaoi_stats{};
   return GWAOI_OK;
 }
