@@ -561,12 +561,12 @@ void launch_bin_tiles(const BinArgs& a, ScanCtx& sc, hipStream_t st) {
 // global atomic; a mover's events are numbered in a register (one thread per mover) and its count is
 // stored once, without atomics.
 #ifndef GW_SWEEP_BLOCK
-#define GW_SWEEP_BLOCK 576
+#define GW_SWEEP_BLOCK 512
 #endif
 #ifndef GW_SWEEP_WAVES_PER_EU
-#define GW_SWEEP_WAVES_PER_EU 5
+#define GW_SWEEP_WAVES_PER_EU 6
 #endif
-constexpr int kSweepBlock = GW_SWEEP_BLOCK;  // 9 waves: a config-2 tile holds ~520 movers (one round, rarely two)
+constexpr int kSweepBlock = GW_SWEEP_BLOCK;  // 8 waves: a config-2 tile holds ~520 movers (one round, a few twice)
 #ifndef GW_EV_LDS
 #define GW_EV_LDS 192
 #endif
@@ -589,11 +589,11 @@ struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint16_t ccs[kRegCells + 8];  // column-major: start in cidx of each region cell (+ total)
   uint16_t cidx[kCap];          // column-major order of the staged records (LDS record indices)
   uint4 rp[kCap];      // staged record, LDS form: {x_start, z_start, x_end, z_end} (float bits)
-  uint4 rm[kCap];      // {r, lo, span, seq_start}: op rank (~0u: no op) and the validity window
+  uint2 rm[kCap];      // {r | G, seq_start | A}: op rank (kNoRank: no op) and the validity mode (lds_record)
   uint32_t rslot[kCap];  // slot (read only when an event is emitted)
 };
-// two blocks per CU (160 KiB of LDS)
-static_assert(sizeof(SweepSmem) <= 163840 / 2, "sweep LDS budget: 2 blocks per CU");
+// three blocks per CU (160 KiB of LDS)
+static_assert(sizeof(SweepSmem) <= 163840 / 3 - 512, "sweep LDS budget: 3 blocks per CU");
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
 uint32_t sweep_block() { return kSweepBlock; }
@@ -750,38 +750,33 @@ __device__ __forceinline__ int judge(const Judge& J, const uint4 ra, const uint4
   return (valid & (before != after)) ? (after ? 2 : 1) : 0;
 }
 
-// The LDS form of a grid record, precomputing what judge() derives per candidate. With r = the
-// record's op rank in this pass (~0u if its entity has no op), the record is a valid candidate for
-// the mover of rank k iff (k - lo) < span (unsigned) and r != k:
-//   ghost (start cell; met only if not acted earlier):       k < r          lo = 0,     span = r
-//   main with a ghost (met only if acted earlier):            k > r          lo = r + 1, span = ~0u - r - 1
-//   main alone, absent at the start (entered in this pass):   k > r          (same)
-//   main alone, present at the start:                         k != r         lo = 0,     span = ~0u
+// The LDS form of a grid record, precomputing what judge() derives per candidate: position quad
+// rp = {x_start, z_start, x_end, z_end} and rm = {r | G, seq_start | A}, r = the record's op rank in
+// this pass (kNoRank if its entity has no op; ranks < capacity <= 2^31 - 1, seqs < 2^31). The record
+// is a valid candidate for the mover of rank k iff r != k and
+//   G (ghost: start cell, met only if not acted earlier):                      k < r
+//   A (main with a ghost, or absent at the start: met only if acted earlier):  k > r
+//   neither (main alone, present at the start):                                any k
 // which is judge()'s `valid` term case by case; positions: start always, end = the binned position
 // (for a ghost the binned position is its start, and a ghost is never used "acted earlier").
+constexpr uint32_t kNoRank = 0x7FFFFFFFu, kTopBit = 0x80000000u;
+
 __device__ __forceinline__ void lds_record(const uint4 ra, const uint4 rb, uint32_t base, uint32_t n_ops, uint4& rp,
-                                           uint4& rm, uint32_t& rslot) {
+                                           uint2& rm, uint32_t& rslot) {
   const uint32_t q = ra.w - base;
-  const uint32_t r = q < n_ops ? q : ~0u;
+  const uint32_t r = q < n_ops ? q : kNoRank;
   const bool ghost = ra.z >= REC_GHOST, hasg = (ra.z & REC_HASG) != 0;
-  uint32_t lo, span;
-  if (ghost) {
-    lo = 0u, span = r;
-  } else if (hasg || rb.z == 0u) {
-    lo = r + 1u, span = ~0u - r - 1u;
-  } else {
-    lo = 0u, span = ~0u;
-  }
+  const bool after = !ghost && (hasg || rb.z == 0u) && r != kNoRank;
   rp = make_uint4(rb.x, rb.y, ra.x, ra.y);
-  rm = make_uint4(r, lo, span, rb.z);
+  rm = make_uint2(r | (ghost ? kTopBit : 0u), rb.z | (after ? kTopBit : 0u));
   rslot = ra.z & REC_SLOT;
 }
 
 // judge() on the LDS form
-__device__ __forceinline__ int judge_lds(const Judge& J, const uint4 rp, const uint4 rm) {
-  const uint32_t r = rm.x, seq0 = rm.w;
+__device__ __forceinline__ int judge_lds(const Judge& J, const uint4 rp, const uint2 rm) {
+  const uint32_t r = rm.x & ~kTopBit, seq0 = rm.y & ~kTopBit;
   const bool ae = r < J.rank;  // acted earlier in this pass
-  const bool valid = ((J.rank - rm.y) < rm.z) & (r != J.rank);
+  const bool valid = (r != J.rank) & (!(rm.x & kTopBit) | !ae) & (!(rm.y & kTopBit) | ae);
   const float px = __uint_as_float(ae ? rp.z : rp.x);
   const float pz = __uint_as_float(ae ? rp.w : rp.y);
   const bool useo = ae | (seq0 > J.q0);  // o's box (o acted last) or m's old box
@@ -885,7 +880,8 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     uint32_t k = 0;
     for (; k + 1 < Rs.total; k += 2) {  // two candidates per iteration: both LDS reads in flight
       const uint32_t j0 = stream_at(Rs, k), j1 = stream_at(Rs, k + 1);
-      const uint4 p0 = sm.rp[j0], q0 = sm.rm[j0], p1 = sm.rp[j1], q1 = sm.rm[j1];
+      const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
+      const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
       const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
       if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
       if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j1], e1 == 2, nent);
@@ -898,7 +894,8 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     // column stream: through the column-major index
     for (k = 0; k + 1 < Cs.total; k += 2) {
       const uint32_t j0 = sm.cidx[stream_at(Cs, k)], j1 = sm.cidx[stream_at(Cs, k + 1)];
-      const uint4 p0 = sm.rp[j0], q0 = sm.rm[j0], p1 = sm.rp[j1], q1 = sm.rm[j1];
+      const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
+      const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
       const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
       if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
       if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j1], e1 == 2, nent);
@@ -915,7 +912,8 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     uint32_t j = sm.lcs[b + c0];
     const uint32_t e = (c0 <= c1) ? (uint32_t)sm.lcs[b + c1 + 1] : j;
     for (; j + 1 < e; j += 2) {  // two candidates per iteration: both LDS reads in flight
-      const uint4 p0 = sm.rp[j], q0 = sm.rm[j], p1 = sm.rp[j + 1], q1 = sm.rm[j + 1];
+      const uint4 p0 = sm.rp[j], p1 = sm.rp[j + 1];
+      const uint2 q0 = sm.rm[j], q1 = sm.rm[j + 1];
       const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
       if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j], e0 == 2, nent);
       if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j + 1], e1 == 2, nent);
@@ -1189,7 +1187,9 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
   GW_STAMP(4, __builtin_amdgcn_s_memrealtime());
 }
 
-// 2 blocks x 9 waves per CU (LDS-bound) need 5 waves per SIMD: at most 96 VGPRs
+// 3 blocks x 8 waves per CU (49 KB of LDS each) = 6 waves per SIMD: at most 80 VGPRs. (A VGPR count
+// that allows fewer waves per SIMD than the blocks need loses a whole block per CU, whatever the
+// occupancy API reports.)
 __global__ void __launch_bounds__(kSweepBlock) __attribute__((amdgpu_waves_per_eu(GW_SWEEP_WAVES_PER_EU)))
 k_sweep(SweepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
