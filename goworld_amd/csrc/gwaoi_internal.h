@@ -147,6 +147,7 @@ struct SweepArgs {
   uint32_t* ctr;
   uint32_t* dense;      // grid indices of movers for k_sweep_dense (boxes beyond the tile's LDS region)
   uint32_t dense_cap;
+  uint32_t dense_hint;  // dense movers of the previous pass (0: launch k_sweep_dense small)
 };
 
 struct RelArgs {

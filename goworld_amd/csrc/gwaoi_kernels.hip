@@ -1479,8 +1479,10 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
   if (a.leave_blocks)
     hipLaunchKernelGGL(k_sweep_leaves, dim3(a.leave_blocks * ((kSweepBlock + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        st, a);
-  // the dense list's length is on the device: a fixed grid that exits at once when it is empty
-  if (a.dense) hipLaunchKernelGGL(k_sweep_dense, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
+  // the dense list's length is on the device: a fixed grid that exits at once when it is empty (a
+  // small one when the previous pass had none; the kernel is grid-stride, any grid is correct)
+  if (a.dense)
+    hipLaunchKernelGGL(k_sweep_dense, dim3(a.dense_hint ? kDenseGrid : 64), dim3(kDenseBlock), 0, st, a);
 }
 
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each
@@ -1551,10 +1553,13 @@ void launch_order(const OrderArgs& o, hipStream_t st) {
 // into mapped (coherent) host memory with system-scope stores; the host spins on the sequence word
 // instead of a DMA copy plus a stream synchronisation.
 __global__ void k_publish(const uint32_t* __restrict__ ctr, uint32_t* pub, uint32_t seq) {
-  if (threadIdx.x != 0) return;
-  for (int i = 0; i < kPubWords; ++i) __hip_atomic_store(&pub[i], ctr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __threadfence_system();
-  __hip_atomic_store(&pub[kPubWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int i = threadIdx.x;
+  if (i < kPubWords) {  // one counter per lane
+    __hip_atomic_store(&pub[i], ctr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();  // complete before the flag below
+  }
+  __syncthreads();
+  if (i == 0) __hip_atomic_store(&pub[kPubWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_t st) {

@@ -160,6 +160,7 @@ struct gwaoi_mgr {
   uint32_t* h_pub = nullptr;     // mapped coherent host memory: [kPubWords] counters + sequence word
   uint32_t* d_pub = nullptr;     // its device address
   uint32_t pub_seq = 0;
+  uint32_t last_dense = ~0u;     // dense movers of the last pass (k_sweep_dense grid size hint)
   struct {                       // the last timed pass, collected once its events are complete
     bool pending = false;
     uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0;
@@ -570,6 +571,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.ctr = m->ctr;
     s.dense = m->d_dense;
     s.dense_cap = m->cap;
+    s.dense_hint = attempt ? ~0u : m->last_dense;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
@@ -636,6 +638,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->dv_x = m->dv_z = nullptr;
   m->pass_id++;
   if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
+  m->last_dense = m->h_ctr[gw::CTR_DENSE];
   m->n_present_dev = m->n_present;
   m->dv_kind = nullptr;
   m->dv_space = nullptr;
