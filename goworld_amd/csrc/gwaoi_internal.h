@@ -11,11 +11,12 @@ namespace gw {
 enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2, OP_KIND = 3, OP_SILENT = 0x80 };
 
 // Device-side error bits (device-staged batches are validated on the GPU).
-enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u, ERR_PRESENT_SLOT = 8u, ERR_BAD_SPACE = 16u };
+enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u, ERR_PRESENT_SLOT = 8u, ERR_BAD_SPACE = 16u,
+                  ERR_BAD_COUNT = 32u };
 
 // Counters block in device memory.
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
-       CTR_DENSE = 7, CTR_HOLES = 8,
+       CTR_DENSE = 7, CTR_HOLES = 8, CTR_NOPS = 9,  // ops of the pass (device-counted batches)
        CTR_TQ = 32,          // k_sweep's per-XCD tile queues (persistent blocks): queue q at CTR_TQ + q * CTR_QSTRIDE,
        CTR_QSTRIDE = 32,     // one 128-B line each (a returning atomic serialises per line)
        CTR_N = 32 + 8 * 32 };
@@ -73,6 +74,7 @@ struct GridView {
 };
 
 struct ApplyArgs {
+  const uint32_t* n_dev;     // non-null: the batch's op count is *n_dev (<= n_ops, the launch bound)
   const uint32_t* op_slot;
   const float* op_x;
   const float* op_z;
@@ -206,6 +208,7 @@ struct OrderArgs {
   const uint32_t* opq;
   uint32_t base, cap;
   int check_ops;
+  const uint32_t* n_dev;  // device-counted batch: ranks >= *n_dev are not ops
 };
 // k_place (+ zeroing side jobs) -> k_slice_sort (+ batch check) -> k_copy_out (if host_out)
 void launch_order(const OrderArgs& o, hipStream_t st);

@@ -104,15 +104,20 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool pred) {
 
 __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  const bool live = i < a.n_ops;
+  const uint32_t n_real = a.n_dev ? *a.n_dev : a.n_ops;
+  const bool live = i < a.n_ops && i < n_real;
+  if (i == 0) {
+    a.ctr[CTR_NOPS] = min(n_real, a.n_ops);
+    if (n_real > a.n_ops) atomicOr(&a.ctr[CTR_ERR], ERR_BAD_COUNT);
+    a.rank_cnt[a.n_ops] = 0u;
+  }
+  if (i < a.n_ops) a.rank_cnt[i] = 0u;  // the sweep stores only non-zero event counts
   uint32_t s = 0, q0 = 0;
   uint8_t kind = OP_MOVE;
   bool ok = live;
   if (live) {
     s = a.op_slot[i];
     kind = a.op_kind ? (uint8_t)(a.op_kind[i] & OP_KIND) : (uint8_t)OP_MOVE;
-    if (i == 0) a.rank_cnt[a.n_ops] = 0u;
-    a.rank_cnt[i] = 0u;  // the sweep stores only non-zero event counts
     if (a.check && s >= a.cap) {
       atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SLOT);
       ok = false;
@@ -1514,7 +1519,7 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
 
 __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-  if (r >= o.n_ops) return;
+  if (r >= o.n_ops || (o.n_dev && r >= *o.n_dev)) return;
   if (o.check_ops) {
     const uint32_t s = o.op_slot[r];
     if (s < o.cap && o.opq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);

@@ -133,6 +133,7 @@ struct gwaoi_mgr {
   const float* dv_z = nullptr;
   const uint8_t* dv_kind = nullptr;  // mixed device batch (gwaoi_stage_ops_device), else null
   const uint32_t* dv_space = nullptr;  // Space of each device Enter (null: Space 0)
+  const uint32_t* dv_count = nullptr;  // device-counted batch: *dv_count ops (dv_n = the bound)
   uint32_t dv_n = 0;
   bool dev_managed = false;          // presence lives on the device only (mixed device batches)
 
@@ -503,6 +504,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemcpyAsync(m->d_leaves, m->h_leaves, m->n_leaves * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
   gw::ApplyArgs a;
+  a.n_dev = dev ? m->dv_count : nullptr;
   a.op_slot = dev ? m->dv_slot : m->d_op_slot;
   a.op_x = dev ? m->dv_x : m->d_op_x;
   a.op_z = dev ? m->dv_z : m->d_op_z;
@@ -595,6 +597,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     o.base = base;
     o.cap = m->cap;
     o.check_ops = dev ? 1 : 0;
+    o.n_dev = dev ? m->dv_count : nullptr;
     gw::launch_order(o, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
@@ -602,7 +605,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     if (m->h_ctr[gw::CTR_ERR]) {
       m->broken = true;
       set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
-              "capacity, 8=Enter of a present slot, 16=Space id out of range); the manager is unusable",
+              "capacity, 8=Enter of a present slot, 16=Space id out of range, 32=op count above its bound); the manager is "
+              "unusable",
               m->h_ctr[gw::CTR_ERR]);
       return GWAOI_ERR_DEVICE_CHECK;
     }
@@ -617,7 +621,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     m->tick_enter += m->h_ctr[gw::CTR_ENTER];
     if (m->timing) {  // read the hipEvents later (collect_timing): waiting on them here costs latency
       m->tpend.pending = true;
-      m->tpend.n_ops = n_ops;
+      m->tpend.n_ops = m->h_ctr[gw::CTR_NOPS];
       m->tpend.nev = nev;
       m->tpend.records = m->h_ctr[gw::CTR_RECORDS];
       m->tpend.ncells = m->grid[ng].ncells;
@@ -630,7 +634,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->ctr_sel ^= 1;
   m->ctr = m->ctr_buf + m->ctr_sel * gw::CTR_N;
   m->tick_passes++;
-  m->tick_ops += n_ops;
+  m->tick_ops += m->h_ctr[gw::CTR_NOPS];
   m->n_ops = 0;
   m->n_leaves = 0;
   m->dv_n = 0;
@@ -642,6 +646,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->n_present_dev = m->n_present;
   m->dv_kind = nullptr;
   m->dv_space = nullptr;
+  m->dv_count = nullptr;
   return GWAOI_OK;
 }
 
@@ -1028,6 +1033,11 @@ int gwaoi_stage_ops_device(gwaoi_mgr* m, const uint32_t* d_slots, const float* d
 
 int gwaoi_stage_ops_device_spaces(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,
                                   const uint8_t* d_kinds, const uint32_t* d_spaces, uint32_t n) {
+  return gwaoi_stage_ops_device_n(m, d_slots, d_x, d_z, d_kinds, d_spaces, nullptr, n);
+}
+
+int gwaoi_stage_ops_device_n(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                             const uint8_t* d_kinds, const uint32_t* d_spaces, const uint32_t* d_n, uint32_t n) {
   RCHK(check_mgr(m));
   if (n && (!d_slots || !d_x || !d_z || !d_kinds)) {
     set_err("stage_ops_device: null array");
@@ -1045,6 +1055,7 @@ int gwaoi_stage_ops_device_spaces(gwaoi_mgr* m, const uint32_t* d_slots, const f
   m->dv_z = d_z;
   m->dv_kind = d_kinds;
   m->dv_space = d_spaces;
+  m->dv_count = d_n;
   m->dv_n = n;
   return GWAOI_OK;
 }

@@ -93,12 +93,14 @@ class Engine:
         check(self._L.gwaoi_stage_moves_device(self._h, ctypes.c_void_p(d_slots), ctypes.c_void_p(d_x),
                                                 ctypes.c_void_p(d_z), n))
 
-    def stage_ops_device(self, d_slots: int, d_x: int, d_z: int, d_kinds: int, n: int, d_spaces: int = 0):
+    def stage_ops_device(self, d_slots: int, d_x: int, d_z: int, d_kinds: int, n: int, d_spaces: int = 0,
+                         d_count: int = 0):
         """Mixed Enter/Leave/Moved batch from device arrays (kinds: GWAOI_OP_*, | GWAOI_OP_SILENT);
-        d_spaces (optional): the Space of each Enter."""
-        check(self._L.gwaoi_stage_ops_device_spaces(self._h, ctypes.c_void_p(d_slots), ctypes.c_void_p(d_x),
-                                                     ctypes.c_void_p(d_z), ctypes.c_void_p(d_kinds),
-                                                     ctypes.c_void_p(d_spaces or None), n))
+        d_spaces (optional): the Space of each Enter; d_count (optional): device address of the op
+        count (then n is only its upper bound)."""
+        check(self._L.gwaoi_stage_ops_device_n(self._h, ctypes.c_void_p(d_slots), ctypes.c_void_p(d_x),
+                                                ctypes.c_void_p(d_z), ctypes.c_void_p(d_kinds),
+                                                ctypes.c_void_p(d_spaces or None), ctypes.c_void_p(d_count or None), n))
 
     def set_stream(self, stream_ptr: int):
         check(self._L.gwaoi_set_stream(self._h, ctypes.c_void_p(stream_ptr)))

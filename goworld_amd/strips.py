@@ -95,8 +95,12 @@ class StripNode:
         self.left = torch.zeros((self.cap, 4), dtype=i32, device=dev)
         self.right = torch.zeros((self.cap, 4), dtype=i32, device=dev)
         self.counts = torch.zeros(4, dtype=i32, device=dev)  # [left, right, n_ops, err]
+        self.h_counts = torch.zeros(4, dtype=i32).pin_memory()  # read after each tick, no extra sync
         self.scratch = torch.zeros(int(self._L.gwaoi_strip_scratch_words(n)), dtype=i32, device=dev)
-        self.stream = torch.cuda.current_stream(dev)
+        # a stream of the node's own (never the null stream: the manager would take that as "its
+        # own stream" and the strip kernels and the pipeline would no longer be ordered)
+        self.stream = torch.cuda.Stream(dev)
+        torch.cuda.synchronize(dev)  # the buffers above were zeroed on the current stream
         lo = max(self.g.ra, 0.0)
         hi = min(self.g.rb, layout.L)
         self.eng = Engine(layout.dist, capacity=n, device=device, bounds=(lo, 0.0, hi, layout.L))
@@ -113,32 +117,42 @@ class StripNode:
     def _err(self):
         return ctypes.c_void_p(self.counts.data_ptr() + 12)
 
-    def _emit_and_tick(self, host_events: bool):
+    def _emit_and_tick(self, host_events: bool, n_bound: int):
+        """The op list goes to the manager with its count in device memory (no host round trip);
+        n_bound bounds it: entities present at the start + records received this tick."""
         L = self._L
         check(L.gwaoi_strip_emit(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz), _ptr(self.ex),
                                  _ptr(self.ez), _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds),
                                  _ptr(self.scratch), ctypes.c_void_p(self.counts.data_ptr() + 8)))
-        c = self.counts.cpu()  # synchronises the stream
+        self.h_counts.copy_(self.counts, non_blocking=True)  # stream-ordered before the tick's kernels
+        n_bound = max(1, min(self.n, int(n_bound)))
+        self.eng.stage_ops_device(self.ids.data_ptr(), self.ox.data_ptr(), self.oz.data_ptr(),
+                                  self.kinds.data_ptr(), n_bound, d_count=self.counts.data_ptr() + 8)
+        ev = self.eng.tick() if host_events else self.eng.tick_device()
+        c = self.h_counts  # complete: the tick waited for every kernel after the copy
         if int(c[3]):
             raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, f"strip {self.rank}: protocol check failed (flags {int(c[3])})")
-        n_ops = int(c[2])
-        self.last_ops = n_ops
-        if n_ops:
-            self.eng.stage_ops_device(self.ids.data_ptr(), self.ox.data_ptr(), self.oz.data_ptr(),
-                                      self.kinds.data_ptr(), n_ops)
-        return self.eng.tick() if host_events else self.eng.tick_device()
+        self.last_ops = int(c[2])
+        return ev
 
     # ---- protocol ----
     def start(self, host_events: bool = False):
         """Tick 0: every entity of the region enters (the seeded workload's initial placement)."""
-        check(self._L.gwaoi_strip_init_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
-                                            ctypes.c_uint64(self.seed), ctypes.c_float(self.layout.L)))
-        self.tick_no = 0
-        return self._emit_and_tick(host_events)
+        with torch.cuda.stream(self.stream):
+            check(self._L.gwaoi_strip_init_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
+                                                ctypes.c_uint64(self.seed), ctypes.c_float(self.layout.L)))
+            self.tick_no = 0
+            return self._emit_and_tick(host_events, self.n)
 
     def prepare(self, t: int, step: float = 1.0, moves: Optional[Tuple[torch.Tensor, ...]] = None):
         """End positions of the owned entities (the seeded walk's tick t, or `moves` = (ids, x, z)
         device tensors) and the records each neighbour needs; returns (left, right) device tensors."""
+        if moves is not None:  # produced on the caller's stream
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            return self._prepare(t, step, moves)
+
+    def _prepare(self, t, step, moves):
         L = self._L
         if moves is None:
             check(L.gwaoi_strip_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz),
@@ -151,21 +165,28 @@ class StripNode:
         check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
                                    _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
                                    ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+        self.tick_no = t
+        if not (self.g.has_left or self.g.has_right):  # nothing to send: no round trip (errors: finish)
+            return self.left[:0], self.right[:0]
         c = self.counts.cpu()
         if int(c[3]):
             raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, f"strip {self.rank}: protocol check failed (flags {int(c[3])})")
-        self.tick_no = t
         return self.left[: int(c[0])], self.right[: int(c[1])]
 
     def finish(self, left_in: torch.Tensor, right_in: torch.Tensor, host_events: bool = False):
         """Absorb the neighbours' records, run the tick; returns the manager's Events (device) or the
         (n, 2) host array of the owned movers' events in canonical order."""
-        for recs in (left_in, right_in):
-            if recs is not None and recs.numel():
-                recs = recs.to(self.device).contiguous()
-                check(self._L.gwaoi_strip_absorb(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
-                                                 _ptr(recs), int(recs.shape[0])))
-        return self._emit_and_tick(host_events)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))  # received on the caller's stream
+        with torch.cuda.stream(self.stream):
+            nin = 0
+            for recs in (left_in, right_in):
+                if recs is not None and recs.numel():
+                    recs = recs.to(self.device).contiguous()
+                    recs.record_stream(self.stream)
+                    nin += int(recs.shape[0])
+                    check(self._L.gwaoi_strip_absorb(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
+                                                     _ptr(recs), int(recs.shape[0])))
+            return self._emit_and_tick(host_events, self.eng.count()[0] + nin)
 
     def close(self):
         self.eng.close()

@@ -127,6 +127,12 @@ int gwaoi_stage_ops_device(gwaoi_mgr* mgr, const uint32_t* d_slots, const float*
  * with GWAOI_OP_SILENT on every op it rebuilds the relation without reporting the pairs. */
 int gwaoi_stage_ops_device_spaces(gwaoi_mgr* mgr, const uint32_t* d_slots, const float* d_x, const float* d_z,
                                   const uint8_t* d_kinds, const uint32_t* d_spaces, uint32_t n);
+/* The same with the op count in device memory: the batch is the first *d_n ops (read on the
+ * device when the pass runs; must be <= n_max, the bound the kernels are launched for). A batch
+ * produced on the GPU (X-strip op lists, GPU-decoded position records) goes in without the host
+ * waiting for its size; gwaoi_events.n_ops reports the count. */
+int gwaoi_stage_ops_device_n(gwaoi_mgr* mgr, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                             const uint8_t* d_kinds, const uint32_t* d_spaces, const uint32_t* d_n, uint32_t n_max);
 
 /* Apply every staged op; blocks until the events are on the host (or in device memory, see flags). */
 #define GWAOI_TICK_DEVICE_EVENTS 1u /* leave events in device memory (no D2H copy) */

@@ -434,3 +434,35 @@ def test_device_enters_into_spaces(gpu, po, silent):
     with pytest.raises(_lib.GwaoiError) as e:
         bad.tick()
     assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK
+
+
+def test_device_counted_batch(gpu, po):
+    """gwaoi_stage_ops_device_n: the op count lives in device memory (n_max only bounds it). The
+    events equal those of the same batch staged with its exact count; a count above the bound fails
+    the batch."""
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine
+    case = H.case_random_ops(seed=77, n=900, nticks=6, ops_per_tick=700, world=500.0, dist=50.0, dup=False)
+    cap = case["cap"]
+    a, b = Engine(case["dist"], capacity=cap), Engine(case["dist"], capacity=cap)
+    orc = po.XZListOracle(case["dist"], cap)
+    bs, bx, bz, bk, bn = DeviceBuffer(4 * cap), DeviceBuffer(4 * cap), DeviceBuffer(4 * cap), DeviceBuffer(cap), \
+        DeviceBuffer(4)
+    for t, ops in enumerate(case["ticks"]):
+        bs.upload(np.asarray([o[1] for o in ops], np.uint32))
+        bx.upload(np.asarray([o[2] for o in ops], np.float32))
+        bz.upload(np.asarray([o[3] for o in ops], np.float32))
+        bk.upload(np.asarray([o[0] for o in ops], np.uint8))
+        bn.upload(np.asarray([len(ops)], np.uint32))
+        want = H.oracle_tick(orc, ops)
+        a.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, len(ops))
+        b.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, cap, d_count=bn.ptr)  # bound = capacity
+        ga, gb = a.tick(), b.tick()
+        assert_same(ga, want, f"exact count tick {t}")
+        assert_same(gb, want, f"device count tick {t}")
+        assert b.last.n_ops == len(ops)
+    bn.upload(np.asarray([5], np.uint32))
+    b.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, 4, d_count=bn.ptr)  # 5 > bound 4
+    with pytest.raises(_lib.GwaoiError) as e:
+        b.tick()
+    assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK
