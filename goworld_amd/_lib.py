@@ -50,6 +50,38 @@ STRIP_SYMBOLS = (
 )
 
 
+# include/gwaoi_sync.h (tick-end sync fan-out and position ingest)
+SYNC_SYMBOLS = (
+    "gwaoi_sync_enable", "gwaoi_sync_get_tables", "gwaoi_sync_set_entities", "gwaoi_sync_set_clients",
+    "gwaoi_sync_set_syncing", "gwaoi_sync_mark", "gwaoi_collect_sync", "gwaoi_ingest_positions",
+)
+GWAOI_SYNC_OWN_CLIENT = 0x01
+GWAOI_SYNC_NEIGHBOR_CLIENTS = 0x02
+GWAOI_SYNC_FROM_CLIENT = 0x80
+GWAOI_SYNC_NO_CLIENT = 0xFFFF
+GWAOI_SYNC_MAX_GATES = 256
+GWAOI_COLLECT_HOST = 0x1
+GWAOI_COLLECT_KEEP_FLAGS = 0x2
+GWAOI_INGEST_HOST_PAYLOAD = 0x1
+
+
+class SyncTables(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_void_p), ("gate", ctypes.c_void_p), ("client_id", ctypes.c_void_p),
+                ("entity_id", ctypes.c_void_p), ("y", ctypes.c_void_p), ("yaw", ctypes.c_void_p),
+                ("capacity", ctypes.c_uint32), ("n_gates", ctypes.c_uint32)]
+
+
+class SyncOut(ctypes.Structure):
+    _fields_ = [("n_records", ctypes.c_uint64), ("n_gates", ctypes.c_uint32),
+                ("gate_off", ctypes.POINTER(ctypes.c_uint64)), ("d_records", ctypes.c_void_p),
+                ("records", ctypes.c_void_p), ("n_entities", ctypes.c_uint32)]
+
+
+class IngestResult(ctypes.Structure):
+    _fields_ = [("n_records", ctypes.c_uint32), ("n_moved", ctypes.c_uint32), ("n_unknown", ctypes.c_uint32),
+                ("n_rejected", ctypes.c_uint32), ("n_passes", ctypes.c_uint32)]
+
+
 class StripGeom(ctypes.Structure):
     _fields_ = [
         ("n", ctypes.c_uint32),
@@ -168,6 +200,14 @@ def load(path: str = SO_PATH):
         "gwaoi_strip_absorb": ([vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_strip_emit": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "gwaoi_strip_scratch_words": ([u32], ctypes.c_size_t),
+        "gwaoi_sync_enable": ([vp, u32], ctypes.c_int),
+        "gwaoi_sync_get_tables": ([vp, ctypes.POINTER(SyncTables)], ctypes.c_int),
+        "gwaoi_sync_set_entities": ([vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_sync_set_clients": ([vp, vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_sync_set_syncing": ([vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_sync_mark": ([vp, vp, vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_collect_sync": ([vp, u32, ctypes.POINTER(SyncOut)], ctypes.c_int),
+        "gwaoi_ingest_positions": ([vp, vp, u64, u32, ctypes.POINTER(IngestResult)], ctypes.c_int),
         "gwaoi_debug_sweep_occupancy": ([ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
                                         ctypes.c_int),
     }

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgwaoi.so")
-SOURCES = ["gwaoi_kernels.hip", "gwaoi_runtime.hip", "gwaoi_strips.hip"]
+SOURCES = ["gwaoi_kernels.hip", "gwaoi_runtime.hip", "gwaoi_strips.hip", "gwaoi_sync.hip"]
 HEADERS = ["gwaoi_internal.h"]
 PUBLIC = ["gwaoi.h", "gwaoi_tools.h", "gwaoi_workload.h", "gwaoi_strips.h"]
 ARCH = os.environ.get("GWAOI_ARCH", "gfx950")

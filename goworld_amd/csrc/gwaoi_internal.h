@@ -224,4 +224,32 @@ void launch_wl_step(const float* xp, const float* zp, float* xo, float* zo, uint
                     uint64_t tick, float L, float s, hipStream_t st);
 void launch_iota(uint32_t* d, uint32_t n, hipStream_t st);
 
+// ---- manager view for the callers either side of the path (gwaoi_sync.hip) ----
+struct SyncState;  // gwaoi_sync.hip
+struct MgrView {
+  int device;
+  hipStream_t stream;
+  uint32_t cap;
+  GridView g;                // the grid of the last pass (main records = current state)
+  const uint32_t* rec_count;  // device: records of that grid (cs[ncells])
+  uint32_t rec_bound;         // host upper bound on them
+  const float* pos_x;
+  const float* pos_z;
+  const uint32_t* seq;        // 0 = absent
+  const uint32_t* space_of;
+  ScanCtx* scan;
+  SyncState** sync;          // the manager's sync state slot (owned by the manager)
+  bool pending;              // ops staged and not yet run
+};
+}  // namespace gw
+struct gwaoi_mgr;
+namespace gw {
+int mgr_view(gwaoi_mgr* m, MgrView* out);
+int mgr_flush(gwaoi_mgr* m);  // run the staged ops now (their events are kept for the next gwaoi_tick)
+// stage a device-counted batch of moves (*d_n <= n_max ops; slots distinct and present, checked on device)
+int mgr_stage_moves_device_n(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                             const uint32_t* d_n, uint32_t n_max);
+void sync_free(SyncState* s);
+void set_error(const char* fmt, ...);
+
 }  // namespace gw

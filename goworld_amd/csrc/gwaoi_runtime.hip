@@ -178,6 +178,8 @@ struct gwaoi_mgr {
   uint32_t tick_passes = 0, tick_ops = 0;
   bool acc_open = false;                      // a pass ran since the last gwaoi_tick
 
+  gw::SyncState* sync = nullptr;  // sync fan-out / ingest state (gwaoi_sync.hip), on demand
+
   // timing
   bool timing = false;
   hipEvent_t tev[5] = {};
@@ -715,6 +717,8 @@ void stage(gwaoi_mgr* m, uint32_t slot, uint8_t kind, float x, float z, uint32_t
 void free_all(gwaoi_mgr* m) {
   hipSetDevice(m->device);
   if (m->stream) hipStreamSynchronize(m->stream);
+  gw::sync_free(m->sync);
+  m->sync = nullptr;
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out};
@@ -894,6 +898,53 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
 
 // ================================================================================================
 // C ABI
+
+namespace gw {
+
+void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+int mgr_view(gwaoi_mgr* m, MgrView* out) {
+  RCHK(check_mgr(m));
+  RCHK(set_dev(m));
+  const Grid& g = m->grid[m->cur];
+  out->device = m->device;
+  out->stream = m->stream;
+  out->cap = m->cap;
+  out->g = {g.rec, g.cs, g.d_geom, g.d_tile_space};
+  out->rec_count = g.cs ? g.cs + g.ncells : nullptr;
+  out->rec_bound = 2 * m->cap;
+  out->pos_x = m->pos_x;
+  out->pos_z = m->pos_z;
+  out->seq = m->seq;
+  out->space_of = m->space_of;
+  out->scan = &m->scan;
+  out->sync = &m->sync;
+  out->pending = m->n_ops || m->dv_n;
+  return GWAOI_OK;
+}
+
+int mgr_flush(gwaoi_mgr* m) {
+  RCHK(check_mgr(m));
+  RCHK(set_dev(m));
+  if (m->n_ops || m->dv_n) RCHK(run_pass(m, true));
+  return GWAOI_OK;
+}
+
+int mgr_stage_moves_device_n(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,
+                             const uint32_t* d_n, uint32_t n_max) {
+  RCHK(gwaoi_stage_moves_device(m, d_slots, d_x, d_z, n_max));
+  m->dv_count = d_n;
+  return GWAOI_OK;
+}
+
+}  // namespace gw
 
 extern "C" {
 

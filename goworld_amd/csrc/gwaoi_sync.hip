@@ -1,0 +1,1110 @@
+// gwaoi_sync.hip — the callers either side of the AOI path, on the GPU (include/gwaoi_sync.h):
+//
+//   * tick-end sync fan-out (CollectEntitySyncInfos, engine/entity/Entity.go:1207-1267): for every
+//     flagged entity, a 48-byte record to its own client and to the client of every AOI neighbour,
+//     grouped per gate. The neighbour set is evaluated from the manager's grid exactly as the relation
+//     export does (N(a,b) = in(L, F), L = later actor), one thread per grid record in cell order so
+//     neighbouring threads walk the same cells. Count walk -> scan -> write walk (entity-major pair list)
+//     -> stable counting sort by gate (per 4096-pair chunk: LDS histogram, scan, wave-ballot multisplit
+//     ranks) that writes the wire records straight into their gate's packet body.
+//
+//   * position ingest (HandleSyncPositionYawFromClient, components/game/GameService.go:398-410): 32-byte
+//     records decoded on the GPU, EntityID -> slot through an open-addressing hash table (host-owned,
+//     mirrored to HBM on change), presence and syncingFromClient checked, accepted records compacted in
+//     payload order into a device-counted Moved batch of the manager. A payload that names a slot twice
+//     is cut at the first repeat and run as consecutive batches, so the events are those of the
+//     reference's sequential loop.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "gwaoi.h"
+#include "gwaoi_device.h"
+#include "gwaoi_internal.h"
+#include "gwaoi_sync.h"
+
+namespace gw {
+
+namespace {
+
+constexpr int kSy = 256;                  // threads per block
+constexpr int kGItems = 16;               // pairs per thread in the gate partition
+constexpr uint32_t kGChunk = kSy * kGItems;  // pairs per chunk (block) of the gate partition
+constexpr uint32_t kHEmpty = 0xFFFFFFFFu;  // hash bucket states (otherwise the bucket holds a slot)
+constexpr uint32_t kHTomb = 0xFFFFFFFEu;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+__host__ __device__ __forceinline__ uint32_t id_hash(uint4 k) {
+  const uint64_t a = ((uint64_t)k.y << 32) | k.x, b = ((uint64_t)k.w << 32) | k.z;
+  uint64_t h = (a * 0x9E3779B97F4A7C15ull) ^ ((b + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full);
+  h ^= h >> 31;
+  h *= 0xD6E8FEB86659FD93ull;
+  h ^= h >> 32;
+  return (uint32_t)h;
+}
+
+__host__ __device__ __forceinline__ bool id_eq(uint4 a, uint4 b) {
+  return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+__host__ __device__ __forceinline__ bool id_zero(uint4 a) { return !(a.x | a.y | a.z | a.w); }
+
+// ------------------------------------------------------------------------------------------------
+// setters: one thread per (deduplicated) entry
+struct ScatArgs {
+  const uint32_t* slot;
+  uint32_t n;
+  int mode;  // 0 entity ids, 1 clients, 2 syncing, 3 mark
+  const uint4* id;
+  const uint16_t* gate;
+  const float* y;
+  const float* yaw;
+  const uint8_t* f;
+  uint8_t* flags;
+  uint16_t* t_gate;
+  uint4* t_cid;
+  uint4* t_eid;
+  float* t_y;
+  float* t_yaw;
+};
+
+__global__ void __launch_bounds__(kSy) k_sync_scatter(ScatArgs a) {
+  const uint32_t i = blockIdx.x * kSy + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t s = a.slot[i];
+  switch (a.mode) {
+    case 0: a.t_eid[s] = a.id[i]; break;
+    case 1:
+      a.t_gate[s] = a.gate[i];
+      a.t_cid[s] = a.id[i];
+      break;
+    case 2: a.flags[s] = (uint8_t)((a.flags[s] & ~GWAOI_SYNC_FROM_CLIENT) | (a.f[i] ? GWAOI_SYNC_FROM_CLIENT : 0u)); break;
+    default:
+      a.t_y[s] = a.y[i];
+      a.t_yaw[s] = a.yaw[i];
+      a.flags[s] = (uint8_t)(a.flags[s] | a.f[i]);
+      break;
+  }
+}
+
+__global__ void __launch_bounds__(kSy) k_hash_scatter(const uint32_t* __restrict__ idx, const uint4* __restrict__ key,
+                                                      const uint32_t* __restrict__ val, uint32_t n, uint4* hkey,
+                                                      uint32_t* hval) {
+  const uint32_t i = blockIdx.x * kSy + threadIdx.x;
+  if (i >= n) return;
+  hkey[idx[i]] = key[i];
+  hval[idx[i]] = val[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// fan-out
+struct FanArgs {
+  GridView g;
+  const uint32_t* rec_count;
+  uint32_t rec_bound;
+  const float* pos_x;
+  const float* pos_z;
+  const uint32_t* space_of;
+  uint8_t* flags;
+  const uint16_t* gate;
+  int clear;            // write pass: clear the sync bits of every collected entity
+  uint32_t* cnt;        // count pass: pairs per grid record ([rec_bound + 1], scanned afterwards)
+  const uint32_t* off;  // write pass: the scanned counts
+  uint2* pairs;         // {entity, receiver} (receiver == entity: own client)
+  uint8_t* pgate;       // gate of each pair
+  uint32_t* n_ent;      // entities collected (count pass)
+};
+
+// Every neighbour o of the entity of main record j whose client exists: f(o). The neighbour set is
+// {o : in(L, F)} with L the later actor (Entity.InterestedBy under the XZ manager, see gwaoi_kernels.hip).
+template <class F>
+__device__ __forceinline__ void client_neighbours(const FanArgs& a, uint32_t s, float sx, float sz, uint32_t qs, F&& f) {
+  const Geom g = a.g.geom[a.space_of[s]];
+  const float D = g.D;
+  const CellBox B = qbox(g, sx, sz);
+  for (int r = B.z0; r <= B.z1; ++r) {
+    row_entries_global(g, a.g.cs, r, B.x0, B.x1, [&](uint32_t j) {
+      const uint4 ra = a.g.rec[j].a;
+      const uint32_t o = ra.z & REC_SLOT;
+      if ((ra.z & REC_GHOST) || o == s) return;
+      const uint32_t qo = a.g.rec[j].b.w;
+      const float ox = __uint_as_float(ra.x), oz = __uint_as_float(ra.y);
+      const bool in = (qo > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz);
+      if (in) {
+        const uint16_t go = a.gate[o];
+        if (go != GWAOI_SYNC_NO_CLIENT) f(o, go);
+      }
+    });
+  }
+}
+
+template <bool kWrite>
+__global__ void __launch_bounds__(kSy) k_fan(FanArgs a) {
+  const uint32_t nrec = *a.rec_count;
+  uint32_t ents = 0;
+  for (uint32_t j = blockIdx.x * kSy + threadIdx.x; j <= a.rec_bound; j += gridDim.x * kSy) {
+    uint32_t c = 0;
+    if (j < nrec) {
+      const uint4 ra = a.g.rec[j].a;
+      const uint32_t s = ra.z & REC_SLOT;
+      const uint8_t fl = (ra.z & REC_GHOST) ? 0 : a.flags[s];
+      const uint32_t want = fl & (GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
+      if (want) {
+        ++ents;
+        uint32_t w = kWrite ? a.off[j] : 0u;
+        const uint16_t gs = a.gate[s];
+        if ((want & GWAOI_SYNC_OWN_CLIENT) && gs != GWAOI_SYNC_NO_CLIENT) {
+          if (kWrite) {
+            a.pairs[w] = make_uint2(s, s);
+            a.pgate[w++] = (uint8_t)gs;
+          }
+          ++c;
+        }
+        if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS) {
+          const float sx = __uint_as_float(ra.x), sz = __uint_as_float(ra.y);
+          const uint32_t qs = a.g.rec[j].b.w;
+          client_neighbours(a, s, sx, sz, qs, [&](uint32_t o, uint16_t go) {
+            if (kWrite) {
+              a.pairs[w] = make_uint2(s, o);
+              a.pgate[w++] = (uint8_t)go;
+            }
+            ++c;
+          });
+        }
+        if (kWrite && a.clear)
+          a.flags[s] = (uint8_t)(fl & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
+      }
+    }
+    if (!kWrite) a.cnt[j] = c;
+  }
+  if (!kWrite) {
+    // one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) ents += __shfl_xor(ents, o, 64);
+    if ((threadIdx.x & 63) == 0 && ents) atomicAdd(a.n_ent, ents);
+  }
+}
+
+struct GateArgs {
+  const uint2* pairs;
+  const uint8_t* pgate;
+  uint32_t n;        // pairs
+  uint32_t nchunks;
+  uint32_t n_gates;
+  int bits;          // ceil(log2(n_gates)), >= 1
+  uint32_t* ghist;   // [n_gates * nchunks + 1], gate-major; scanned between the two kernels
+  const uint4* cid;
+  const uint4* eid;
+  const float* pos_x;
+  const float* pos_z;
+  const float* y;
+  const float* yaw;
+  uint4* out;        // 3 uint4 per record
+  uint32_t* goff;    // [n_gates + 1]
+};
+
+__global__ void __launch_bounds__(kSy) k_gate_hist(GateArgs a) {
+  __shared__ uint32_t h[GWAOI_SYNC_MAX_GATES];
+  for (uint32_t g = threadIdx.x; g < a.n_gates; g += kSy) h[g] = 0;
+  __syncthreads();
+  const uint32_t b0 = blockIdx.x * kGChunk;
+#pragma unroll 4
+  for (int k = 0; k < kGItems; ++k) {
+    const uint32_t i = b0 + k * kSy + threadIdx.x;
+    if (i < a.n) atomicAdd(&h[a.pgate[i]], 1u);
+  }
+  __syncthreads();
+  for (uint32_t g = threadIdx.x; g < a.n_gates; g += kSy) a.ghist[g * a.nchunks + blockIdx.x] = h[g];
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.ghist[a.n_gates * a.nchunks] = 0;
+}
+
+// Stable partition of one chunk by gate: rounds of 256 pairs; inside a wave, lanes of the same gate
+// are found with one ballot per gate bit; across the block's 4 waves, per-wave gate counts in LDS.
+__global__ void __launch_bounds__(kSy) k_gate_scatter(GateArgs a) {
+  __shared__ uint32_t run[GWAOI_SYNC_MAX_GATES];         // pairs of each gate placed by earlier rounds
+  __shared__ uint32_t wc[kSy / 64][GWAOI_SYNC_MAX_GATES];  // this round: pairs of each gate per wave
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (uint32_t g = threadIdx.x; g < a.n_gates; g += kSy) {
+    run[g] = a.ghist[g * a.nchunks + blockIdx.x];  // chunk's base in the gate-major output
+#pragma unroll
+    for (int k = 0; k < kSy / 64; ++k) wc[k][g] = 0;
+  }
+  __syncthreads();
+  const uint32_t b0 = blockIdx.x * kGChunk;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (int k = 0; k < kGItems; ++k) {
+    const uint32_t i = b0 + k * kSy + threadIdx.x;
+    const bool live = i < a.n;
+    const uint32_t g = live ? a.pgate[i] : 0u;
+    unsigned long long same = __ballot(live);
+    for (int b = 0; b < a.bits; ++b) {
+      const unsigned long long v = __ballot(live && ((g >> b) & 1u));
+      same &= ((g >> b) & 1u) ? v : ~v;
+    }
+    const bool leader = live && !(same & lt);
+    if (leader) wc[w][g] = (uint32_t)__popcll(same);
+    __syncthreads();
+    uint32_t pos = 0;
+    if (live) {
+      pos = run[g] + (uint32_t)__popcll(same & lt);
+      for (int q = 0; q < w; ++q) pos += wc[q][g];
+    }
+    __syncthreads();
+    if (leader) {
+      atomicAdd(&run[g], (uint32_t)__popcll(same));
+      wc[w][g] = 0;
+    }
+    if (live) {
+      const uint2 p = a.pairs[i];
+      const uint32_t e = p.x, r = p.y;
+      uint4* o = a.out + (size_t)pos * 3;
+      o[0] = a.cid[r];
+      o[1] = a.eid[e];
+      o[2] = make_uint4(__float_as_uint(a.pos_x[e]), __float_as_uint(a.y[e]), __float_as_uint(a.pos_z[e]),
+                        __float_as_uint(a.yaw[e]));
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_gate_offsets(GateArgs a) {
+  const uint32_t g = threadIdx.x + blockIdx.x * blockDim.x;
+  if (g <= a.n_gates) a.goff[g] = a.ghist[g * a.nchunks];
+}
+
+// ------------------------------------------------------------------------------------------------
+// ingest
+struct IngArgs {
+  const uint4* rec;  // 2 uint4 per record
+  uint32_t n;        // records in the payload
+  uint32_t seg;      // first record of this batch
+  uint32_t hmask;
+  const uint4* hkey;
+  const uint32_t* hval;
+  const uint32_t* seq;
+  uint8_t* flags;
+  float* y;
+  float* yaw;
+  uint32_t* res;     // per record: slot, or kNone (not accepted)
+  uint32_t* first;   // per slot: first record of this batch naming it (kNone between batches)
+  uint32_t* ctr;     // [0] cut, [1] unknown, [2] rejected
+  uint32_t* bcnt;    // per block: accepted records of the batch, scanned -> offsets; [nb] = total
+  uint32_t* op_slot;
+  float* op_x;
+  float* op_z;
+};
+
+__device__ __forceinline__ void wave_add(uint32_t* p, uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(p, v);
+}
+
+// resolve every record once: slot or kNone, with the unknown / rejected counts
+__global__ void __launch_bounds__(kSy) k_ing_resolve(IngArgs a) {
+  const uint32_t i = blockIdx.x * kSy + threadIdx.x;
+  uint32_t unk = 0, rej = 0;
+  if (i < a.n) {
+    const uint4 id = a.rec[2 * i];
+    uint32_t b = id_hash(id) & a.hmask, slot = kNone;
+    for (;;) {
+      const uint32_t v = a.hval[b];
+      if (v == kHEmpty) break;
+      if (v != kHTomb && id_eq(a.hkey[b], id)) {
+        slot = v;
+        break;
+      }
+      b = (b + 1) & a.hmask;
+    }
+    if (slot == kNone) {
+      unk = 1;
+    } else if (!a.seq[slot] || !(a.flags[slot] & GWAOI_SYNC_FROM_CLIENT)) {
+      rej = 1;
+      slot = kNone;
+    }
+    a.res[i] = slot;
+  }
+  wave_add(&a.ctr[1], unk);
+  wave_add(&a.ctr[2], rej);
+}
+
+// first record of the batch [seg, n) naming each slot
+__global__ void __launch_bounds__(kSy) k_ing_first(IngArgs a) {
+  const uint32_t i = a.seg + blockIdx.x * kSy + threadIdx.x;
+  if (i < a.n) {
+    const uint32_t s = a.res[i];
+    if (s != kNone) atomicMin(&a.first[s], i);
+  }
+}
+
+// cut = the first record that repeats a slot (ctr[0], preset to n)
+__global__ void __launch_bounds__(kSy) k_ing_cut(IngArgs a) {
+  const uint32_t i = a.seg + blockIdx.x * kSy + threadIdx.x;
+  uint32_t c = kNone;
+  if (i < a.n) {
+    const uint32_t s = a.res[i];
+    if (s != kNone && a.first[s] != i) c = i;
+  }
+  for (int o = 32; o > 0; o >>= 1) c = min(c, (uint32_t)__shfl_xor(c, o, 64));
+  if ((threadIdx.x & 63) == 0 && c != kNone) atomicMin(&a.ctr[0], c);
+}
+
+__device__ __forceinline__ bool ing_take(const IngArgs& a, uint32_t i, uint32_t cut) {
+  return i < cut && a.res[i] != kNone;
+}
+
+__global__ void __launch_bounds__(kSy) k_ing_count(IngArgs a) {
+  const uint32_t i = a.seg + blockIdx.x * kSy + threadIdx.x;
+  const bool t = ing_take(a, i, min(a.ctr[0], a.n));
+  const unsigned long long m = __ballot(t);
+  __shared__ uint32_t wsum[kSy / 64];
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int k = 0; k < kSy / 64; ++k) s += wsum[k];
+    a.bcnt[blockIdx.x] = s;
+  }
+}
+
+// accepted records of [seg, cut) -> the Moved batch in payload order, plus setPositionYaw's y/yaw and
+// sifSyncNeighborClients (Entity.go:1195-1202, fromClient). Every record of [seg, n) resets `first`.
+__global__ void __launch_bounds__(kSy) k_ing_emit(IngArgs a) {
+  const uint32_t i = a.seg + blockIdx.x * kSy + threadIdx.x;
+  const uint32_t cut = min(a.ctr[0], a.n);
+  const bool t = ing_take(a, i, cut);
+  const unsigned long long m = __ballot(t);
+  __shared__ uint32_t wsum[kSy / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+  __syncthreads();
+  uint32_t pos = a.bcnt[blockIdx.x] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+  for (int k = 0; k < w; ++k) pos += wsum[k];
+  if (i < a.n) {
+    const uint32_t s = a.res[i];
+    if (s != kNone) a.first[s] = kNone;
+    if (t) {
+      const uint4 v = a.rec[2 * i + 1];
+      a.op_slot[pos] = s;
+      a.op_x[pos] = __uint_as_float(v.x);
+      a.op_z[pos] = __uint_as_float(v.z);
+      a.y[s] = __uint_as_float(v.y);
+      a.yaw[s] = __uint_as_float(v.w);
+      a.flags[s] = (uint8_t)(a.flags[s] | GWAOI_SYNC_NEIGHBOR_CLIENTS);
+    }
+  }
+}
+
+__global__ void k_fill_u32(uint32_t* p, uint32_t v, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
+}
+
+uint32_t blocks_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + kSy - 1) / kSy); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+struct SyncState {
+  int device = 0;
+  uint32_t cap = 0, n_gates = 0;
+  uint8_t* flags = nullptr;
+  uint16_t* gate = nullptr;
+  uint4* cid = nullptr;
+  uint4* eid = nullptr;
+  float* y = nullptr;
+  float* yaw = nullptr;
+  // EntityID -> slot: host-owned open addressing table, mirrored to HBM
+  uint32_t hcap = 0, n_tomb = 0;
+  uint4* d_hkey = nullptr;
+  uint32_t* d_hval = nullptr;
+  std::vector<uint4> h_hkey;
+  std::vector<uint32_t> h_hval;
+  std::vector<uint4> h_id_of;      // slot -> registered id (zero: none)
+  std::vector<uint32_t> h_bucket;  // slot -> its bucket
+  std::vector<uint32_t> dirty;
+  std::vector<uint8_t> is_dirty;
+  bool dirty_all = true;
+  std::vector<uint32_t> h_mark;  // setters' last-wins dedup (generation stamps)
+  uint32_t mark_gen = 0;
+  // collect scratch
+  uint32_t* cnt = nullptr;
+  uint32_t cnt_n = 0;
+  uint2* pairs = nullptr;
+  uint8_t* pgate = nullptr;
+  uint64_t pairs_cap = 0, pgate_cap = 0;
+  uint32_t* ghist = nullptr;
+  uint64_t ghist_cap = 0;
+  uint4* out = nullptr;
+  uint64_t out_cap = 0;  // records
+  uint8_t* h_out = nullptr;
+  uint64_t h_out_cap = 0;
+  uint32_t* d_goff = nullptr;
+  uint32_t* h_small = nullptr;  // pinned: [0..3] counters, [4..] gate offsets
+  std::vector<uint64_t> goff64;
+  ScanCtx scan;
+  uint32_t scan_words = 0;
+  // ingest scratch
+  uint8_t* d_payload = nullptr;
+  uint64_t payload_cap = 0;
+  uint32_t* res = nullptr;
+  uint32_t res_cap = 0;
+  uint32_t* first = nullptr;
+  uint32_t* ictr = nullptr;
+  uint32_t* bcnt = nullptr;
+  uint32_t bcnt_cap = 0;
+  uint32_t* op_slot = nullptr;
+  float* op_x = nullptr;
+  float* op_z = nullptr;
+};
+
+void sync_free(SyncState* s) {
+  if (!s) return;
+  void* p[] = {s->flags, s->gate, s->cid, s->eid, s->y, s->yaw, s->d_hkey, s->d_hval, s->cnt, s->pairs, s->pgate,
+               s->ghist, s->out, s->d_goff, s->scan.status, s->d_payload, s->res, s->first, s->ictr, s->bcnt,
+               s->op_slot, s->op_x, s->op_z};
+  for (void* q : p)
+    if (q) hipFree(q);
+  if (s->h_out) hipHostFree(s->h_out);
+  if (s->h_small) hipHostFree(s->h_small);
+  delete s;
+}
+
+namespace {
+
+#define SCHK(x)                                                                               \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) {                                                                   \
+      gw::set_error("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_));           \
+      return GWAOI_ERR_HIP;                                                                   \
+    }                                                                                         \
+  } while (0)
+#define SRCHK(x)                   \
+  do {                             \
+    int r_ = (x);                  \
+    if (r_ != GWAOI_OK) return r_; \
+  } while (0)
+
+template <class T>
+int dgrow(T** p, uint64_t* cap, uint64_t need) {
+  if (*p && *cap >= need) return GWAOI_OK;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  const uint64_t n = std::max<uint64_t>(need + need / 4, 1024);
+  if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) {
+    *p = nullptr;
+    *cap = 0;
+    set_error("hipMalloc(%llu bytes) failed", (unsigned long long)(n * sizeof(T)));
+    return GWAOI_ERR_NOMEM;
+  }
+  *cap = n;
+  return GWAOI_OK;
+}
+
+template <class T>
+int dgrow32(T** p, uint32_t* cap, uint64_t need) {
+  uint64_t c = *cap;
+  SRCHK(dgrow(p, &c, need));
+  *cap = (uint32_t)std::min<uint64_t>(c, 0xFFFFFFFFull);
+  return GWAOI_OK;
+}
+
+int ensure_scan(SyncState* s, uint32_t n) {
+  const uint32_t w = scan_part_words(n) + 2;
+  if (s->scan.status && s->scan_words >= w) return GWAOI_OK;
+  if (s->scan.status) hipFree(s->scan.status);
+  s->scan.status = nullptr;
+  uint64_t c = 0;
+  SRCHK(dgrow(&s->scan.status, &c, std::max<uint32_t>(w, 1026)));
+  s->scan_words = (uint32_t)c;
+  return GWAOI_OK;
+}
+
+int get_state(gwaoi_mgr* m, MgrView* v, SyncState** s) {
+  SRCHK(mgr_view(m, v));
+  *s = *v->sync;
+  if (!*s) {
+    set_error("sync state not enabled (gwaoi_sync_enable)");
+    return GWAOI_ERR_STATE;
+  }
+  return GWAOI_OK;
+}
+
+// indices of the entries that win for their slot (the last one), in array order
+int last_wins(SyncState* s, const uint32_t* slots, uint32_t n, std::vector<uint32_t>* idx) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (slots[i] >= s->cap) {
+      set_error("slot %u >= capacity %u", slots[i], s->cap);
+      return GWAOI_ERR_INVALID;
+    }
+  if (++s->mark_gen == 0) {
+    std::fill(s->h_mark.begin(), s->h_mark.end(), 0u);
+    s->mark_gen = 1;
+  }
+  idx->clear();
+  for (uint32_t i = n; i-- > 0;) {
+    if (s->h_mark[slots[i]] == s->mark_gen) continue;
+    s->h_mark[slots[i]] = s->mark_gen;
+    idx->push_back(i);
+  }
+  std::reverse(idx->begin(), idx->end());
+  return GWAOI_OK;
+}
+
+// upload host arrays, run k_sync_scatter, free (setters are the rare path)
+struct Up {
+  std::vector<void*> bufs;
+  ~Up() {
+    for (void* p : bufs) hipFree(p);
+  }
+  template <class T>
+  int put(const std::vector<T>& h, const T** d) {
+    *d = nullptr;
+    if (h.empty()) return GWAOI_OK;
+    void* p = nullptr;
+    if (hipMalloc(&p, h.size() * sizeof(T)) != hipSuccess) {
+      set_error("hipMalloc failed");
+      return GWAOI_ERR_NOMEM;
+    }
+    bufs.push_back(p);
+    SCHK(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    *d = (const T*)p;
+    return GWAOI_OK;
+  }
+};
+
+int run_scatter(const MgrView& v, SyncState* s, ScatArgs a) {
+  a.flags = s->flags;
+  a.t_gate = s->gate;
+  a.t_cid = s->cid;
+  a.t_eid = s->eid;
+  a.t_y = s->y;
+  a.t_yaw = s->yaw;
+  if (a.n) hipLaunchKernelGGL(k_sync_scatter, dim3(blocks_for(a.n)), dim3(kSy), 0, v.stream, a);
+  SCHK(hipGetLastError());
+  SCHK(hipStreamSynchronize(v.stream));
+  return GWAOI_OK;
+}
+
+void mark_dirty(SyncState* s, uint32_t b) {
+  if (s->dirty_all || s->is_dirty[b]) return;
+  s->is_dirty[b] = 1;
+  s->dirty.push_back(b);
+  if (s->dirty.size() > s->hcap / 16) s->dirty_all = true;
+}
+
+// rebuild the host table without tombstones
+void rehash(SyncState* s) {
+  std::fill(s->h_hval.begin(), s->h_hval.end(), kHEmpty);
+  const uint32_t mask = s->hcap - 1;
+  for (uint32_t slot = 0; slot < s->cap; ++slot) {
+    const uint4 k = s->h_id_of[slot];
+    if (id_zero(k)) continue;
+    uint32_t b = id_hash(k) & mask;
+    while (s->h_hval[b] != kHEmpty) b = (b + 1) & mask;
+    s->h_hkey[b] = k;
+    s->h_hval[b] = slot;
+    s->h_bucket[slot] = b;
+  }
+  s->n_tomb = 0;
+  s->dirty_all = true;
+}
+
+int upload_hash(const MgrView& v, SyncState* s) {
+  if (s->dirty_all) {
+    SCHK(hipMemcpyAsync(s->d_hkey, s->h_hkey.data(), (size_t)s->hcap * sizeof(uint4), hipMemcpyHostToDevice, v.stream));
+    SCHK(hipMemcpyAsync(s->d_hval, s->h_hval.data(), (size_t)s->hcap * sizeof(uint32_t), hipMemcpyHostToDevice,
+                        v.stream));
+    SCHK(hipStreamSynchronize(v.stream));
+    for (uint32_t b : s->dirty) s->is_dirty[b] = 0;
+    s->dirty.clear();
+    s->dirty_all = false;
+    return GWAOI_OK;
+  }
+  if (s->dirty.empty()) return GWAOI_OK;
+  std::vector<uint32_t> idx(s->dirty), val(idx.size());
+  std::vector<uint4> key(idx.size());
+  for (size_t i = 0; i < idx.size(); ++i) {
+    key[i] = s->h_hkey[idx[i]];
+    val[i] = s->h_hval[idx[i]];
+    s->is_dirty[idx[i]] = 0;
+  }
+  s->dirty.clear();
+  Up up;
+  const uint32_t *d_idx, *d_val;
+  const uint4* d_key;
+  SRCHK(up.put(idx, &d_idx));
+  SRCHK(up.put(val, &d_val));
+  SRCHK(up.put(key, &d_key));
+  hipLaunchKernelGGL(k_hash_scatter, dim3(blocks_for(idx.size())), dim3(kSy), 0, v.stream, d_idx, d_key, d_val,
+                     (uint32_t)idx.size(), s->d_hkey, s->d_hval);
+  SCHK(hipGetLastError());
+  SCHK(hipStreamSynchronize(v.stream));
+  return GWAOI_OK;
+}
+
+}  // namespace
+}  // namespace gw
+
+using gw::SyncState;
+
+extern "C" {
+
+int gwaoi_sync_enable(gwaoi_mgr* m, uint32_t n_gates) {
+  gw::MgrView v;
+  SRCHK(gw::mgr_view(m, &v));
+  if (*v.sync) {
+    gw::set_error("sync_enable: already enabled");
+    return GWAOI_ERR_STATE;
+  }
+  if (n_gates == 0 || n_gates > GWAOI_SYNC_MAX_GATES) {
+    gw::set_error("sync_enable: n_gates %u not in [1, %u]", n_gates, GWAOI_SYNC_MAX_GATES);
+    return GWAOI_ERR_INVALID;
+  }
+  SyncState* s = new (std::nothrow) SyncState();
+  if (!s) return GWAOI_ERR_NOMEM;
+  s->device = v.device;
+  s->cap = v.cap;
+  s->n_gates = n_gates;
+  const size_t C = v.cap;
+  s->hcap = 1024;
+  while (s->hcap < 2 * C) s->hcap <<= 1;
+  bool ok = hipMalloc((void**)&s->flags, C) == hipSuccess && hipMalloc((void**)&s->gate, C * 2) == hipSuccess &&
+            hipMalloc((void**)&s->cid, C * 16) == hipSuccess && hipMalloc((void**)&s->eid, C * 16) == hipSuccess &&
+            hipMalloc((void**)&s->y, C * 4) == hipSuccess && hipMalloc((void**)&s->yaw, C * 4) == hipSuccess &&
+            hipMalloc((void**)&s->d_hkey, (size_t)s->hcap * 16) == hipSuccess &&
+            hipMalloc((void**)&s->d_hval, (size_t)s->hcap * 4) == hipSuccess &&
+            hipMalloc((void**)&s->first, C * 4) == hipSuccess && hipMalloc((void**)&s->ictr, 64) == hipSuccess &&
+            hipHostMalloc((void**)&s->h_small, (8 + GWAOI_SYNC_MAX_GATES + 1) * 4, hipHostMallocDefault) == hipSuccess &&
+            hipMalloc((void**)&s->d_goff, (GWAOI_SYNC_MAX_GATES + 1) * 4) == hipSuccess;
+  if (ok) {
+    ok = hipMemsetAsync(s->flags, 0, C, v.stream) == hipSuccess &&
+         hipMemsetAsync(s->gate, 0xFF, C * 2, v.stream) == hipSuccess &&
+         hipMemsetAsync(s->cid, 0, C * 16, v.stream) == hipSuccess &&
+         hipMemsetAsync(s->eid, 0, C * 16, v.stream) == hipSuccess &&
+         hipMemsetAsync(s->y, 0, C * 4, v.stream) == hipSuccess && hipMemsetAsync(s->yaw, 0, C * 4, v.stream) == hipSuccess &&
+         hipMemsetAsync(s->first, 0xFF, C * 4, v.stream) == hipSuccess &&
+         hipMemsetAsync(s->d_hval, 0xFF, (size_t)s->hcap * 4, v.stream) == hipSuccess &&
+         hipStreamSynchronize(v.stream) == hipSuccess;
+  }
+  if (!ok) {
+    gw::set_error("sync_enable: device allocation failed");
+    gw::sync_free(s);
+    return GWAOI_ERR_NOMEM;
+  }
+  s->h_hkey.assign(s->hcap, make_uint4(0, 0, 0, 0));
+  s->h_hval.assign(s->hcap, gw::kHEmpty);
+  s->h_id_of.assign(C, make_uint4(0, 0, 0, 0));
+  s->h_bucket.assign(C, gw::kNone);
+  s->is_dirty.assign(s->hcap, 0);
+  s->h_mark.assign(C, 0);
+  s->dirty_all = false;  // device table already empty
+  *v.sync = s;
+  return GWAOI_OK;
+}
+
+int gwaoi_sync_get_tables(gwaoi_mgr* m, gwaoi_sync_tables* out) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (!out) return GWAOI_ERR_INVALID;
+  out->flags = s->flags;
+  out->gate = s->gate;
+  out->client_id = (uint8_t*)s->cid;
+  out->entity_id = (uint8_t*)s->eid;
+  out->y = s->y;
+  out->yaw = s->yaw;
+  out->capacity = s->cap;
+  out->n_gates = s->n_gates;
+  return GWAOI_OK;
+}
+
+int gwaoi_sync_set_entities(gwaoi_mgr* m, const uint32_t* slots, const uint8_t* ids, uint32_t n) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (n && (!slots || !ids)) {
+    gw::set_error("sync_set_entities: null array");
+    return GWAOI_ERR_INVALID;
+  }
+  std::vector<uint32_t> idx;
+  SRCHK(gw::last_wins(s, slots, n, &idx));
+  const uint32_t mask = s->hcap - 1;
+  std::vector<uint32_t> us;
+  std::vector<uint4> uk;
+  // pass 1: unregister the slots' old ids (so ids may move between slots within one call)
+  for (uint32_t i : idx) {
+    const uint32_t slot = slots[i];
+    uint4 k;
+    memcpy(&k, ids + (size_t)16 * i, 16);
+    const uint4 old = s->h_id_of[slot];
+    if (!gw::id_zero(old) && !gw::id_eq(old, k)) {
+      const uint32_t b = s->h_bucket[slot];
+      s->h_hval[b] = gw::kHTomb;
+      ++s->n_tomb;
+      gw::mark_dirty(s, b);
+      s->h_id_of[slot] = make_uint4(0, 0, 0, 0);
+      s->h_bucket[slot] = gw::kNone;
+    }
+  }
+  // pass 2: register the new ones
+  int rc = GWAOI_OK;
+  for (uint32_t i : idx) {
+    const uint32_t slot = slots[i];
+    uint4 k;
+    memcpy(&k, ids + (size_t)16 * i, 16);
+    us.push_back(slot);
+    uk.push_back(k);
+    if (gw::id_zero(k) || gw::id_eq(s->h_id_of[slot], k)) continue;
+    uint32_t b = gw::id_hash(k) & mask, free_b = gw::kNone;
+    bool dup = false;
+    for (;;) {
+      const uint32_t hv = s->h_hval[b];
+      if (hv == gw::kHEmpty) break;
+      if (hv == gw::kHTomb) {
+        if (free_b == gw::kNone) free_b = b;
+      } else if (gw::id_eq(s->h_hkey[b], k)) {
+        dup = true;
+        break;
+      }
+      b = (b + 1) & mask;
+    }
+    if (dup) {
+      gw::set_error("sync_set_entities: entity id of slot %u is already registered to slot %u", slot, s->h_hval[b]);
+      rc = GWAOI_ERR_INVALID;
+      uk.back() = make_uint4(0, 0, 0, 0);
+      continue;
+    }
+    if (free_b != gw::kNone) {
+      b = free_b;
+      --s->n_tomb;
+    }
+    s->h_hkey[b] = k;
+    s->h_hval[b] = slot;
+    s->h_id_of[slot] = k;
+    s->h_bucket[slot] = b;
+    gw::mark_dirty(s, b);
+  }
+  if (s->n_tomb > s->hcap / 4) gw::rehash(s);
+  gw::Up up;
+  gw::ScatArgs a = {};
+  a.mode = 0;
+  a.n = (uint32_t)us.size();
+  SRCHK(up.put(us, &a.slot));
+  SRCHK(up.put(uk, &a.id));
+  SRCHK(gw::run_scatter(v, s, a));
+  return rc;
+}
+
+int gwaoi_sync_set_clients(gwaoi_mgr* m, const uint32_t* slots, const uint16_t* gates, const uint8_t* cids,
+                           uint32_t n) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (n && (!slots || !gates || !cids)) {
+    gw::set_error("sync_set_clients: null array");
+    return GWAOI_ERR_INVALID;
+  }
+  for (uint32_t i = 0; i < n; ++i)
+    if (gates[i] != GWAOI_SYNC_NO_CLIENT && gates[i] >= s->n_gates) {
+      gw::set_error("sync_set_clients: gate index %u >= n_gates %u", gates[i], s->n_gates);
+      return GWAOI_ERR_INVALID;
+    }
+  std::vector<uint32_t> idx;
+  SRCHK(gw::last_wins(s, slots, n, &idx));
+  std::vector<uint32_t> us;
+  std::vector<uint16_t> ug;
+  std::vector<uint4> uc;
+  for (uint32_t i : idx) {
+    uint4 k;
+    memcpy(&k, cids + (size_t)16 * i, 16);
+    us.push_back(slots[i]);
+    ug.push_back(gates[i]);
+    uc.push_back(k);
+  }
+  gw::Up up;
+  gw::ScatArgs a = {};
+  a.mode = 1;
+  a.n = (uint32_t)us.size();
+  SRCHK(up.put(us, &a.slot));
+  SRCHK(up.put(ug, &a.gate));
+  SRCHK(up.put(uc, &a.id));
+  return gw::run_scatter(v, s, a);
+}
+
+int gwaoi_sync_set_syncing(gwaoi_mgr* m, const uint32_t* slots, const uint8_t* on, uint32_t n) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (n && (!slots || !on)) {
+    gw::set_error("sync_set_syncing: null array");
+    return GWAOI_ERR_INVALID;
+  }
+  std::vector<uint32_t> idx;
+  SRCHK(gw::last_wins(s, slots, n, &idx));
+  std::vector<uint32_t> us;
+  std::vector<uint8_t> uf;
+  for (uint32_t i : idx) {
+    us.push_back(slots[i]);
+    uf.push_back(on[i] ? 1 : 0);
+  }
+  gw::Up up;
+  gw::ScatArgs a = {};
+  a.mode = 2;
+  a.n = (uint32_t)us.size();
+  SRCHK(up.put(us, &a.slot));
+  SRCHK(up.put(uf, &a.f));
+  return gw::run_scatter(v, s, a);
+}
+
+int gwaoi_sync_mark(gwaoi_mgr* m, const uint32_t* slots, const float* y, const float* yaw, const uint8_t* flags,
+                    uint32_t n) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (n && (!slots || !y || !yaw || !flags)) {
+    gw::set_error("sync_mark: null array");
+    return GWAOI_ERR_INVALID;
+  }
+  for (uint32_t i = 0; i < n; ++i)
+    if (flags[i] & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS)) {
+      gw::set_error("sync_mark: flags 0x%x: only GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS", flags[i]);
+      return GWAOI_ERR_INVALID;
+    }
+  std::vector<uint32_t> idx;
+  SRCHK(gw::last_wins(s, slots, n, &idx));
+  // flags accumulate over every entry of a slot (|=), y/yaw: the last entry
+  std::vector<uint8_t> acc(idx.size());
+  {
+    std::vector<std::pair<uint32_t, uint32_t>> sp;
+    sp.reserve(idx.size());
+    for (uint32_t k = 0; k < idx.size(); ++k) sp.push_back({slots[idx[k]], k});
+    std::sort(sp.begin(), sp.end());
+    for (uint32_t i = 0; i < n; ++i) {
+      auto it = std::lower_bound(sp.begin(), sp.end(), std::make_pair(slots[i], 0u));
+      acc[it->second] |= flags[i];
+    }
+  }
+  std::vector<uint32_t> us;
+  std::vector<float> uy, uyaw;
+  for (uint32_t k = 0; k < idx.size(); ++k) {
+    us.push_back(slots[idx[k]]);
+    uy.push_back(y[idx[k]]);
+    uyaw.push_back(yaw[idx[k]]);
+  }
+  gw::Up up;
+  gw::ScatArgs a = {};
+  a.mode = 3;
+  a.n = (uint32_t)us.size();
+  SRCHK(up.put(us, &a.slot));
+  SRCHK(up.put(uy, &a.y));
+  SRCHK(up.put(uyaw, &a.yaw));
+  SRCHK(up.put(acc, &a.f));
+  return gw::run_scatter(v, s, a);
+}
+
+int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (!out) return GWAOI_ERR_INVALID;
+  if (v.pending) {
+    gw::set_error("collect_sync: ops are staged; run gwaoi_tick first (the reference collects after the tick)");
+    return GWAOI_ERR_STATE;
+  }
+  memset(out, 0, sizeof *out);
+  out->n_gates = s->n_gates;
+  s->goff64.assign(s->n_gates + 1, 0);
+  out->gate_off = s->goff64.data();
+  if (!v.g.rec) return GWAOI_OK;  // no pass has run: nothing is present
+  hipStream_t st = v.stream;
+  const uint32_t bound = v.rec_bound;
+  SRCHK(gw::dgrow32(&s->cnt, &s->cnt_n, (uint64_t)bound + 1));
+  SRCHK(gw::ensure_scan(s, bound + 1));
+  gw::FanArgs f = {};
+  f.g = v.g;
+  f.rec_count = v.rec_count;
+  f.rec_bound = bound;
+  f.pos_x = v.pos_x;
+  f.pos_z = v.pos_z;
+  f.space_of = v.space_of;
+  f.flags = s->flags;
+  f.gate = s->gate;
+  f.clear = !(opts & GWAOI_COLLECT_KEEP_FLAGS);
+  f.cnt = s->cnt;
+  f.n_ent = s->ictr + 8;
+  SCHK(hipMemsetAsync(s->ictr + 8, 0, 4, st));
+  const uint32_t fan_blocks = std::min<uint32_t>(gw::blocks_for((uint64_t)bound + 1), 8192);
+  hipLaunchKernelGGL(gw::k_fan<false>, dim3(fan_blocks), dim3(gw::kSy), 0, st, f);
+  gw::launch_scan(s->scan, s->cnt, bound + 1, st);
+  SCHK(hipMemcpyAsync(s->h_small, s->cnt + bound, 4, hipMemcpyDeviceToHost, st));
+  SCHK(hipMemcpyAsync(s->h_small + 1, s->ictr + 8, 4, hipMemcpyDeviceToHost, st));
+  SCHK(hipStreamSynchronize(st));
+  const uint32_t M = s->h_small[0];
+  out->n_entities = s->h_small[1];
+  if (M == 0) {
+    if (f.clear) {  // nothing to write, but the flags of the collected entities still clear
+      f.off = s->cnt;
+      hipLaunchKernelGGL(gw::k_fan<true>, dim3(fan_blocks), dim3(gw::kSy), 0, st, f);
+      SCHK(hipStreamSynchronize(st));
+    }
+    return GWAOI_OK;
+  }
+  SRCHK(gw::dgrow(&s->pairs, &s->pairs_cap, M));
+  SRCHK(gw::dgrow(&s->pgate, &s->pgate_cap, M));
+  f.off = s->cnt;
+  f.pairs = s->pairs;
+  f.pgate = s->pgate;
+  hipLaunchKernelGGL(gw::k_fan<true>, dim3(fan_blocks), dim3(gw::kSy), 0, st, f);
+
+  gw::GateArgs g = {};
+  g.pairs = s->pairs;
+  g.pgate = s->pgate;
+  g.n = M;
+  g.nchunks = (M + gw::kGChunk - 1) / gw::kGChunk;
+  g.n_gates = s->n_gates;
+  g.bits = 1;
+  while ((1u << g.bits) < s->n_gates) ++g.bits;
+  const uint64_t hn = (uint64_t)g.nchunks * s->n_gates + 1;
+  SRCHK(gw::dgrow(&s->ghist, &s->ghist_cap, hn));
+  SRCHK(gw::ensure_scan(s, (uint32_t)hn));
+  g.ghist = s->ghist;
+  g.cid = s->cid;
+  g.eid = s->eid;
+  g.pos_x = v.pos_x;
+  g.pos_z = v.pos_z;
+  g.y = s->y;
+  g.yaw = s->yaw;
+  SRCHK(gw::dgrow(&s->out, &s->out_cap, (uint64_t)M * 3));
+  g.out = s->out;
+  g.goff = s->d_goff;
+  hipLaunchKernelGGL(gw::k_gate_hist, dim3(g.nchunks), dim3(gw::kSy), 0, st, g);
+  gw::launch_scan(s->scan, s->ghist, (uint32_t)hn, st);
+  hipLaunchKernelGGL(gw::k_gate_scatter, dim3(g.nchunks), dim3(gw::kSy), 0, st, g);
+  hipLaunchKernelGGL(gw::k_gate_offsets, dim3(1), dim3(GWAOI_SYNC_MAX_GATES + 64), 0, st, g);
+  SCHK(hipGetLastError());
+  SCHK(hipMemcpyAsync(s->h_small + 8, s->d_goff, (s->n_gates + 1) * 4, hipMemcpyDeviceToHost, st));
+  const uint64_t bytes = (uint64_t)M * GWAOI_SYNC_RECORD_BYTES;
+  if (opts & GWAOI_COLLECT_HOST) {
+    if (s->h_out_cap < bytes) {
+      if (s->h_out) hipHostFree(s->h_out);
+      s->h_out = nullptr;
+      s->h_out_cap = 0;
+      const uint64_t nb = bytes + bytes / 4;
+      if (hipHostMalloc((void**)&s->h_out, nb, hipHostMallocDefault) != hipSuccess) {
+        s->h_out = nullptr;
+        gw::set_error("collect_sync: hipHostMalloc(%llu) failed", (unsigned long long)nb);
+        return GWAOI_ERR_NOMEM;
+      }
+      s->h_out_cap = nb;
+    }
+    SCHK(hipMemcpyAsync(s->h_out, s->out, bytes, hipMemcpyDeviceToHost, st));
+    out->records = s->h_out;
+  }
+  SCHK(hipStreamSynchronize(st));
+  for (uint32_t k = 0; k <= s->n_gates; ++k) s->goff64[k] = s->h_small[8 + k];
+  out->n_records = M;
+  out->d_records = (const uint8_t*)s->out;
+  return GWAOI_OK;
+}
+
+int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes, uint32_t opts,
+                           gwaoi_ingest_result* out) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (out) memset(out, 0, sizeof *out);
+  if (bytes % GWAOI_INGEST_RECORD_BYTES) {
+    gw::set_error("ingest_positions: %llu bytes is not a whole number of 32-byte records", (unsigned long long)bytes);
+    return GWAOI_ERR_INVALID;
+  }
+  if (bytes / GWAOI_INGEST_RECORD_BYTES > 0x7FFFFFFFull) {
+    gw::set_error("ingest_positions: payload too large");
+    return GWAOI_ERR_INVALID;
+  }
+  const uint32_t n = (uint32_t)(bytes / GWAOI_INGEST_RECORD_BYTES);
+  if (n && !payload) {
+    gw::set_error("ingest_positions: null payload");
+    return GWAOI_ERR_INVALID;
+  }
+  if (!(opts & GWAOI_INGEST_HOST_PAYLOAD) && ((uintptr_t)payload & 15)) {
+    gw::set_error("ingest_positions: device payload must be 16-byte aligned");
+    return GWAOI_ERR_INVALID;
+  }
+  if (out) out->n_records = n;
+  if (!n) return GWAOI_OK;
+  // the records come after every op already staged: presence is read on the device
+  SRCHK(gw::mgr_flush(m));
+  SRCHK(gw::mgr_view(m, &v));
+  SRCHK(gw::upload_hash(v, s));
+  hipStream_t st = v.stream;
+  const uint8_t* src = payload;
+  if (opts & GWAOI_INGEST_HOST_PAYLOAD) {
+    SRCHK(gw::dgrow(&s->d_payload, &s->payload_cap, bytes));
+    SCHK(hipMemcpyAsync(s->d_payload, payload, bytes, hipMemcpyHostToDevice, st));
+    src = s->d_payload;
+  }
+  const uint32_t nb = gw::blocks_for(n);
+  SRCHK(gw::dgrow32(&s->res, &s->res_cap, n));
+  SRCHK(gw::dgrow32(&s->bcnt, &s->bcnt_cap, (uint64_t)nb + 1));
+  SRCHK(gw::ensure_scan(s, nb + 1));
+  if (!s->op_slot) {
+    const size_t C = s->cap;
+    if (hipMalloc((void**)&s->op_slot, C * 4) != hipSuccess || hipMalloc((void**)&s->op_x, C * 4) != hipSuccess ||
+        hipMalloc((void**)&s->op_z, C * 4) != hipSuccess) {
+      gw::set_error("ingest_positions: device allocation failed");
+      return GWAOI_ERR_NOMEM;
+    }
+  }
+  gw::IngArgs a = {};
+  a.rec = (const uint4*)src;
+  a.n = n;
+  a.hmask = s->hcap - 1;
+  a.hkey = s->d_hkey;
+  a.hval = s->d_hval;
+  a.seq = v.seq;
+  a.flags = s->flags;
+  a.y = s->y;
+  a.yaw = s->yaw;
+  a.res = s->res;
+  a.first = s->first;
+  a.ctr = s->ictr;
+  a.bcnt = s->bcnt;
+  a.op_slot = s->op_slot;
+  a.op_x = s->op_x;
+  a.op_z = s->op_z;
+  SCHK(hipMemsetAsync(s->ictr, 0, 16, st));
+  hipLaunchKernelGGL(gw::k_ing_resolve, dim3(nb), dim3(gw::kSy), 0, st, a);
+  uint32_t seg = 0, passes = 0, moved = 0;
+  for (;;) {
+    const uint32_t nseg = gw::blocks_for(n - seg);
+    a.seg = seg;
+    hipLaunchKernelGGL(gw::k_fill_u32, dim3(1), dim3(64), 0, st, s->ictr, n, 1u);
+    hipLaunchKernelGGL(gw::k_ing_first, dim3(nseg), dim3(gw::kSy), 0, st, a);
+    hipLaunchKernelGGL(gw::k_ing_cut, dim3(nseg), dim3(gw::kSy), 0, st, a);
+    hipLaunchKernelGGL(gw::k_ing_count, dim3(nseg), dim3(gw::kSy), 0, st, a);
+    hipLaunchKernelGGL(gw::k_fill_u32, dim3(1), dim3(64), 0, st, s->bcnt + nseg, 0u, 1u);
+    gw::launch_scan(s->scan, s->bcnt, nseg + 1, st);
+    hipLaunchKernelGGL(gw::k_ing_emit, dim3(nseg), dim3(gw::kSy), 0, st, a);
+    SCHK(hipGetLastError());
+    const uint32_t bound = std::min<uint32_t>(n - seg, s->cap);
+    SRCHK(gw::mgr_stage_moves_device_n(m, s->op_slot, s->op_x, s->op_z, s->bcnt + nseg, bound));
+    SCHK(hipMemcpyAsync(s->h_small, s->ictr, 12, hipMemcpyDeviceToHost, st));
+    SCHK(hipMemcpyAsync(s->h_small + 4, s->bcnt + nseg, 4, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    ++passes;
+    moved += s->h_small[4];
+    const uint32_t cut = std::min(s->h_small[0], n);
+    if (cut >= n) break;
+    SRCHK(gw::mgr_flush(m));  // run this batch now; the next starts at the repeat
+    seg = cut;
+  }
+  if (out) {
+    out->n_moved = moved;
+    out->n_unknown = s->h_small[1];
+    out->n_rejected = s->h_small[2];
+    out->n_passes = passes;
+  }
+  return GWAOI_OK;
+}
+
+}  // extern "C"

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_functions():
     names = set()
-    for h in ("gwaoi.h", "gwaoi_tools.h", "gwaoi_strips.h"):
+    for h in ("gwaoi.h", "gwaoi_tools.h", "gwaoi_strips.h", "gwaoi_sync.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_ ]*[\s\*]+(gwaoi_[a-z0-9_]+)\s*\(", src, re.M):
@@ -29,7 +29,7 @@ def test_header_declares_boundary():
 def test_library_exports_every_declared_symbol(gwaoi_lib):
     from goworld_amd import _lib
     names = declared_functions()
-    assert set(names) == set(_lib.ABI_SYMBOLS) | set(_lib.TOOL_SYMBOLS) | set(_lib.STRIP_SYMBOLS)
+    assert set(names) == set(_lib.ABI_SYMBOLS) | set(_lib.TOOL_SYMBOLS) | set(_lib.STRIP_SYMBOLS) | set(_lib.SYNC_SYMBOLS)
     for n in names:
         assert hasattr(gwaoi_lib, n), n
         assert ctypes.cast(getattr(gwaoi_lib, n), ctypes.c_void_p).value

@@ -1,0 +1,328 @@
+"""Parity tests of the callers either side of the AOI path (include/gwaoi_sync.h), through the C ABI:
+
+  * tick-end sync fan-out (CollectEntitySyncInfos, Entity.go:1221-1267) against oracle/sync_ref.py over
+    the AOI oracle's relation: per gate, the multiset of 48-byte records must be identical (byte for
+    byte), and so must the syncInfoFlag state afterwards;
+  * position ingest (HandleSyncPositionYawFromClient, GameService.go:398-410) against the same
+    restatement driving the go-aoi list oracle record by record: identical canonical events, counts,
+    and Y/yaw/flag tables.
+
+Parity with go-aoi itself is UNPINNED (DESIGN.md "Oracle"); these tests pin the GPU against the CPU
+restatements only. CPU-only tests (marked not gpu) check the restatement against hand-worked cases.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import aoi_harness as H  # noqa: E402
+from oracle import sync_ref as R  # noqa: E402
+
+
+def rand_ids(rng, n):
+    ids = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    ids[:, 0] = (np.arange(n) % 251 + 1).astype(np.uint8)  # never all-zero
+    ids[:, 1] = (np.arange(n) // 251 % 256).astype(np.uint8)
+    ids[:, 2] = (np.arange(n) // (251 * 256)).astype(np.uint8)
+    return ids
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU: the restatement on hand-worked cases
+
+def test_oracle_collect_hand_case():
+    # 3 entities; relation 0-1, 1-2. Entity 1 flagged both, 0 flagged own, 2 unflagged.
+    rp = np.array([0, 1, 3, 4])
+    cols = np.array([1, 0, 2, 1])
+    cap = 3
+    flags = np.array([R.OWN_CLIENT, R.OWN_CLIENT | R.NEIGHBOR_CLIENTS, 0], np.uint8)
+    gate = np.array([0, R.NO_CLIENT, 1], np.uint16)
+    cid = np.arange(48, dtype=np.uint8).reshape(3, 16)
+    eid = (np.arange(48, dtype=np.uint8) + 100).reshape(3, 16)
+    x = np.array([1, 2, 3], np.float32)
+    out, fl = R.collect_entity_sync_infos(rp, cols, np.ones(cap, bool), flags, gate, cid, eid, x, x * 2, x * 3,
+                                          x * 4, 2)
+    # entity 0: own client (gate 0). entity 1: no own client; neighbours 0 (gate 0) and 2 (gate 1)
+    assert sorted(out) == [0, 1]
+    assert len(out[0]) == 2 and len(out[1]) == 1
+    r1 = out[1][0]
+    assert bytes(r1[:16]) == bytes(cid[2]) and bytes(r1[16:32]) == bytes(eid[1])
+    assert np.frombuffer(bytes(r1[32:48]), "<f4").tolist() == [2.0, 4.0, 6.0, 8.0]
+    assert fl.tolist() == [0, 0, 0]
+
+
+def test_oracle_ingest_hand_case():
+    ids = {bytes([1] * 16): 0, bytes([2] * 16): 1, bytes([3] * 16): 2}
+    present = np.array([True, True, False])
+    flags = np.array([R.FROM_CLIENT, 0, R.FROM_CLIENT], np.uint8)
+    y = np.zeros(3, np.float32)
+    yaw = np.zeros(3, np.float32)
+    recs = np.zeros(5, R.INGEST_RECORD)
+    for i, (k, v) in enumerate([(1, 10.0), (2, 20.0), (3, 30.0), (9, 40.0), (1, 50.0)]):
+        recs[i]["entity_id"] = bytes([k] * 16)
+        recs[i]["x"], recs[i]["y"], recs[i]["z"], recs[i]["yaw"] = v, v + 1, v + 2, v + 3
+    moves, unk, rej = R.ingest_positions(recs, ids, present, flags, y, yaw)
+    assert moves == [(0, 10.0, 12.0), (0, 50.0, 52.0)]
+    assert (unk, rej) == (1, 2)
+    assert y[0] == 51.0 and yaw[0] == 53.0 and flags[0] == R.FROM_CLIENT | R.NEIGHBOR_CLIENTS
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU
+
+def world(po, n, L, dist, seed, nticks=2, spaces=None):
+    """Run a seeded walk on the GPU and the list oracle; returns (eng, orc, x, z)."""
+    from goworld_amd.engine import Engine
+    case = H.case_walk(seed, n, L, nticks, dist, workload=po)
+    eng = Engine(dist, capacity=n, bounds=(0.0, 0.0, L, L))
+    orc = po.XZListOracle(dist, n) if n <= 4000 else po.GridOracle(dist, n, (0, 0, L, L))
+    x = np.zeros(n, np.float32)
+    z = np.zeros(n, np.float32)
+    for t, ops in enumerate(case["ticks"]):
+        want = H.oracle_tick(orc, ops)
+        got = H.gpu_tick(eng, ops)
+        assert np.array_equal(got, want), f"tick {t}: " + H.fmt_diff(got, want)
+        for _, s, xx, zz in ops:
+            x[s], z[s] = xx, zz
+    return eng, orc, x, z
+
+
+def fill_sync(sy, rng, n, n_gates, client_frac=0.6, flag_p=(0.25, 0.25, 0.25, 0.25)):
+    ids = rand_ids(rng, n)
+    cids = rand_ids(rng, n)[:, ::-1].copy()
+    gates = rng.integers(0, n_gates, n).astype(np.uint16)
+    gates[rng.random(n) >= client_frac] = R.NO_CLIENT
+    flags = rng.choice(4, n, p=flag_p).astype(np.uint8)
+    y = rng.uniform(-50, 50, n).astype(np.float32)
+    yaw = rng.uniform(-3.2, 3.2, n).astype(np.float32)
+    slots = np.arange(n, dtype=np.uint32)
+    sy.set_entities(slots, ids)
+    sy.set_clients(slots, gates, cids)
+    sy.mark(slots, y, yaw, flags)
+    return dict(ids=ids, cids=cids, gates=gates, flags=flags, y=y, yaw=yaw)
+
+
+def check_collect(sy, orc, st, x, z, n_gates, present=None, keep=False):
+    rp, cols = orc.relation()
+    n = len(x)
+    present = np.ones(n, bool) if present is None else present
+    want, flags_after = R.collect_entity_sync_infos(rp, cols, present, st["flags"], st["gates"], st["cids"],
+                                                    st["ids"], x, st["y"], z, st["yaw"], n_gates)
+    got = sy.collect_entity_sync_infos(keep_flags=keep)
+    assert sorted(got) == sorted(want), (sorted(got), sorted(want))
+    for g in want:
+        gg = R.canonical_records(got[g])
+        assert np.array_equal(gg, want[g]), f"gate {g}: {len(gg)} vs {len(want[g])} records"
+    fl, _, _, _ = sy.read_tables()
+    assert np.array_equal(fl, st["flags"] if keep else flags_after)
+    return got, flags_after
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,L,dist,n_gates,seed", [
+    (2000, 1600.0, 100.0, 5, 1),      # config-1 density
+    (3000, 700.0, 60.0, 1, 2),        # dense, one gate (1 ballot bit)
+    (1500, 2000.0, 100.0, 256, 3),    # 256 gates (8 ballot bits)
+    (200000, 15652.0, 100.0, 8, 4),   # config-2 density, 200k entities (grid oracle)
+])
+def test_collect_sync_parity(gpu, oracle_lib, n, L, dist, n_gates, seed):
+    from goworld_amd.sync import EntitySync
+    eng, orc, x, z = world(oracle_lib, n, L, dist, seed)
+    sy = EntitySync(eng, n_gates)
+    rng = np.random.default_rng(seed)
+    st = fill_sync(sy, rng, n, n_gates)
+    got, flags_after = check_collect(sy, orc, st, x, z, n_gates)
+    out = sy.last
+    assert out.n_entities == int(np.count_nonzero(st["flags"] & 3))
+    # gate offsets partition the records
+    offs = [int(out.gate_off[g]) for g in range(n_gates + 1)]
+    assert offs[0] == 0 and offs[-1] == out.n_records and offs == sorted(offs)
+    # flags were cleared: a second collect is empty
+    again = sy.collect_entity_sync_infos()
+    assert not again and sy.last.n_records == 0
+
+
+@pytest.mark.gpu
+def test_collect_keep_flags_and_own_only(gpu, oracle_lib):
+    from goworld_amd.sync import EntitySync
+    n = 1200
+    eng, orc, x, z = world(oracle_lib, n, 900.0, 100.0, 7)
+    sy = EntitySync(eng, 3)
+    rng = np.random.default_rng(7)
+    st = fill_sync(sy, rng, n, 3, client_frac=0.9, flag_p=(0.5, 0.5, 0.0, 0.0))  # own-client only
+    got, _ = check_collect(sy, orc, st, x, z, 3, keep=True)
+    assert sum(len(v) for v in got.values()) <= n
+    got2, _ = check_collect(sy, orc, st, x, z, 3, keep=False)  # flags still set: same records
+    for g in got:
+        assert np.array_equal(R.canonical_records(got[g]), R.canonical_records(got2[g]))
+
+
+@pytest.mark.gpu
+def test_collect_requires_tick(gpu, oracle_lib):
+    from goworld_amd import _lib
+    from goworld_amd.sync import EntitySync
+    eng, orc, x, z = world(oracle_lib, 500, 600.0, 100.0, 9)
+    sy = EntitySync(eng, 2)
+    eng.moved(3, 10.0, 10.0)
+    with pytest.raises(_lib.GwaoiError) as e:
+        sy.collect_entity_sync_infos()
+    assert e.value.code == _lib.GWAOI_ERR_STATE
+    eng.tick()
+    sy.collect_entity_sync_infos()
+
+
+@pytest.mark.gpu
+def test_collect_after_leaves(gpu, oracle_lib):
+    """Entities that left are not collected; their flags stay (they are outside the manager)."""
+    from goworld_amd.sync import EntitySync
+    n = 1500
+    eng, orc, x, z = world(oracle_lib, n, 1000.0, 100.0, 11)
+    rng = np.random.default_rng(11)
+    gone = rng.choice(n, 200, replace=False)
+    ops = [(H.LEAVE, int(s), 0.0, 0.0) for s in gone]
+    assert np.array_equal(H.gpu_tick(eng, ops), H.oracle_tick(orc, ops))
+    sy = EntitySync(eng, 4)
+    st = fill_sync(sy, rng, n, 4)
+    present = np.ones(n, bool)
+    present[gone] = False
+    check_collect(sy, orc, st, x, z, 4, present=present)
+
+
+def ingest_case(rng, n, ids, present, syncing, n_rec, L, dup_frac=0.05):
+    """A payload: mostly syncing present entities, some unknown ids, some non-syncing/absent ones,
+    some entities repeated (forcing the payload to be cut)."""
+    recs = np.zeros(n_rec, R.INGEST_RECORD)
+    base = rng.permutation(n)[:n_rec]
+    k = 0
+    for i in range(n_rec):
+        r = rng.random()
+        if r < 0.05:
+            eid = rand_ids(rng, 1)[0]
+            eid[3:] = 0xEE  # not registered
+        elif r < 0.05 + dup_frac and i > 0:
+            eid = ids[base[rng.integers(0, k)]] if k else ids[base[0]]
+        else:
+            eid = ids[base[k]]
+            k += 1
+        recs[i]["entity_id"] = eid.tobytes()
+        recs[i]["x"], recs[i]["z"] = rng.uniform(0, L, 2).astype(np.float32)
+        recs[i]["y"], recs[i]["yaw"] = rng.uniform(-5, 5, 2).astype(np.float32)
+    return recs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,device_payload,dup", [(1, False, 0.0), (2, False, 0.05), (3, True, 0.05),
+                                                     (4, False, 0.3)])
+def test_ingest_parity(gpu, oracle_lib, seed, device_payload, dup):
+    from goworld_amd.engine import DeviceBuffer
+    from goworld_amd.sync import EntitySync
+    n, L, dist = 2000, 1200.0, 100.0
+    eng, orc, x, z = world(oracle_lib, n, L, dist, 20 + seed)
+    rng = np.random.default_rng(seed)
+    # some entities leave (absent: rejected by the ingest)
+    gone = rng.choice(n, 100, replace=False)
+    ops = [(H.LEAVE, int(s), 0.0, 0.0) for s in gone]
+    assert np.array_equal(H.gpu_tick(eng, ops), H.oracle_tick(orc, ops))
+    present = np.ones(n, bool)
+    present[gone] = False
+    sy = EntitySync(eng, 4)
+    st = fill_sync(sy, rng, n, 4, flag_p=(1.0, 0, 0, 0))
+    syncing = rng.random(n) < 0.85
+    sy.set_client_syncing(np.arange(n, dtype=np.uint32), syncing.astype(np.uint8))
+    recs = ingest_case(rng, n, st["ids"], present, syncing, 1500, L, dup_frac=dup)
+    # oracle
+    id_to_slot = {st["ids"][s].tobytes(): s for s in range(n)}
+    oflags = st["flags"].copy() | np.where(syncing, R.FROM_CLIENT, 0).astype(np.uint8)
+    oy, oyaw = st["y"].copy(), st["yaw"].copy()
+    moves, unk, rej = R.ingest_positions(recs, id_to_slot, present, oflags, oy, oyaw)
+    want = H.oracle_tick(orc, [(H.MOVE, s, xx, zz) for s, xx, zz in moves])
+    # GPU
+    if device_payload:
+        buf = DeviceBuffer(recs.nbytes)
+        buf.upload(recs.view(np.uint8))
+        res = sy.ingest_device(buf.ptr, recs.nbytes)
+    else:
+        res = sy.handle_sync_position_yaw_from_client(recs.view(np.uint8))
+    got = eng.tick()
+    assert (res.n_records, res.n_moved, res.n_unknown, res.n_rejected) == (len(recs), len(moves), unk, rej)
+    if dup == 0.0:
+        assert res.n_passes == 1
+    assert np.array_equal(got, want), H.fmt_diff(got, want)
+    fl, _, gy, gyaw = sy.read_tables()
+    assert np.array_equal(fl, oflags)
+    assert np.array_equal(gy.view(np.uint32), oy.view(np.uint32))
+    assert np.array_equal(gyaw.view(np.uint32), oyaw.view(np.uint32))
+    rg, ro = eng.relation(), orc.relation()
+    assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1])
+
+
+@pytest.mark.gpu
+def test_ingest_then_collect_round_trip(gpu, oracle_lib):
+    """One game tick: client positions in -> AOI tick -> sync packets out (GameService.go:88-192)."""
+    from goworld_amd.sync import EntitySync
+    n, L = 3000, 1600.0
+    eng, orc, x, z = world(oracle_lib, n, L, 100.0, 31)
+    rng = np.random.default_rng(31)
+    sy = EntitySync(eng, 6)
+    st = fill_sync(sy, rng, n, 6, flag_p=(1.0, 0, 0, 0))
+    sy.set_client_syncing(np.arange(n, dtype=np.uint32), np.ones(n, np.uint8))
+    recs = np.zeros(n, R.INGEST_RECORD)
+    order = rng.permutation(n)
+    recs["entity_id"] = [st["ids"][s].tobytes() for s in order]
+    nx = np.clip(x[order] + rng.uniform(-1, 1, n).astype(np.float32), 0, L).astype(np.float32)
+    nz = np.clip(z[order] + rng.uniform(-1, 1, n).astype(np.float32), 0, L).astype(np.float32)
+    recs["x"], recs["z"] = nx, nz
+    recs["y"] = rng.uniform(0, 3, n).astype(np.float32)
+    recs["yaw"] = rng.uniform(0, 3, n).astype(np.float32)
+    res = sy.handle_sync_position_yaw_from_client(recs.view(np.uint8))
+    assert res.n_moved == n and res.n_passes == 1
+    want = H.oracle_tick(orc, [(H.MOVE, int(s), float(a), float(b)) for s, a, b in zip(order, nx, nz)])
+    got = eng.tick()
+    assert np.array_equal(got, want), H.fmt_diff(got, want)
+    x[order], z[order] = nx, nz
+    st["y"][order] = recs["y"]
+    st["yaw"][order] = recs["yaw"]
+    st["flags"][:] = R.NEIGHBOR_CLIENTS  # setPositionYaw(fromClient) marks neighbour sync only
+    st["flags"] |= R.FROM_CLIENT
+    check_collect(sy, orc, st, x, z, 6)
+
+
+@pytest.mark.gpu
+def test_entity_id_registry(gpu, oracle_lib):
+    from goworld_amd import _lib
+    from goworld_amd.sync import EntitySync
+    n = 400
+    eng, orc, x, z = world(oracle_lib, n, 500.0, 100.0, 41)
+    sy = EntitySync(eng, 2)
+    rng = np.random.default_rng(41)
+    st = fill_sync(sy, rng, n, 2, flag_p=(1.0, 0, 0, 0))
+    sy.set_client_syncing(np.arange(n, dtype=np.uint32), np.ones(n, np.uint8))
+    # the same id on a second slot is refused
+    with pytest.raises(_lib.GwaoiError) as e:
+        sy.set_entities(np.array([5], np.uint32), st["ids"][6:7])
+    assert e.value.code == _lib.GWAOI_ERR_INVALID
+    # move id of slot 7 to slot 8 (slot 8's old id is dropped), unregister slot 9
+    sy.set_entities(np.array([7, 8, 9], np.uint32), np.stack([np.zeros(16, np.uint8), st["ids"][7],
+                                                               np.zeros(16, np.uint8)]))
+    recs = np.zeros(3, R.INGEST_RECORD)
+    for i, s in enumerate([7, 8, 9]):
+        recs[i]["entity_id"] = st["ids"][s].tobytes()
+        recs[i]["x"], recs[i]["z"] = 250.0, 250.0
+    res = sy.handle_sync_position_yaw_from_client(recs.view(np.uint8))
+    # ids[7] -> slot 8 now; ids[8] and ids[9] unknown
+    assert (res.n_moved, res.n_unknown) == (1, 2)
+    want = H.oracle_tick(orc, [(H.MOVE, 8, 250.0, 250.0)])
+    assert np.array_equal(eng.tick(), want)
+    # many re-registrations (tombstones, rehash) keep lookups right
+    for k in range(6):
+        perm = rng.permutation(n).astype(np.uint32)
+        sy.set_entities(perm, st["ids"])
+        recs = np.zeros(n, R.INGEST_RECORD)
+        recs["entity_id"] = [i.tobytes() for i in st["ids"]]
+        recs["x"], recs["z"] = x[perm], z[perm]
+        res = sy.handle_sync_position_yaw_from_client(recs.view(np.uint8))
+        assert res.n_moved == n and res.n_unknown == 0
+        want = H.oracle_tick(orc, [(H.MOVE, int(perm[i]), float(x[perm[i]]), float(z[perm[i]])) for i in range(n)])
+        assert np.array_equal(eng.tick(), want)
