@@ -13,6 +13,8 @@ collectives are the timing barrier and the max-over-ranks of the elapsed time.
 Other workloads (--workload; the JSON line names the one measured):
   config3  512 Spaces x 2,000 entities per GPU in one manager (4,096 Spaces over 8 GPUs), L = 1,600
   skew     config 5: 4 Spaces x 1M per GPU, D = 50/100/200/400, 10% of the entities in 64 hotspots
+  gametick one GoWorld game tick per step at config-2 scale: client position records ingested on the GPU,
+           the AOI tick, and the sync fan-out into per-gate packet bodies (include/gwaoi_sync.h)
   strips   config 4: ONE world of 2M entities per GPU (16M, L = 140,000 at 8 GPUs) cut into X-strips,
            halo records exchanged with the neighbour GPUs every tick (torch.distributed = RCCL/xGMI)
 
@@ -296,6 +298,139 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     }
 
 
+def run_gametick(args, rank, world, dev, sync_all, allmax):
+    """One GoWorld game tick per step at config-2 scale (SURVEY.md 8(f) rows 1-2 around the AOI path):
+    the tick's client position records (32 B each, [EntityID | x y z yaw], resident in HBM) are ingested
+    (HandleSyncPositionYawFromClient, GameService.go:398-410), the AOI tick runs, and the sync fan-out
+    (CollectEntitySyncInfos, Entity.go:1221-1267) writes every gate's packet body into HBM."""
+    import numpy as np
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine, wl_init_spaces, wl_iota, wl_step_spaces
+    from goworld_amd.sync import EntitySync
+
+    n, L, D = args.n, args.L, args.dist
+    seed = args.seed + rank
+    W, K = args.warmup, args.steps
+    T = W + K + 1
+    L_ = _lib.load()
+    t_setup = time.perf_counter()
+    snap = DeviceBuffer(2 * 4 * n * T, dev)
+    slots = DeviceBuffer(4 * n, dev)
+    wl_iota(dev, slots.ptr, n)
+
+    def px(t):
+        return snap.ptr + (2 * t) * 4 * n
+
+    def pz(t):
+        return snap.ptr + (2 * t + 1) * 4 * n
+
+    wl_init_spaces(dev, px(0), pz(0), n, 1, seed, L, 0, 0.0, 10)
+    for t in range(1, T):
+        wl_step_spaces(dev, px(t - 1), pz(t - 1), px(t), pz(t), n, 1, seed, t, L, 1.0)
+    # entity ids: slot number in the first 4 bytes, a fixed tag after; clients: a fraction of the slots
+    ids = np.zeros((n, 16), np.uint8)
+    ids[:, :4] = np.arange(n, dtype=np.uint32).view(np.uint8).reshape(n, 4)
+    ids[:, 4:] = np.frombuffer(b"GWAOI-ENTITY", np.uint8)
+    d_ids = DeviceBuffer(16 * n, dev)
+    d_ids.upload(ids)
+    payload = DeviceBuffer(32 * n * T, dev)
+    for t in range(1, T):
+        _lib.check(L_.gwaoi_wl_pack_ingest(dev, d_ids.ptr, px(t), pz(t), n, t, payload.ptr + 32 * n * t))
+    eng = Engine(capacity=n, device=dev, spaces=[(D, (0.0, 0.0, L, L))])
+    kinds = DeviceBuffer(n, dev)
+    kinds.upload(np.full(n, _lib.GWAOI_OP_ENTER | _lib.GWAOI_OP_SILENT, np.uint8))
+    eng.stage_ops_device(slots.ptr, px(0), pz(0), kinds.ptr, n)
+    eng.tick_device()
+    kinds.free()
+    sy = EntitySync(eng, args.gates)
+    all_slots = np.arange(n, dtype=np.uint32)
+    sy.set_entities(all_slots, ids)
+    has_client = (all_slots.astype(np.uint64) * 2654435761 % 1000) < int(args.client_frac * 1000)
+    gates = np.where(has_client, all_slots % args.gates, _lib.GWAOI_SYNC_NO_CLIENT).astype(np.uint16)
+    sy.set_clients(all_slots, gates, ids[:, ::-1].copy())
+    sy.set_client_syncing(all_slots, np.ones(n, np.uint8))
+    log(f"[rank {rank}] gametick setup {time.perf_counter() - t_setup:.1f}s: {n} entities, "
+        f"{int(has_client.sum())} with clients on {args.gates} gates")
+
+    def step(t, lat):
+        t0 = time.perf_counter()
+        r = sy.ingest_device(payload.ptr + 32 * n * t, 32 * n)
+        t1 = time.perf_counter()
+        eng.tick_device()
+        t2 = time.perf_counter()
+        o = sy.collect_raw(0)
+        t3 = time.perf_counter()
+        if lat is not None:
+            lat.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0, int(o.n_records), int(r.n_moved)))
+
+    for t in range(1, W + 1):
+        step(t, None)
+    eng.set_timing(True)
+    eng.reset_stats()
+    sync_all()
+    lat = []
+    t0 = time.perf_counter()
+    for t in range(W + 1, W + K + 1):
+        step(t, lat)
+    sync_all()
+    elapsed = allmax(time.perf_counter() - t0)
+    st = eng.stats()
+    eng.close()
+    if rank != 0:
+        return None
+    a = np.asarray(lat, dtype=np.float64)
+    ms = a[:, :4].mean(axis=0) * 1e3
+    recs = float(a[:, 4].mean())
+    moved = float(a[:, 5].mean())
+    ticks = max(1, st["ticks"])
+    rec_grid = st["grid_records"] / ticks
+    # algorithmic bytes: fan-out = records written (48 B) + per entity state read once (flag 1, gate 2,
+    # EntityID 16, x y z yaw 16) + the grid records walked once (32 B); ingest = payload read (32 B) +
+    # hash probe (16 B key + 4 B slot) + the staged Moved (12 B) + flag/y/yaw written (9 B)
+    b_fan = 48.0 * recs + 35.0 * n + 32.0 * rec_grid
+    b_ing = (32.0 + 20.0 + 12.0 + 9.0) * n
+    fan_gbs = b_fan / (ms[2] * 1e-3) / 1e9
+    ing_gbs = b_ing / (ms[0] * 1e-3) / 1e9
+    return {
+        "metric": "GoWorld game tick (client position ingest + AOI tick + sync fan-out) entity-updates/s at 1M "
+                  "entities per Space",
+        "value": n * K * world / elapsed,
+        "unit": "entity-updates/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": DATA + "; ingest payload packed on device (32-B records, slot order)",
+        "config": {
+            "workload": f"game tick at config 2 scale: {n} entities, L={L:.0f}, D={D}, every entity's client sends "
+                        f"its position each tick; {args.client_frac:.0%} of the entities have a client, "
+                        f"{args.gates} gates",
+            "entities_per_gpu": n, "world_L": L, "aoi_dist": D, "seed": hex(seed - rank),
+            "client_frac": args.client_frac, "gates": args.gates,
+            "parallelism": "independent Spaces, one manager per GPU" if world > 1 else "1 GPU",
+        },
+        "p50_step_ms": percentile(list(a[:, 3] * 1e3), 50),
+        "p99_step_ms": percentile(list(a[:, 3] * 1e3), 99),
+        "stage_ms": {"ingest": ms[0], "aoi_tick": ms[1], "collect_sync": ms[2]},
+        "aoi_stage_ms": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
+        "moved_per_tick": moved,
+        "sync_records_per_tick": recs,
+        "sync_bytes_per_tick": 48.0 * recs,
+        "events_per_tick": st["events"] / ticks,
+        "roofline": {
+            "bound": "hbm", "kernel": "collect_sync (whole call, host wall time incl. 2 syncs)",
+            "achieved": fan_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": fan_gbs / HBM_PEAK_GBS,
+            "traffic": None, "algorithmic_bytes_per_launch": b_fan,
+            "ingest": {"achieved": ing_gbs, "frac": ing_gbs / HBM_PEAK_GBS, "algorithmic_bytes": b_ing},
+        },
+        "cpu_baseline": None,
+    }
+
+
 def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
     """config 4: one world of per_gpu * world entities (density of config 2) in X-strips, one per rank."""
     import torch
@@ -381,7 +516,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=["config2", "config3", "skew", "skew50", "strips"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "config3", "skew", "skew50", "strips", "gametick"], default="config2")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--L", type=float, default=35000.0)
     ap.add_argument("--dist", type=float, default=100.0)
@@ -389,6 +524,8 @@ def main():
     ap.add_argument("--spaces", type=int, default=512, help="config3: Spaces per GPU")
     ap.add_argument("--per-gpu", type=int, default=2_000_000, help="strips: entities per GPU")
     ap.add_argument("--seed-strips", type=lambda s: int(s, 0), default=0x5EED0004)
+    ap.add_argument("--gates", type=int, default=8, help="gametick: gates (dense indices)")
+    ap.add_argument("--client-frac", type=float, default=0.25, help="gametick: fraction of entities with a client")
     ap.add_argument("--latency-ticks", type=int, default=200, help="extra ticks with events delivered to host")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -438,6 +575,8 @@ def main():
 
     if args.workload == "strips":
         result = run_strips(args, rank, world, dev, sync_all, allmax, via_cpu=(backend == "gloo"))
+    elif args.workload == "gametick":
+        result = run_gametick(args, rank, world, dev, sync_all, allmax)
     else:
         result = run_spaces(args, rank, world, dev, sync_all, allmax)
 

@@ -39,7 +39,7 @@ TOOL_SYMBOLS = (
     "gwaoi_dev_sync", "gwaoi_wl_init", "gwaoi_wl_step", "gwaoi_wl_iota", "gwaoi_wl_init_spaces",
     "gwaoi_wl_step_spaces", "gwaoi_debug_set_next_seq",
     "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_sweep_lds", "gwaoi_debug_read_stamps",
-    "gwaoi_debug_sweep_occupancy",
+    "gwaoi_debug_sweep_occupancy", "gwaoi_wl_pack_ingest",
 )
 
 
@@ -200,6 +200,7 @@ def load(path: str = SO_PATH):
         "gwaoi_strip_absorb": ([vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_strip_emit": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "gwaoi_strip_scratch_words": ([u32], ctypes.c_size_t),
+        "gwaoi_wl_pack_ingest": ([ctypes.c_int, vp, vp, vp, u32, u32, vp], ctypes.c_int),
         "gwaoi_sync_enable": ([vp, u32], ctypes.c_int),
         "gwaoi_sync_get_tables": ([vp, ctypes.POINTER(SyncTables)], ctypes.c_int),
         "gwaoi_sync_set_entities": ([vp, vp, vp, u32], ctypes.c_int),

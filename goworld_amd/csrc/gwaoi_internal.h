@@ -233,6 +233,8 @@ struct MgrView {
   GridView g;                // the grid of the last pass (main records = current state)
   const uint32_t* rec_count;  // device: records of that grid (cs[ncells])
   uint32_t rec_bound;         // host upper bound on them
+  uint32_t ncells;            // cells of that grid (cs has ncells + 1 entries)
+  uint32_t ntiles;            // tiles of that grid (over all Spaces)
   const float* pos_x;
   const float* pos_z;
   const uint32_t* seq;        // 0 = absent

@@ -920,6 +920,8 @@ int mgr_view(gwaoi_mgr* m, MgrView* out) {
   out->g = {g.rec, g.cs, g.d_geom, g.d_tile_space};
   out->rec_count = g.cs ? g.cs + g.ncells : nullptr;
   out->rec_bound = 2 * m->cap;
+  out->ncells = g.ncells;
+  out->ntiles = g.ntiles;
   out->pos_x = m->pos_x;
   out->pos_z = m->pos_z;
   out->seq = m->seq;

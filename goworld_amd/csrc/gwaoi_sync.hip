@@ -112,9 +112,59 @@ struct FanArgs {
   uint32_t* cnt;        // count pass: pairs per grid record ([rec_bound + 1], scanned afterwards)
   const uint32_t* off;  // write pass: the scanned counts
   uint2* pairs;         // {entity, receiver} (receiver == entity: own client)
-  uint8_t* pgate;       // gate of each pair
   uint32_t* n_ent;      // entities collected (count pass)
+  // client sub-grid: the main records of entities WITH a client, in grid order (the only candidates
+  // a fan-out can name), with their own cell starts over the same cell keys
+  const uint32_t* ccs;  // [ncells + 1]
+  const uint4* crec;    // {x, z, seq_end, slot}
+  const uint8_t* cgate;
+  const uint32_t* cpos;  // scanned sub-grid positions (own client: the entity's own sub-grid record)
+  const uint4* eid;
+  const float* y;
+  const float* yaw;
+  uint4* info;          // write pass: per grid record of a collected entity {EntityID}, {x, y, z, yaw}
 };
+
+struct ClientGridArgs {
+  const Rec* rec;
+  const uint32_t* cs;
+  const uint32_t* rec_count;
+  uint32_t rec_bound;
+  uint32_t ncells;
+  const uint16_t* gate;
+  uint32_t* cpos;  // [rec_bound + 1]: 0/1, scanned -> position in the sub-grid
+  uint32_t* ccs;
+  uint4* crec;
+  uint8_t* cgate;
+  const uint4* cid;
+  uint4* ccid;     // client id of each sub-grid record (fan-out reads are then spatially local)
+};
+
+__device__ __forceinline__ bool cg_take(const ClientGridArgs& a, uint32_t j, uint32_t nrec) {
+  if (j >= nrec) return false;
+  const uint32_t z = a.rec[j].a.z;
+  return !(z & REC_GHOST) && a.gate[z & REC_SLOT] != GWAOI_SYNC_NO_CLIENT;
+}
+
+__global__ void __launch_bounds__(kSy) k_cg_flag(ClientGridArgs a) {
+  const uint32_t nrec = *a.rec_count;
+  for (uint32_t j = blockIdx.x * kSy + threadIdx.x; j <= a.rec_bound; j += gridDim.x * kSy)
+    a.cpos[j] = cg_take(a, j, nrec) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(kSy) k_cg_build(ClientGridArgs a) {
+  const uint32_t nrec = *a.rec_count;
+  const uint32_t nth = gridDim.x * kSy;
+  for (uint32_t j = blockIdx.x * kSy + threadIdx.x; j < nrec; j += nth) {
+    if (!cg_take(a, j, nrec)) continue;
+    const Rec r = a.rec[j];
+    const uint32_t s = r.a.z & REC_SLOT, p = a.cpos[j];
+    a.crec[p] = make_uint4(r.a.x, r.a.y, r.b.w, s);
+    a.cgate[p] = (uint8_t)a.gate[s];
+    a.ccid[p] = a.cid[s];
+  }
+  for (uint32_t c = blockIdx.x * kSy + threadIdx.x; c <= a.ncells; c += nth) a.ccs[c] = a.cpos[a.cs[c]];
+}
 
 // Every neighbour o of the entity of main record j whose client exists: f(o). The neighbour set is
 // {o : in(L, F)} with L the later actor (Entity.InterestedBy under the XZ manager, see gwaoi_kernels.hip).
@@ -124,81 +174,156 @@ __device__ __forceinline__ void client_neighbours(const FanArgs& a, uint32_t s, 
   const float D = g.D;
   const CellBox B = qbox(g, sx, sz);
   for (int r = B.z0; r <= B.z1; ++r) {
-    row_entries_global(g, a.g.cs, r, B.x0, B.x1, [&](uint32_t j) {
-      const uint4 ra = a.g.rec[j].a;
-      const uint32_t o = ra.z & REC_SLOT;
-      if ((ra.z & REC_GHOST) || o == s) return;
-      const uint32_t qo = a.g.rec[j].b.w;
-      const float ox = __uint_as_float(ra.x), oz = __uint_as_float(ra.y);
-      const bool in = (qo > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz);
-      if (in) {
-        const uint16_t go = a.gate[o];
-        if (go != GWAOI_SYNC_NO_CLIENT) f(o, go);
-      }
+    row_entries_global(g, a.ccs, r, B.x0, B.x1, [&](uint32_t j) {
+      const uint4 c = a.crec[j];
+      const uint32_t o = c.w;
+      if (o == s) return;
+      const float ox = __uint_as_float(c.x), oz = __uint_as_float(c.y);
+      const bool in = (c.z > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz);
+      if (in) f(j, a.cgate[j]);
     });
   }
 }
 
+// Tile-staged walk: one block per grid tile; the client sub-grid's cell starts and ends of the tile
+// plus a halo of `reach` cells are staged in LDS, so a row segment costs two LDS reads instead of two
+// dependent global loads. Entities whose box leaves the region (reach 0, coarse grids) walk the
+// global table. Same per-record outputs as k_fan (count, pairs in walk order, info, flag clear).
+constexpr int kFanRegCells = kSweepRegCells;
+constexpr int kFanLdsPairs = 4096;  // 32 KB: a round of 256 entities at ~16 pairs each
 template <bool kWrite>
-__global__ void __launch_bounds__(kSy) k_fan(FanArgs a) {
-  const uint32_t nrec = *a.rec_count;
+__global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
+  __shared__ uint32_t lst[kFanRegCells], len_[kFanRegCells];
+  __shared__ uint32_t red[kSy / 64];
+  __shared__ uint2 lpairs[kWrite ? kFanLdsPairs : 1];
+  const uint32_t t = blockIdx.x;
+  const uint32_t sp = a.g.tile_space[t];
+  const Geom g = a.g.geom[sp];
+  const int lt = (int)(t - g.tile_base);
+  const int tx = lt % g.ntx, tz = lt / g.ntx;
+  const uint32_t k0 = g.base + ((uint32_t)lt << kTileCellShift);
+  const uint32_t j0 = a.g.cs[k0], j1 = a.g.cs[k0 + kTileCells];
+  if (j0 == j1) return;
+  const int R = g.reach;
+  const int cx0 = max(tx * kTile - R, 0), cx1 = min(tx * kTile + kTile - 1 + R, g.ncx - 1);
+  const int cz0 = max(tz * kTile - R, 0), cz1 = min(tz * kTile + kTile - 1 + R, g.ncz - 1);
+  const int W = cx1 - cx0 + 1, Hh = cz1 - cz0 + 1;
+  const bool lds = R > 0 && W * Hh <= kFanRegCells;
+  if (lds) {
+    for (int i = threadIdx.x; i < W * Hh; i += kSy) {
+      const int cx = cx0 + i % W, cz = cz0 + i / W;
+      const uint32_t k = cell_key(g, cx, cz);
+      lst[i] = a.ccs[k];
+      len_[i] = a.ccs[k + 1];
+    }
+  }
+  __syncthreads();
   uint32_t ents = 0;
-  for (uint32_t j = blockIdx.x * kSy + threadIdx.x; j <= a.rec_bound; j += gridDim.x * kSy) {
+  // one record: count (and, in the write pass, emit) its pairs through `put`
+  auto visit = [&](uint32_t j, auto&& put) {
     uint32_t c = 0;
-    if (j < nrec) {
-      const uint4 ra = a.g.rec[j].a;
-      const uint32_t s = ra.z & REC_SLOT;
-      const uint8_t fl = (ra.z & REC_GHOST) ? 0 : a.flags[s];
-      const uint32_t want = fl & (GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
-      if (want) {
-        ++ents;
-        uint32_t w = kWrite ? a.off[j] : 0u;
-        const uint16_t gs = a.gate[s];
-        if ((want & GWAOI_SYNC_OWN_CLIENT) && gs != GWAOI_SYNC_NO_CLIENT) {
-          if (kWrite) {
-            a.pairs[w] = make_uint2(s, s);
-            a.pgate[w++] = (uint8_t)gs;
-          }
-          ++c;
-        }
-        if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS) {
-          const float sx = __uint_as_float(ra.x), sz = __uint_as_float(ra.y);
-          const uint32_t qs = a.g.rec[j].b.w;
-          client_neighbours(a, s, sx, sz, qs, [&](uint32_t o, uint16_t go) {
-            if (kWrite) {
-              a.pairs[w] = make_uint2(s, o);
-              a.pgate[w++] = (uint8_t)go;
+    const uint4 ra = a.g.rec[j].a;
+    const uint32_t s = ra.z & REC_SLOT;
+    const uint8_t fl = (ra.z & REC_GHOST) ? 0 : a.flags[s];
+    const uint32_t want = fl & (GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
+    if (want) {
+      ++ents;
+      uint32_t w = kWrite ? a.off[j] : 0u;
+      const uint32_t w0 = w;
+      uint4 eid = make_uint4(0, 0, 0, 0);
+      float yy = 0.0f, yw = 0.0f;
+      if (kWrite) {  // issued before the walk: independent of it
+        eid = a.eid[s];
+        yy = a.y[s];
+        yw = a.yaw[s];
+      }
+      const uint16_t gs = a.gate[s];
+      if ((want & GWAOI_SYNC_OWN_CLIENT) && gs != GWAOI_SYNC_NO_CLIENT) {
+        if (kWrite) put(w++, make_uint2(j, a.cpos[j]));
+        ++c;
+      }
+      if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS) {
+        const float sx = __uint_as_float(ra.x), sz = __uint_as_float(ra.y);
+        const uint32_t qs = a.g.rec[j].b.w;
+        const CellBox B = qbox(g, sx, sz);
+        if (lds && B.x0 >= cx0 && B.x1 <= cx1 && B.z0 >= cz0 && B.z1 <= cz1) {
+          const float D = g.D;
+          for (int r = B.z0; r <= B.z1; ++r) {
+            const int rb = (r - cz0) * W - cx0;
+            // the row's cells split at tile boundaries into contiguous key ranges
+            for (int lo = B.x0; lo <= B.x1;) {
+              const int hi = min(B.x1, (lo | (kTile - 1)));
+              const uint32_t e = len_[rb + hi];
+              for (uint32_t q = lst[rb + lo]; q < e; ++q) {
+                const uint4 cr = a.crec[q];
+                const float ox = __uint_as_float(cr.x), oz = __uint_as_float(cr.y);
+                const bool in = cr.w != s && ((cr.z > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz));
+                if (in) {
+                  if (kWrite) put(w++, make_uint2(j, q));
+                  ++c;
+                }
+              }
+              lo = hi + 1;
             }
+          }
+        } else {
+          client_neighbours(a, s, sx, sz, qs, [&](uint32_t cj, uint8_t) {
+            if (kWrite) put(w++, make_uint2(j, cj));
             ++c;
           });
         }
-        if (kWrite && a.clear)
-          a.flags[s] = (uint8_t)(fl & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
+      }
+      if (kWrite) {
+        if (w != w0) {
+          a.info[2 * (size_t)j] = eid;
+          a.info[2 * (size_t)j + 1] = make_uint4(ra.x, __float_as_uint(yy), ra.y, __float_as_uint(yw));
+        }
+        if (a.clear) a.flags[s] = (uint8_t)(fl & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
       }
     }
-    if (!kWrite) a.cnt[j] = c;
+    return c;
+  };
+  for (uint32_t jb = j0; jb < j1; jb += kSy) {
+    const uint32_t j = jb + threadIdx.x;
+    if (!kWrite) {
+      if (j < j1) a.cnt[j] = visit(j, [](uint32_t, uint2) {});
+      continue;
+    }
+    // write pass, per round of kSy records: their output is the contiguous range [off[jb], off[je]),
+    // staged in LDS and copied out coalesced when it fits (else written directly)
+    const uint32_t pb = a.off[jb], pe = a.off[min(jb + kSy, j1)];
+    if (pe - pb <= (uint32_t)kFanLdsPairs) {
+      if (j < j1) visit(j, [&](uint32_t w, uint2 v) { lpairs[w - pb] = v; });
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < pe - pb; i += kSy) a.pairs[pb + i] = lpairs[i];
+      __syncthreads();
+    } else if (j < j1) {
+      uint2* pairs = a.pairs;
+      visit(j, [&](uint32_t w, uint2 v) { pairs[w] = v; });
+    }
   }
   if (!kWrite) {
-    // one atomic per wave
     for (int o = 32; o > 0; o >>= 1) ents += __shfl_xor(ents, o, 64);
-    if ((threadIdx.x & 63) == 0 && ents) atomicAdd(a.n_ent, ents);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ents;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (int k = 0; k < kSy / 64; ++k) tot += red[k];
+      if (tot) atomicAdd(a.n_ent, tot);
+    }
   }
 }
 
 struct GateArgs {
   const uint2* pairs;
-  const uint8_t* pgate;
+  const uint8_t* cgate;  // gate of a pair = gate of its receiver's sub-grid record
   uint32_t n;        // pairs
   uint32_t nchunks;
   uint32_t n_gates;
   int bits;          // ceil(log2(n_gates)), >= 1
   uint32_t* ghist;   // [n_gates * nchunks + 1], gate-major; scanned between the two kernels
-  const uint4* cid;
-  const uint4* eid;
-  const float* pos_x;
-  const float* pos_z;
-  const float* y;
-  const float* yaw;
+  const uint4* ccid;
+  const uint4* info;
   uint4* out;        // 3 uint4 per record
   uint32_t* goff;    // [n_gates + 1]
 };
@@ -211,7 +336,7 @@ __global__ void __launch_bounds__(kSy) k_gate_hist(GateArgs a) {
 #pragma unroll 4
   for (int k = 0; k < kGItems; ++k) {
     const uint32_t i = b0 + k * kSy + threadIdx.x;
-    if (i < a.n) atomicAdd(&h[a.pgate[i]], 1u);
+    if (i < a.n) atomicAdd(&h[a.cgate[a.pairs[i].y]], 1u);
   }
   __syncthreads();
   for (uint32_t g = threadIdx.x; g < a.n_gates; g += kSy) a.ghist[g * a.nchunks + blockIdx.x] = h[g];
@@ -235,7 +360,8 @@ __global__ void __launch_bounds__(kSy) k_gate_scatter(GateArgs a) {
   for (int k = 0; k < kGItems; ++k) {
     const uint32_t i = b0 + k * kSy + threadIdx.x;
     const bool live = i < a.n;
-    const uint32_t g = live ? a.pgate[i] : 0u;
+    const uint2 p = live ? a.pairs[i] : make_uint2(0u, 0u);
+    const uint32_t g = live ? a.cgate[p.y] : 0u;
     unsigned long long same = __ballot(live);
     for (int b = 0; b < a.bits; ++b) {
       const unsigned long long v = __ballot(live && ((g >> b) & 1u));
@@ -255,13 +381,11 @@ __global__ void __launch_bounds__(kSy) k_gate_scatter(GateArgs a) {
       wc[w][g] = 0;
     }
     if (live) {
-      const uint2 p = a.pairs[i];
-      const uint32_t e = p.x, r = p.y;
+      // p = {grid record of the entity, sub-grid record of the receiver}
       uint4* o = a.out + (size_t)pos * 3;
-      o[0] = a.cid[r];
-      o[1] = a.eid[e];
-      o[2] = make_uint4(__float_as_uint(a.pos_x[e]), __float_as_uint(a.y[e]), __float_as_uint(a.pos_z[e]),
-                        __float_as_uint(a.yaw[e]));
+      o[0] = a.ccid[p.y];
+      o[1] = a.info[2 * (size_t)p.x];
+      o[2] = a.info[2 * (size_t)p.x + 1];
     }
     __syncthreads();
   }
@@ -398,6 +522,14 @@ __global__ void k_fill_u32(uint32_t* p, uint32_t v, uint32_t n) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
 
+__global__ void __launch_bounds__(kSy) k_wl_pack_ingest(const uint4* __restrict__ ids, const float* __restrict__ x,
+                                                        const float* __restrict__ z, uint32_t n, float yaw, uint4* out) {
+  const uint32_t i = blockIdx.x * kSy + threadIdx.x;
+  if (i >= n) return;
+  out[2 * i] = ids[i];
+  out[2 * i + 1] = make_uint4(__float_as_uint(x[i]), 0u, __float_as_uint(z[i]), __float_as_uint(yaw));
+}
+
 uint32_t blocks_for(uint64_t n) { return (uint32_t)std::max<uint64_t>(1, (n + kSy - 1) / kSy); }
 
 }  // namespace
@@ -428,9 +560,19 @@ struct SyncState {
   // collect scratch
   uint32_t* cnt = nullptr;
   uint32_t cnt_n = 0;
+  uint32_t* cpos = nullptr;
+  uint32_t cpos_n = 0;
+  uint32_t* ccs = nullptr;
+  uint32_t ccs_n = 0;
+  uint4* crec = nullptr;
+  uint8_t* cgate = nullptr;
+  uint32_t crec_n = 0, cgate_n = 0;
+  uint4* ccid = nullptr;
+  uint32_t ccid_n = 0;
+  uint4* info = nullptr;
+  uint64_t info_cap = 0;
   uint2* pairs = nullptr;
-  uint8_t* pgate = nullptr;
-  uint64_t pairs_cap = 0, pgate_cap = 0;
+  uint64_t pairs_cap = 0;
   uint32_t* ghist = nullptr;
   uint64_t ghist_cap = 0;
   uint4* out = nullptr;
@@ -458,7 +600,8 @@ struct SyncState {
 
 void sync_free(SyncState* s) {
   if (!s) return;
-  void* p[] = {s->flags, s->gate, s->cid, s->eid, s->y, s->yaw, s->d_hkey, s->d_hval, s->cnt, s->pairs, s->pgate,
+  void* p[] = {s->flags, s->gate, s->cid, s->eid, s->y, s->yaw, s->d_hkey, s->d_hval, s->cnt, s->cpos, s->ccs,
+               s->crec, s->cgate, s->ccid, s->info, s->pairs,
                s->ghist, s->out, s->d_goff, s->scan.status, s->d_payload, s->res, s->first, s->ictr, s->bcnt,
                s->op_slot, s->op_x, s->op_z};
   for (void* q : p)
@@ -920,7 +1063,40 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   const uint32_t bound = v.rec_bound;
   SRCHK(gw::dgrow32(&s->cnt, &s->cnt_n, (uint64_t)bound + 1));
   SRCHK(gw::ensure_scan(s, bound + 1));
+  // client sub-grid
+  SRCHK(gw::dgrow32(&s->cpos, &s->cpos_n, (uint64_t)bound + 1));
+  SRCHK(gw::dgrow32(&s->ccs, &s->ccs_n, (uint64_t)v.ncells + 1));
+  SRCHK(gw::dgrow32(&s->crec, &s->crec_n, s->cap));
+  SRCHK(gw::dgrow32(&s->cgate, &s->cgate_n, s->cap));
+  SRCHK(gw::dgrow32(&s->ccid, &s->ccid_n, s->cap));
+  SRCHK(gw::dgrow(&s->info, &s->info_cap, 2 * ((uint64_t)bound + 1)));
+  gw::ClientGridArgs cg = {};
+  cg.rec = v.g.rec;
+  cg.cs = v.g.cs;
+  cg.rec_count = v.rec_count;
+  cg.rec_bound = bound;
+  cg.ncells = v.ncells;
+  cg.gate = s->gate;
+  cg.cpos = s->cpos;
+  cg.ccs = s->ccs;
+  cg.crec = s->crec;
+  cg.cgate = s->cgate;
+  cg.cid = s->cid;
+  cg.ccid = s->ccid;
+  const uint32_t fan_blocks = std::min<uint32_t>(gw::blocks_for((uint64_t)bound + 1), 8192);
+  SRCHK(gw::ensure_scan(s, std::max(bound, v.ncells) + 1));
+  hipLaunchKernelGGL(gw::k_cg_flag, dim3(fan_blocks), dim3(gw::kSy), 0, st, cg);
+  gw::launch_scan(s->scan, s->cpos, bound + 1, st);
+  hipLaunchKernelGGL(gw::k_cg_build, dim3(fan_blocks), dim3(gw::kSy), 0, st, cg);
   gw::FanArgs f = {};
+  f.ccs = s->ccs;
+  f.crec = s->crec;
+  f.cgate = s->cgate;
+  f.cpos = s->cpos;
+  f.eid = s->eid;
+  f.y = s->y;
+  f.yaw = s->yaw;
+  f.info = s->info;
   f.g = v.g;
   f.rec_count = v.rec_count;
   f.rec_bound = bound;
@@ -933,8 +1109,10 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   f.cnt = s->cnt;
   f.n_ent = s->ictr + 8;
   SCHK(hipMemsetAsync(s->ictr + 8, 0, 4, st));
-  const uint32_t fan_blocks = std::min<uint32_t>(gw::blocks_for((uint64_t)bound + 1), 8192);
-  hipLaunchKernelGGL(gw::k_fan<false>, dim3(fan_blocks), dim3(gw::kSy), 0, st, f);
+  SCHK(hipMemsetAsync(s->cnt, 0, ((size_t)bound + 1) * 4, st));
+  const uint32_t ntiles = v.ntiles;
+  if (!ntiles) return GWAOI_OK;
+  hipLaunchKernelGGL(gw::k_fan_tile<false>, dim3(ntiles), dim3(gw::kSy), 0, st, f);
   gw::launch_scan(s->scan, s->cnt, bound + 1, st);
   SCHK(hipMemcpyAsync(s->h_small, s->cnt + bound, 4, hipMemcpyDeviceToHost, st));
   SCHK(hipMemcpyAsync(s->h_small + 1, s->ictr + 8, 4, hipMemcpyDeviceToHost, st));
@@ -944,21 +1122,19 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   if (M == 0) {
     if (f.clear) {  // nothing to write, but the flags of the collected entities still clear
       f.off = s->cnt;
-      hipLaunchKernelGGL(gw::k_fan<true>, dim3(fan_blocks), dim3(gw::kSy), 0, st, f);
+      hipLaunchKernelGGL(gw::k_fan_tile<true>, dim3(ntiles), dim3(gw::kSy), 0, st, f);
       SCHK(hipStreamSynchronize(st));
     }
     return GWAOI_OK;
   }
   SRCHK(gw::dgrow(&s->pairs, &s->pairs_cap, M));
-  SRCHK(gw::dgrow(&s->pgate, &s->pgate_cap, M));
   f.off = s->cnt;
   f.pairs = s->pairs;
-  f.pgate = s->pgate;
-  hipLaunchKernelGGL(gw::k_fan<true>, dim3(fan_blocks), dim3(gw::kSy), 0, st, f);
+  hipLaunchKernelGGL(gw::k_fan_tile<true>, dim3(ntiles), dim3(gw::kSy), 0, st, f);
 
   gw::GateArgs g = {};
   g.pairs = s->pairs;
-  g.pgate = s->pgate;
+  g.cgate = s->cgate;
   g.n = M;
   g.nchunks = (M + gw::kGChunk - 1) / gw::kGChunk;
   g.n_gates = s->n_gates;
@@ -968,12 +1144,8 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   SRCHK(gw::dgrow(&s->ghist, &s->ghist_cap, hn));
   SRCHK(gw::ensure_scan(s, (uint32_t)hn));
   g.ghist = s->ghist;
-  g.cid = s->cid;
-  g.eid = s->eid;
-  g.pos_x = v.pos_x;
-  g.pos_z = v.pos_z;
-  g.y = s->y;
-  g.yaw = s->yaw;
+  g.ccid = s->ccid;
+  g.info = s->info;
   SRCHK(gw::dgrow(&s->out, &s->out_cap, (uint64_t)M * 3));
   g.out = s->out;
   g.goff = s->d_goff;
@@ -1104,6 +1276,21 @@ int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes,
     out->n_rejected = s->h_small[2];
     out->n_passes = passes;
   }
+  return GWAOI_OK;
+}
+
+int gwaoi_wl_pack_ingest(int device, const uint8_t* d_ids, const float* d_x, const float* d_z, uint32_t n,
+                         uint32_t tick, uint8_t* d_out) {
+  SCHK(hipSetDevice(device));
+  if (!n) return GWAOI_OK;
+  if (!d_ids || !d_x || !d_z || !d_out || ((uintptr_t)d_ids & 15) || ((uintptr_t)d_out & 15)) {
+    gw::set_error("wl_pack_ingest: null or unaligned array");
+    return GWAOI_ERR_INVALID;
+  }
+  hipLaunchKernelGGL(gw::k_wl_pack_ingest, dim3(gw::blocks_for(n)), dim3(gw::kSy), 0, nullptr, (const uint4*)d_ids,
+                     d_x, d_z, n, (float)tick * 0.01f, (uint4*)d_out);
+  SCHK(hipGetLastError());
+  SCHK(hipDeviceSynchronize());
   return GWAOI_OK;
 }
 

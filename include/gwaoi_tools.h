@@ -34,6 +34,10 @@ int gwaoi_wl_init_spaces(int device, float* d_x, float* d_z, uint32_t n_per, uin
 int gwaoi_wl_step_spaces(int device, const float* d_xprev, const float* d_zprev, float* d_xout, float* d_zout,
                          uint32_t n_per, uint32_t nspaces, uint64_t seed0, uint64_t tick, float L, float s);
 
+/* Bench tool: pack n ingest records (include/gwaoi_sync.h, 32 B each: d_ids[i] | x[i], y, z[i], yaw) into
+ * d_out, with y = 0 and yaw = tick * 0.01 — the client position stream of one tick, resident in HBM. */
+int gwaoi_wl_pack_ingest(int device, const uint8_t* d_ids, const float* d_x, const float* d_z, uint32_t n,
+                         uint32_t tick, uint8_t* d_out);
 /* Test hook: set the manager's next op sequence number (exercises the sequence renormalisation that
  * otherwise runs every ~2^31 ops). */
 struct gwaoi_mgr;

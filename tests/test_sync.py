@@ -72,11 +72,13 @@ def test_oracle_ingest_hand_case():
 # ------------------------------------------------------------------------------------------------
 # GPU
 
-def world(po, n, L, dist, seed, nticks=2, spaces=None):
+def world(po, n, L, dist, seed, nticks=2, cells_per_dist=None):
     """Run a seeded walk on the GPU and the list oracle; returns (eng, orc, x, z)."""
     from goworld_amd.engine import Engine
     case = H.case_walk(seed, n, L, nticks, dist, workload=po)
     eng = Engine(dist, capacity=n, bounds=(0.0, 0.0, L, L))
+    if cells_per_dist:
+        eng.debug_set_cells_per_dist(cells_per_dist)
     orc = po.XZListOracle(dist, n) if n <= 4000 else po.GridOracle(dist, n, (0, 0, L, L))
     x = np.zeros(n, np.float32)
     z = np.zeros(n, np.float32)
@@ -142,6 +144,18 @@ def test_collect_sync_parity(gpu, oracle_lib, n, L, dist, n_gates, seed):
     # flags were cleared: a second collect is empty
     again = sy.collect_entity_sync_infos()
     assert not again and sy.last.n_records == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cpd", [1.0, 10.0])
+def test_collect_cell_sizes(gpu, oracle_lib, cpd):
+    """Coarse cells (small LDS halo) and fine cells (halo beyond the LDS region: global-table walk)."""
+    from goworld_amd.sync import EntitySync
+    n = 2500
+    eng, orc, x, z = world(oracle_lib, n, 1500.0, 100.0, 13, nticks=3, cells_per_dist=cpd)
+    sy = EntitySync(eng, 7)
+    st = fill_sync(sy, np.random.default_rng(13), n, 7)
+    check_collect(sy, orc, st, x, z, 7)
 
 
 @pytest.mark.gpu
