@@ -140,6 +140,10 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     from goworld_amd.engine import DeviceBuffer, Engine, wl_init_spaces, wl_iota, wl_step_spaces
 
     name, n_per, nsp, dists, L, seed0, nhot, sigma, hot_every = spaces_workload(args, rank)
+    if args.dists:  # A/B: the same workload with other per-Space distances (one Space per entry)
+        dists = [float(v) for v in args.dists.split(",")]
+        nsp = len(dists)
+        name += f" [dists overridden: {dists}]"
     n = n_per * nsp
     W, K, H = args.warmup, args.steps, args.latency_ticks
     T = W + K + H + 1
@@ -163,6 +167,8 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     eng = Engine(capacity=n, device=dev, spaces=[(d, (0.0, 0.0, L, L)) for d in dists])
     if args.cells_per_dist:
         eng.debug_set_cells_per_dist(args.cells_per_dist)
+    if args.cell_side:
+        eng.debug_set_cell_side(args.cell_side)
     if args.sweep_lds != 1:
         eng._L.gwaoi_debug_set_sweep_lds(eng.handle, args.sweep_lds)
     # bulk restore (untimed): one device-staged pass of SILENT Enters into their Spaces; the relation
@@ -530,6 +536,8 @@ def main():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cells-per-dist", type=float, default=None)
+    ap.add_argument("--dists", default=None, help="skew workloads: comma list of per-Space D (A/B)")
+    ap.add_argument("--cell-side", type=float, default=None, help="absolute cell side for every Space (A/B)")
     ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
     ap.add_argument("--stamps", default=None, help="diagnostic GW_STAMPS build: dump the last sweep's per-block "
                                                    "phase timestamps to this .npy file")

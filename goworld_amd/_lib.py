@@ -38,7 +38,7 @@ TOOL_SYMBOLS = (
     "gwaoi_device_count", "gwaoi_dev_malloc", "gwaoi_dev_free", "gwaoi_dev_htod", "gwaoi_dev_dtoh",
     "gwaoi_dev_sync", "gwaoi_wl_init", "gwaoi_wl_step", "gwaoi_wl_iota", "gwaoi_wl_init_spaces",
     "gwaoi_wl_step_spaces", "gwaoi_debug_set_next_seq",
-    "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_sweep_lds", "gwaoi_debug_read_stamps",
+    "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_cell_side", "gwaoi_debug_set_sweep_lds", "gwaoi_debug_read_stamps",
     "gwaoi_debug_sweep_occupancy", "gwaoi_wl_pack_ingest",
 )
 
@@ -191,6 +191,7 @@ def load(path: str = SO_PATH):
         "gwaoi_wl_step_spaces": ([ctypes.c_int, vp, vp, vp, vp, u32, u32, u64, u64, f32, f32], ctypes.c_int),
         "gwaoi_debug_set_next_seq": ([vp, u32], ctypes.c_int),
         "gwaoi_debug_set_cells_per_dist": ([vp, f32], ctypes.c_int),
+        "gwaoi_debug_set_cell_side": ([vp, f32], ctypes.c_int),
         "gwaoi_debug_set_sweep_lds": ([vp, ctypes.c_int], ctypes.c_int),
         "gwaoi_debug_read_stamps": ([vp, ctypes.c_size_t], ctypes.c_int),
         "gwaoi_strip_init_walk": ([vp, vp, vp, vp, vp, u64, f32], ctypes.c_int),

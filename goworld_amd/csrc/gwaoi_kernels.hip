@@ -1463,25 +1463,131 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
   }
 }
 
+// Per-op slices are sorted by .y (other | ENTER bit: LEAVE first, then other ascending), inside one
+// kernel without global atomics (a shared work-list counter bumped by every wave serialises at ~88
+// returning atomics per us): slices of up to kSmallSlice events (config 2: ~0.3 per op) are sorted in
+// registers by their op's thread (an odd-even transposition network, static indices only); up to 64
+// by the op's wave (each lane holds one event and counts the events ordered before it); longer ones
+// (crowds: hundreds per mover) by the whole block: chunks of kBigChunk events are bitonic-sorted in
+// LDS, and a slice of several chunks is merged by rank: an element's final index is its index in its
+// sorted chunk plus, for every other chunk, the count of elements ordered before it there (binary
+// search; ties go to the earlier chunk, so the merge is stable). The chunks are parked in ev_tmp,
+// free once k_place has run (its uint2 view has 2 x slots >= n entries).
+constexpr uint32_t kSmallSlice = 8;
+constexpr uint32_t kBigChunk = 2048;
+__device__ __forceinline__ uint2 ld_cg(const uint2* p) {  // bypass the CU cache: written by this block
+  return make_uint2(__hip_atomic_load(&p->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(&p->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ void sort_long_slice(const OrderArgs& o, uint32_t b, uint32_t len, uint2* sk) {
+  uint2* tmp = reinterpret_cast<uint2*>(const_cast<uint4*>(o.ev_tmp));
+  const uint32_t nch = (len + kBigChunk - 1) / kBigChunk;
+  for (uint32_t c = 0; c < nch; ++c) {
+    const uint32_t c0 = c * kBigChunk, cl = min(kBigChunk, len - c0);
+    uint32_t P = 64;
+    while (P < cl) P <<= 1;
+    for (uint32_t i = threadIdx.x; i < P; i += kBlock)
+      sk[i] = i < cl ? o.ev_out[b + c0 + i] : make_uint2(0xffffffffu, 0xffffffffu);
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = threadIdx.x; i < P; i += kBlock) {
+          const uint32_t l = i ^ j;
+          if (l > i) {
+            const uint2 u = sk[i], v = sk[l];
+            if ((u.y > v.y) == ((i & k) == 0)) {
+              sk[i] = v;
+              sk[l] = u;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    uint2* dst = nch == 1 ? o.ev_out + b : tmp + b + c0;
+    for (uint32_t i = threadIdx.x; i < cl; i += kBlock) dst[i] = sk[i];
+    __syncthreads();
+  }
+  if (nch > 1) {
+    __threadfence();
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < len; i += kBlock) {
+      const uint2 v = ld_cg(tmp + b + i);
+      const uint32_t c = i / kBigChunk;
+      uint32_t pos = i - c * kBigChunk;
+      for (uint32_t c2 = 0; c2 < nch; ++c2) {
+        if (c2 == c) continue;
+        const uint2* ch = tmp + b + c2 * kBigChunk;
+        uint32_t lo = 0, hi = min(kBigChunk, len - c2 * kBigChunk);
+        while (lo < hi) {  // earlier chunks: count keys <= v (ties before); later: keys < v
+          const uint32_t mid = (lo + hi) >> 1;
+          const uint32_t ky = ld_cg(ch + mid).y;
+          if (c2 < c ? ky <= v.y : ky < v.y) lo = mid + 1;
+          else hi = mid;
+        }
+        pos += lo;
+      }
+      o.ev_out[b + pos] = v;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
+  __shared__ uint2 sk[kBigChunk];
+  __shared__ uint32_t bigq[kBlock];
+  __shared__ uint32_t nbig;
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-  if (r >= o.n_ops || (o.n_dev && r >= *o.n_dev)) return;
-  if (o.check_ops) {
+  const bool op = r < o.n_ops && !(o.n_dev && r >= *o.n_dev);
+  if (op && o.check_ops) {
     const uint32_t s = o.op_slot[r];
     if (s < o.cap && o.opq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
   }
   uint32_t slots, n;
-  if (!ev_fits(o.g, &slots, &n)) return;
-  const uint32_t b = o.rank_off[r], e = o.rank_off[r + 1];
-  uint2* ev = o.ev_out;
-  for (uint32_t i = b + 1; i < e; ++i) {
-    const uint2 v = ev[i];
-    uint32_t k = i;
-    while (k > b && ev[k - 1].y > v.y) {
-      ev[k] = ev[k - 1];
-      --k;
+  if (!ev_fits(o.g, &slots, &n)) return;  // grid-uniform
+  if (threadIdx.x == 0) nbig = 0;
+  const uint32_t b = op ? o.rank_off[r] : 0u, len = op ? o.rank_off[r + 1] - b : 0u;
+  if (len >= 2u && len <= kSmallSlice) {
+    uint2 v[kSmallSlice];
+#pragma unroll
+    for (uint32_t i = 0; i < kSmallSlice; ++i) v[i] = i < len ? o.ev_out[b + i] : make_uint2(0u, 0xffffffffu);
+#pragma unroll
+    for (uint32_t p = 0; p < kSmallSlice; ++p) {
+#pragma unroll
+      for (uint32_t i = p & 1u; i + 1 < kSmallSlice; i += 2) {
+        const uint2 x = v[i], y = v[i + 1];
+        const bool sw = x.y > y.y;  // strict: equal keys keep their order (stable)
+        v[i] = sw ? y : x;
+        v[i + 1] = sw ? x : y;
+      }
     }
-    ev[k] = v;
+#pragma unroll
+    for (uint32_t i = 0; i < kSmallSlice; ++i)
+      if (i < len) o.ev_out[b + i] = v[i];
+  }
+  // medium slices: the op's wave, one slice at a time
+  const uint32_t lane = threadIdx.x & 63u;
+  for (unsigned long long mm = __ballot(len > kSmallSlice && len <= 64u); mm; mm &= mm - 1ull) {
+    const int src = __ffsll((long long)mm) - 1;
+    const uint32_t mb = __shfl(b, src, 64), ml = __shfl(len, src, 64);
+    const uint2 v = lane < ml ? o.ev_out[mb + lane] : make_uint2(0u, 0xffffffffu);
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < ml; ++j) {
+      const uint32_t kj = __shfl(v.y, (int)j, 64);
+      pos += (kj < v.y || (kj == v.y && j < lane)) ? 1u : 0u;
+    }
+    if (lane < ml) o.ev_out[mb + pos] = v;
+  }
+  // long slices: the whole block
+  __syncthreads();
+  if (len > 64u) bigq[atomicAdd(&nbig, 1u)] = r;  // LDS atomic
+  __syncthreads();
+  const uint32_t nb = nbig;
+  for (uint32_t q = 0; q < nb; ++q) {
+    const uint32_t rq = bigq[q];
+    const uint32_t bq = o.rank_off[rq];
+    sort_long_slice(o, bq, o.rank_off[rq + 1] - bq, sk);
   }
 }
 
@@ -1495,8 +1601,9 @@ __global__ void __launch_bounds__(kBlock) k_copy_out(OrderArgs o) {
 
 void launch_order(const OrderArgs& o, hipStream_t st) {
   hipLaunchKernelGGL(k_place, dim3(1024), dim3(kBlock), 0, st, o);
-  if (o.n_ops)
+  if (o.n_ops) {
     hipLaunchKernelGGL(k_slice_sort, dim3((o.n_ops + kBlock - 1) / kBlock), dim3(kBlock), 0, st, o);
+  }
   if (o.host_out) hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, o);
 }
 

@@ -107,6 +107,8 @@ struct gwaoi_mgr {
   uint32_t nspaces = 0;
   std::vector<SpaceHost> spaces;
   float cells_per_dist = 4.0f;
+  float cell_side = 0.0f;  // > 0: absolute cell side for every Space (test hook), else D / cells_per_dist
+  bool density_cells = true;  // finer cells for crowded large-D Spaces (compute_geometry); off once a hook sets the size
   uint32_t max_cells = 0;
   bool broken = false;
 
@@ -212,6 +214,8 @@ void space_extent(const SpaceHost& sh, float* x0, float* z0, float* x1, float* z
   *z1 = sh.seen_maxz + 0.125f * wz + D;
 }
 
+constexpr double kCellOccupancy = 0.5;  // planned entities per cell (config 2: 1M in 35,000^2, cells of 25)
+
 void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
   out.resize(m->nspaces);
   const uint64_t share = std::max<uint64_t>(gw::kTileCells, m->max_cells / std::max<uint32_t>(1, m->nspaces));
@@ -222,7 +226,17 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
     space_extent(sh, &x0, &z0, &x1, &z1);
     if (!std::isfinite(x0) || !std::isfinite(x1) || !(x1 > x0)) { x0 = -1000.f; x1 = 1000.f; }
     if (!std::isfinite(z0) || !std::isfinite(z1) || !(z1 > z0)) { z0 = -1000.f; z1 = 1000.f; }
-    double c = (double)sh.desc.dist / (double)m->cells_per_dist;
+    double c = m->cell_side > 0 ? (double)m->cell_side : (double)sh.desc.dist / (double)m->cells_per_dist;
+    if (m->density_cells && !sh.auto_extent) {
+      // D / 4 cells hold ~0.5 entities at config-2 density (D 100). A large-D Space at that density
+      // gets cells of the same side instead of D / 4 (down to D / 16): a mover's ring of border cells
+      // then holds proportionally fewer candidates. Density is planned from the capacity share over
+      // the Space's declared extent.
+      const double area = ((double)x1 - x0) * ((double)z1 - z0);
+      const double pop = (double)m->cap / std::max<uint32_t>(1, m->nspaces);
+      const double cr = std::sqrt(kCellOccupancy * area / std::max(1.0, pop));
+      if (cr < 0.75 * c) c = std::max(cr, (double)sh.desc.dist / 16.0);
+    }
     if (!(c > 0)) c = 1.0;
     // tiles of kTile x kTile cells; cell counts padded to whole tiles
     auto dims = [&](double cc, int64_t* tx, int64_t* tz) {
@@ -1360,6 +1374,16 @@ int gwaoi_debug_set_cells_per_dist(gwaoi_mgr* m, float cpd) {
   RCHK(check_mgr(m));
   if (!(cpd > 0) || cpd > 64) return GWAOI_ERR_INVALID;
   m->cells_per_dist = cpd;
+  m->density_cells = false;
+  m->geom_dirty = true;
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_cell_side(gwaoi_mgr* m, float side) {
+  RCHK(check_mgr(m));
+  if (!(side >= 0) || !std::isfinite(side)) return GWAOI_ERR_INVALID;
+  m->cell_side = side;
+  m->density_cells = false;
   m->geom_dirty = true;
   return GWAOI_OK;
 }

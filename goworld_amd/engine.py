@@ -175,6 +175,9 @@ class Engine:
     def debug_set_cells_per_dist(self, v: float):
         check(self._L.gwaoi_debug_set_cells_per_dist(self._h, v))
 
+    def debug_set_cell_side(self, v: float):
+        check(self._L.gwaoi_debug_set_cell_side(self._h, v))
+
 
 class DeviceBuffer:
     """Raw device allocation via libgwaoi (no torch dependency)."""

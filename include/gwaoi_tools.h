@@ -46,6 +46,8 @@ int gwaoi_debug_set_next_seq(struct gwaoi_mgr* mgr, uint32_t next_seq);
 int gwaoi_debug_set_sweep_lds(struct gwaoi_mgr* mgr, int enable);
 /* Test hook: cell size = D / cells_per_dist for grids built from now on (default 4). */
 int gwaoi_debug_set_cells_per_dist(struct gwaoi_mgr* mgr, float cells_per_dist);
+/* Test hook: absolute cell side for every Space (0 = back to D / cells_per_dist). */
+int gwaoi_debug_set_cell_side(struct gwaoi_mgr* mgr, float side);
 /* Diagnostic builds only (GW_STAMPS=1): per-block phase timestamps of the last sweep launch
  * (8 x uint64 per block). Returns GWAOI_ERR_INVALID/-1 in a product build. */
 int gwaoi_debug_read_stamps(void* host, size_t bytes);

@@ -466,3 +466,21 @@ def test_device_counted_batch(gpu, po):
     with pytest.raises(_lib.GwaoiError) as e:
         b.tick()
     assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK
+
+
+def test_long_event_slices(gpu, po):
+    """A crowd of 5,000 inside one AOI box: the i-th Enter raises i events, so per-op event slices run
+    from 0 to 4,999 and the canonical ordering takes every path (insertion sort for short slices, one
+    LDS bitonic chunk, and several chunks merged by rank past 4,096); a Leave and a teleport out of the
+    crowd then raise 4,999 each. Bit-exact against oracle (i)."""
+    rng = np.random.default_rng(0x511CE)
+    n = 5000
+    x = rng.uniform(0.0, 90.0, n).astype(np.float32)
+    z = rng.uniform(0.0, 90.0, n).astype(np.float32)
+    case = {"name": "crowd", "dist": 100.0, "cap": n, "bounds": (-500.0, -500.0, 500.0, 500.0), "ticks": [
+        [(H.ENTER, i, float(x[i]), float(z[i])) for i in range(n)],
+        [(H.LEAVE, 17, 0.0, 0.0), (H.MOVE, 3, 400.0, 400.0), (H.MOVE, 9, float(x[9]) + 0.5, float(z[9]))],
+        [(H.MOVE, 3, float(x[3]), float(z[3])), (H.ENTER, 17, 45.0, 45.0)],
+    ]}
+    eng, _ = run_against_oracle(po, case, check_relation_every=0)
+    eng.close()
