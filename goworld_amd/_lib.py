@@ -31,7 +31,7 @@ ABI_SYMBOLS = (
     "gwaoi_stage_ops_device",
     "gwaoi_stage_ops_device_spaces",
     "gwaoi_stage_ops_device_n",
-    "gwaoi_tick", "gwaoi_tick_ex", "gwaoi_count", "gwaoi_export_relation", "gwaoi_set_timing",
+    "gwaoi_tick", "gwaoi_tick_ex", "gwaoi_count", "gwaoi_export_relation", "gwaoi_relation_device", "gwaoi_set_timing",
     "gwaoi_get_stats", "gwaoi_reset_stats", "gwaoi_version", "gwaoi_last_error",
 )
 TOOL_SYMBOLS = (
@@ -101,6 +101,11 @@ class GwaoiError(RuntimeError):
 
 class Event(ctypes.Structure):
     _fields_ = [("mover", ctypes.c_uint32), ("other", ctypes.c_uint32)]
+
+
+class RelationView(ctypes.Structure):
+    """gwaoi_relation_view (include/gwaoi.h): device-resident CSR of the relation."""
+    _fields_ = [("row_ptr", ctypes.c_void_p), ("cols", ctypes.c_void_p), ("nnz", ctypes.c_uint64)]
 
 
 class Events(ctypes.Structure):
@@ -173,6 +178,7 @@ def load(path: str = SO_PATH):
         "gwaoi_tick_ex": ([vp, u32, ctypes.POINTER(Events)], ctypes.c_int),
         "gwaoi_count": ([vp, u32p, u32p], ctypes.c_int),
         "gwaoi_export_relation": ([vp, u32p, u32p, u64, ctypes.POINTER(u64)], ctypes.c_int),
+        "gwaoi_relation_device": ([vp, ctypes.POINTER(RelationView)], ctypes.c_int),
         "gwaoi_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
         "gwaoi_get_stats": ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
         "gwaoi_reset_stats": ([vp], ctypes.c_int),

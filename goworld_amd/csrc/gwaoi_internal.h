@@ -214,7 +214,7 @@ struct OrderArgs {
 void launch_order(const OrderArgs& o, hipStream_t st);
 void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_t st);
 void launch_relation(const RelArgs& a, hipStream_t st);
-void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, hipStream_t st);
+void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, uint32_t* tmp, hipStream_t st);
 void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st);
 void launch_wl_init_spaces(float* x, float* z, uint32_t n_per, uint32_t nspaces, uint64_t seed0, float L,
                            uint32_t nhot, float sigma, uint32_t hot_every, hipStream_t st);

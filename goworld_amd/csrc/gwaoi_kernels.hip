@@ -1305,11 +1305,15 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
 // number of cells they come from. A mover's events are numbered by a ballot prefix on top of the
 // wave-uniform running count and written with one atomic per 64 candidates.
 constexpr int kDenseBlock = 256;
-constexpr int kDenseGrid = 1536;      // 6 waves per SIMD (<= 80 VGPRs): every wave resident
+#ifndef GW_DENSE_WPE
+#define GW_DENSE_WPE 6
+#endif
+constexpr int kDenseGrid = 256 * GW_DENSE_WPE;  // GW_DENSE_WPE waves per SIMD: every wave resident
 constexpr uint32_t kEvChunk = 128;    // event slots a wave reserves at a time (one returning atomic
                                       // on the shared counter each: ~11 ns apiece when serialised)
 
-__global__ void __launch_bounds__(kDenseBlock) k_sweep_dense(SweepArgs a) {
+__global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_DENSE_WPE)))
+k_sweep_dense(SweepArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t wave = (blockIdx.x * kDenseBlock + threadIdx.x) >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
   const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
@@ -1475,28 +1479,35 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
 // free once k_place has run (its uint2 view has 2 x slots >= n entries).
 constexpr uint32_t kSmallSlice = 8;
 constexpr uint32_t kBigChunk = 2048;
-__device__ __forceinline__ uint2 ld_cg(const uint2* p) {  // bypass the CU cache: written by this block
-  return make_uint2(__hip_atomic_load(&p->x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                    __hip_atomic_load(&p->y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+__device__ __forceinline__ uint32_t seg_key(const uint2 v) { return v.y; }
+__device__ __forceinline__ uint32_t seg_key(const uint32_t v) { return v; }
+template <class T> __device__ __forceinline__ T seg_pad();
+template <> __device__ __forceinline__ uint2 seg_pad<uint2>() { return make_uint2(0xffffffffu, 0xffffffffu); }
+template <> __device__ __forceinline__ uint32_t seg_pad<uint32_t>() { return 0xffffffffu; }
+__device__ __forceinline__ uint32_t ld_cg(const uint32_t* p) {  // bypass the CU cache: written by this block
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint2 ld_cg(const uint2* p) {
+  return make_uint2(ld_cg(&p->x), ld_cg(&p->y));
 }
 
-__device__ void sort_long_slice(const OrderArgs& o, uint32_t b, uint32_t len, uint2* sk) {
-  uint2* tmp = reinterpret_cast<uint2*>(const_cast<uint4*>(o.ev_tmp));
+// one long segment d[0, len), the whole block (kBlock threads); tmp[0, len) is scratch
+template <class T>
+__device__ void seg_sort_long(T* __restrict__ d, T* __restrict__ tmp, uint32_t len, T* sk) {
   const uint32_t nch = (len + kBigChunk - 1) / kBigChunk;
   for (uint32_t c = 0; c < nch; ++c) {
     const uint32_t c0 = c * kBigChunk, cl = min(kBigChunk, len - c0);
     uint32_t P = 64;
     while (P < cl) P <<= 1;
-    for (uint32_t i = threadIdx.x; i < P; i += kBlock)
-      sk[i] = i < cl ? o.ev_out[b + c0 + i] : make_uint2(0xffffffffu, 0xffffffffu);
+    for (uint32_t i = threadIdx.x; i < P; i += kBlock) sk[i] = i < cl ? d[c0 + i] : seg_pad<T>();
     __syncthreads();
     for (uint32_t k = 2; k <= P; k <<= 1) {
       for (uint32_t j = k >> 1; j > 0; j >>= 1) {
         for (uint32_t i = threadIdx.x; i < P; i += kBlock) {
           const uint32_t l = i ^ j;
           if (l > i) {
-            const uint2 u = sk[i], v = sk[l];
-            if ((u.y > v.y) == ((i & k) == 0)) {
+            const T u = sk[i], v = sk[l];
+            if ((seg_key(u) > seg_key(v)) == ((i & k) == 0)) {
               sk[i] = v;
               sk[l] = u;
             }
@@ -1505,7 +1516,7 @@ __device__ void sort_long_slice(const OrderArgs& o, uint32_t b, uint32_t len, ui
         __syncthreads();
       }
     }
-    uint2* dst = nch == 1 ? o.ev_out + b : tmp + b + c0;
+    T* dst = nch == 1 ? d : tmp + c0;
     for (uint32_t i = threadIdx.x; i < cl; i += kBlock) dst[i] = sk[i];
     __syncthreads();
   }
@@ -1513,31 +1524,87 @@ __device__ void sort_long_slice(const OrderArgs& o, uint32_t b, uint32_t len, ui
     __threadfence();
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < len; i += kBlock) {
-      const uint2 v = ld_cg(tmp + b + i);
+      const T v = ld_cg(tmp + i);
+      const uint32_t kv = seg_key(v);
       const uint32_t c = i / kBigChunk;
       uint32_t pos = i - c * kBigChunk;
       for (uint32_t c2 = 0; c2 < nch; ++c2) {
         if (c2 == c) continue;
-        const uint2* ch = tmp + b + c2 * kBigChunk;
+        const T* ch = tmp + c2 * kBigChunk;
         uint32_t lo = 0, hi = min(kBigChunk, len - c2 * kBigChunk);
         while (lo < hi) {  // earlier chunks: count keys <= v (ties before); later: keys < v
           const uint32_t mid = (lo + hi) >> 1;
-          const uint32_t ky = ld_cg(ch + mid).y;
-          if (c2 < c ? ky <= v.y : ky < v.y) lo = mid + 1;
+          const uint32_t ky = seg_key(ld_cg(ch + mid));
+          if (c2 < c ? ky <= kv : ky < kv) lo = mid + 1;
           else hi = mid;
         }
         pos += lo;
       }
-      o.ev_out[b + pos] = v;
+      d[pos] = v;
     }
     __syncthreads();
   }
 }
 
+// Segmented sort, one segment per thread of the block: segment [b, b + len) of d (len = 0: none).
+// Every thread of the block must call it. Short segments by their thread, medium by their wave,
+// long ones by the block; tmp mirrors d (scratch for segments longer than one LDS chunk).
+template <class T>
+__device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uint32_t len, T* sk, uint2* bigq,
+                         uint32_t* nbig) {
+  if (threadIdx.x == 0) *nbig = 0;
+  if (len >= 2u && len <= kSmallSlice) {
+    T v[kSmallSlice];
+#pragma unroll
+    for (uint32_t i = 0; i < kSmallSlice; ++i) v[i] = i < len ? d[b + i] : seg_pad<T>();
+#pragma unroll
+    for (uint32_t p = 0; p < kSmallSlice; ++p) {
+#pragma unroll
+      for (uint32_t i = p & 1u; i + 1 < kSmallSlice; i += 2) {
+        const T x = v[i], y = v[i + 1];
+        const bool sw = seg_key(x) > seg_key(y);  // strict: equal keys keep their order (stable)
+        v[i] = sw ? y : x;
+        v[i + 1] = sw ? x : y;
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kSmallSlice; ++i)
+      if (i < len) d[b + i] = v[i];
+  }
+  // medium segments: the wave, one at a time; each lane holds one element and counts the elements
+  // ordered before it (key, then position: stable)
+  const uint32_t lane = threadIdx.x & 63u;
+  for (unsigned long long mm = __ballot(len > kSmallSlice && len <= 64u); mm; mm &= mm - 1ull) {
+    const int src = __ffsll((long long)mm) - 1;
+    const uint32_t mb = __shfl(b, src, 64), ml = __shfl(len, src, 64);
+    const T v = lane < ml ? d[mb + lane] : seg_pad<T>();
+    const uint32_t kv = seg_key(v);
+    uint32_t pos = 0;
+    for (uint32_t j = 0; j < ml; ++j) {
+      const uint32_t kj = __shfl(kv, (int)j, 64);
+      pos += (kj < kv || (kj == kv && j < lane)) ? 1u : 0u;
+    }
+    if (lane < ml) d[mb + pos] = v;
+  }
+  // long segments: the whole block
+  __syncthreads();
+  if (len > 64u) bigq[atomicAdd(nbig, 1u)] = make_uint2(b, len);  // LDS atomic
+  __syncthreads();
+  const uint32_t nb = *nbig;
+  for (uint32_t q = 0; q < nb; ++q) {
+    const uint2 sg = bigq[q];
+    seg_sort_long(d + sg.x, tmp + sg.x, sg.y, sk);
+  }
+}
+
+struct SegSmem {
+  uint2 bigq[kBlock];
+  uint32_t nbig;
+};
+
 __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
   __shared__ uint2 sk[kBigChunk];
-  __shared__ uint32_t bigq[kBlock];
-  __shared__ uint32_t nbig;
+  __shared__ SegSmem ss;
   const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
   const bool op = r < o.n_ops && !(o.n_dev && r >= *o.n_dev);
   if (op && o.check_ops) {
@@ -1546,49 +1613,9 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
   }
   uint32_t slots, n;
   if (!ev_fits(o.g, &slots, &n)) return;  // grid-uniform
-  if (threadIdx.x == 0) nbig = 0;
   const uint32_t b = op ? o.rank_off[r] : 0u, len = op ? o.rank_off[r + 1] - b : 0u;
-  if (len >= 2u && len <= kSmallSlice) {
-    uint2 v[kSmallSlice];
-#pragma unroll
-    for (uint32_t i = 0; i < kSmallSlice; ++i) v[i] = i < len ? o.ev_out[b + i] : make_uint2(0u, 0xffffffffu);
-#pragma unroll
-    for (uint32_t p = 0; p < kSmallSlice; ++p) {
-#pragma unroll
-      for (uint32_t i = p & 1u; i + 1 < kSmallSlice; i += 2) {
-        const uint2 x = v[i], y = v[i + 1];
-        const bool sw = x.y > y.y;  // strict: equal keys keep their order (stable)
-        v[i] = sw ? y : x;
-        v[i + 1] = sw ? x : y;
-      }
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < kSmallSlice; ++i)
-      if (i < len) o.ev_out[b + i] = v[i];
-  }
-  // medium slices: the op's wave, one slice at a time
-  const uint32_t lane = threadIdx.x & 63u;
-  for (unsigned long long mm = __ballot(len > kSmallSlice && len <= 64u); mm; mm &= mm - 1ull) {
-    const int src = __ffsll((long long)mm) - 1;
-    const uint32_t mb = __shfl(b, src, 64), ml = __shfl(len, src, 64);
-    const uint2 v = lane < ml ? o.ev_out[mb + lane] : make_uint2(0u, 0xffffffffu);
-    uint32_t pos = 0;
-    for (uint32_t j = 0; j < ml; ++j) {
-      const uint32_t kj = __shfl(v.y, (int)j, 64);
-      pos += (kj < v.y || (kj == v.y && j < lane)) ? 1u : 0u;
-    }
-    if (lane < ml) o.ev_out[mb + pos] = v;
-  }
-  // long slices: the whole block
-  __syncthreads();
-  if (len > 64u) bigq[atomicAdd(&nbig, 1u)] = r;  // LDS atomic
-  __syncthreads();
-  const uint32_t nb = nbig;
-  for (uint32_t q = 0; q < nb; ++q) {
-    const uint32_t rq = bigq[q];
-    const uint32_t bq = o.rank_off[rq];
-    sort_long_slice(o, bq, o.rank_off[rq + 1] - bq, sk);
-  }
+  // ev_tmp is free once k_place has run; its uint2 view has 2 x slots >= n entries
+  seg_sort(o.ev_out, reinterpret_cast<uint2*>(const_cast<uint4*>(o.ev_tmp)), b, len, sk, ss.bigq, &ss.nbig);
 }
 
 // Deliver the ordered events to mapped pinned host memory (GPU-initiated PCIe writes), so the host
@@ -1662,24 +1689,18 @@ void launch_relation(const RelArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_relation, dim3((a.cap + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
 }
 
+// neighbours of each row in ascending slot order (the segmented sort of k_slice_sort)
 __global__ void __launch_bounds__(kBlock) k_row_sort(const uint32_t* __restrict__ row_ptr, uint32_t cap,
-                                                     uint32_t* __restrict__ cols) {
+                                                     uint32_t* __restrict__ cols, uint32_t* __restrict__ tmp) {
+  __shared__ uint32_t sk[kBigChunk];
+  __shared__ SegSmem ss;
   const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-  if (s >= cap) return;
-  const uint32_t b = row_ptr[s], e = row_ptr[s + 1];
-  for (uint32_t i = b + 1; i < e; ++i) {
-    const uint32_t v = cols[i];
-    uint32_t k = i;
-    while (k > b && cols[k - 1] > v) {
-      cols[k] = cols[k - 1];
-      --k;
-    }
-    cols[k] = v;
-  }
+  const uint32_t b = s < cap ? row_ptr[s] : 0u, len = s < cap ? row_ptr[s + 1] - b : 0u;
+  seg_sort(cols, tmp, b, len, sk, ss.bigq, &ss.nbig);
 }
 
-void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, hipStream_t st) {
-  hipLaunchKernelGGL(k_row_sort, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, st, row_ptr, cap, cols);
+void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, uint32_t* tmp, hipStream_t st) {
+  hipLaunchKernelGGL(k_row_sort, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, st, row_ptr, cap, cols, tmp);
 }
 
 // ---------------------------------------------------------------------------------------------

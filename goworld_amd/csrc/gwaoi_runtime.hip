@@ -144,6 +144,9 @@ struct gwaoi_mgr {
   uint32_t *seq = nullptr, *space_of = nullptr, *old_seq = nullptr, *opq = nullptr;
   uint32_t *key_of = nullptr, *local_of = nullptr;
   uint32_t *d_op_slot = nullptr, *d_op_space = nullptr, *d_leaves = nullptr, *d_dense = nullptr;
+  // relation view (gwaoi_relation_device): CSR in HBM, allocated on first use, grown on demand
+  uint32_t *rel_rp = nullptr, *rel_cols = nullptr, *rel_tmp = nullptr;
+  uint64_t rel_cap = 0;
   float *d_op_x = nullptr, *d_op_z = nullptr;
   uint8_t* d_op_kind = nullptr;
   Grid grid[2];
@@ -735,7 +738,8 @@ void free_all(gwaoi_mgr* m) {
   m->sync = nullptr;
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
-                   m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out};
+                   m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out,
+                   m->rel_rp, m->rel_cols, m->rel_tmp};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
@@ -1156,10 +1160,10 @@ int gwaoi_count(const gwaoi_mgr* m, uint32_t* n_present, uint32_t* n_staged) {
   return GWAOI_OK;
 }
 
-int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint64_t cols_cap, uint64_t* nnz) {
+int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   RCHK(check_mgr(m));
-  if (!row_ptr || !nnz || (cols_cap && !cols)) {
-    set_err("export_relation: null argument");
+  if (!out) {
+    set_err("relation_device: null argument");
     return GWAOI_ERR_INVALID;
   }
   RCHK(set_dev(m));
@@ -1169,9 +1173,8 @@ int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint6
     reset_tick(m);
   }
   hipStream_t st = m->stream;
+  if (!m->rel_rp) RCHK(dalloc(&m->rel_rp, (size_t)m->cap + 1));
   const Grid& g = m->grid[m->cur];
-  uint32_t* d_rp = nullptr;
-  RCHK(dalloc(&d_rp, (size_t)m->cap + 1));
   gw::RelArgs a;
   a.g = {g.rec, g.cs, g.d_geom, g.d_tile_space};
   a.pos_x = m->pos_x;
@@ -1180,41 +1183,54 @@ int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint6
   a.space_of = m->space_of;
   a.cap = m->cap;
   a.row_ptr = nullptr;
-  a.row_cnt = d_rp;
+  a.row_cnt = m->rel_rp;
   a.cols = nullptr;
-  hipError_t e = hipMemsetAsync(d_rp + m->cap, 0, sizeof(uint32_t), st);
+  // count pass, scan, then the row lengths' total is the one value the host must know (allocation)
+  HIPCHK(hipMemsetAsync(m->rel_rp + m->cap, 0, sizeof(uint32_t), st));
   gw::launch_relation(a, st);
-  gw::launch_scan(m->scan, d_rp, m->cap + 1, st);
+  gw::launch_scan(m->scan, m->rel_rp, m->cap + 1, st);
   uint32_t total = 0;
-  if (e == hipSuccess) e = hipMemcpyAsync(&total, d_rp + m->cap, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) {
-    hipFree(d_rp);
-    set_err("export_relation: %s", hipGetErrorString(e));
-    return GWAOI_ERR_HIP;
+  HIPCHK(hipMemcpyAsync(&total, m->rel_rp + m->cap, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (total > m->rel_cap) {
+    if (m->rel_cols) hipFree(m->rel_cols);
+    if (m->rel_tmp) hipFree(m->rel_tmp);
+    m->rel_cols = m->rel_tmp = nullptr;
+    m->rel_cap = 0;
+    const uint64_t want = (uint64_t)total + total / 4 + 1024;
+    RCHK(dalloc(&m->rel_cols, want));
+    RCHK(dalloc(&m->rel_tmp, want));
+    m->rel_cap = want;
   }
-  *nnz = total;
-  if (total > cols_cap) {
-    hipFree(d_rp);
-    set_err("export_relation: cols_cap %llu < nnz %u", (unsigned long long)cols_cap, total);
+  a.row_ptr = m->rel_rp;
+  a.cols = m->rel_cols;
+  gw::launch_relation(a, st);
+  gw::launch_row_sort(m->rel_rp, m->cap, m->rel_cols, m->rel_tmp, st);
+  HIPCHK(hipGetLastError());
+  out->row_ptr = m->rel_rp;
+  out->cols = m->rel_cols;
+  out->nnz = total;
+  return GWAOI_OK;
+}
+
+int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint64_t cols_cap, uint64_t* nnz) {
+  RCHK(check_mgr(m));
+  if (!row_ptr || !nnz || (cols_cap && !cols)) {
+    set_err("export_relation: null argument");
     return GWAOI_ERR_INVALID;
   }
-  uint32_t* d_cols = nullptr;
-  int r = dalloc(&d_cols, std::max<uint32_t>(total, 1));
-  if (r) {
-    hipFree(d_rp);
-    return r;
+  gwaoi_relation_view v;
+  RCHK(gwaoi_relation_device(m, &v));
+  *nnz = v.nnz;
+  if (v.nnz > cols_cap) {
+    set_err("export_relation: cols_cap %llu < nnz %llu", (unsigned long long)cols_cap, (unsigned long long)v.nnz);
+    return GWAOI_ERR_INVALID;
   }
-  a.row_ptr = d_rp;
-  a.cols = d_cols;
-  gw::launch_relation(a, st);
-  gw::launch_row_sort(d_rp, m->cap, d_cols, st);
-  e = hipMemcpyAsync(row_ptr, d_rp, ((size_t)m->cap + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess && total)
-    e = hipMemcpyAsync(cols, d_cols, (size_t)total * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+  hipStream_t st = m->stream;
+  hipError_t e = hipMemcpyAsync(row_ptr, v.row_ptr, ((size_t)m->cap + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && v.nnz)
+    e = hipMemcpyAsync(cols, v.cols, (size_t)v.nnz * sizeof(uint32_t), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  hipFree(d_rp);
-  hipFree(d_cols);
   if (e != hipSuccess) {
     set_err("export_relation: %s", hipGetErrorString(e));
     return GWAOI_ERR_HIP;

@@ -153,6 +153,13 @@ class Engine:
                 continue
             check(rc)
 
+    def relation_device(self):
+        """Device-resident CSR view of the relation: (row_ptr device address, cols device address, nnz),
+        manager-owned, valid until the next pass (gwaoi_relation_device)."""
+        v = _lib.RelationView()
+        check(self._L.gwaoi_relation_device(self._h, ctypes.byref(v)))
+        return v.row_ptr, v.cols, int(v.nnz)
+
     # ---- timing ----
     def set_timing(self, on: bool = True):
         check(self._L.gwaoi_set_timing(self._h, 1 if on else 0))

@@ -149,6 +149,18 @@ int gwaoi_count(const gwaoi_mgr* mgr, uint32_t* n_present, uint32_t* n_staged);
 int gwaoi_export_relation(gwaoi_mgr* mgr, uint32_t* row_ptr, uint32_t* cols, uint64_t cols_cap,
                           uint64_t* nnz);
 
+/* The same relation as a device-resident CSR view (the replay sink's neighbour sets,
+ * Entity.InterestedIn / InterestedBy, Entity.go:53-54,236-246, which under the XZ manager are one
+ * symmetric set per entity). row_ptr[capacity + 1] and cols[nnz] are HBM buffers owned by the manager
+ * (rows in ascending slot order), built on the manager's stream and valid until the next call that
+ * runs a pass. Pending ops are flushed first, as in gwaoi_export_relation. */
+typedef struct {
+  const uint32_t* row_ptr;
+  const uint32_t* cols;
+  uint64_t nnz;
+} gwaoi_relation_view;
+int gwaoi_relation_device(gwaoi_mgr* mgr, gwaoi_relation_view* out);
+
 /* Per-stage device time of the pipeline, accumulated over ticks while timing is enabled (hipEvents on
  * the manager's stream). */
 typedef struct {

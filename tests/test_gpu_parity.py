@@ -471,8 +471,9 @@ def test_device_counted_batch(gpu, po):
 def test_long_event_slices(gpu, po):
     """A crowd of 5,000 inside one AOI box: the i-th Enter raises i events, so per-op event slices run
     from 0 to 4,999 and the canonical ordering takes every path (insertion sort for short slices, one
-    LDS bitonic chunk, and several chunks merged by rank past 4,096); a Leave and a teleport out of the
-    crowd then raise 4,999 each. Bit-exact against oracle (i)."""
+    LDS bitonic chunk, and several chunks merged by rank past 2,048); a Leave and a teleport out of the
+    crowd then raise 4,999 each. Bit-exact against oracle (i), the relation (rows of 4,999 neighbours)
+    too."""
     rng = np.random.default_rng(0x511CE)
     n = 5000
     x = rng.uniform(0.0, 90.0, n).astype(np.float32)
@@ -482,5 +483,7 @@ def test_long_event_slices(gpu, po):
         [(H.LEAVE, 17, 0.0, 0.0), (H.MOVE, 3, 400.0, 400.0), (H.MOVE, 9, float(x[9]) + 0.5, float(z[9]))],
         [(H.MOVE, 3, float(x[3]), float(z[3])), (H.ENTER, 17, 45.0, 45.0)],
     ]}
-    eng, _ = run_against_oracle(po, case, check_relation_every=0)
+    eng, _ = run_against_oracle(po, case, check_relation_every=1)  # rows of 4,999: chunked row sort
+    rp_dev, cols_dev, nnz = eng.relation_device()
+    assert rp_dev and cols_dev and nnz == len(eng.relation()[1])
     eng.close()
