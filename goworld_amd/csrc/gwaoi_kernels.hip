@@ -1654,26 +1654,29 @@ void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_
 // ---------------------------------------------------------------------------------------------
 // Relation export: row s = {o : N(s,o)} = {o : in(L, F)}, L = later actor, over the END-of-pass
 // state (main records only). Count pass (row_ptr null) then fill pass; rows sorted afterwards.
+// One thread per MAIN record of the last pass's grid (its current state: binned = current position,
+// b.w = current seq), in grid order, so the lanes of a wave walk overlapping boxes of neighbouring
+// cells and their candidate gathers share cache lines (slot order would scatter them). The pair test
+// is the reference's from the perspective of whichever member acted last (N(a,b) = in(L, F)).
 __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
-  const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
-  if (s >= a.cap) return;
-  const uint32_t qs = a.seq[s];
-  if (!qs) {
-    if (!a.row_ptr) a.row_cnt[s] = 0;
-    return;
-  }
+  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= *a.n_rec) return;
+  const uint4 ma = a.g.rec[j].a;
+  if (ma.z & REC_GHOST) return;
+  const uint32_t s = ma.z & REC_SLOT;
+  const uint32_t qs = a.g.rec[j].b.w;
   const Geom g = a.g.geom[a.space_of[s]];
-  const float sx = a.pos_x[s], sz = a.pos_z[s];
+  const float sx = __uint_as_float(ma.x), sz = __uint_as_float(ma.y);
   const float D = g.D;
   const CellBox B = qbox(g, sx, sz);
   uint32_t n = 0;
   uint32_t w = a.row_ptr ? a.row_ptr[s] : 0u;
   for (int r = B.z0; r <= B.z1; ++r) {
-    row_entries_global(g, a.g.cs, r, B.x0, B.x1, [&](uint32_t j) {
-      const uint4 ra = a.g.rec[j].a;
+    row_entries_global(g, a.g.cs, r, B.x0, B.x1, [&](uint32_t k) {
+      const uint4 ra = a.g.rec[k].a;
       const uint32_t o = ra.z & REC_SLOT;
       if ((ra.z & REC_GHOST) || o == s) return;
-      const uint32_t qo = a.g.rec[j].b.w;  // end-of-pass seq
+      const uint32_t qo = a.g.rec[k].b.w;  // end-of-pass seq
       const float ox = __uint_as_float(ra.x), oz = __uint_as_float(ra.y);
       const bool in = (qo > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz);
       if (in) {
@@ -1686,7 +1689,8 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
 }
 
 void launch_relation(const RelArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_relation, dim3((a.cap + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+  if (a.rec_bound)
+    hipLaunchKernelGGL(k_relation, dim3((a.rec_bound + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
 }
 
 // neighbours of each row in ascending slot order (the segmented sort of k_slice_sort)
