@@ -191,10 +191,17 @@ __device__ __forceinline__ void client_neighbours(const FanArgs& a, uint32_t s, 
 // global table. Same per-record outputs as k_fan (count, pairs in walk order, info, flag clear).
 constexpr int kFanRegCells = kSweepRegCells;
 constexpr int kFanLdsPairs = 4096;  // 32 KB: a round of 256 entities at ~16 pairs each
+constexpr int kFanLdsRecs = 896;    // 14 KB of staged sub-grid records (a uniform region holds ~200); keeps
+                                    // the write pass at 3 blocks per CU
+constexpr int kFanCellsPerThread = (kFanRegCells + kSy - 1) / kSy;
 template <bool kWrite>
 __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
-  __shared__ uint32_t lst[kFanRegCells], len_[kFanRegCells];
+  // The region's sub-grid records are copied into LDS in row-major cell order, so one row of a box is
+  // ONE contiguous LDS range: cst[i] = first staged record of region cell i (cst[W * Hh] = total).
+  __shared__ uint16_t cst[kFanRegCells + 1];
+  __shared__ uint4 crl[kFanLdsRecs];  // {x, z, seq_end, sub-grid index}
   __shared__ uint32_t red[kSy / 64];
+  __shared__ uint32_t tot_sh;
   __shared__ uint2 lpairs[kWrite ? kFanLdsPairs : 1];
   const uint32_t t = blockIdx.x;
   const uint32_t sp = a.g.tile_space[t];
@@ -208,13 +215,40 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
   const int cx0 = max(tx * kTile - R, 0), cx1 = min(tx * kTile + kTile - 1 + R, g.ncx - 1);
   const int cz0 = max(tz * kTile - R, 0), cz1 = min(tz * kTile + kTile - 1 + R, g.ncz - 1);
   const int W = cx1 - cx0 + 1, Hh = cz1 - cz0 + 1;
-  const bool lds = R > 0 && W * Hh <= kFanRegCells;
+  const int ncell = W * Hh;
+  bool lds = R > 0 && ncell <= kFanRegCells;  // block-uniform
   if (lds) {
-    for (int i = threadIdx.x; i < W * Hh; i += kSy) {
-      const int cx = cx0 + i % W, cz = cz0 + i / W;
-      const uint32_t k = cell_key(g, cx, cz);
-      lst[i] = a.ccs[k];
-      len_[i] = a.ccs[k + 1];
+    // per-thread chunk of consecutive region cells -> block exclusive scan of their record counts
+    const int c0 = threadIdx.x * kFanCellsPerThread, c1 = min(c0 + kFanCellsPerThread, ncell);
+    uint32_t sum = 0;
+    for (int i = c0; i < c1; ++i) {
+      const uint32_t k = cell_key(g, cx0 + i % W, cz0 + i / W);
+      sum += a.ccs[k + 1] - a.ccs[k];
+    }
+    const int lane = threadIdx.x & 63;
+    uint32_t inc = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) red[threadIdx.x >> 6] = inc;
+    __syncthreads();
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) inc += red[w];
+    if (threadIdx.x == kSy - 1) tot_sh = inc;
+    __syncthreads();
+    const uint32_t tot = tot_sh;
+    lds = tot <= (uint32_t)kFanLdsRecs;
+    if (lds) {
+      uint32_t p = inc - sum;
+      for (int i = c0; i < c1; ++i) {
+        const uint32_t k = cell_key(g, cx0 + i % W, cz0 + i / W);
+        cst[i] = (uint16_t)p;
+        for (uint32_t q = a.ccs[k], e = a.ccs[k + 1]; q < e; ++q, ++p) {
+          const uint4 c = a.crec[q];
+          crl[p] = make_uint4(c.x, c.y, c.z, q);
+        }
+      }
+      if (threadIdx.x == 0) cst[ncell] = (uint16_t)tot;
     }
   }
   __syncthreads();
@@ -248,22 +282,19 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
         const CellBox B = qbox(g, sx, sz);
         if (lds && B.x0 >= cx0 && B.x1 <= cx1 && B.z0 >= cz0 && B.z1 <= cz1) {
           const float D = g.D;
+          // the entity's own sub-grid record (only an entity with a client has one)
+          const uint32_t selfq = gs != GWAOI_SYNC_NO_CLIENT ? a.cpos[j] : 0xffffffffu;
           for (int r = B.z0; r <= B.z1; ++r) {
             const int rb = (r - cz0) * W - cx0;
-            // the row's cells split at tile boundaries into contiguous key ranges
-            for (int lo = B.x0; lo <= B.x1;) {
-              const int hi = min(B.x1, (lo | (kTile - 1)));
-              const uint32_t e = len_[rb + hi];
-              for (uint32_t q = lst[rb + lo]; q < e; ++q) {
-                const uint4 cr = a.crec[q];
-                const float ox = __uint_as_float(cr.x), oz = __uint_as_float(cr.y);
-                const bool in = cr.w != s && ((cr.z > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz));
-                if (in) {
-                  if (kWrite) put(w++, make_uint2(j, q));
-                  ++c;
-                }
+            const uint32_t e = cst[rb + B.x1 + 1];
+            for (uint32_t p = cst[rb + B.x0]; p < e; ++p) {
+              const uint4 cr = crl[p];
+              const float ox = __uint_as_float(cr.x), oz = __uint_as_float(cr.y);
+              const bool in = cr.w != selfq && ((cr.z > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz));
+              if (in) {
+                if (kWrite) put(w++, make_uint2(j, cr.w));
+                ++c;
               }
-              lo = hi + 1;
             }
           }
         } else {
