@@ -64,4 +64,45 @@ __device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t
   }
 }
 
+// Stage the records of a tile's region (cells [cx0, cx0 + W) x [cz0, cz0 + ncell / W), row-major) into
+// LDS in row-major cell order, so the cells [x0, x1] of region row r are ONE contiguous LDS range
+// [cst[r W + x0], cst[r W + x1 + 1]). load(q) gives the staged form of global record q. Every thread of
+// the block calls it; it ends with a barrier. Returns false (block-uniform, nothing staged) when the
+// region holds more than `cap` records. red: kThreads / 64 words of LDS scratch.
+template <int kThreads, int kMaxCells, class Load>
+__device__ bool stage_region(const Geom& g, const uint32_t* __restrict__ cs, int cx0, int cz0, int W, int ncell,
+                             uint16_t* cst, uint4* out, uint32_t cap, uint32_t* red, uint32_t* tot_sh, Load&& load) {
+  constexpr int kPer = (kMaxCells + kThreads - 1) / kThreads;
+  const int c0 = threadIdx.x * kPer, c1 = min(c0 + kPer, ncell);
+  uint32_t sum = 0;
+  for (int i = c0; i < c1; ++i) {
+    const uint32_t k = cell_key(g, cx0 + i % W, cz0 + i / W);
+    sum += cs[k + 1] - cs[k];
+  }
+  const int lane = threadIdx.x & 63;
+  uint32_t inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) red[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) inc += red[w];
+  if (threadIdx.x == kThreads - 1) *tot_sh = inc;
+  __syncthreads();
+  const uint32_t tot = *tot_sh;
+  const bool fits = tot <= cap;
+  if (fits) {
+    uint32_t p = inc - sum;
+    for (int i = c0; i < c1; ++i) {
+      const uint32_t k = cell_key(g, cx0 + i % W, cz0 + i / W);
+      cst[i] = (uint16_t)p;
+      for (uint32_t q = cs[k], e = cs[k + 1]; q < e; ++q, ++p) out[p] = load(q);
+    }
+    if (threadIdx.x == 0) cst[ncell] = (uint16_t)tot;
+  }
+  __syncthreads();
+  return fits;
+}
+
 }  // namespace gw

@@ -162,8 +162,7 @@ struct RelArgs {
   const uint32_t* row_ptr;  // null in the count pass
   uint32_t* row_cnt;        // count pass output (zeroed beforehand: absent slots have no record)
   uint32_t* cols;
-  const uint32_t* n_rec;    // records of the grid (cs[ncells])
-  uint32_t rec_bound;       // host upper bound on them (launch size)
+  uint32_t ntiles;          // tiles of the grid (one block each)
 };
 
 // Scan scratch (the chunk sums of launch_scan), owned by the stream's manager.

@@ -1654,53 +1654,120 @@ void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_
 // ---------------------------------------------------------------------------------------------
 // Relation export: row s = {o : N(s,o)} = {o : in(L, F)}, L = later actor, over the END-of-pass
 // state (main records only). Count pass (row_ptr null) then fill pass; rows sorted afterwards.
-// One thread per MAIN record of the last pass's grid (its current state: binned = current position,
-// b.w = current seq), in grid order, so the lanes of a wave walk overlapping boxes of neighbouring
-// cells and their candidate gathers share cache lines (slot order would scatter them). The pair test
-// is the reference's from the perspective of whichever member acted last (N(a,b) = in(L, F)).
+// One block per grid tile: the records of the tile plus a halo of `reach` cells are staged in LDS in
+// row-major cell order (stage_region), so a box row is one contiguous LDS range; the block's threads
+// take the tile's main records (binned = current position, b.w = current seq) in grid order. A box
+// that leaves the region, or a region over the LDS budget (crowds), walks the global grid. The pair
+// test is the reference's from the perspective of whichever member acted last (N(a,b) = in(L, F)).
+constexpr int kRelLdsRecs = 1536;  // 24 KB (a config-2 region holds ~850 records)
 __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
-  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= *a.n_rec) return;
-  const uint4 ma = a.g.rec[j].a;
-  if (ma.z & REC_GHOST) return;
-  const uint32_t s = ma.z & REC_SLOT;
-  const uint32_t qs = a.g.rec[j].b.w;
-  const Geom g = a.g.geom[a.space_of[s]];
-  const float sx = __uint_as_float(ma.x), sz = __uint_as_float(ma.y);
+  __shared__ uint16_t cst[kSweepRegCells + 1];
+  __shared__ uint4 rl[kRelLdsRecs];  // {x, z, seq_end, slot | flags}
+  __shared__ uint32_t red[kBlock / 64];
+  __shared__ uint32_t tot_sh;
+  const uint32_t t = blockIdx.x;
+  const Geom g = a.g.geom[a.g.tile_space[t]];
+  const int lt = (int)(t - g.tile_base);
+  const int tx = lt % g.ntx, tz = lt / g.ntx;
+  const uint32_t k0 = g.base + ((uint32_t)lt << kTileCellShift);
+  const uint32_t j0 = a.g.cs[k0], j1 = a.g.cs[k0 + kTileCells];
+  if (j0 == j1) return;
+  const int R = g.reach;
+  const int cx0 = max(tx * kTile - R, 0), cx1 = min(tx * kTile + kTile - 1 + R, g.ncx - 1);
+  const int cz0 = max(tz * kTile - R, 0), cz1 = min(tz * kTile + kTile - 1 + R, g.ncz - 1);
+  const int W = cx1 - cx0 + 1, ncell = W * (cz1 - cz0 + 1);
+  const bool lds = R > 0 && ncell <= kSweepRegCells &&
+                   stage_region<kBlock, kSweepRegCells>(g, a.g.cs, cx0, cz0, W, ncell, cst, rl, kRelLdsRecs, red,
+                                                        &tot_sh, [&](uint32_t q) {
+                                                          const Rec r = a.g.rec[q];
+                                                          return make_uint4(r.a.x, r.a.y, r.b.w, r.a.z);
+                                                        });
   const float D = g.D;
-  const CellBox B = qbox(g, sx, sz);
-  uint32_t n = 0;
-  uint32_t w = a.row_ptr ? a.row_ptr[s] : 0u;
-  for (int r = B.z0; r <= B.z1; ++r) {
-    row_entries_global(g, a.g.cs, r, B.x0, B.x1, [&](uint32_t k) {
-      const uint4 ra = a.g.rec[k].a;
-      const uint32_t o = ra.z & REC_SLOT;
-      if ((ra.z & REC_GHOST) || o == s) return;
-      const uint32_t qo = a.g.rec[k].b.w;  // end-of-pass seq
-      const float ox = __uint_as_float(ra.x), oz = __uint_as_float(ra.y);
+  for (uint32_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
+    const uint4 ma = a.g.rec[j].a;
+    if (ma.z & REC_GHOST) continue;
+    const uint32_t s = ma.z & REC_SLOT;
+    const uint32_t qs = a.g.rec[j].b.w;
+    const float sx = __uint_as_float(ma.x), sz = __uint_as_float(ma.y);
+    const CellBox B = qbox(g, sx, sz);
+    uint32_t n = 0;
+    uint32_t w = a.row_ptr ? a.row_ptr[s] : 0u;
+    auto judge = [&](uint32_t rz, uint32_t qo, float ox, float oz) {
+      const uint32_t o = rz & REC_SLOT;
+      if ((rz & REC_GHOST) || o == s) return;
       const bool in = (qo > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz);
       if (in) {
         if (a.row_ptr) a.cols[w++] = o;
         ++n;
       }
-    });
+    };
+    if (lds && B.x0 >= cx0 && B.x1 <= cx1 && B.z0 >= cz0 && B.z1 <= cz1) {
+      for (int r = B.z0; r <= B.z1; ++r) {
+        const int rb = (r - cz0) * W - cx0;
+        const uint32_t e = cst[rb + B.x1 + 1];
+        for (uint32_t p = cst[rb + B.x0]; p < e; ++p) {
+          const uint4 c = rl[p];
+          judge(c.w, c.z, __uint_as_float(c.x), __uint_as_float(c.y));
+        }
+      }
+    } else {
+      for (int r = B.z0; r <= B.z1; ++r) {
+        row_entries_global(g, a.g.cs, r, B.x0, B.x1, [&](uint32_t k) {
+          const uint4 ra = a.g.rec[k].a;
+          judge(ra.z, a.g.rec[k].b.w, __uint_as_float(ra.x), __uint_as_float(ra.y));
+        });
+      }
+    }
+    if (!a.row_ptr) a.row_cnt[s] = n;
   }
-  if (!a.row_ptr) a.row_cnt[s] = n;
 }
 
 void launch_relation(const RelArgs& a, hipStream_t st) {
-  if (a.rec_bound)
-    hipLaunchKernelGGL(k_relation, dim3((a.rec_bound + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+  if (a.ntiles) hipLaunchKernelGGL(k_relation, dim3(a.ntiles), dim3(kBlock), 0, st, a);
 }
 
-// neighbours of each row in ascending slot order (the segmented sort of k_slice_sort)
+// Neighbours of each row in ascending slot order. One block = 256 consecutive rows, whose entries are
+// ONE contiguous range of cols: staged in LDS with coalesced loads, then every entry is ranked inside
+// its row by a scan of the row in LDS (lanes of one row read the same words: broadcasts) and stored at
+// its final place. Blocks whose range or longest row is too large take the segmented sort of
+// k_slice_sort (registers / wave / LDS bitonic chunks merged by rank).
+constexpr uint32_t kRowLds = 10240;     // 40 KB of staged entries (a 1M config-2 block holds ~8.3k)
+constexpr uint32_t kRowRankMax = 512;   // longest row ranked by the LDS scan (cost grows as len^2)
 __global__ void __launch_bounds__(kBlock) k_row_sort(const uint32_t* __restrict__ row_ptr, uint32_t cap,
                                                      uint32_t* __restrict__ cols, uint32_t* __restrict__ tmp) {
-  __shared__ uint32_t sk[kBigChunk];
+  __shared__ uint32_t v[kRowLds];  // also the fallback's bitonic chunk (kBigChunk <= kRowLds)
+  __shared__ uint8_t rid[kRowLds];  // row (thread) of each staged entry
+  __shared__ uint32_t ro[kBlock + 1];
   __shared__ SegSmem ss;
-  const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
+  static_assert(kBigChunk <= kRowLds && kBlock <= 256, "fallback chunk aliases v; row ids fit a byte");
+  const uint32_t s0 = blockIdx.x * kBlock, s = s0 + threadIdx.x;
   const uint32_t b = s < cap ? row_ptr[s] : 0u, len = s < cap ? row_ptr[s + 1] - b : 0u;
-  seg_sort(cols, tmp, b, len, sk, ss.bigq, &ss.nbig);
+  const uint32_t b0 = row_ptr[s0], e0 = row_ptr[min(s0 + (uint32_t)kBlock, cap)];
+  const uint32_t n = e0 - b0;
+  const bool long_row = __syncthreads_or(len > kRowRankMax) != 0;
+  if (n > kRowLds || long_row) {  // block-uniform
+    seg_sort(cols, tmp, b, len, v, ss.bigq, &ss.nbig);
+    return;
+  }
+  ro[threadIdx.x] = (s < cap ? b : e0) - b0;
+  if (threadIdx.x == 0) ro[kBlock] = n;
+  for (uint32_t i = 0; i < len; ++i) rid[b - b0 + i] = (uint8_t)threadIdx.x;
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) v[i] = cols[b0 + i];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+    const uint32_t r = rid[i];
+    const uint32_t rs = ro[r], re = ro[r + 1];
+    const uint32_t key = v[i];
+    // rank = entries ordered before this one (key, then position: stable); independent LDS reads,
+    // unrolled so several are in flight
+    uint32_t pos = rs;
+#pragma unroll 8
+    for (uint32_t j = rs; j < re; ++j) {
+      const uint32_t k = v[j];
+      pos += (k < key || (k == key && j < i)) ? 1u : 0u;
+    }
+    cols[b0 + pos] = key;
+  }
 }
 
 void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, uint32_t* tmp, hipStream_t st) {

@@ -1185,8 +1185,7 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   a.row_ptr = nullptr;
   a.row_cnt = m->rel_rp;
   a.cols = nullptr;
-  a.n_rec = g.cs + g.ncells;
-  a.rec_bound = g.ncells ? 2 * m->cap : 0u;  // main + ghost records at most
+  a.ntiles = g.ncells ? g.ntiles : 0u;
   // count pass, scan, then the row lengths' total is the one value the host must know (allocation)
   HIPCHK(hipMemsetAsync(m->rel_rp, 0, ((size_t)m->cap + 1) * sizeof(uint32_t), st));
   gw::launch_relation(a, st);

@@ -193,7 +193,6 @@ constexpr int kFanRegCells = kSweepRegCells;
 constexpr int kFanLdsPairs = 4096;  // 32 KB: a round of 256 entities at ~16 pairs each
 constexpr int kFanLdsRecs = 896;    // 14 KB of staged sub-grid records (a uniform region holds ~200); keeps
                                     // the write pass at 3 blocks per CU
-constexpr int kFanCellsPerThread = (kFanRegCells + kSy - 1) / kSy;
 template <bool kWrite>
 __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
   // The region's sub-grid records are copied into LDS in row-major cell order, so one row of a box is
@@ -216,42 +215,12 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
   const int cz0 = max(tz * kTile - R, 0), cz1 = min(tz * kTile + kTile - 1 + R, g.ncz - 1);
   const int W = cx1 - cx0 + 1, Hh = cz1 - cz0 + 1;
   const int ncell = W * Hh;
-  bool lds = R > 0 && ncell <= kFanRegCells;  // block-uniform
-  if (lds) {
-    // per-thread chunk of consecutive region cells -> block exclusive scan of their record counts
-    const int c0 = threadIdx.x * kFanCellsPerThread, c1 = min(c0 + kFanCellsPerThread, ncell);
-    uint32_t sum = 0;
-    for (int i = c0; i < c1; ++i) {
-      const uint32_t k = cell_key(g, cx0 + i % W, cz0 + i / W);
-      sum += a.ccs[k + 1] - a.ccs[k];
-    }
-    const int lane = threadIdx.x & 63;
-    uint32_t inc = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t v = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += v;
-    }
-    if (lane == 63) red[threadIdx.x >> 6] = inc;
-    __syncthreads();
-    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) inc += red[w];
-    if (threadIdx.x == kSy - 1) tot_sh = inc;
-    __syncthreads();
-    const uint32_t tot = tot_sh;
-    lds = tot <= (uint32_t)kFanLdsRecs;
-    if (lds) {
-      uint32_t p = inc - sum;
-      for (int i = c0; i < c1; ++i) {
-        const uint32_t k = cell_key(g, cx0 + i % W, cz0 + i / W);
-        cst[i] = (uint16_t)p;
-        for (uint32_t q = a.ccs[k], e = a.ccs[k + 1]; q < e; ++q, ++p) {
-          const uint4 c = a.crec[q];
-          crl[p] = make_uint4(c.x, c.y, c.z, q);
-        }
-      }
-      if (threadIdx.x == 0) cst[ncell] = (uint16_t)tot;
-    }
-  }
-  __syncthreads();
+  const bool lds = R > 0 && ncell <= kFanRegCells &&
+                   stage_region<kSy, kFanRegCells>(g, a.ccs, cx0, cz0, W, ncell, cst, crl, kFanLdsRecs, red, &tot_sh,
+                                                   [&](uint32_t q) {
+                                                     const uint4 c = a.crec[q];
+                                                     return make_uint4(c.x, c.y, c.z, q);
+                                                   });
   uint32_t ents = 0;
   // one record: count (and, in the write pass, emit) its pairs through `put`
   auto visit = [&](uint32_t j, auto&& put) {
