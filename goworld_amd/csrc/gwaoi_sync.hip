@@ -345,9 +345,18 @@ __global__ void __launch_bounds__(kSy) k_gate_hist(GateArgs a) {
 
 // Stable partition of one chunk by gate: rounds of 256 pairs; inside a wave, lanes of the same gate
 // are found with one ballot per gate bit; across the block's 4 waves, per-wave gate counts in LDS.
+// A round's records are staged in LDS in partition order (its records of one gate are one run, and
+// land in one contiguous output range), then copied out 16 B per lane over consecutive addresses,
+// so the stores cover whole lines instead of one 48-B record per lane.
 __global__ void __launch_bounds__(kSy) k_gate_scatter(GateArgs a) {
   __shared__ uint32_t run[GWAOI_SYNC_MAX_GATES];         // pairs of each gate placed by earlier rounds
   __shared__ uint32_t wc[kSy / 64][GWAOI_SYNC_MAX_GATES];  // this round: pairs of each gate per wave
+  __shared__ uint32_t gst[GWAOI_SYNC_MAX_GATES];         // this round: first staged record of each gate
+  __shared__ uint32_t red[kSy / 64];
+  __shared__ uint32_t nlive_sh;
+  __shared__ uint4 lrec[3 * kSy];                          // staged records (3 x 16 B each)
+  __shared__ uint32_t lpos[kSy];                           // output record index of each staged record
+  static_assert(GWAOI_SYNC_MAX_GATES <= kSy, "one thread per gate in the round scan");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (uint32_t g = threadIdx.x; g < a.n_gates; g += kSy) {
     run[g] = a.ghist[g * a.nchunks + blockIdx.x];  // chunk's base in the gate-major output
@@ -370,22 +379,42 @@ __global__ void __launch_bounds__(kSy) k_gate_scatter(GateArgs a) {
     const bool leader = live && !(same & lt);
     if (leader) wc[w][g] = (uint32_t)__popcll(same);
     __syncthreads();
-    uint32_t pos = 0;
+    // exclusive scan of the round's per-gate totals (thread t = gate t)
+    uint32_t tot = 0;
+    if (threadIdx.x < a.n_gates) {
+#pragma unroll
+      for (int q = 0; q < kSy / 64; ++q) tot += wc[q][threadIdx.x];
+    }
+    uint32_t inc = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += v;
+    }
+    if (lane == 63) red[w] = inc;
+    __syncthreads();
+    for (int q = 0; q < w; ++q) inc += red[q];
+    if (threadIdx.x < a.n_gates) gst[threadIdx.x] = inc - tot;
+    if (threadIdx.x == kSy - 1) nlive_sh = inc;
+    __syncthreads();
     if (live) {
-      pos = run[g] + (uint32_t)__popcll(same & lt);
-      for (int q = 0; q < w; ++q) pos += wc[q][g];
+      // p = {grid record of the entity, sub-grid record of the receiver}
+      uint32_t r = (uint32_t)__popcll(same & lt);
+      for (int q = 0; q < w; ++q) r += wc[q][g];
+      const uint32_t li = gst[g] + r;
+      lpos[li] = run[g] + r;
+      lrec[3 * li] = a.ccid[p.y];
+      lrec[3 * li + 1] = a.info[2 * (size_t)p.x];
+      lrec[3 * li + 2] = a.info[2 * (size_t)p.x + 1];
     }
     __syncthreads();
     if (leader) {
-      atomicAdd(&run[g], (uint32_t)__popcll(same));
+      atomicAdd(&run[g], (uint32_t)__popcll(same));  // one leader per (wave, gate)
       wc[w][g] = 0;
     }
-    if (live) {
-      // p = {grid record of the entity, sub-grid record of the receiver}
-      uint4* o = a.out + (size_t)pos * 3;
-      o[0] = a.ccid[p.y];
-      o[1] = a.info[2 * (size_t)p.x];
-      o[2] = a.info[2 * (size_t)p.x + 1];
+    const uint32_t nq = 3 * nlive_sh;
+    for (uint32_t q = threadIdx.x; q < nq; q += kSy) {
+      const uint32_t li = q / 3;
+      a.out[(size_t)lpos[li] * 3 + (q - 3 * li)] = lrec[q];
     }
     __syncthreads();
   }
