@@ -39,7 +39,7 @@ TOOL_SYMBOLS = (
     "gwaoi_dev_sync", "gwaoi_wl_init", "gwaoi_wl_step", "gwaoi_wl_iota", "gwaoi_wl_init_spaces",
     "gwaoi_wl_step_spaces", "gwaoi_debug_set_next_seq",
     "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_cell_side", "gwaoi_debug_set_sweep_lds", "gwaoi_debug_read_stamps",
-    "gwaoi_debug_sweep_occupancy", "gwaoi_wl_pack_ingest",
+    "gwaoi_debug_sweep_occupancy", "gwaoi_wl_pack_ingest", "gwaoi_debug_set_index_limit",
 )
 
 
@@ -79,7 +79,7 @@ class SyncOut(ctypes.Structure):
 
 class IngestResult(ctypes.Structure):
     _fields_ = [("n_records", ctypes.c_uint32), ("n_moved", ctypes.c_uint32), ("n_unknown", ctypes.c_uint32),
-                ("n_rejected", ctypes.c_uint32), ("n_passes", ctypes.c_uint32)]
+                ("n_rejected", ctypes.c_uint32), ("n_passes", ctypes.c_uint32), ("n_nonfinite", ctypes.c_uint32)]
 
 
 class StripGeom(ctypes.Structure):
@@ -200,6 +200,7 @@ def load(path: str = SO_PATH):
         "gwaoi_debug_set_cell_side": ([vp, f32], ctypes.c_int),
         "gwaoi_debug_set_sweep_lds": ([vp, ctypes.c_int], ctypes.c_int),
         "gwaoi_debug_read_stamps": ([vp, ctypes.c_size_t], ctypes.c_int),
+        "gwaoi_debug_set_index_limit": ([vp, u64], ctypes.c_int),
         "gwaoi_strip_init_walk": ([vp, vp, vp, vp, vp, u64, f32], ctypes.c_int),
         "gwaoi_strip_walk": ([vp, vp, vp, vp, vp, vp, vp, u64, u64, f32, f32, vp], ctypes.c_int),
         "gwaoi_strip_ingest": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),

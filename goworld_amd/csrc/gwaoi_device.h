@@ -21,6 +21,16 @@ __device__ __forceinline__ int cellc(float v, float o, float inv, int n) {
   return (int)f;
 }
 
+// cellc for the UPPER bound of a range: a NaN bound (from an infinite coordinate; the ABI rejects
+// non-finite coordinates, so only a corrupted state gets here) widens to the last cell instead of
+// collapsing to cell 0, so a cell range is never narrower than the exact predicate needs.
+__device__ __forceinline__ int cellc_hi(float v, float o, float inv, int n) {
+  float f = (v - o) * inv;
+  if (!(f < (float)n)) return n - 1;
+  if (!(f >= 0.0f)) return 0;
+  return (int)f;
+}
+
 // in(c, p): p inside the box of an entity at c (go-aoi Mark/GetClearMarkedNeighbors bounds).
 __device__ __forceinline__ bool inbox(float cx, float cz, float D, float px, float pz) {
   const float lx = cx - D, hx = cx + D, lz = cz - D, hz = cz + D;
@@ -35,9 +45,9 @@ __device__ __forceinline__ CellBox qbox(const Geom& g, float cx, float cz) {
   const float mx = (fabsf(cx) + g.D) * kMargin, mz = (fabsf(cz) + g.D) * kMargin;
   CellBox b;
   b.x0 = cellc((cx - g.D) - mx, g.x0, g.inv_c, g.ncx);
-  b.x1 = cellc((cx + g.D) + mx, g.x0, g.inv_c, g.ncx);
+  b.x1 = cellc_hi((cx + g.D) + mx, g.x0, g.inv_c, g.ncx);
   b.z0 = cellc((cz - g.D) - mz, g.z0, g.inv_c, g.ncz);
-  b.z1 = cellc((cz + g.D) + mz, g.z0, g.inv_c, g.ncz);
+  b.z1 = cellc_hi((cz + g.D) + mz, g.z0, g.inv_c, g.ncz);
   return b;
 }
 

@@ -12,7 +12,10 @@ enum : uint8_t { OP_MOVE = 0, OP_ENTER = 1, OP_LEAVE = 2, OP_KIND = 3, OP_SILENT
 
 // Device-side error bits (device-staged batches are validated on the GPU).
 enum : uint32_t { ERR_DUP_SLOT = 1u, ERR_ABSENT_SLOT = 2u, ERR_BAD_SLOT = 4u, ERR_PRESENT_SLOT = 8u, ERR_BAD_SPACE = 16u,
-                  ERR_BAD_COUNT = 32u };
+                  ERR_BAD_COUNT = 32u, ERR_BAD_COORD = 64u };
+
+// IEEE binary32 bit test: not NaN, not +-Inf (the ABI rejects non-finite coordinates)
+__host__ __device__ __forceinline__ bool finite_bits(uint32_t b) { return (b & 0x7f800000u) != 0x7f800000u; }
 
 // Counters block in device memory.
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
@@ -119,6 +122,8 @@ struct BinArgs {
   uint32_t* thist;            // [ntiles * nblk + 1]
   const uint32_t* tile_space;  // tile -> space
   Rec* trec;                  // records bucketed by tile (the other grid's buffer: unused this pass)
+  const uint8_t* op_kind;     // the pass's op kinds (null: all moves), for tile_walk
+  uint32_t* tile_walk;        // [ntiles] out: 1 = the tile holds a reported mover (k_sweep skips the rest)
 };
 // Slots per block of the tile-bucketed build, and the largest tile count its LDS histogram holds
 // (larger grids use the cell-atomic build).
@@ -131,6 +136,9 @@ struct SweepArgs {
   const float* old_z;
   const uint32_t* old_seq;
   const uint32_t* space_of;
+  const float* pos_x;  // current (end-of-pass) state: movers of the dense list (slots)
+  const float* pos_z;
+  const uint32_t* opq;
   uint32_t base;       // seq of op 0 of this pass
   uint32_t n_ops;
   uint32_t n_rec;      // upper bound on records in the grid (flat variant grid size)
@@ -147,9 +155,10 @@ struct SweepArgs {
   uint32_t ev_cap;
   uint32_t* rank_cnt;
   uint32_t* ctr;
-  uint32_t* dense;      // grid indices of movers for k_sweep_dense (boxes beyond the tile's LDS region)
+  uint32_t* dense;      // slots of movers for k_sweep_dense (boxes beyond the tile's LDS region)
   uint32_t dense_cap;
   uint32_t dense_hint;  // dense movers of the previous pass (0: launch k_sweep_dense small)
+  const uint32_t* tile_walk;  // per tile: holds a reported mover (null: k_sweep scans the tile's records)
 };
 
 struct RelArgs {
@@ -163,6 +172,7 @@ struct RelArgs {
   uint32_t* row_cnt;        // count pass output (zeroed beforehand: absent slots have no record)
   uint32_t* cols;
   uint32_t ntiles;          // tiles of the grid (one block each)
+  unsigned long long* total64;  // count pass: sum of the row lengths in 64 bits (uint32 overflow guard)
 };
 
 // Scan scratch (the chunk sums of launch_scan), owned by the stream's manager.
@@ -243,6 +253,7 @@ struct MgrView {
   ScanCtx* scan;
   SyncState** sync;          // the manager's sync state slot (owned by the manager)
   bool pending;              // ops staged and not yet run
+  uint64_t index_limit;      // largest uint32-indexed output accepted (2^32 - 1; lowered by a test hook)
 };
 }  // namespace gw
 struct gwaoi_mgr;

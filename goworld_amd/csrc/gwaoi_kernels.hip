@@ -78,6 +78,10 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
       } else if (a.check && kind == OP_ENTER && a.op_space && a.op_space[i] >= a.nspaces) {
         atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SPACE);
         ok = false;
+      } else if (a.check && kind != OP_LEAVE &&
+                 !(finite_bits(__float_as_uint(a.op_x[i])) && finite_bits(__float_as_uint(a.op_z[i])))) {
+        atomicOr(&a.ctr[CTR_ERR], ERR_BAD_COORD);
+        ok = false;
       }
     }
   }
@@ -397,6 +401,12 @@ __device__ __forceinline__ uint32_t tile_cell(const TileMap& m, float x, float z
   return (uint32_t)(((cz & (kTile - 1)) << kTileShift) | (cx & (kTile - 1)));
 }
 
+// a main record of this pass's op that is not OP_SILENT (k_sweep walks exactly these; cf. is_walker)
+__device__ __forceinline__ bool bin_walker(const BinArgs& a, const uint4 ra) {
+  const uint32_t r = ra.w - a.base;
+  return !(ra.z & REC_GHOST) && r < a.n_ops && !(a.op_kind && (a.op_kind[r] & OP_SILENT));
+}
+
 __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   __shared__ uint32_t cnt[kTileCells];
   __shared__ uint32_t ws[kBlock / 64];
@@ -423,18 +433,21 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
     c3 = tile_cell(g, __uint_as_float(a3.x), __uint_as_float(a3.y));
   }
   __syncthreads();
+  bool walk = false;  // the tile holds a mover whose events are reported (k_sweep skips the others)
   if (small) {
-    if (on0) atomicAdd(&cnt[c0], 1u);
-    if (on1) atomicAdd(&cnt[c1], 1u);
-    if (on2) atomicAdd(&cnt[c2], 1u);
-    if (on3) atomicAdd(&cnt[c3], 1u);
+    if (on0) atomicAdd(&cnt[c0], 1u), walk |= bin_walker(a, a0);
+    if (on1) atomicAdd(&cnt[c1], 1u), walk |= bin_walker(a, a1);
+    if (on2) atomicAdd(&cnt[c2], 1u), walk |= bin_walker(a, a2);
+    if (on3) atomicAdd(&cnt[c3], 1u), walk |= bin_walker(a, a3);
   } else {
     for (uint32_t j = b + threadIdx.x; j < e; j += kBlock) {
       const uint4 ra = a.trec[j].a;
       atomicAdd(&cnt[tile_cell(g, __uint_as_float(ra.x), __uint_as_float(ra.y))], 1u);
+      walk |= bin_walker(a, ra);
     }
   }
-  __syncthreads();
+  const int any_walker = __syncthreads_or(walk);
+  if (threadIdx.x == 0) a.tile_walk[t] = any_walker ? 1u : 0u;
   // exclusive scan of the 1024 counts (4 per thread, consecutive)
   constexpr int kPer = kTileCells / kBlock;
   static_assert(kPer == 4, "one uint4 of counts per thread");
@@ -530,18 +543,23 @@ constexpr int kCap = GW_CAP;  // max records staged (config 2: ~1030 +- 32 in a 
 constexpr int kMaxRows = 48;
 constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
+constexpr int kKeyBins = 128;  // mover sort keys: candidate count (clamped), kKeyBins - 1 = row walk
+#ifndef GW_SWEEP_SORT
+#define GW_SWEEP_SORT 1  // order a tile's movers by candidate count (0: listing order, A/B)
+#endif
 struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint32_t n, enter, base, item;
-  uint32_t qk, pad0, pad1, pad2;  // qk: tile queues this block has found empty
+  uint32_t qk, nmv, pad1, pad2;  // qk: tile queues this block has found empty; nmv: movers in mv
   uint32_t ws[16];              // block-scan scratch
-  uint32_t gsp[kMaxRows * 3];   // global start of each (region row, tile part)
+  uint32_t hist[kKeyBins];      // movers per sort key, then (scanned) each key's first position in mv
   uint4 ev[kEvLds];             // event queue
   uint16_t lcs[kRegCells + 8];  // row-major: LDS start of each region cell (+ total)
   uint16_t ccs[kRegCells + 8];  // column-major: start in cidx of each region cell (+ total)
   uint16_t cidx[kCap];          // column-major order of the staged records (LDS record indices)
+  uint16_t mv[kCap];            // the tile's movers (LDS record indices), heaviest candidate stream first
   uint4 rp[kCap];      // staged record, LDS form: {x_start, z_start, x_end, z_end} (float bits)
   uint2 rm[kCap];      // {r | G, seq_start | A}: op rank (kNoRank: no op) and the validity mode (lds_record)
-  uint32_t rslot[kCap];  // slot (read only when an event is emitted)
+  uint32_t rslot[kCap];  // slot (read only when an event is emitted); while staging: grid index | kCoreBit
 };
 // three blocks per CU (160 KiB of LDS)
 static_assert(sizeof(SweepSmem) <= 163840 / 3 - 512, "sweep LDS budget: 3 blocks per CU");
@@ -555,6 +573,10 @@ uint32_t sweep_block() { return kSweepBlock; }
 template <class Q>
 __device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, uint32_t local, uint32_t mover,
                                      uint32_t other, bool enter, uint32_t& nent) {
+#if GW_ABL_NOEMIT  // ablation (timing only): events counted, not queued
+  nent += enter ? 1u : 0u;
+  return;
+#endif
   const uint4 rec = make_uint4(rank, local, mover, other | (enter ? 0x80000000u : 0u));
   const uint32_t li = atomicAdd(&sm.n, 1u);
   if (li < (uint32_t)kEvLds) {
@@ -587,8 +609,7 @@ struct Walk {
   bool ring;
 };
 
-__device__ __forceinline__ Walk make_walk(const Mover& m, const Geom& g) {
-  const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
+__device__ __forceinline__ Walk make_walk(const Mover& m, const Geom& g, const CellBox& A0, const CellBox& A1) {
   Walk w;
   w.ring = false;
   if (m.valid0 && m.valid1) {
@@ -619,6 +640,10 @@ __device__ __forceinline__ Walk make_walk(const Mover& m, const Geom& g) {
   return w;
 }
 
+__device__ __forceinline__ Walk make_walk(const Mover& m, const Geom& g) {
+  return make_walk(m, g, qbox(g, m.mx0, m.mz0), qbox(g, m.mx1, m.mz1));
+}
+
 // The two column segments of row r (empty segment: c0 > c1).
 __device__ __forceinline__ void walk_row(const Walk& w, int r, int& a0, int& a1, int& b0, int& b1) {
   a0 = 1, a1 = 0, b0 = 1, b1 = 0;
@@ -643,8 +668,7 @@ __device__ __forceinline__ void walk_row(const Walk& w, int r, int& a0, int& a1,
 
 // segf(r, c0, c1) for each segment (possibly empty), rows relative to the lane's window.
 template <class SegF>
-__device__ __forceinline__ void walk_cells(const Mover& m, const Geom& g, SegF&& segf) {
-  const Walk w = make_walk(m, g);
+__device__ __forceinline__ void walk_cells(const Walk& w, SegF&& segf) {
   const int h = w.z1 - w.z0;
   for (int rel = 0; __any(rel <= h); ++rel) {  // vote over the ACTIVE lanes: wave-uniform trip count
     const int r = w.z0 + rel;
@@ -744,7 +768,7 @@ __device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& q, const
                                                  uint32_t& nent) {
   const Judge J = make_judge(m, a.base);
   uint32_t local = 0;
-  walk_cells(m, g, [&](int r, int c0, int c1) {
+  walk_cells(make_walk(m, g), [&](int r, int c0, int c1) {
     row_entries_global(g, a.g.cs, r, c0, c1, [&](uint32_t j) {
       const uint4 ra = a.g.rec[j].a;
       const int ev = judge(J, ra, a.g.rec[j].b);
@@ -821,12 +845,12 @@ __device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const 
   return true;
 }
 
-__device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Region& R,
-                                              const Geom& g, uint32_t& nent) {
+__device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Walk& w,
+                                              const Region& R, const Geom& g, uint32_t& nent) {
   const Judge J = make_judge(m, a.base);
   uint32_t local = 0;
   RingStream Rs, Cs;
-  if (ring_plan(make_walk(m, g), R, sm, Rs, Cs)) {
+  if (ring_plan(w, R, sm, Rs, Cs)) {
     // row stream: LDS record indices directly
     uint32_t k = 0;
     for (; k + 1 < Rs.total; k += 2) {  // two candidates per iteration: both LDS reads in flight
@@ -858,7 +882,7 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     }
     return local;
   }
-  walk_cells(m, g, [&](int r, int c0, int c1) {
+  walk_cells(w, [&](int r, int c0, int c1) {
     const int b = (r - R.zr0) * R.ncols - R.xr0;
     uint32_t j = sm.lcs[b + c0];
     const uint32_t e = (c0 <= c1) ? (uint32_t)sm.lcs[b + c1 + 1] : j;
@@ -897,57 +921,91 @@ __device__ __forceinline__ uint32_t block_excl_scan_big(uint32_t v, uint32_t* ws
 }
 
 constexpr int kCellsPerThread = (kRegCells + kSweepBlock - 1) / kSweepBlock;
+constexpr int kStageIters = (kCap + kSweepBlock - 1) / kSweepBlock;  // staged records per thread
+constexpr uint32_t kCoreBit = 0x80000000u;  // staging map: the record lies in the tile itself, not its halo
 
-// Stage the region: per-cell counts from the cell starts, a block scan into the LDS cell-start
-// table, then a flat copy (thread per record: region row by binary search, tile part by two
-// compares, two 16-B loads). Returns the staged count (block-uniform); a count > kCap means "does
-// not fit" and nothing was copied.
-__device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, const Region& R, SweepSmem& sm,
-                                          uint32_t base, uint32_t n_ops) {
-  const int pt0 = R.xr0 >> kTileShift;  // tile column of the region's first column
-  uint32_t n[kCellsPerThread];
+__device__ __forceinline__ bool is_walker(const SweepArgs& a, const uint4 ra);
+
+// q = n / d for 0 <= n < 2^20, 1 <= d < 2^11 (region cell indices): float reciprocal, then one
+// correction step each way (exact; avoids the ~30-instruction integer division sequence)
+__device__ __forceinline__ int small_div(int n, int d) {
+  int q = (int)(((float)n + 0.5f) * (1.0f / (float)d));
+  q -= (q * d > n) ? 1 : 0;
+  q += ((q + 1) * d <= n) ? 1 : 0;
+  return q;
+}
+
+// Stage the region of tile (tcx, tcz: the tile's first column / row inside the region). Per cell
+// (kCellsPerThread consecutive cells per thread, every cell-start load issued up front): counts, a
+// block scan into the row-major LDS cell-start table, and per record its grid index, written into
+// rslot by the cell's thread (kCoreBit: the cell is the tile's own). Then the column-major tables,
+// then a flat copy: thread per record, grid index from LDS, one 32-B gather each (a thread's gathers
+// issued together), LDS form. The tile's reported movers are listed in mv (unordered), or, when
+// their boxes leave the region, appended to the dense list (k_sweep_dense). Returns the staged count
+// (block-uniform); a count > kCap means "does not fit" and nothing was staged.
+__device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, const Region& R, int tcx, int tcz,
+                                          SweepSmem& sm) {
+  uint32_t n[kCellsPerThread], s0[kCellsPerThread];
   uint32_t sum = 0;
   const int c0 = threadIdx.x * kCellsPerThread;
+  // this thread's cells are consecutive in row-major order: one division, then a carry (ncols >= kTile)
+  const int rr0 = small_div(c0, R.ncols), col0 = c0 - rr0 * R.ncols;
+  {
+    int rr = rr0, col = col0;
 #pragma unroll
-  for (int k = 0; k < kCellsPerThread; ++k) {
-    const int c = c0 + k;
-    n[k] = 0;
-    if (c < R.ncells) {
-      const int rr = c / R.ncols, col = R.xr0 + (c - rr * R.ncols);
-      const uint32_t key = cell_key(g, col, R.zr0 + rr);
-      const uint32_t s0 = gv.cs[key];
-      n[k] = gv.cs[key + 1] - s0;
-      if (col == R.xr0 || (col & (kTile - 1)) == 0) sm.gsp[rr * 3 + ((col >> kTileShift) - pt0)] = s0;
+    for (int k = 0; k < kCellsPerThread; ++k) {
+      n[k] = 0;
+      s0[k] = 0;
+      if (c0 + k < R.ncells) {
+        const uint32_t key = cell_key(g, R.xr0 + col, R.zr0 + rr);
+        s0[k] = a.g.cs[key];
+        n[k] = a.g.cs[key + 1] - s0[k];
+      }
+      sum += n[k];
+      if (++col == R.ncols) col = 0, ++rr;
     }
-    sum += n[k];
   }
   uint32_t total;
   uint32_t pre = block_excl_scan_big(sum, sm.ws, &total);
   if (total > (uint32_t)kCap) return total;
+  {
+    int rr = rr0, col = col0;
 #pragma unroll
-  for (int k = 0; k < kCellsPerThread; ++k) {
-    if (c0 + k < R.ncells) sm.lcs[c0 + k] = (uint16_t)pre;
-    pre += n[k];
+    for (int k = 0; k < kCellsPerThread; ++k) {
+      const int c = c0 + k;
+      if (c < R.ncells) {
+        sm.lcs[c] = (uint16_t)pre;
+        const uint32_t core =
+            ((uint32_t)(rr - tcz) < (uint32_t)kTile && (uint32_t)(col - tcx) < (uint32_t)kTile) ? kCoreBit : 0u;
+        for (uint32_t q = 0; q < n[k]; ++q) sm.rslot[pre + q] = (s0[k] + q) | core;
+      }
+      pre += n[k];
+      if (++col == R.ncols) col = 0, ++rr;
+    }
   }
-  if (threadIdx.x == 0) sm.lcs[R.ncells] = (uint16_t)total;
+  if (threadIdx.x == 0) {
+    sm.lcs[R.ncells] = (uint16_t)total;
+    sm.nmv = 0;
+  }
+  if (threadIdx.x < kKeyBins) sm.hist[threadIdx.x] = 0u;
   __syncthreads();
   // column-major cell starts (cell counts from the row-major table) and the column-major index
   // array: cell (rr, cc) is column-major cell cc * nrows + rr
   {
     uint32_t cn[kCellsPerThread], cl[kCellsPerThread];
     uint32_t sum2 = 0;
+    int cc = small_div(c0, R.nrows), rr = c0 - cc * R.nrows;  // column-major: cell cc * nrows + rr
 #pragma unroll
     for (int k = 0; k < kCellsPerThread; ++k) {
-      const int cm = c0 + k;
       cn[k] = 0;
       cl[k] = 0;
-      if (cm < R.ncells) {
-        const int cc = cm / R.nrows, rr = cm - cc * R.nrows;
+      if (c0 + k < R.ncells) {
         const int c = rr * R.ncols + cc;
         cl[k] = sm.lcs[c];
         cn[k] = sm.lcs[c + 1] - cl[k];
       }
       sum2 += cn[k];
+      if (++rr == R.nrows) rr = 0, ++cc;
     }
     uint32_t tot2;
     uint32_t pre2 = block_excl_scan_big(sum2, sm.ws, &tot2);
@@ -959,30 +1017,28 @@ __device__ __forceinline__ uint32_t stage(const GridView& gv, const Geom& g, con
     }
     if (threadIdx.x == 0) sm.ccs[R.ncells] = (uint16_t)total;
   }
-  const int p1c = ((pt0 + 1) << kTileShift) - R.xr0, p2c = p1c + kTile;
-  for (uint32_t i = threadIdx.x; i < total; i += kSweepBlock) {
-    int lo = 0, hi = R.nrows;  // find rr with lcs[rr * ncols] <= i < lcs[(rr + 1) * ncols]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (sm.lcs[mid * R.ncols] <= i) lo = mid;
-      else hi = mid;
+  uint32_t src[kStageIters];
+  Rec r[kStageIters];
+#pragma unroll
+  for (int k = 0; k < kStageIters; ++k) {
+    const uint32_t i = threadIdx.x + k * kSweepBlock;
+    src[k] = i < total ? sm.rslot[i] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kStageIters; ++k) {
+    const uint32_t i = threadIdx.x + k * kSweepBlock;
+    if (i < total) r[k] = a.g.rec[src[k] & ~kCoreBit];
+  }
+#pragma unroll
+  for (int k = 0; k < kStageIters; ++k) {
+    const uint32_t i = threadIdx.x + k * kSweepBlock;
+    bool lm = false;
+    if (i < total) {
+      lds_record(r[k].a, r[k].b, a.base, a.n_ops, sm.rp[i], sm.rm[i], sm.rslot[i]);
+      lm = (src[k] & kCoreBit) && is_walker(a, r[k].a);
     }
-    const int rb = lo * R.ncols;
-    // tile parts of the row start at region column 0, then at each multiple of kTile
-    int p = 0, pc = 0;
-    if (p1c < R.ncols && sm.lcs[rb + p1c] <= i) {
-      p = 1;
-      pc = p1c;
-      if (p2c < R.ncols && sm.lcs[rb + p2c] <= i) {
-        p = 2;
-        pc = p2c;
-      }
-    }
-    const uint32_t src = sm.gsp[lo * 3 + p] + (i - sm.lcs[rb + pc]);
-    {
-      const Rec r = gv.rec[src];
-      lds_record(r.a, r.b, base, n_ops, sm.rp[i], sm.rm[i], sm.rslot[i]);
-    }
+    const uint32_t li = wave_append(&sm.nmv, lm);  // wave-uniform call: the trip count is a constant
+    if (lm) sm.mv[li] = (uint16_t)i;
   }
   return total;
 }
@@ -999,6 +1055,24 @@ __device__ __forceinline__ Mover mover_of(const uint4 ra, const uint4 rb, uint32
   m.mz0 = __uint_as_float(rb.y);
   m.mx1 = __uint_as_float(ra.x);
   m.mz1 = __uint_as_float(ra.y);
+  m.D = D;
+  return m;
+}
+
+// a mover (main record of an op of this pass) from its slot's state: end = current position,
+// start = the start-of-pass state k_apply recorded (mover_of of its grid record, without the gather)
+__device__ __forceinline__ Mover slot_mover(const SweepArgs& a, uint32_t s, float D) {
+  Mover m;
+  m.slot = s;
+  m.q = a.opq[s];
+  m.q0 = a.old_seq[s];
+  m.rank = m.q - a.base;
+  m.valid0 = m.q0 != 0;
+  m.valid1 = true;
+  m.mx0 = a.old_x[s];
+  m.mz0 = a.old_z[s];
+  m.mx1 = a.pos_x[s];
+  m.mz1 = a.pos_z[s];
   m.D = D;
   return m;
 }
@@ -1055,67 +1129,139 @@ __device__ __forceinline__ bool is_walker(const SweepArgs& a, const uint4 ra) {
   return is_mover(ra, a.base, a.n_ops) && !(a.op_kind && (a.op_kind[ra.w - a.base] & OP_SILENT));
 }
 
-// One work item of k_sweep: a tile (stage its region, walk its movers); the block's LDS event queue
-// is flushed with one global atomic at the end.
+// a mover from its staged LDS record (lds_record's form; movers are main records of this pass's ops)
+__device__ __forceinline__ Mover lds_mover(const SweepSmem& sm, uint32_t i, uint32_t base, float D) {
+  const uint4 p = sm.rp[i];
+  const uint2 q = sm.rm[i];
+  Mover m;
+  m.slot = sm.rslot[i];
+  m.rank = q.x & ~kTopBit;
+  m.q = base + m.rank;
+  m.q0 = q.y & ~kTopBit;
+  m.valid0 = m.q0 != 0;
+  m.valid1 = true;
+  m.mx0 = __uint_as_float(p.x);
+  m.mz0 = __uint_as_float(p.y);
+  m.mx1 = __uint_as_float(p.z);
+  m.mz1 = __uint_as_float(p.w);
+  m.D = D;
+  return m;
+}
+
+// One work item of k_sweep: a tile. Stage its region; order its movers by the length of their
+// candidate streams (LDS counting sort, heaviest first) so the lanes of a wave walk streams of about
+// the same length; walk them, one thread per mover, consecutive rounds of the block in alternating
+// direction (a tile holds ~520 movers for 512 threads: the few of the second round pair with the
+// lightest of the first). The block's LDS event queue is flushed with one global atomic at the end.
 __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, const uint32_t item) {
   uint32_t nent = 0;  // enter events of this thread's movers
-  {
-    const uint32_t t = item;
+  const uint32_t t = item;
+  if (a.tile_walk) {
+    if (!a.tile_walk[t]) return;  // block-uniform: no reported mover in the tile (flag from k_bin_tsort)
+  } else {
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
-    // does the tile hold a mover of this pass? (block-uniform exit otherwise)
     bool mine = false;
     for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_walker(a, a.g.rec[j].a);
     if (!__syncthreads_or(mine)) return;  // nothing queued: the caller's barrier follows
-    const uint32_t sp = a.g.tile_space[t];
-    const Geom g = a.g.geom[sp];
-    bool lds = a.use_lds && g.reach > 0;
-    Region R;
-    if (lds) {
-      const uint32_t tl = t - g.tile_base;
-      const int tz = (int)(tl / (uint32_t)g.ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)g.ntx);
-      R.zr0 = max(0, tz * kTile - g.reach);
-      R.zr1 = min(g.ncz - 1, tz * kTile + kTile - 1 + g.reach);
-      R.xr0 = max(0, tx * kTile - g.reach);
-      R.xr1 = min(g.ncx - 1, tx * kTile + kTile - 1 + g.reach);
-      R.ncols = R.xr1 - R.xr0 + 1;
-      R.nrows = R.zr1 - R.zr0 + 1;
-      R.ncells = R.nrows * R.ncols;
-      lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= 3 * kTile;
-    }
-    if (lds) {
-      GW_STAMP(1, __builtin_amdgcn_s_memrealtime());
-      const uint32_t nst = stage(a.g, g, R, sm, a.base, a.n_ops);
-      lds = nst <= (uint32_t)kCap;  // block-uniform
-      __syncthreads();
-      GW_STAMP(2, __builtin_amdgcn_s_memrealtime());
-      GW_STAMP(5, nst);
-      GW_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
-                      ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32));
-    }
-    if (a.use_lds == 2) {  // ablation (timing only): staging without the candidate walk
-      for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
-        const uint4 ra = a.g.rec[j].a;
-        if (is_mover(ra, a.base, a.n_ops)) a.rank_cnt[ra.w - a.base] = 0;
+  }
+  const uint32_t sp = a.g.tile_space[t];
+  const Geom g = a.g.geom[sp];
+  bool lds = a.use_lds && g.reach > 0;
+  Region R;
+  int tcx = 0, tcz = 0;
+  if (lds) {
+    const uint32_t tl = t - g.tile_base;
+    const int tz = (int)(tl / (uint32_t)g.ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)g.ntx);
+    R.zr0 = max(0, tz * kTile - g.reach);
+    R.zr1 = min(g.ncz - 1, tz * kTile + kTile - 1 + g.reach);
+    R.xr0 = max(0, tx * kTile - g.reach);
+    R.xr1 = min(g.ncx - 1, tx * kTile + kTile - 1 + g.reach);
+    R.ncols = R.xr1 - R.xr0 + 1;
+    R.nrows = R.zr1 - R.zr0 + 1;
+    R.ncells = R.nrows * R.ncols;
+    tcx = tx * kTile - R.xr0;
+    tcz = tz * kTile - R.zr0;
+    lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= 3 * kTile;
+  }
+  if (lds) {
+    GW_STAMP(1, __builtin_amdgcn_s_memrealtime());
+    const uint32_t nst = stage(a, g, R, tcx, tcz, sm);
+    lds = nst <= (uint32_t)kCap;  // block-uniform
+    __syncthreads();
+    GW_STAMP(2, __builtin_amdgcn_s_memrealtime());
+    GW_STAMP(5, nst);
+    GW_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                    ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32));
+  }
+  if (!lds) {
+    // region over the LDS budget (crowds, large D): every mover of the tile to k_sweep_dense
+    const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
+    for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
+      const uint4 ra = a.g.rec[j].a;
+      if (!is_walker(a, ra)) continue;
+      const uint32_t di = wave_append(&a.ctr[CTR_DENSE], true);
+      if (di < a.dense_cap) {
+        a.dense[di] = ra.z & REC_SLOT;
+        continue;
       }
-    } else {
-      for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
-        const uint4 ra = a.g.rec[j].a;
-        if (!is_walker(a, ra)) continue;
-        const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
-        uint32_t cnt;
-        const bool in_lds = lds && R.holds(qbox(g, m.mx1, m.mz1)) && (!m.valid0 || R.holds(qbox(g, m.mx0, m.mz0)));
-        // movers whose boxes leave the staged region (teleports, a region over the LDS budget: dense
-        // crowds, large D) go to k_sweep_dense: one wave per mover, candidates 64 at a time
+      const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
+      const uint32_t cnt = sweep_global(a, sm, m, g, nent);
+      if (cnt) a.rank_cnt[m.rank] = cnt;
+    }
+  } else {
+    const uint32_t nm = sm.nmv;
+    // sort key: the mover's candidate count (ring streams), or the top key for a row walk. Per mover
+    // slot of this thread: key << 22 | rank inside the key << 11 | LDS record index (kCap < 2^11).
+    static_assert(kCap < 2048 && kKeyBins <= 1024, "packed mover sort entry");
+    uint32_t ent[kStageIters];
+#pragma unroll
+    for (int k = 0; k < kStageIters; ++k) {
+      const uint32_t p = threadIdx.x + k * kSweepBlock;
+      ent[k] = 0;
+      if (p < nm) {
+        const uint32_t i = sm.mv[p];
+        const Mover m = lds_mover(sm, i, a.base, g.D);
+        const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
+        uint32_t key = kKeyBins - 1u;  // row walks, and movers that leave the region (k_sweep_dense)
+#if GW_SWEEP_SORT
+        RingStream Rs, Cs;
+        if (R.holds(A1) && (!m.valid0 || R.holds(A0)) && ring_plan(make_walk(m, g, A0, A1), R, sm, Rs, Cs))
+          key = min(Rs.total + Cs.total, (uint32_t)kKeyBins - 2u);
+#else
+        (void)A0, (void)A1;
+#endif
+        ent[k] = key << 22 | atomicAdd(&sm.hist[key], 1u) << 11 | i;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {  // descending exclusive scan of the key histogram: key kKeyBins-1 first
+      const uint32_t b0 = kKeyBins - 1 - 2 * threadIdx.x, b1 = b0 - 1;
+      const uint32_t h0 = sm.hist[b0], h1 = sm.hist[b1];
+      const uint32_t ex = wave_incl_scan(h0 + h1) - (h0 + h1);
+      sm.hist[b0] = ex;
+      sm.hist[b1] = ex + h0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kStageIters; ++k)
+      if (threadIdx.x + k * kSweepBlock < nm)
+        sm.mv[sm.hist[ent[k] >> 22] + ((ent[k] >> 11) & 2047u)] = (uint16_t)(ent[k] & 2047u);
+    __syncthreads();
+    if (a.use_lds != 2) {  // 2: ablation (timing only), staging and ordering without the walk
+      for (uint32_t r = 0; r * kSweepBlock < nm; ++r) {
+        const uint32_t p = r * kSweepBlock + ((r & 1u) ? (uint32_t)(kSweepBlock - 1) - threadIdx.x : threadIdx.x);
+        if (p >= nm) continue;
+        const Mover m = lds_mover(sm, sm.mv[p], a.base, g.D);
+        const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
+        // movers whose boxes leave the staged region (teleports) go to k_sweep_dense: one wave per
+        // mover, candidates 64 at a time
+        const bool in_lds = R.holds(A1) && (!m.valid0 || R.holds(A0));
         const uint32_t di = wave_append(&a.ctr[CTR_DENSE], !in_lds);
         if (!in_lds) {
-          if (di < a.dense_cap) {
-            a.dense[di] = j;
-            continue;
-          }
-          cnt = sweep_global(a, sm, m, g, nent);
-        } else {
-          cnt = sweep_lds(a, sm, m, R, g, nent);
+          if (di < a.dense_cap) a.dense[di] = m.slot;
+          continue;
         }
+        const uint32_t cnt = sweep_lds(a, sm, m, make_walk(m, g, A0, A1), R, g, nent);
         if (cnt) a.rank_cnt[m.rank] = cnt;  // zeroed by k_apply (one coalesced pass instead of a scatter)
       }
     }
@@ -1158,6 +1304,7 @@ k_sweep(SweepArgs a) {
     sm.enter = 0;
   }
   __syncthreads();
+  GW_STAMP(0, __builtin_amdgcn_s_memrealtime());
   sweep_item(a, sm, __builtin_amdgcn_readfirstlane(sm.item));
   return;
 #endif
@@ -1321,10 +1468,8 @@ k_sweep_dense(SweepArgs a) {
   uint32_t nent = 0;
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
   for (uint32_t d = wave; d < nd; d += nwaves) {
-    const uint32_t j0 = a.dense[d];
-    const uint4 ma = a.g.rec[j0].a, mb = a.g.rec[j0].b;
-    const Geom g = a.g.geom[a.space_of[ma.z & REC_SLOT]];
-    const Mover m = mover_of(ma, mb, a.base, g.D);
+    const Geom g = a.g.geom[a.space_of[a.dense[d]]];
+    const Mover m = slot_mover(a, a.dense[d], g.D);
     const Judge J = make_judge(m, a.base);
     uint32_t local = 0;      // wave-uniform
     uint32_t pk = 0, pe = 0;  // this lane's cell-key range [pk, pe) (one tile part of one row segment)
@@ -1683,6 +1828,7 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
                                                           return make_uint4(r.a.x, r.a.y, r.b.w, r.a.z);
                                                         });
   const float D = g.D;
+  unsigned long long rsum = 0;  // count pass: this thread's row lengths
   for (uint32_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
     const uint4 ma = a.g.rec[j].a;
     if (ma.z & REC_GHOST) continue;
@@ -1718,7 +1864,11 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
         });
       }
     }
-    if (!a.row_ptr) a.row_cnt[s] = n;
+    if (!a.row_ptr) a.row_cnt[s] = n, rsum += n;
+  }
+  if (!a.row_ptr) {  // one 64-bit atomic per wave: the host checks the total before it sizes cols
+    for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o, 64);
+    if ((threadIdx.x & 63) == 0 && rsum) atomicAdd(a.total64, rsum);
   }
 }
 

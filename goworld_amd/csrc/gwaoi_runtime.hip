@@ -147,6 +147,8 @@ struct gwaoi_mgr {
   // relation view (gwaoi_relation_device): CSR in HBM, allocated on first use, grown on demand
   uint32_t *rel_rp = nullptr, *rel_cols = nullptr, *rel_tmp = nullptr;
   uint64_t rel_cap = 0;
+  unsigned long long* rel_tot = nullptr;  // device: the count pass's 64-bit entry total
+  uint64_t index_limit = 0xFFFFFFFFull;   // uint32-indexed outputs (relation view, fan-out) fail above it
   float *d_op_x = nullptr, *d_op_z = nullptr;
   uint8_t* d_op_kind = nullptr;
   Grid grid[2];
@@ -158,6 +160,7 @@ struct gwaoi_mgr {
   uint32_t part_words = 0;
   gw::ScanCtx scan;
   uint32_t* thist = nullptr;     // tile-bucketed build: [max tiles * nblk + 1]
+  uint32_t* tile_walk = nullptr; // tile-bucketed build: per tile of the pass's grid, holds a reported mover
   uint32_t nblk = 0;
   uint32_t* ctr_buf = nullptr;   // [2][CTR_N]: pass P uses half P&1 and zeroes the other (k_place)
   uint32_t* ctr = nullptr;       // current half
@@ -364,7 +367,7 @@ bool tile_build(const Grid& g) { return g.ntiles <= gw::kMaxLdsTiles; }
 // Build grid `gi` from the per-slot state (pos, seq, space_of).
 // Build grid `gi` for the pass whose ops have seqs [base, base + n_ops) (n_ops = 0: the current
 // state only, no ghosts).
-int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops) {
+int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_t* op_kind) {
   Grid& g = m->grid[gi];
   const bool tiles = tile_build(g);
   if (!tiles && g.cs_zeroed < g.ncells + 1)
@@ -392,6 +395,8 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops) {
   b.thist = m->thist;
   b.tile_space = g.d_tile_space;
   b.trec = m->grid[gi ^ 1].rec;  // the other grid's records are not read by this pass
+  b.op_kind = op_kind;
+  b.tile_walk = m->tile_walk;
   if (tiles) {
     gw::launch_bin_tiles(b, m->scan, m->stream);
   } else {
@@ -416,7 +421,7 @@ int renormalise(gwaoi_mgr* m) {
   for (size_t i = 0; i < v.size(); ++i) q[v[i].second] = (uint32_t)i + 1;
   HIPCHK(hipMemcpy(m->seq, q.data(), m->cap * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemsetAsync(m->opq, 0, (size_t)m->cap * sizeof(uint32_t), m->stream));  // stale op seqs
-  RCHK(build_grid(m, m->cur, 0, 0));
+  RCHK(build_grid(m, m->cur, 0, 0, nullptr));
   m->next_seq = (uint32_t)v.size() + 1;
   HIPCHK(hipStreamSynchronize(m->stream));
   return GWAOI_OK;
@@ -550,7 +555,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   HIPCHK(hipGetLastError());
   if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
 
-  RCHK(build_grid(m, ng, base, n_ops));
+  RCHK(build_grid(m, ng, base, n_ops, a.op_kind));
   if (m->timing) HIPCHK(hipEventRecord(m->tev[2], st));
 
   const uint32_t n_new = dev ? m->n_present_dev : m->n_present;
@@ -577,6 +582,9 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.old_z = m->old_z;
     s.old_seq = m->old_seq;
     s.space_of = m->space_of;
+    s.pos_x = m->pos_x;
+    s.pos_z = m->pos_z;
+    s.opq = m->opq;
     s.base = base;
     s.n_ops = n_ops;
     s.op_slot = a.op_slot;
@@ -593,6 +601,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.dense = m->d_dense;
     s.dense_cap = m->cap;
     s.dense_hint = attempt ? ~0u : m->last_dense;
+    s.tile_walk = tile_build(G) ? m->tile_walk : nullptr;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
@@ -624,8 +633,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     if (m->h_ctr[gw::CTR_ERR]) {
       m->broken = true;
       set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
-              "capacity, 8=Enter of a present slot, 16=Space id out of range, 32=op count above its bound); the manager is "
-              "unusable",
+              "capacity, 8=Enter of a present slot, 16=Space id out of range, 32=op count above its bound, "
+              "64=non-finite coordinate); the manager is unusable",
               m->h_ctr[gw::CTR_ERR]);
       return GWAOI_ERR_DEVICE_CHECK;
     }
@@ -667,6 +676,16 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->dv_space = nullptr;
   m->dv_count = nullptr;
   return GWAOI_OK;
+}
+
+// Non-finite coordinates are refused (GWAOI_ERR_INVALID). go-aoi accepts them, and a NaN node in its
+// sorted lists stops every Mark walk that reaches it, so third parties lose neighbours (the list
+// restatement in the test suite reproduces that); that behaviour depends on list position, not
+// on positions, and is not what a game wants from a client float. Deliberate divergence.
+int check_coord(const char* what, uint32_t slot, float x, float z) {
+  if (std::isfinite(x) && std::isfinite(z)) return GWAOI_OK;
+  set_err("%s: slot %u: non-finite coordinate (%g, %g) refused", what, slot, (double)x, (double)z);
+  return GWAOI_ERR_INVALID;
 }
 
 int check_mgr(const gwaoi_mgr* m) {
@@ -739,7 +758,7 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp};
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
@@ -829,6 +848,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   const uint64_t max_tiles = m->max_cells / gw::kTileCells + 1;
   const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
   chk(dalloc(&m->thist, thist_n));
+  chk(dalloc(&m->tile_walk, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
   // the scan has at most 1024 chunks up to 16.7M items (scan_ipt), more beyond
   m->part_words = std::max<uint32_t>(1024 + 2, gw::scan_part_words((uint32_t)std::max<uint64_t>(
                                                    {(uint64_t)m->max_cells, (uint64_t)capacity, thist_n}) + 1));
@@ -947,6 +967,7 @@ int mgr_view(gwaoi_mgr* m, MgrView* out) {
   out->scan = &m->scan;
   out->sync = &m->sync;
   out->pending = m->n_ops || m->dv_n;
+  out->index_limit = m->index_limit;
   return GWAOI_OK;
 }
 
@@ -1007,6 +1028,7 @@ int gwaoi_enter_space(gwaoi_mgr* m, uint32_t space, uint32_t slot, float x, floa
     set_err("enter: slot %u is already in a Space", slot);
     return GWAOI_ERR_STATE;
   }
+  RCHK(check_coord("enter", slot, x, z));
   RCHK(set_dev(m));
   RCHK(before_stage(m, slot));
   note_coord(m, space, x, z);
@@ -1025,6 +1047,31 @@ int gwaoi_stage_enters(gwaoi_mgr* m, uint32_t space, const uint32_t* slots, cons
   if (n && (!slots || !x || !z)) {
     set_err("stage_enters: null array");
     return GWAOI_ERR_INVALID;
+  }
+  RCHK(host_staging_ok(m));
+  // validate the whole array first: nothing is staged unless every entry is acceptable
+  if (space >= m->nspaces) {
+    set_err("stage_enters: space %u out of range", space);
+    return GWAOI_ERR_INVALID;
+  }
+  std::vector<uint32_t> seen;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t s = slots[i];
+    if (s >= m->cap) {
+      set_err("stage_enters: entry %u: slot %u out of range", i, s);
+      return GWAOI_ERR_INVALID;
+    }
+    RCHK(check_coord("stage_enters", s, x[i], z[i]));
+    if (m->h_present[s]) {
+      set_err("stage_enters: entry %u: slot %u is already in a Space", i, s);
+      return GWAOI_ERR_STATE;
+    }
+    seen.push_back(s);
+  }
+  std::sort(seen.begin(), seen.end());
+  if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) {
+    set_err("stage_enters: a slot enters twice");
+    return GWAOI_ERR_STATE;
   }
   for (uint32_t i = 0; i < n; ++i) RCHK(gwaoi_enter_space(m, space, slots[i], x[i], z[i]));
   return GWAOI_OK;
@@ -1060,6 +1107,7 @@ int gwaoi_moved(gwaoi_mgr* m, uint32_t slot, float x, float z) {
     set_err("moved: slot %u is not in a Space", slot);
     return GWAOI_ERR_STATE;
   }
+  RCHK(check_coord("moved", slot, x, z));
   RCHK(set_dev(m));
   RCHK(before_stage(m, slot));
   note_coord(m, m->h_space_of[slot], x, z);
@@ -1072,6 +1120,20 @@ int gwaoi_stage_moves(gwaoi_mgr* m, const uint32_t* slots, const float* x, const
   if (n && (!slots || !x || !z)) {
     set_err("stage_moves: null array");
     return GWAOI_ERR_INVALID;
+  }
+  RCHK(host_staging_ok(m));
+  // validate the whole array first (Moved changes no presence): all entries are staged or none
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t s = slots[i];
+    if (s >= m->cap) {
+      set_err("stage_moves: entry %u: slot %u out of range", i, s);
+      return GWAOI_ERR_INVALID;
+    }
+    if (!m->h_present[s]) {
+      set_err("stage_moves: entry %u: slot %u is not in a Space", i, s);
+      return GWAOI_ERR_STATE;
+    }
+    RCHK(check_coord("stage_moves", s, x[i], z[i]));
   }
   for (uint32_t i = 0; i < n; ++i) RCHK(gwaoi_moved(m, slots[i], x[i], z[i]));
   return GWAOI_OK;
@@ -1174,6 +1236,7 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   }
   hipStream_t st = m->stream;
   if (!m->rel_rp) RCHK(dalloc(&m->rel_rp, (size_t)m->cap + 1));
+  if (!m->rel_tot) RCHK(dalloc(&m->rel_tot, 1));
   const Grid& g = m->grid[m->cur];
   gw::RelArgs a;
   a.g = {g.rec, g.cs, g.d_geom, g.d_tile_space};
@@ -1186,13 +1249,21 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   a.row_cnt = m->rel_rp;
   a.cols = nullptr;
   a.ntiles = g.ncells ? g.ntiles : 0u;
+  a.total64 = m->rel_tot;
   // count pass, scan, then the row lengths' total is the one value the host must know (allocation)
   HIPCHK(hipMemsetAsync(m->rel_rp, 0, ((size_t)m->cap + 1) * sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(m->rel_tot, 0, sizeof(unsigned long long), st));
   gw::launch_relation(a, st);
-  gw::launch_scan(m->scan, m->rel_rp, m->cap + 1, st);
-  uint32_t total = 0;
-  HIPCHK(hipMemcpyAsync(&total, m->rel_rp + m->cap, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  unsigned long long total64 = 0;
+  HIPCHK(hipMemcpyAsync(&total64, m->rel_tot, sizeof total64, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (total64 > m->index_limit) {  // row_ptr is uint32: a scan past 2^32 - 1 would wrap
+    set_err("relation_device: %llu directed entries exceed the view's uint32 row offsets (limit %llu)",
+            (unsigned long long)total64, (unsigned long long)m->index_limit);
+    return GWAOI_ERR_NOMEM;
+  }
+  gw::launch_scan(m->scan, m->rel_rp, m->cap + 1, st);
+  const uint32_t total = (uint32_t)total64;
   if (total > m->rel_cap) {
     if (m->rel_cols) hipFree(m->rel_cols);
     if (m->rel_tmp) hipFree(m->rel_tmp);
@@ -1385,6 +1456,12 @@ int gwaoi_debug_read_stamps(void* host, size_t bytes) {
   const int r = gw::read_stamps(host, bytes);
   if (r) set_err("debug_read_stamps: library not built with GW_STAMPS=1");
   return r;
+}
+
+int gwaoi_debug_set_index_limit(gwaoi_mgr* m, uint64_t limit) {
+  RCHK(check_mgr(m));
+  m->index_limit = std::min<uint64_t>(limit, 0xFFFFFFFFull);
+  return GWAOI_OK;
 }
 
 int gwaoi_debug_set_cells_per_dist(gwaoi_mgr* m, float cpd) {

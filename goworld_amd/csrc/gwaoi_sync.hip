@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "gwaoi.h"
@@ -74,7 +75,14 @@ __global__ void __launch_bounds__(kSy) k_sync_scatter(ScatArgs a) {
   if (i >= a.n) return;
   const uint32_t s = a.slot[i];
   switch (a.mode) {
-    case 0: a.t_eid[s] = a.id[i]; break;
+    case 0:
+      a.t_eid[s] = a.id[i];
+      if (a.f[i]) {  // a new entity in the slot: nothing of the previous one carries over
+        a.flags[s] = 0;
+        a.t_gate[s] = GWAOI_SYNC_NO_CLIENT;
+        a.t_cid[s] = make_uint4(0, 0, 0, 0);
+      }
+      break;
     case 1:
       a.t_gate[s] = a.gate[i];
       a.t_cid[s] = a.id[i];
@@ -86,6 +94,14 @@ __global__ void __launch_bounds__(kSy) k_sync_scatter(ScatArgs a) {
       a.flags[s] = (uint8_t)(a.flags[s] | a.f[i]);
       break;
   }
+}
+
+// collect, after the fan-out: the sync bits of slots absent from the manager clear without records
+// (the fan-out visits present entities only; the reference clears every collected flag, Entity.go:1226)
+__global__ void __launch_bounds__(kSy) k_clear_absent(uint8_t* flags, const uint32_t* seq, uint32_t cap) {
+  for (uint32_t s = blockIdx.x * kSy + threadIdx.x; s < cap; s += gridDim.x * kSy)
+    if (!seq[s] && (flags[s] & (GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS)))
+      flags[s] = (uint8_t)(flags[s] & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
 }
 
 __global__ void __launch_bounds__(kSy) k_hash_scatter(const uint32_t* __restrict__ idx, const uint4* __restrict__ key,
@@ -113,6 +129,7 @@ struct FanArgs {
   const uint32_t* off;  // write pass: the scanned counts
   uint2* pairs;         // {entity, receiver} (receiver == entity: own client)
   uint32_t* n_ent;      // entities collected (count pass)
+  unsigned long long* npairs64;  // count pass: pair total in 64 bits (uint32 overflow guard)
   // client sub-grid: the main records of entities WITH a client, in grid order (the only candidates
   // a fan-out can name), with their own cell starts over the same cell keys
   const uint32_t* ccs;  // [ncells + 1]
@@ -283,10 +300,15 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
     }
     return c;
   };
+  unsigned long long psum = 0;  // count pass: this thread's pairs
   for (uint32_t jb = j0; jb < j1; jb += kSy) {
     const uint32_t j = jb + threadIdx.x;
     if (!kWrite) {
-      if (j < j1) a.cnt[j] = visit(j, [](uint32_t, uint2) {});
+      if (j < j1) {
+        const uint32_t c = visit(j, [](uint32_t, uint2) {});
+        a.cnt[j] = c;
+        psum += c;
+      }
       continue;
     }
     // write pass, per round of kSy records: their output is the contiguous range [off[jb], off[je]),
@@ -303,6 +325,8 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
     }
   }
   if (!kWrite) {
+    for (int o = 32; o > 0; o >>= 1) psum += __shfl_xor(psum, o, 64);
+    if ((threadIdx.x & 63) == 0 && psum) atomicAdd(a.npairs64, psum);
     for (int o = 32; o > 0; o >>= 1) ents += __shfl_xor(ents, o, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ents;
     __syncthreads();
@@ -440,7 +464,7 @@ struct IngArgs {
   float* yaw;
   uint32_t* res;     // per record: slot, or kNone (not accepted)
   uint32_t* first;   // per slot: first record of this batch naming it (kNone between batches)
-  uint32_t* ctr;     // [0] cut, [1] unknown, [2] rejected
+  uint32_t* ctr;     // [0] cut, [1] unknown, [2] rejected, [3] non-finite x or z
   uint32_t* bcnt;    // per block: accepted records of the batch, scanned -> offsets; [nb] = total
   uint32_t* op_slot;
   float* op_x;
@@ -455,7 +479,7 @@ __device__ __forceinline__ void wave_add(uint32_t* p, uint32_t v) {
 // resolve every record once: slot or kNone, with the unknown / rejected counts
 __global__ void __launch_bounds__(kSy) k_ing_resolve(IngArgs a) {
   const uint32_t i = blockIdx.x * kSy + threadIdx.x;
-  uint32_t unk = 0, rej = 0;
+  uint32_t unk = 0, rej = 0, nonf = 0;
   if (i < a.n) {
     const uint4 id = a.rec[2 * i];
     uint32_t b = id_hash(id) & a.hmask, slot = kNone;
@@ -473,11 +497,18 @@ __global__ void __launch_bounds__(kSy) k_ing_resolve(IngArgs a) {
     } else if (!a.seq[slot] || !(a.flags[slot] & GWAOI_SYNC_FROM_CLIENT)) {
       rej = 1;
       slot = kNone;
+    } else {
+      const uint4 v = a.rec[2 * i + 1];  // a client float that is NaN / +-Inf is dropped
+      if (!finite_bits(v.x) || !finite_bits(v.z)) {
+        nonf = 1;
+        slot = kNone;
+      }
     }
     a.res[i] = slot;
   }
   wave_add(&a.ctr[1], unk);
   wave_add(&a.ctr[2], rej);
+  wave_add(&a.ctr[3], nonf);
 }
 
 // first record of the batch [seg, n) naming each slot
@@ -901,8 +932,40 @@ int gwaoi_sync_set_entities(gwaoi_mgr* m, const uint32_t* slots, const uint8_t* 
   std::vector<uint32_t> idx;
   SRCHK(gw::last_wins(s, slots, n, &idx));
   const uint32_t mask = s->hcap - 1;
+  auto lookup = [&](const uint4& k) -> uint32_t {  // slot holding id k now, or kNone
+    for (uint32_t b = gw::id_hash(k) & mask;; b = (b + 1) & mask) {
+      const uint32_t hv = s->h_hval[b];
+      if (hv == gw::kHEmpty) return gw::kNone;
+      if (hv != gw::kHTomb && gw::id_eq(s->h_hkey[b], k)) return hv;
+    }
+  };
+  // validate first, so a failing call changes nothing: in the state after the call no id may be
+  // held by two slots (an id may move to another slot in the same call if its old slot changes too)
+  {
+    std::unordered_map<uint64_t, std::vector<std::pair<uint4, uint32_t>>> fresh;  // new ids of the call
+    std::unordered_map<uint32_t, bool> in_call;
+    for (uint32_t i : idx) in_call[slots[i]] = true;
+    for (uint32_t i : idx) {
+      uint4 k;
+      memcpy(&k, ids + (size_t)16 * i, 16);
+      if (gw::id_zero(k)) continue;
+      auto& bucket = fresh[((uint64_t)k.y << 32 | k.x) ^ ((uint64_t)k.w << 32 | k.z)];
+      for (auto& e : bucket)
+        if (gw::id_eq(e.first, k)) {
+          gw::set_error("sync_set_entities: slots %u and %u are given the same entity id", e.second, slots[i]);
+          return GWAOI_ERR_INVALID;
+        }
+      bucket.push_back({k, slots[i]});
+      const uint32_t owner = lookup(k);
+      if (owner != gw::kNone && owner != slots[i] && !in_call.count(owner)) {
+        gw::set_error("sync_set_entities: entity id of slot %u is already registered to slot %u", slots[i], owner);
+        return GWAOI_ERR_INVALID;
+      }
+    }
+  }
   std::vector<uint32_t> us;
   std::vector<uint4> uk;
+  std::vector<uint8_t> reset;  // the slot's entity changes: its flags and client are reset
   // pass 1: unregister the slots' old ids (so ids may move between slots within one call)
   for (uint32_t i : idx) {
     const uint32_t slot = slots[i];
@@ -926,6 +989,7 @@ int gwaoi_sync_set_entities(gwaoi_mgr* m, const uint32_t* slots, const uint8_t* 
     memcpy(&k, ids + (size_t)16 * i, 16);
     us.push_back(slot);
     uk.push_back(k);
+    reset.push_back(gw::id_eq(s->h_id_of[slot], k) ? 0 : 1);
     if (gw::id_zero(k) || gw::id_eq(s->h_id_of[slot], k)) continue;
     uint32_t b = gw::id_hash(k) & mask, free_b = gw::kNone;
     bool dup = false;
@@ -940,8 +1004,9 @@ int gwaoi_sync_set_entities(gwaoi_mgr* m, const uint32_t* slots, const uint8_t* 
       }
       b = (b + 1) & mask;
     }
-    if (dup) {
-      gw::set_error("sync_set_entities: entity id of slot %u is already registered to slot %u", slot, s->h_hval[b]);
+    if (dup) {  // excluded by the validation above
+      gw::set_error("sync_set_entities: internal: entity id of slot %u is already registered to slot %u", slot,
+                    s->h_hval[b]);
       rc = GWAOI_ERR_INVALID;
       uk.back() = make_uint4(0, 0, 0, 0);
       continue;
@@ -963,6 +1028,7 @@ int gwaoi_sync_set_entities(gwaoi_mgr* m, const uint32_t* slots, const uint8_t* 
   a.n = (uint32_t)us.size();
   SRCHK(up.put(us, &a.slot));
   SRCHK(up.put(uk, &a.id));
+  SRCHK(up.put(reset, &a.f));
   SRCHK(gw::run_scatter(v, s, a));
   return rc;
 }
@@ -1087,8 +1153,16 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   out->n_gates = s->n_gates;
   s->goff64.assign(s->n_gates + 1, 0);
   out->gate_off = s->goff64.data();
-  if (!v.g.rec) return GWAOI_OK;  // no pass has run: nothing is present
   hipStream_t st = v.stream;
+  if (!(opts & GWAOI_COLLECT_KEEP_FLAGS)) {  // absent slots: their sync bits clear without records
+    hipLaunchKernelGGL(gw::k_clear_absent, dim3(std::min<uint32_t>(gw::blocks_for(s->cap), 4096)), dim3(gw::kSy), 0, st,
+                       s->flags, v.seq, s->cap);
+    SCHK(hipGetLastError());
+  }
+  if (!v.g.rec) {  // no pass has run: nothing is present
+    SCHK(hipStreamSynchronize(st));
+    return GWAOI_OK;
+  }
   const uint32_t bound = v.rec_bound;
   SRCHK(gw::dgrow32(&s->cnt, &s->cnt_n, (uint64_t)bound + 1));
   SRCHK(gw::ensure_scan(s, bound + 1));
@@ -1137,17 +1211,26 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   f.clear = !(opts & GWAOI_COLLECT_KEEP_FLAGS);
   f.cnt = s->cnt;
   f.n_ent = s->ictr + 8;
-  SCHK(hipMemsetAsync(s->ictr + 8, 0, 4, st));
+  f.npairs64 = (unsigned long long*)(s->ictr + 10);
+  SCHK(hipMemsetAsync(s->ictr + 8, 0, 16, st));
   SCHK(hipMemsetAsync(s->cnt, 0, ((size_t)bound + 1) * 4, st));
   const uint32_t ntiles = v.ntiles;
   if (!ntiles) return GWAOI_OK;
   hipLaunchKernelGGL(gw::k_fan_tile<false>, dim3(ntiles), dim3(gw::kSy), 0, st, f);
   gw::launch_scan(s->scan, s->cnt, bound + 1, st);
   SCHK(hipMemcpyAsync(s->h_small, s->cnt + bound, 4, hipMemcpyDeviceToHost, st));
-  SCHK(hipMemcpyAsync(s->h_small + 1, s->ictr + 8, 4, hipMemcpyDeviceToHost, st));
+  // [4] entities collected, [6..7] the 64-bit pair total
+  SCHK(hipMemcpyAsync(s->h_small + 4, s->ictr + 8, 16, hipMemcpyDeviceToHost, st));
   SCHK(hipStreamSynchronize(st));
+  uint64_t M64;
+  memcpy(&M64, s->h_small + 6, sizeof M64);
+  if (M64 > v.index_limit) {  // pair offsets are uint32: the scanned counts would have wrapped
+    gw::set_error("collect_sync: %llu records exceed the fan-out's uint32 offsets (limit %llu)",
+                  (unsigned long long)M64, (unsigned long long)v.index_limit);
+    return GWAOI_ERR_NOMEM;
+  }
   const uint32_t M = s->h_small[0];
-  out->n_entities = s->h_small[1];
+  out->n_entities = s->h_small[4];
   if (M == 0) {
     if (f.clear) {  // nothing to write, but the flags of the collected entities still clear
       f.off = s->cnt;
@@ -1289,7 +1372,7 @@ int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes,
     SCHK(hipGetLastError());
     const uint32_t bound = std::min<uint32_t>(n - seg, s->cap);
     SRCHK(gw::mgr_stage_moves_device_n(m, s->op_slot, s->op_x, s->op_z, s->bcnt + nseg, bound));
-    SCHK(hipMemcpyAsync(s->h_small, s->ictr, 12, hipMemcpyDeviceToHost, st));
+    SCHK(hipMemcpyAsync(s->h_small, s->ictr, 16, hipMemcpyDeviceToHost, st));
     SCHK(hipMemcpyAsync(s->h_small + 4, s->bcnt + nseg, 4, hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));
     ++passes;
@@ -1304,6 +1387,7 @@ int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes,
     out->n_unknown = s->h_small[1];
     out->n_rejected = s->h_small[2];
     out->n_passes = passes;
+    out->n_nonfinite = s->h_small[3];
   }
   return GWAOI_OK;
 }

@@ -185,6 +185,9 @@ class Engine:
     def debug_set_cell_side(self, v: float):
         check(self._L.gwaoi_debug_set_cell_side(self._h, v))
 
+    def debug_set_index_limit(self, v: int):
+        check(self._L.gwaoi_debug_set_index_limit(self._h, int(v)))
+
 
 class DeviceBuffer:
     """Raw device allocation via libgwaoi (no torch dependency)."""

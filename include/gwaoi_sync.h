@@ -103,6 +103,9 @@ typedef struct {
   uint32_t n_unknown;   /* EntityID not registered (entity not found: ignored, EntityManager.go:482-486) */
   uint32_t n_rejected;  /* registered but not in the manager or not syncing from its client (ignored) */
   uint32_t n_passes;    /* pipeline batches used (> 1 when an entity repeats in the payload) */
+  uint32_t n_nonfinite; /* accepted id, but x or z is NaN / +-Inf: dropped (deliberate divergence: the
+                           reference's list manager takes it, and a NaN node then cuts other entities'
+                           Mark walks) */
 } gwaoi_ingest_result;
 /* Decode bytes/32 records and stage them (after any ops already staged). All but the last batch are
  * run immediately (their events are kept for the next gwaoi_tick, like any sub-pass); the last is

@@ -51,6 +51,10 @@ int gwaoi_debug_set_cell_side(struct gwaoi_mgr* mgr, float side);
 /* Diagnostic builds only (GW_STAMPS=1): per-block phase timestamps of the last sweep launch
  * (8 x uint64 per block). Returns GWAOI_ERR_INVALID/-1 in a product build. */
 int gwaoi_debug_read_stamps(void* host, size_t bytes);
+/* Test hook: the largest entry count the relation view (gwaoi_relation_device) and the sync fan-out
+ * (gwaoi_collect_sync) accept before failing with GWAOI_ERR_NOMEM (default and maximum 2^32 - 1: their
+ * offsets are uint32). Lowering it exercises the overflow guard without a 2^32-entry workload. */
+int gwaoi_debug_set_index_limit(struct gwaoi_mgr* mgr, uint64_t limit);
 /* Diagnostics: resident sweep workgroups per CU (HIP occupancy API) and the sweep's LDS bytes. */
 int gwaoi_debug_sweep_occupancy(int device, int* blocks_per_cu, int* lds_bytes);
 

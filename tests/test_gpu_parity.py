@@ -487,3 +487,41 @@ def test_long_event_slices(gpu, po):
     rp_dev, cols_dev, nnz = eng.relation_device()
     assert rp_dev and cols_dev and nnz == len(eng.relation()[1])
     eng.close()
+
+
+def test_nonfinite_refused(gpu):
+    """NaN / +-Inf coordinates are refused (deliberate divergence): go-aoi's list manager
+    takes them and a NaN node then cuts other entities' Mark walks (tests/test_oracle.py::
+    test_nonfinite_coordinates_in_the_list_manager). Host calls return GWAOI_ERR_INVALID and stage
+    nothing (batches are validated whole); a device batch fails its device check."""
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine
+    eng = Engine(100.0, 16)
+    eng.enter(0, 0.0, 0.0)
+    eng.enter(1, 10.0, 0.0)
+    assert eng.tick().tolist() == [[1, 0 | H.EV_ENTER]]
+    for bad in (float("nan"), float("inf"), float("-inf")):
+        with pytest.raises(_lib.GwaoiError) as e:
+            eng.enter(2, bad, 0.0)
+        assert e.value.code == _lib.GWAOI_ERR_INVALID
+        with pytest.raises(_lib.GwaoiError) as e:
+            eng.moved(0, 0.0, bad)
+        assert e.value.code == _lib.GWAOI_ERR_INVALID
+    with pytest.raises(_lib.GwaoiError) as e:  # one bad entry: none of the batch is staged
+        eng.stage_moves(np.array([0, 1], np.uint32), np.array([1.0, float("nan")], np.float32),
+                        np.zeros(2, np.float32))
+    assert e.value.code == _lib.GWAOI_ERR_INVALID and eng.count() == (2, 0)
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng.stage_enters(np.array([2, 3], np.uint32), np.array([1.0, 2.0], np.float32),
+                         np.array([0.0, float("inf")], np.float32))
+    assert e.value.code == _lib.GWAOI_ERR_INVALID and eng.count() == (2, 0)
+    eng.moved(0, 150.0, 0.0)  # the manager is still usable
+    assert eng.tick().tolist() == [[0, 1]]
+    bs, bx, bz = DeviceBuffer(8), DeviceBuffer(8), DeviceBuffer(8)
+    bs.upload(np.array([0, 1], np.uint32))
+    bx.upload(np.array([1.0, float("nan")], np.float32))
+    bz.upload(np.zeros(2, np.float32))
+    eng.stage_moves_device(bs.ptr, bx.ptr, bz.ptr, 2)
+    with pytest.raises(_lib.GwaoiError) as e:
+        eng.tick()
+    assert e.value.code == _lib.GWAOI_ERR_DEVICE_CHECK

@@ -168,3 +168,32 @@ def _load_gold():
 
 
 _load_gold()
+
+
+def test_nonfinite_coordinates_in_the_list_manager(po):
+    """What the reference does with a NaN coordinate (client floats reach Moved unchecked,
+    /root/reference/components/game/GameService.go:404-408): in the list restatement (oracle (i)) a
+    node moved to NaN bubbles one place towards the head (no comparison with NaN is true) and then
+    sits in the middle of the sorted X list, where every later Mark walk that reaches it stops. A
+    third party then loses neighbours that are inside its box — behaviour that depends on list
+    position, not on positions. libgwaoi refuses non-finite coordinates instead (GWAOI_ERR_INVALID;
+    tests/test_gpu_parity.py::test_nonfinite_refused)."""
+    o = po.XZListOracle(100.0, 4)
+    for slot, x in ((3, -10.0), (0, 0.0), (1, 20.0), (2, 10.0)):  # X list: D(-10) A(0) C(10) B(20)
+        o.enter(slot, x, 0.0)
+    o.take_events()
+    o.moved(2, float("nan"), 0.0)  # C -> NaN: its box is NaN-bounded, it leaves everyone
+    ev = o.take_events()
+    assert sorted(map(tuple, ev.tolist())) == [(2, 0), (2, 1), (2, 3)]
+    o.moved(3, -11.0, 0.0)  # D steps 1 unit left: A (11 away) and B (31 away) are inside its box
+    ev = o.take_events()
+    assert sorted(map(tuple, ev.tolist())) == [(3, 0), (3, 1)]  # LEAVEs: D's X walk stopped at C
+    # +Inf is ordered (it bubbles to the tail) and only another +Inf is inside its box
+    o2 = po.XZListOracle(100.0, 3)
+    o2.enter(0, 0.0, 0.0)
+    o2.enter(1, 20.0, 0.0)
+    o2.take_events()
+    o2.enter(2, float("inf"), 0.0)
+    assert len(o2.take_events()) == 0
+    o2.moved(0, 1.0, 0.0)
+    assert len(o2.take_events()) == 0

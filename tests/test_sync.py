@@ -106,17 +106,40 @@ def fill_sync(sy, rng, n, n_gates, client_frac=0.6, flag_p=(0.25, 0.25, 0.25, 0.
     return dict(ids=ids, cids=cids, gates=gates, flags=flags, y=y, yaw=yaw)
 
 
+def check_gate_grouping(got, st):
+    """include/gwaoi_sync.h: inside a gate, records are grouped by entity (one contiguous run each) and
+    an entity's own-client record comes first in its run (checked on the unsorted output)."""
+    slot_of = {st["ids"][s].tobytes(): s for s in range(len(st["ids"]))}
+    for g, recs in got.items():
+        eids = [bytes(r) for r in recs["entity_id"]]
+        seen = set()
+        for i, e in enumerate(eids):
+            if i and eids[i - 1] == e:
+                continue
+            assert e not in seen, f"gate {g}: entity {slot_of[e]} in two runs"
+            seen.add(e)
+            s = slot_of[e]
+            own = (st["flags"][s] & R.OWN_CLIENT) and st["gates"][s] == g
+            if own:
+                assert bytes(recs["client_id"][i]) == st["cids"][s].tobytes(), f"gate {g}: own record of {s} not first"
+
+
 def check_collect(sy, orc, st, x, z, n_gates, present=None, keep=False):
     rp, cols = orc.relation()
     n = len(x)
     present = np.ones(n, bool) if present is None else present
     want, flags_after = R.collect_entity_sync_infos(rp, cols, present, st["flags"], st["gates"], st["cids"],
                                                     st["ids"], x, st["y"], z, st["yaw"], n_gates)
+    # product contract (gwaoi_sync.h): the sync bits of slots absent from the manager clear without
+    # records (entities outside AOI managers are collected on the Go side)
+    flags_after = flags_after.copy()
+    flags_after[~present] &= ~np.uint8(R.OWN_CLIENT | R.NEIGHBOR_CLIENTS)
     got = sy.collect_entity_sync_infos(keep_flags=keep)
     assert sorted(got) == sorted(want), (sorted(got), sorted(want))
     for g in want:
         gg = R.canonical_records(got[g])
         assert np.array_equal(gg, want[g]), f"gate {g}: {len(gg)} vs {len(want[g])} records"
+    check_gate_grouping(got, st)
     fl, _, _, _ = sy.read_tables()
     assert np.array_equal(fl, st["flags"] if keep else flags_after)
     return got, flags_after
@@ -189,7 +212,8 @@ def test_collect_requires_tick(gpu, oracle_lib):
 
 @pytest.mark.gpu
 def test_collect_after_leaves(gpu, oracle_lib):
-    """Entities that left are not collected; their flags stay (they are outside the manager)."""
+    """Entities that left are not collected, and their sync bits clear (they are outside the manager;
+    the Go side collects entities outside AOI managers)."""
     from goworld_amd.sync import EntitySync
     n = 1500
     eng, orc, x, z = world(oracle_lib, n, 1000.0, 100.0, 11)
@@ -313,13 +337,35 @@ def test_entity_id_registry(gpu, oracle_lib):
     rng = np.random.default_rng(41)
     st = fill_sync(sy, rng, n, 2, flag_p=(1.0, 0, 0, 0))
     sy.set_client_syncing(np.arange(n, dtype=np.uint32), np.ones(n, np.uint8))
-    # the same id on a second slot is refused
+    # the same id on a second slot is refused, and a refused call changes nothing (validated whole)
     with pytest.raises(_lib.GwaoiError) as e:
         sy.set_entities(np.array([5], np.uint32), st["ids"][6:7])
     assert e.value.code == _lib.GWAOI_ERR_INVALID
+    fresh = np.full((1, 16), 0xAB, np.uint8)
+    with pytest.raises(_lib.GwaoiError) as e:
+        sy.set_entities(np.array([4, 5], np.uint32), np.concatenate([fresh, st["ids"][6:7]]))
+    assert e.value.code == _lib.GWAOI_ERR_INVALID
+    with pytest.raises(_lib.GwaoiError) as e:  # two slots given one id in the same call
+        sy.set_entities(np.array([4, 5], np.uint32), np.concatenate([fresh, fresh]))
+    assert e.value.code == _lib.GWAOI_ERR_INVALID
+    probe = np.zeros(2, R.INGEST_RECORD)
+    probe[0]["entity_id"], probe[1]["entity_id"] = st["ids"][4].tobytes(), fresh[0].tobytes()
+    probe["x"], probe["z"] = x[4], z[4]
+    res = sy.handle_sync_position_yaw_from_client(probe.view(np.uint8))
+    assert (res.n_moved, res.n_unknown) == (1, 1)  # slot 4 still holds its old id
+    eng.tick()
+    # a new entity in a slot starts clean: flags, syncing and client of the previous one are dropped
+    sy.mark(np.array([10], np.uint32), np.zeros(1, np.float32), np.zeros(1, np.float32),
+            np.array([R.OWN_CLIENT | R.NEIGHBOR_CLIENTS], np.uint8))
+    sy.set_entities(np.array([10], np.uint32), fresh)
+    fl, gt, _, _ = sy.read_tables()
+    assert fl[10] == 0 and gt[10] == R.NO_CLIENT
+    sy.set_entities(np.array([10], np.uint32), st["ids"][10:11])
+    sy.set_client_syncing(np.array([10], np.uint32), np.ones(1, np.uint8))
     # move id of slot 7 to slot 8 (slot 8's old id is dropped), unregister slot 9
     sy.set_entities(np.array([7, 8, 9], np.uint32), np.stack([np.zeros(16, np.uint8), st["ids"][7],
                                                                np.zeros(16, np.uint8)]))
+    sy.set_client_syncing(np.array([8], np.uint32), np.ones(1, np.uint8))  # a new entity in slot 8
     recs = np.zeros(3, R.INGEST_RECORD)
     for i, s in enumerate([7, 8, 9]):
         recs[i]["entity_id"] = st["ids"][s].tobytes()
@@ -333,6 +379,7 @@ def test_entity_id_registry(gpu, oracle_lib):
     for k in range(6):
         perm = rng.permutation(n).astype(np.uint32)
         sy.set_entities(perm, st["ids"])
+        sy.set_client_syncing(np.arange(n, dtype=np.uint32), np.ones(n, np.uint8))  # new entities: syncing again
         recs = np.zeros(n, R.INGEST_RECORD)
         recs["entity_id"] = [i.tobytes() for i in st["ids"]]
         recs["x"], recs["z"] = x[perm], z[perm]
@@ -340,3 +387,27 @@ def test_entity_id_registry(gpu, oracle_lib):
         assert res.n_moved == n and res.n_unknown == 0
         want = H.oracle_tick(orc, [(H.MOVE, int(perm[i]), float(x[perm[i]]), float(z[perm[i]])) for i in range(n)])
         assert np.array_equal(eng.tick(), want)
+
+
+@pytest.mark.gpu
+def test_ingest_drops_nonfinite(gpu, oracle_lib):
+    """A client record whose x or z is NaN / +-Inf is dropped and counted (gwaoi_ingest_result.n_nonfinite;
+    deliberate divergence); y / yaw / flags of its entity are untouched."""
+    from goworld_amd.sync import EntitySync
+    n = 300
+    eng, orc, x, z = world(oracle_lib, n, 500.0, 100.0, 51)
+    sy = EntitySync(eng, 2)
+    st = fill_sync(sy, np.random.default_rng(51), n, 2, flag_p=(1.0, 0, 0, 0))
+    sy.set_client_syncing(np.arange(n, dtype=np.uint32), np.ones(n, np.uint8))
+    recs = np.zeros(4, R.INGEST_RECORD)
+    for i, (s, xx, zz) in enumerate([(1, float("nan"), 5.0), (2, 7.0, float("inf")), (3, 250.0, 250.0),
+                                     (4, float("-inf"), 1.0)]):
+        recs[i]["entity_id"] = st["ids"][s].tobytes()
+        recs[i]["x"], recs[i]["z"], recs[i]["y"], recs[i]["yaw"] = xx, zz, 9.0, 9.0
+    res = sy.handle_sync_position_yaw_from_client(recs.view(np.uint8))
+    assert (res.n_moved, res.n_nonfinite, res.n_rejected, res.n_unknown) == (1, 3, 0, 0)
+    want = H.oracle_tick(orc, [(H.MOVE, 3, 250.0, 250.0)])
+    assert np.array_equal(eng.tick(), want)
+    fl, _, gy, _ = sy.read_tables()
+    assert gy[3] == 9.0 and all(gy[s] == st["y"][s] for s in (1, 2, 4))
+    assert all(fl[s] == R.FROM_CLIENT for s in (1, 2, 4))
