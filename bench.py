@@ -146,7 +146,8 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         name += f" [dists overridden: {dists}]"
     n = n_per * nsp
     W, K, H = args.warmup, args.steps, args.latency_ticks
-    T = W + K + H + 1
+    HS = args.host_staged_ticks
+    T = W + K + H + HS + 1
     L_ = _lib.load()
 
     # ---- untimed setup: positions for every tick generated on the device ----
@@ -212,17 +213,56 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         if L_.gwaoi_debug_sweep_occupancy(dev, ctypes.byref(occ), ctypes.byref(ldsb)) == 0:
             log(f"[rank 0] sweep: {occ.value} resident blocks per CU, {ldsb.value} B LDS per block")
     if args.stamps and rank == 0:
-        buf = np.zeros(8 * 16384, dtype=np.uint64)
+        buf = np.zeros(16 * 16384, dtype=np.uint64)
         _lib.check(L_.gwaoi_debug_read_stamps(buf.ctypes.data, buf.nbytes))
-        np.save(args.stamps, buf.reshape(-1, 8))
+        np.save(args.stamps, buf.reshape(-1, 16))
 
     # ---- host-delivered latency (PCIe-inclusive; reported, never `value`) ----
     lat_host = []
-    for t in range(W + K + 1, T):
+    for t in range(W + K + 1, W + K + H + 1):
         ts = time.perf_counter()
         eng.stage_moves_device(slots.ptr, px(t), pz(t), n)
         eng.tick_raw()
         lat_host.append(time.perf_counter() - ts)
+
+    # ---- SURVEY 8(d) latency: from gwaoi_stage_moves with HOST arrays (the cgo wrapper's one call per
+    # tick) to the events in the pinned host buffer; then the events replayed into per-entity hash sets
+    # (tools/replay_sets.c: Entity.interest/uninterest, 4 set ops per pair event, Entity.go:227-246) ----
+    lat_hs, stage_hs, replay_s, replay_bad = [], [], [], 0
+    rs = None
+    if HS and args.replay and nsp == 1:
+        try:
+            from tools.replay import ReplaySets
+            rp_h, cols_h = eng.relation()
+            rs = ReplaySets(2 * len(cols_h))
+            t_ld = time.perf_counter()
+            rs.load_relation(rp_h, cols_h)
+            log(f"[rank {rank}] replay sets: {rs.size()} entries loaded in {time.perf_counter() - t_ld:.1f}s")
+            del rp_h, cols_h
+        except Exception as e:  # the tool is a bench aid: report, never fail the GPU line
+            log(f"[rank {rank}] replay sets unavailable: {e!r}")
+            rs = None
+    if HS:
+        eng.adopt_device_state()  # the restore was a device batch: host staging from here on
+    slots_h = np.arange(n, dtype=np.uint32)
+    xh = np.empty(n, np.float32)
+    zh = np.empty(n, np.float32)
+    for t in range(W + K + H + 1, T):
+        _lib.check(L_.gwaoi_dev_dtoh(dev, xh.ctypes.data, ctypes.c_void_p(px(t)), 4 * n))  # untimed
+        _lib.check(L_.gwaoi_dev_dtoh(dev, zh.ctypes.data, ctypes.c_void_p(pz(t)), 4 * n))
+        ts = time.perf_counter()
+        eng.stage_moves(slots_h, xh, zh)
+        t1 = time.perf_counter()
+        ev = eng.tick_raw()
+        te = time.perf_counter()
+        lat_hs.append(te - ts)
+        stage_hs.append(t1 - ts)
+        if rs is not None and ev.count:
+            tr = time.perf_counter()
+            replay_bad += rs.replay(ctypes.cast(ev.events, ctypes.c_void_p).value, int(ev.count))
+            replay_s.append(time.perf_counter() - tr)
+    if rs is not None:
+        rs.close()
 
     # relation size for the SURVEY §8(d) formula (directed entries |S|)
     nnz = None
@@ -282,6 +322,14 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         "p99_tick_ms": percentile(lat, 99) * 1e3,
         "p50_tick_ms_host_events": percentile(lat_host, 50) * 1e3 if lat_host else None,
         "p99_tick_ms_host_events": percentile(lat_host, 99) * 1e3 if lat_host else None,
+        "p50_tick_ms_host_staged": percentile(lat_hs, 50) * 1e3 if lat_hs else None,
+        "p99_tick_ms_host_staged": percentile(lat_hs, 99) * 1e3 if lat_hs else None,
+        "host_stage_ms": percentile(stage_hs, 50) * 1e3 if stage_hs else None,
+        "replay_ms": percentile(replay_s, 50) * 1e3 if replay_s else None,
+        "replay_note": ("events replayed into per-entity InterestedIn/InterestedBy hash sets in C, 4 set ops per "
+                        "pair event (tools/replay_sets.c); host_staged = gwaoi_stage_moves(host arrays) -> events "
+                        f"in pinned host memory, {len(lat_hs)} ticks" + (f"; {replay_bad} inconsistent set ops"
+                                                                          if replay_s else "")) if lat_hs else None,
         "events_per_tick": ev_per_tick,
         "relation_directed_entries": nnz,
         "relation_view_ms": rel_ms,
@@ -542,6 +590,10 @@ def main():
     ap.add_argument("--gates", type=int, default=8, help="gametick: gates (dense indices)")
     ap.add_argument("--client-frac", type=float, default=0.25, help="gametick: fraction of entities with a client")
     ap.add_argument("--latency-ticks", type=int, default=200, help="extra ticks with events delivered to host")
+    ap.add_argument("--host-staged-ticks", type=int, default=50,
+                    help="extra ticks staged from host arrays (gwaoi_stage_moves), events to host, replayed")
+    ap.add_argument("--no-replay", dest="replay", action="store_false",
+                    help="skip the C replay of events into per-entity hash sets")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cells-per-dist", type=float, default=None)

@@ -545,7 +545,7 @@ constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative t
 
 constexpr int kKeyBins = 128;  // mover sort keys: candidate count (clamped), kKeyBins - 1 = row walk
 #ifndef GW_SWEEP_SORT
-#define GW_SWEEP_SORT 1  // order a tile's movers by candidate count (0: listing order, A/B)
+#define GW_SWEEP_SORT 0  // 1: order a tile's movers by candidate count (A/B: no gain measured, 6 us/block)
 #endif
 struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint32_t n, enter, base, item;
@@ -845,58 +845,78 @@ __device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const 
   return true;
 }
 
+// Queue events of a wave into the block's LDS queue: one LDS atomic per call for the whole wave (a
+// ballot, the leader's add, a shuffle). Every lane of the wave that reached the call passes `has`;
+// queue overflow spills to ev_tmp with one global atomic per wave.
+__device__ __forceinline__ void emit_wave(const SweepArgs& a, SweepSmem& sm, bool has, const uint4 rec) {
+#if GW_ABL_NOEMIT  // ablation (timing only): events counted, not queued
+  return;
+#endif
+  const uint32_t li = wave_append(&sm.n, has);
+  const bool spill = has && li >= (uint32_t)kEvLds;
+  if (has && !spill) sm.ev[li] = rec;
+  const uint32_t gi = wave_append(&a.ctr[CTR_EVENTS], spill);
+  if (spill && gi < a.ev_cap) a.ev_tmp[gi] = rec;
+}
+
+// Judge candidates 0..total-1 of one stream (idx(k) = LDS record index of candidate k), 64 at a time:
+// the hot loop only records which candidates raise an event and of which kind (bit k of two per-lane
+// masks); the events are then queued a round at a time, every lane with a set bit at once
+// (emit_wave). No atomic, branch or LDS write sits in the candidate loop itself. (32-candidate chunks
+// with 32-bit masks: the register allocator spills 5x more in this kernel, measured slower.)
+template <class IdxF>
+__device__ __forceinline__ void judge_stream(const SweepArgs& a, SweepSmem& sm, const Judge& J, const Mover& m,
+                                             uint32_t total, IdxF&& idx, uint32_t& local, uint32_t& nent) {
+  for (uint32_t b = 0; __any(b < total); b += 64) {
+    const uint32_t n = b < total ? min(total - b, 64u) : 0u;
+    unsigned long long hit = 0, ent = 0;
+    uint32_t k = 0;
+    for (; k + 1 < n; k += 2) {  // two candidates per iteration: both LDS reads in flight
+      const uint32_t j0 = idx(b + k), j1 = idx(b + k + 1);
+      const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
+      const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
+      const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
+      hit |= ((unsigned long long)(e0 != 0) << k) | ((unsigned long long)(e1 != 0) << (k + 1));
+      ent |= ((unsigned long long)(e0 == 2) << k) | ((unsigned long long)(e1 == 2) << (k + 1));
+    }
+    if (k < n) {
+      const uint32_t j0 = idx(b + k);
+      const int e0 = judge_lds(J, sm.rp[j0], sm.rm[j0]);
+      hit |= (unsigned long long)(e0 != 0) << k;
+      ent |= (unsigned long long)(e0 == 2) << k;
+    }
+    while (__any(hit != 0)) {
+      const bool has = hit != 0;
+      uint4 rec = make_uint4(0, 0, 0, 0);
+      if (has) {
+        const int bit = __ffsll((long long)hit) - 1;
+        const bool enter = (ent >> bit) & 1ull;
+        rec = make_uint4(m.rank, local++, m.slot, sm.rslot[idx(b + (uint32_t)bit)] | (enter ? 0x80000000u : 0u));
+        nent += enter ? 1u : 0u;
+        hit &= hit - 1ull;
+      }
+      emit_wave(a, sm, has, rec);
+    }
+  }
+}
+
 __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Walk& w,
                                               const Region& R, const Geom& g, uint32_t& nent) {
   const Judge J = make_judge(m, a.base);
   uint32_t local = 0;
   RingStream Rs, Cs;
   if (ring_plan(w, R, sm, Rs, Cs)) {
-    // row stream: LDS record indices directly
-    uint32_t k = 0;
-    for (; k + 1 < Rs.total; k += 2) {  // two candidates per iteration: both LDS reads in flight
-      const uint32_t j0 = stream_at(Rs, k), j1 = stream_at(Rs, k + 1);
-      const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
-      const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
-      const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
-      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
-      if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j1], e1 == 2, nent);
-    }
-    if (k < Rs.total) {
-      const uint32_t j0 = stream_at(Rs, k);
-      const int e0 = judge_lds(J, sm.rp[j0], sm.rm[j0]);
-      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
-    }
-    // column stream: through the column-major index
-    for (k = 0; k + 1 < Cs.total; k += 2) {
-      const uint32_t j0 = sm.cidx[stream_at(Cs, k)], j1 = sm.cidx[stream_at(Cs, k + 1)];
-      const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
-      const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
-      const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
-      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
-      if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j1], e1 == 2, nent);
-    }
-    if (k < Cs.total) {
-      const uint32_t j0 = sm.cidx[stream_at(Cs, k)];
-      const int e0 = judge_lds(J, sm.rp[j0], sm.rm[j0]);
-      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j0], e0 == 2, nent);
-    }
+    // row stream: LDS record indices directly; column stream: through the column-major index
+    judge_stream(a, sm, J, m, Rs.total, [&](uint32_t k) { return stream_at(Rs, k); }, local, nent);
+    judge_stream(a, sm, J, m, Cs.total, [&](uint32_t k) { return (uint32_t)sm.cidx[stream_at(Cs, k)]; }, local,
+                 nent);
     return local;
   }
   walk_cells(w, [&](int r, int c0, int c1) {
     const int b = (r - R.zr0) * R.ncols - R.xr0;
-    uint32_t j = sm.lcs[b + c0];
+    const uint32_t j = sm.lcs[b + c0];
     const uint32_t e = (c0 <= c1) ? (uint32_t)sm.lcs[b + c1 + 1] : j;
-    for (; j + 1 < e; j += 2) {  // two candidates per iteration: both LDS reads in flight
-      const uint4 p0 = sm.rp[j], p1 = sm.rp[j + 1];
-      const uint2 q0 = sm.rm[j], q1 = sm.rm[j + 1];
-      const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
-      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j], e0 == 2, nent);
-      if (e1) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j + 1], e1 == 2, nent);
-    }
-    if (j < e) {
-      const int e0 = judge_lds(J, sm.rp[j], sm.rm[j]);
-      if (e0) emit(a, sm, m.rank, local++, m.slot, sm.rslot[j], e0 == 2, nent);
-    }
+    judge_stream(a, sm, J, m, e - j, [&](uint32_t k) { return j + k; }, local, nent);
   });
   return local;
 }
@@ -919,6 +939,24 @@ __device__ __forceinline__ uint32_t block_excl_scan_big(uint32_t v, uint32_t* ws
   *total = tot;
   return pre + inc - v;
 }
+
+// Diagnostic build only (GW_STAMPS=1, scripts/variants.py): per-block timestamps of the sweep's
+// phases, read back with gwaoi_debug_read_stamps. The product build compiles none of this.
+#ifndef GW_STAMPS
+#define GW_STAMPS 0
+#endif
+#if GW_STAMPS
+constexpr int kStampWords = 16;
+__device__ unsigned long long gw_stamps[kStampWords * 16384];
+#define GW_STAMP(k, v)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0 && sm.item < 16384) gw_stamps[sm.item * kStampWords + (k)] = (v); \
+  } while (0)
+#else
+#define GW_STAMP(k, v) \
+  do {                 \
+  } while (0)
+#endif
 
 constexpr int kCellsPerThread = (kRegCells + kSweepBlock - 1) / kSweepBlock;
 constexpr int kStageIters = (kCap + kSweepBlock - 1) / kSweepBlock;  // staged records per thread
@@ -967,6 +1005,7 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
   }
   uint32_t total;
   uint32_t pre = block_excl_scan_big(sum, sm.ws, &total);
+  GW_STAMP(8, __builtin_amdgcn_s_memrealtime());  // cell starts loaded and scanned
   if (total > (uint32_t)kCap) return total;
   {
     int rr = rr0, col = col0;
@@ -977,7 +1016,10 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
         sm.lcs[c] = (uint16_t)pre;
         const uint32_t core =
             ((uint32_t)(rr - tcz) < (uint32_t)kTile && (uint32_t)(col - tcx) < (uint32_t)kTile) ? kCoreBit : 0u;
-        for (uint32_t q = 0; q < n[k]; ++q) sm.rslot[pre + q] = (s0[k] + q) | core;
+        for (uint32_t q = 0; q < n[k]; ++q) {
+          sm.rslot[pre + q] = (s0[k] + q) | core;
+          sm.mv[pre + q] = (uint16_t)(rr << 7 | col);  // the record's region cell (read by the column pass)
+        }
       }
       pre += n[k];
       if (++col == R.ncols) col = 0, ++rr;
@@ -989,20 +1031,20 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
   }
   if (threadIdx.x < kKeyBins) sm.hist[threadIdx.x] = 0u;
   __syncthreads();
-  // column-major cell starts (cell counts from the row-major table) and the column-major index
-  // array: cell (rr, cc) is column-major cell cc * nrows + rr
+  GW_STAMP(9, __builtin_amdgcn_s_memrealtime());  // row-major table and source map written
+  // column-major cell starts (cell counts from the row-major table; cell (rr, cc) is column-major
+  // cell cc * nrows + rr), then the column-major index array by one scatter per record: record i of
+  // region cell (rr, cc) goes to ccs[cc * nrows + rr] + (i - lcs[rr * ncols + cc])
   {
-    uint32_t cn[kCellsPerThread], cl[kCellsPerThread];
+    uint32_t cn[kCellsPerThread];
     uint32_t sum2 = 0;
-    int cc = small_div(c0, R.nrows), rr = c0 - cc * R.nrows;  // column-major: cell cc * nrows + rr
+    int cc = small_div(c0, R.nrows), rr = c0 - cc * R.nrows;
 #pragma unroll
     for (int k = 0; k < kCellsPerThread; ++k) {
       cn[k] = 0;
-      cl[k] = 0;
       if (c0 + k < R.ncells) {
         const int c = rr * R.ncols + cc;
-        cl[k] = sm.lcs[c];
-        cn[k] = sm.lcs[c + 1] - cl[k];
+        cn[k] = sm.lcs[c + 1] - sm.lcs[c];
       }
       sum2 += cn[k];
       if (++rr == R.nrows) rr = 0, ++cc;
@@ -1012,11 +1054,21 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
 #pragma unroll
     for (int k = 0; k < kCellsPerThread; ++k) {
       if (c0 + k < R.ncells) sm.ccs[c0 + k] = (uint16_t)pre2;
-      for (uint32_t i = 0; i < cn[k]; ++i) sm.cidx[pre2 + i] = (uint16_t)(cl[k] + i);
       pre2 += cn[k];
     }
     if (threadIdx.x == 0) sm.ccs[R.ncells] = (uint16_t)total;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kStageIters; ++k) {
+      const uint32_t i = threadIdx.x + k * kSweepBlock;
+      if (i < total) {
+        const uint32_t cell = sm.mv[i], r = cell >> 7, c = cell & 127u;
+        sm.cidx[sm.ccs[c * R.nrows + r] + (i - sm.lcs[r * R.ncols + c])] = (uint16_t)i;
+      }
+    }
+    __syncthreads();  // mv is reused for the mover list below
   }
+  GW_STAMP(10, __builtin_amdgcn_s_memrealtime());  // column-major tables
   uint32_t src[kStageIters];
   Rec r[kStageIters];
 #pragma unroll
@@ -1040,6 +1092,7 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
     const uint32_t li = wave_append(&sm.nmv, lm);  // wave-uniform call: the trip count is a constant
     if (lm) sm.mv[li] = (uint16_t)i;
   }
+  GW_STAMP(11, __builtin_amdgcn_s_memrealtime());  // records gathered and staged (thread 0)
   return total;
 }
 
@@ -1094,24 +1147,6 @@ __device__ __forceinline__ Mover leaver(const SweepArgs& a, uint32_t i, float D)
   return m;
 }
 
-// Diagnostic build only (GW_STAMPS=1, scripts/variants.py): per-block timestamps of the sweep's
-// phases, read back with gwaoi_debug_read_stamps. The product build compiles none of this.
-#ifndef GW_STAMPS
-#define GW_STAMPS 0
-#endif
-#if GW_STAMPS
-constexpr int kStampWords = 8;
-__device__ unsigned long long gw_stamps[kStampWords * 16384];
-#define GW_STAMP(k, v)                                                              \
-  do {                                                                              \
-    if (threadIdx.x == 0 && sm.item < 16384) gw_stamps[sm.item * kStampWords + (k)] = (v); \
-  } while (0)
-#else
-#define GW_STAMP(k, v) \
-  do {                 \
-  } while (0)
-#endif
-
 // XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD
 // b % 8), each with its own L2. Give XCD x a contiguous run of tiles, visited in order, so the halo a
 // tile shares with its predecessor is still in that XCD's L2. A bijection on [0, n).
@@ -1148,11 +1183,10 @@ __device__ __forceinline__ Mover lds_mover(const SweepSmem& sm, uint32_t i, uint
   return m;
 }
 
-// One work item of k_sweep: a tile. Stage its region; order its movers by the length of their
-// candidate streams (LDS counting sort, heaviest first) so the lanes of a wave walk streams of about
-// the same length; walk them, one thread per mover, consecutive rounds of the block in alternating
-// direction (a tile holds ~520 movers for 512 threads: the few of the second round pair with the
-// lightest of the first). The block's LDS event queue is flushed with one global atomic at the end.
+// One work item of k_sweep: a tile. Stage its region (which lists the tile's movers); walk them, one
+// thread per mover, consecutive rounds of the block in alternating direction (a tile holds ~520
+// movers for 512 threads). The block's LDS event queue is flushed with one global atomic at the end.
+// (GW_SWEEP_SORT=1 orders the movers by candidate-stream length first: measured no faster.)
 __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, const uint32_t item) {
   uint32_t nent = 0;  // enter events of this thread's movers
   const uint32_t t = item;
@@ -1210,6 +1244,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     }
   } else {
     const uint32_t nm = sm.nmv;
+#if GW_SWEEP_SORT  // A/B: order the movers by candidate count (the lanes of a wave then walk similar streams)
     // sort key: the mover's candidate count (ring streams), or the top key for a row walk. Per mover
     // slot of this thread: key << 22 | rank inside the key << 11 | LDS record index (kCap < 2^11).
     static_assert(kCap < 2048 && kKeyBins <= 1024, "packed mover sort entry");
@@ -1223,17 +1258,14 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
         const Mover m = lds_mover(sm, i, a.base, g.D);
         const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
         uint32_t key = kKeyBins - 1u;  // row walks, and movers that leave the region (k_sweep_dense)
-#if GW_SWEEP_SORT
         RingStream Rs, Cs;
         if (R.holds(A1) && (!m.valid0 || R.holds(A0)) && ring_plan(make_walk(m, g, A0, A1), R, sm, Rs, Cs))
           key = min(Rs.total + Cs.total, (uint32_t)kKeyBins - 2u);
-#else
-        (void)A0, (void)A1;
-#endif
         ent[k] = key << 22 | atomicAdd(&sm.hist[key], 1u) << 11 | i;
       }
     }
     __syncthreads();
+    GW_STAMP(12, __builtin_amdgcn_s_memrealtime());  // sort keys counted
     if (threadIdx.x < 64) {  // descending exclusive scan of the key histogram: key kKeyBins-1 first
       const uint32_t b0 = kKeyBins - 1 - 2 * threadIdx.x, b1 = b0 - 1;
       const uint32_t h0 = sm.hist[b0], h1 = sm.hist[b1];
@@ -1247,6 +1279,8 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
       if (threadIdx.x + k * kSweepBlock < nm)
         sm.mv[sm.hist[ent[k] >> 22] + ((ent[k] >> 11) & 2047u)] = (uint16_t)(ent[k] & 2047u);
     __syncthreads();
+    GW_STAMP(13, __builtin_amdgcn_s_memrealtime());  // movers ordered: the walk starts
+#endif
     if (a.use_lds != 2) {  // 2: ablation (timing only), staging and ordering without the walk
       for (uint32_t r = 0; r * kSweepBlock < nm; ++r) {
         const uint32_t p = r * kSweepBlock + ((r & 1u) ? (uint32_t)(kSweepBlock - 1) - threadIdx.x : threadIdx.x);

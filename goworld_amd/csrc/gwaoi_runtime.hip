@@ -1135,7 +1135,34 @@ int gwaoi_stage_moves(gwaoi_mgr* m, const uint32_t* slots, const float* x, const
     }
     RCHK(check_coord("stage_moves", s, x[i], z[i]));
   }
-  for (uint32_t i = 0; i < n; ++i) RCHK(gwaoi_moved(m, slots[i], x[i], z[i]));
+  if (!n) return GWAOI_OK;
+  RCHK(set_dev(m));
+  if (m->dv_n) RCHK(run_pass(m, true));
+  // bulk path (the cgo wrapper's one call per tick): runs of entries without a repeated slot are
+  // stamped, then copied into the pinned staging arrays; a repeated slot flushes the batch first
+  // (sub-pass), exactly as gwaoi_moved would
+  bool any_auto = false;
+  for (const SpaceHost& sh : m->spaces) any_auto |= sh.auto_extent;
+  uint32_t i = 0;
+  while (i < n) {
+    uint32_t e = i;
+    const uint32_t room = m->cap - m->n_ops;  // a pass holds at most cap ops (one per slot)
+    for (; e < n && e - i < room; ++e) {
+      const uint32_t s = slots[e];
+      if (m->h_stamp[s] == m->pass_id) break;
+      m->h_stamp[s] = m->pass_id;
+      m->h_op_space[m->n_ops + (e - i)] = m->h_space_of[s];
+      if (any_auto) note_coord(m, m->h_space_of[s], x[e], z[e]);
+    }
+    const uint32_t k = e - i, o = m->n_ops;
+    std::memcpy(m->h_op_slot + o, slots + i, (size_t)k * sizeof(uint32_t));
+    std::memcpy(m->h_op_x + o, x + i, (size_t)k * sizeof(float));
+    std::memcpy(m->h_op_z + o, z + i, (size_t)k * sizeof(float));
+    std::memset(m->h_op_kind + o, gw::OP_MOVE, k);
+    m->n_ops += k;
+    i = e;
+    if (i < n) RCHK(run_pass(m, true));  // slots[i] already has an op in this batch
+  }
   return GWAOI_OK;
 }
 
@@ -1190,6 +1217,28 @@ int gwaoi_stage_ops_device_n(gwaoi_mgr* m, const uint32_t* d_slots, const float*
   m->dv_space = d_spaces;
   m->dv_count = d_n;
   m->dv_n = n;
+  return GWAOI_OK;
+}
+
+int gwaoi_adopt_device_state(gwaoi_mgr* m) {
+  RCHK(check_mgr(m));
+  RCHK(set_dev(m));
+  if (m->n_ops || m->dv_n) {
+    set_err("adopt_device_state: ops are staged; run gwaoi_tick first");
+    return GWAOI_ERR_STATE;
+  }
+  std::vector<uint32_t> q(m->cap), sp(m->cap);
+  HIPCHK(hipStreamSynchronize(m->stream));
+  HIPCHK(hipMemcpy(q.data(), m->seq, (size_t)m->cap * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(sp.data(), m->space_of, (size_t)m->cap * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  uint32_t np = 0;
+  for (uint32_t s = 0; s < m->cap; ++s) {
+    m->h_present[s] = q[s] != 0;
+    m->h_space_of[s] = sp[s];
+    np += q[s] != 0;
+  }
+  m->n_present = m->n_present_dev = np;
+  m->dev_managed = false;
   return GWAOI_OK;
 }
 

@@ -102,6 +102,10 @@ class Engine:
                                                 ctypes.c_void_p(d_z), ctypes.c_void_p(d_kinds),
                                                 ctypes.c_void_p(d_spaces or None), ctypes.c_void_p(d_count or None), n))
 
+    def adopt_device_state(self):
+        """Host-staged calls are accepted again after mixed device batches (gwaoi_adopt_device_state)."""
+        check(self._L.gwaoi_adopt_device_state(self._h))
+
     def set_stream(self, stream_ptr: int):
         check(self._L.gwaoi_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
 

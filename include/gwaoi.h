@@ -134,6 +134,11 @@ int gwaoi_stage_ops_device_spaces(gwaoi_mgr* mgr, const uint32_t* d_slots, const
 int gwaoi_stage_ops_device_n(gwaoi_mgr* mgr, const uint32_t* d_slots, const float* d_x, const float* d_z,
                              const uint8_t* d_kinds, const uint32_t* d_spaces, const uint32_t* d_n, uint32_t n_max);
 
+/* After mixed device batches (e.g. a silent bulk restore from HBM, EntityManager.go:591-652): pull the
+ * presence state back into the host mirror so the host-staged calls above are accepted again. No op may
+ * be staged. Auto-extent Spaces do not see the adopted coordinates (give restored Spaces extents). */
+int gwaoi_adopt_device_state(gwaoi_mgr* mgr);
+
 /* Apply every staged op; blocks until the events are on the host (or in device memory, see flags). */
 #define GWAOI_TICK_DEVICE_EVENTS 1u /* leave events in device memory (no D2H copy) */
 int gwaoi_tick(gwaoi_mgr* mgr, gwaoi_events* out);

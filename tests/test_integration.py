@@ -162,3 +162,36 @@ def test_index_limit_guards(gpu, oracle_lib):
     assert e.value.code == _lib.GWAOI_ERR_NOMEM
     eng.debug_set_index_limit(1 << 40)  # clamped to 2^32 - 1
     check_collect(sy, orc, st, x, z, 3)
+
+
+@pytest.mark.gpu
+def test_adopt_device_state_then_host_staging(gpu, oracle_lib):
+    """A silent bulk restore from HBM (mixed device batch, EntityManager.go:591-652) followed by host-staged
+    Moved calls: gwaoi_adopt_device_state pulls presence back to the host mirror; events then equal the
+    list oracle's for the same calls."""
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine
+    case = H.case_walk(0x5EED00AD, 4000, 1400.0, 4, workload=oracle_lib)
+    n = 4000
+    x0 = np.asarray([o[2] for o in case["ticks"][0]], np.float32)
+    z0 = np.asarray([o[3] for o in case["ticks"][0]], np.float32)
+    eng = Engine(100.0, n, bounds=case["bounds"])
+    bs, bx, bz, bk = DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(n)
+    bs.upload(np.arange(n, dtype=np.uint32))
+    bx.upload(x0)
+    bz.upload(z0)
+    bk.upload(np.full(n, _lib.GWAOI_OP_ENTER | _lib.GWAOI_OP_SILENT, np.uint8))
+    eng.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, n)
+    assert len(eng.tick()) == 0
+    with pytest.raises(_lib.GwaoiError):
+        eng.moved(0, 1.0, 1.0)  # presence lives on the device
+    eng.adopt_device_state()
+    assert eng.count() == (n, 0)
+    orc = oracle_lib.XZListOracle(100.0, n)
+    orc.bulk_enter(np.arange(n, dtype=np.uint32), x0, z0)
+    for t, ops in enumerate(case["ticks"][1:], 1):
+        want = H.oracle_tick(orc, ops)
+        got = H.gpu_tick(eng, ops)
+        assert np.array_equal(got, want), f"tick {t}: " + H.fmt_diff(got, want)
+    rg, ro = eng.relation(), orc.relation()
+    assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1])

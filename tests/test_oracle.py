@@ -197,3 +197,26 @@ def test_nonfinite_coordinates_in_the_list_manager(po):
     assert len(o2.take_events()) == 0
     o2.moved(0, 1.0, 0.0)
     assert len(o2.take_events()) == 0
+
+
+def test_replay_tool_tracks_the_relation(po):
+    """tools/replay_sets.c (bench.py's replay_ms): replaying a tick's events into InterestedIn /
+    InterestedBy sets keeps them equal to the relation, with no inconsistent set operation."""
+    import __graft_entry__ as G
+    G.build_tools()
+    from tools.replay import ReplaySets
+    case = H.case_walk(0x5EED0001, 3000, 1200.0, 3, workload=po)
+    orc = po.XZListOracle(100.0, 3000)
+    H.oracle_tick(orc, case["ticks"][0])
+    rp, cols = orc.relation()
+    rs = ReplaySets(2 * len(cols))
+    rs.load_relation(rp, cols)
+    assert rs.size() == 2 * len(cols)
+    for ops in case["ticks"][1:]:
+        ev = np.ascontiguousarray(H.oracle_tick(orc, ops))
+        assert len(ev) > 0
+        assert rs.replay(ev.ctypes.data, len(ev)) == 0
+        assert rs.size() == 2 * len(orc.relation()[1])
+    bad = np.ascontiguousarray(ev[-1:])  # replaying the last change of a pair again is inconsistent
+    assert rs.replay(bad.ctypes.data, 1) == 4
+    rs.close()

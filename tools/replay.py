@@ -1,0 +1,41 @@
+"""ctypes front end of tools/replay_sets.c (bench tool): the Go-side callback sink — four hash-set
+operations per pair event (Entity.interest / uninterest, /root/reference/engine/entity/Entity.go:227-246)."""
+import ctypes
+import os
+
+import numpy as np
+
+_SO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_bin", "libreplay.so")
+
+
+class ReplaySets:
+    def __init__(self, expect_entries: int):
+        L = ctypes.CDLL(_SO)
+        vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
+        L.rs_create.argtypes, L.rs_create.restype = [u64], vp
+        L.rs_destroy.argtypes = [vp]
+        L.rs_load_relation.argtypes = [vp, vp, vp, u32]
+        L.rs_replay.argtypes, L.rs_replay.restype = [vp, vp, u64], u64
+        L.rs_size.argtypes, L.rs_size.restype = [vp], u64
+        self._L = L
+        self._h = L.rs_create(int(expect_entries))
+        if not self._h:
+            raise MemoryError("rs_create")
+
+    def load_relation(self, row_ptr: np.ndarray, cols: np.ndarray):
+        rp = np.ascontiguousarray(row_ptr, np.uint32)
+        c = np.ascontiguousarray(cols, np.uint32)
+        self._L.rs_load_relation(self._h, rp.ctypes.data, c.ctypes.data, len(rp) - 1)
+
+    def replay(self, events_ptr: int, count: int) -> int:
+        """Replay `count` events at host address events_ptr ({mover, other|ENTER} u32 pairs); returns
+        the number of inconsistent set operations (0 = the events are exactly the relation's changes)."""
+        return int(self._L.rs_replay(self._h, ctypes.c_void_p(events_ptr), int(count)))
+
+    def size(self) -> int:
+        return int(self._L.rs_size(self._h))
+
+    def close(self):
+        if self._h:
+            self._L.rs_destroy(self._h)
+            self._h = None
