@@ -46,7 +46,9 @@ TOOL_SYMBOLS = (
 # include/gwaoi_strips.h (X-strip partition over several GPUs)
 STRIP_SYMBOLS = (
     "gwaoi_strip_init_walk", "gwaoi_strip_walk", "gwaoi_strip_ingest", "gwaoi_strip_select",
-    "gwaoi_strip_absorb", "gwaoi_strip_emit", "gwaoi_strip_scratch_words",
+    "gwaoi_strip_absorb", "gwaoi_strip_emit", "gwaoi_strip_scratch_words", "gwaoi_strip_init_skew",
+    "gwaoi_strip_absorb_n", "gwaoi_strip_comm_id", "gwaoi_strip_comm_init", "gwaoi_strip_comm_destroy",
+    "gwaoi_strip_exchange",
 )
 
 
@@ -209,6 +211,12 @@ def load(path: str = SO_PATH):
         "gwaoi_strip_absorb": ([vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_strip_emit": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "gwaoi_strip_scratch_words": ([u32], ctypes.c_size_t),
+        "gwaoi_strip_init_skew": ([vp, vp, vp, vp, vp, u64, f32, u32, f32, u32], ctypes.c_int),
+        "gwaoi_strip_absorb_n": ([vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_strip_comm_id": ([vp], ctypes.c_int),
+        "gwaoi_strip_comm_init": ([vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
+        "gwaoi_strip_comm_destroy": ([vp], ctypes.c_int),
+        "gwaoi_strip_exchange": ([vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp, u32, vp, vp, vp], ctypes.c_int),
         "gwaoi_wl_pack_ingest": ([ctypes.c_int, vp, vp, vp, u32, u32, vp], ctypes.c_int),
         "gwaoi_sync_enable": ([vp, u32], ctypes.c_int),
         "gwaoi_sync_get_tables": ([vp, ctypes.POINTER(SyncTables)], ctypes.c_int),

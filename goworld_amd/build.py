@@ -14,9 +14,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgwaoi.so")
-SOURCES = ["gwaoi_kernels.hip", "gwaoi_runtime.hip", "gwaoi_strips.hip", "gwaoi_sync.hip"]
+SOURCES = ["gwaoi_kernels.hip", "gwaoi_runtime.hip", "gwaoi_strips.hip", "gwaoi_sync.hip", "gwaoi_comm.hip"]
 HEADERS = ["gwaoi_internal.h"]
-PUBLIC = ["gwaoi.h", "gwaoi_tools.h", "gwaoi_workload.h", "gwaoi_strips.h"]
+PUBLIC = ["gwaoi.h", "gwaoi_tools.h", "gwaoi_workload.h", "gwaoi_strips.h", "gwaoi_sync.h"]
 ARCH = os.environ.get("GWAOI_ARCH", "gfx950")
 
 
@@ -50,6 +50,7 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
         f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
         *[f"-D{d}" for d in defines],
         *[os.path.join(CSRC, f) for f in SOURCES],
+        "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib",  # the X-strip halo exchange (gwaoi_comm.hip)
         "-o", out + ".tmp",
     ]
     if verbose:

@@ -67,6 +67,23 @@ __global__ void __launch_bounds__(kSBlock) k_strip_init_walk(gwaoi_strip_geom g,
   flags[i] = f;
 }
 
+__global__ void __launch_bounds__(kSBlock) k_strip_init_skew(gwaoi_strip_geom g, uint8_t* flags, float* ex, float* ez,
+                                                             uint64_t seed, float L, uint32_t nhot, float sigma,
+                                                             uint32_t hot_every) {
+  const uint32_t i = blockIdx.x * kSBlock + threadIdx.x;
+  if (i >= g.n) return;
+  const float x = gww_skew_init_coord(seed, g.n, i, 0, L, nhot, sigma, hot_every);
+  const float z = gww_skew_init_coord(seed, g.n, i, 1, L, nhot, sigma, hot_every);
+  uint8_t f = 0;
+  if (in_range(x, g.ra, g.rb)) {
+    f |= GWAOI_STRIP_END;
+    ex[i] = x;
+    ez[i] = z;
+  }
+  if (in_range(x, g.xa, g.xb)) f |= GWAOI_STRIP_OWNED;
+  flags[i] = f;
+}
+
 __global__ void __launch_bounds__(kSBlock) k_strip_walk(gwaoi_strip_geom g, uint8_t* flags, const float* sx,
                                                         const float* sz, float* ex, float* ez, uint64_t seed,
                                                         uint64_t tick, float L, float step, uint32_t* err) {
@@ -132,8 +149,9 @@ __global__ void __launch_bounds__(kSBlock) k_strip_select(gwaoi_strip_geom g, co
 }
 
 __global__ void __launch_bounds__(kSBlock) k_strip_absorb(uint8_t* flags, float* ex, float* ez, const uint4* recs,
-                                                          uint32_t n) {
+                                                          uint32_t n, const uint32_t* d_n) {
   const uint32_t k = blockIdx.x * kSBlock + threadIdx.x;
+  if (d_n) n = min(n, *d_n);  // received count (device): the launch covers the message's capacity
   if (k >= n) return;
   const uint4 r = recs[k];
   ex[r.x] = __uint_as_float(r.y);
@@ -264,7 +282,25 @@ int gwaoi_strip_absorb(void* stream, uint8_t* flags, float* ex, float* ez, const
   if (!flags || !ex || !ez || (n && !d_recs)) return GWAOI_ERR_INVALID;
   if (n)
     hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n), dim3(gw::kSBlock), 0, (hipStream_t)stream, flags, ex, ez,
-                       reinterpret_cast<const uint4*>(d_recs), n);
+                       reinterpret_cast<const uint4*>(d_recs), n, (const uint32_t*)nullptr);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_absorb_n(void* stream, uint8_t* flags, float* ex, float* ez, const uint32_t* d_recs, const uint32_t* d_n,
+                         uint32_t n_max) {
+  if (!flags || !ex || !ez || !d_n || (n_max && !d_recs)) return GWAOI_ERR_INVALID;
+  if (n_max)
+    hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n_max), dim3(gw::kSBlock), 0, (hipStream_t)stream, flags, ex,
+                       ez, reinterpret_cast<const uint4*>(d_recs), n_max, d_n);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_init_skew(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* ex, float* ez, uint64_t seed,
+                          float L, uint32_t nhot, float sigma, uint32_t hot_every) {
+  if (!g || !flags || !ex || !ez) return GWAOI_ERR_INVALID;
+  if (g->n)
+    hipLaunchKernelGGL(gw::k_strip_init_skew, gw::blocks_for(g->n), dim3(gw::kSBlock), 0, (hipStream_t)stream, *g,
+                       flags, ex, ez, seed, L, nhot, sigma, hot_every);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 

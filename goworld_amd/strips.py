@@ -32,21 +32,49 @@ f32 = np.float32
 
 
 class StripLayout:
-    """Equal-width strips over [0, L) in x; the halo covers D + the largest per-tick step."""
+    """Strips over [0, L) in x: equal widths (config 4's uniform world), or explicit inner edges (e.g.
+    x-quantiles of a skewed crowd, config 5: from_quantiles). The halo covers D + the largest per-tick
+    step."""
 
-    def __init__(self, world: int, L: float, dist: float, max_step: float, margin: Optional[float] = None):
+    def __init__(self, world: int, L: float, dist: float, max_step: float, margin: Optional[float] = None,
+                 edges: Optional[Sequence[float]] = None):
         self.world, self.L, self.dist, self.max_step = int(world), float(L), float(dist), float(max_step)
         # query boxes are widened by (|c| + D) * 2^-20 before they become cell ranges; the halo keeps a
         # margin far above that and above float rounding of the bounds
         if margin is None:
             margin = max(1.0, (self.L + self.dist) * 2.0 ** -16)
         self.halo = float(f32(self.dist + self.max_step + margin))
-        if self.world > 1 and self.L / self.world <= 2 * self.halo + self.max_step:
-            raise ValueError(f"strips of width {self.L / self.world} are too narrow for a halo of {self.halo}")
+        if edges is None:
+            edges = [rank * self.L / self.world for rank in range(1, self.world)]
+        if len(edges) != self.world - 1:
+            raise ValueError(f"{self.world} strips need {self.world - 1} inner edges, got {len(edges)}")
+        self.edges = [float(f32(e)) for e in edges]
+        lo = [0.0] + self.edges
+        hi = self.edges + [self.L]
+        for r in range(self.world):
+            if self.world > 1 and hi[r] - lo[r] <= 2 * self.halo + self.max_step:
+                raise ValueError(f"strip {r} of width {hi[r] - lo[r]} is too narrow for a halo of {self.halo}")
+
+    @classmethod
+    def from_quantiles(cls, world: int, x: np.ndarray, L: float, dist: float, max_step: float,
+                       margin: Optional[float] = None) -> "StripLayout":
+        """Inner edges at the x-quantiles of the entities (equal entity counts per strip, SURVEY.md §8(e)
+        config 5), each strip kept wider than 2 halo + step (narrow quantile strips are merged into
+        their neighbours' width by pushing the edge out)."""
+        probe = cls(1, L, dist, max_step, margin)
+        min_w = 2 * probe.halo + max_step + 1.0
+        q = np.quantile(np.asarray(x, dtype=np.float64), [r / world for r in range(1, world)]) if world > 1 else []
+        edges, prev = [], 0.0
+        for r, e in enumerate(q):
+            left = world - 1 - r  # strips still to place right of this edge
+            e = min(max(float(e), prev + min_w), L - left * min_w)
+            edges.append(e)
+            prev = e
+        return cls(world, L, dist, max_step, margin, edges=edges)
 
     def bounds(self, rank: int) -> Tuple[float, float]:
-        xa = -math.inf if rank == 0 else float(f32(rank * self.L / self.world))
-        xb = math.inf if rank == self.world - 1 else float(f32((rank + 1) * self.L / self.world))
+        xa = -math.inf if rank == 0 else self.edges[rank - 1]
+        xb = math.inf if rank == self.world - 1 else self.edges[rank]
         return xa, xb
 
     def owner_of(self, x: np.ndarray) -> np.ndarray:
@@ -77,8 +105,10 @@ class StripNode:
     """The strip of GPU `rank`: per-id state, the region's gwaoi manager, the per-tick kernels."""
 
     def __init__(self, layout: StripLayout, rank: int, n: int, device: int = 0, seed: int = 0x5EED0004,
-                 halo_cap: Optional[int] = None):
+                 halo_cap: Optional[int] = None, skew: Optional[Tuple[int, float, int]] = None):
+        """skew = (nhot, sigma, hot_every): the skewed-crowd placement of config 5 instead of uniform."""
         self.layout, self.rank, self.n, self.seed = layout, int(rank), int(n), int(seed)
+        self.skew = skew
         self.g = layout.geom(rank, n)
         self.device = torch.device("cuda", device)
         self._L = _lib.load()
@@ -89,12 +119,14 @@ class StripNode:
         self.ids = torch.zeros(n, dtype=i32, device=dev)
         self.ox, self.oz = torch.zeros(n, dtype=fl, device=dev), torch.zeros(n, dtype=fl, device=dev)
         self.kinds = torch.zeros(n, dtype=u8, device=dev)
-        # the halo of one side holds ~ 2 H L density entities; keep room for several times that
-        cap = halo_cap or max(4096, int(8 * layout.halo * layout.L * n / (layout.L * layout.L)) + 4096)
+        # the halo of one side holds ~ 2 H L density entities; keep room for several times that (a skewed
+        # crowd can put a hotspot on an edge: more)
+        cap = halo_cap or max(4096, int((32 if skew else 8) * layout.halo * layout.L * n / (layout.L * layout.L)) + 4096)
         self.cap = min(cap, n) if n else 1
         self.left = torch.zeros((self.cap, 4), dtype=i32, device=dev)
         self.right = torch.zeros((self.cap, 4), dtype=i32, device=dev)
         self.counts = torch.zeros(4, dtype=i32, device=dev)  # [left, right, n_ops, err]
+        self.left_in, self.right_in, self.counts_in = None, None, None  # RCCL receive buffers (tick_rccl)
         self.h_counts = torch.zeros(4, dtype=i32).pin_memory()  # read after each tick, no extra sync
         self.scratch = torch.zeros(int(self._L.gwaoi_strip_scratch_words(n)), dtype=i32, device=dev)
         # a stream of the node's own (never the null stream: the manager would take that as "its
@@ -139,8 +171,16 @@ class StripNode:
     def start(self, host_events: bool = False):
         """Tick 0: every entity of the region enters (the seeded workload's initial placement)."""
         with torch.cuda.stream(self.stream):
-            check(self._L.gwaoi_strip_init_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
-                                                ctypes.c_uint64(self.seed), ctypes.c_float(self.layout.L)))
+            if self.skew:
+                nhot, sigma, every = self.skew
+                check(self._L.gwaoi_strip_init_skew(self._s(), self._g(), _ptr(self.flags), _ptr(self.ex),
+                                                    _ptr(self.ez), ctypes.c_uint64(self.seed),
+                                                    ctypes.c_float(self.layout.L), int(nhot), ctypes.c_float(sigma),
+                                                    int(every)))
+            else:
+                check(self._L.gwaoi_strip_init_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.ex),
+                                                    _ptr(self.ez), ctypes.c_uint64(self.seed),
+                                                    ctypes.c_float(self.layout.L)))
             self.tick_no = 0
             return self._emit_and_tick(host_events, self.n)
 
@@ -188,8 +228,84 @@ class StripNode:
                                                      _ptr(recs), int(recs.shape[0])))
             return self._emit_and_tick(host_events, self.eng.count()[0] + nin)
 
+    def tick_rccl(self, t: int, comm: "StripComm", host_events: bool = False, step: float = 1.0,
+                  moves: Optional[Tuple[torch.Tensor, ...]] = None, peers: Optional[Tuple[int, int]] = None):
+        """One whole tick with the halo exchange over RCCL inside libgwaoi (gwaoi_strip_exchange): walk /
+        ingest, select, exchange, absorb, emit and the AOI pipeline all enqueued on the node's stream,
+        no host round trip before the pipeline's own end-of-pass read. peers = (left, right) rank or -1
+        (default: the neighbouring ranks)."""
+        if self.left_in is None:
+            dev = self.device
+            self.left_in = torch.zeros((self.cap, 4), dtype=torch.int32, device=dev)
+            self.right_in = torch.zeros((self.cap, 4), dtype=torch.int32, device=dev)
+            self.counts_in = torch.zeros(2, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize(dev)
+        if peers is None:
+            peers = (self.rank - 1 if self.g.has_left else -1, self.rank + 1 if self.g.has_right else -1)
+        if moves is not None:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        L = self._L
+        with torch.cuda.stream(self.stream):
+            if moves is None:
+                check(L.gwaoi_strip_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz),
+                                         _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed), ctypes.c_uint64(t),
+                                         ctypes.c_float(self.layout.L), ctypes.c_float(step), self._err()))
+            else:
+                ids, x, z = moves
+                check(L.gwaoi_strip_ingest(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
+                                           _ptr(self.ez), _ptr(ids), _ptr(x), _ptr(z), int(ids.numel()), self._err()))
+            check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
+                                       _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
+                                       ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+            check(L.gwaoi_strip_exchange(comm.handle, self._s(), int(peers[0]), int(peers[1]), _ptr(self.left),
+                                         _ptr(self.right), _ptr(self.counts), self.cap, _ptr(self.left_in),
+                                         _ptr(self.right_in), _ptr(self.counts_in)))
+            for k, recs in enumerate((self.left_in, self.right_in)):
+                if peers[k] >= 0:
+                    check(L.gwaoi_strip_absorb_n(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
+                                                 _ptr(recs), ctypes.c_void_p(self.counts_in.data_ptr() + 4 * k),
+                                                 self.cap))
+            self.tick_no = t
+            return self._emit_and_tick(host_events, self.eng.count()[0] + 2 * self.cap)
+
     def close(self):
         self.eng.close()
+
+
+class StripComm:
+    """The RCCL communicator of a strip world inside libgwaoi (gwaoi_strip_comm_*): one rank per GPU.
+    The 128-byte id is made on rank 0 and handed to the ranks by the caller (from_dist: over
+    torch.distributed; a Go deployment uses its own transport)."""
+
+    def __init__(self, comm_id: bytes, world: int, rank: int, device: int):
+        L = _lib.load()
+        self._L = L
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(comm_id)
+        check(L.gwaoi_strip_comm_init(buf, int(world), int(rank), int(device), ctypes.byref(h)))
+        self.handle = h
+        self.world, self.rank = int(world), int(rank)
+
+    @staticmethod
+    def make_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        check(_lib.load().gwaoi_strip_comm_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def from_dist(cls, rank: int, world: int, device: int) -> "StripComm":
+        import torch.distributed as dist
+        t = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            t[:] = torch.frombuffer(bytearray(cls.make_id()), dtype=torch.uint8)
+        obj = [bytes(t.numpy())]
+        dist.broadcast_object_list(obj, src=0)
+        return cls(obj[0], world, rank, device)
+
+    def close(self):
+        if self.handle and self.handle.value:
+            self._L.gwaoi_strip_comm_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
 
 
 class LoopbackExchange:

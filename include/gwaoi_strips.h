@@ -19,8 +19,9 @@
  *
  * Per tick: (1) end positions of owned entities (gwaoi_strip_walk: the bench's seeded walk, or
  * gwaoi_strip_ingest: external moves); (2) gwaoi_strip_select: owned entities with start or end x
- * within the neighbours' regions -> two record lists; (3) the host exchanges them with the
- * neighbours (torch.distributed send/recv = RCCL on xGMI); (4) gwaoi_strip_absorb the received lists;
+ * within the neighbours' regions -> two record lists; (3) gwaoi_strip_exchange swaps them with the
+ * neighbours over RCCL/xGMI on the GPU's stream (or the host moves them: any transport);
+ * (4) gwaoi_strip_absorb[_n] the received lists;
  * (5) gwaoi_strip_emit: the op list in id order + the state advance; (6) gwaoi_stage_ops_device +
  * gwaoi_tick. Host side: goworld_amd/strips.py. All functions enqueue on `stream` (a hipStream_t;
  * NULL = the null stream) and return at once; counts land in device memory.
@@ -79,6 +80,33 @@ int gwaoi_strip_emit(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, fl
                      const float* ez, uint32_t* d_ids, float* d_x, float* d_z, uint8_t* d_kinds, uint32_t* d_scratch,
                      uint32_t* d_n_ops);
 size_t gwaoi_strip_scratch_words(uint32_t n);
+
+/* Skewed-crowd variant of gwaoi_strip_init_walk (gww_skew_init_coord). */
+int gwaoi_strip_init_skew(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* ex, float* ez,
+                          uint64_t seed, float L, uint32_t nhot, float sigma, uint32_t hot_every);
+/* gwaoi_strip_absorb with the record count in device memory (min(*d_n, n_max) records). */
+int gwaoi_strip_absorb_n(void* stream, uint8_t* flags, float* ex, float* ez, const uint32_t* d_recs,
+                         const uint32_t* d_n, uint32_t n_max);
+
+/* ---- the halo exchange over RCCL (xGMI), device-resident end to end ----
+ * One communicator per strip world, one rank per GPU. Rank 0 makes the id; the caller hands the 128
+ * bytes to every rank over whatever channel the deployment has (the game processes' own transport,
+ * torch.distributed in goworld_amd/strips.py); then every rank calls gwaoi_strip_comm_init. */
+#define GWAOI_STRIP_COMM_ID_BYTES 128 /* ncclUniqueId */
+typedef struct gwaoi_strip_comm gwaoi_strip_comm;
+int gwaoi_strip_comm_id(uint8_t* id /* [GWAOI_STRIP_COMM_ID_BYTES] */);
+int gwaoi_strip_comm_init(const uint8_t* id, int nranks, int rank, int device, gwaoi_strip_comm** out);
+int gwaoi_strip_comm_destroy(gwaoi_strip_comm* comm);
+/* One tick's exchange, one RCCL group enqueued on `stream`, no host synchronisation: to left_peer the
+ * count d_counts[0] and the records d_left[0..cap), from it d_counts_in[0] and d_left_in[0..cap); the
+ * same with right_peer, d_counts[1] / d_right / d_counts_in[1] / d_right_in. A peer < 0 means no
+ * neighbour on that side (its received count is set to 0). Messages have fixed sizes (cap records of
+ * 4 x uint32), so the select lists' counts never travel to the host; absorb with
+ * gwaoi_strip_absorb_n(d_left_in, d_counts_in + 0, cap) and (d_right_in, d_counts_in + 1, cap). A
+ * peer equal to the caller's own rank is a loopback (send and receive match in issue order). */
+int gwaoi_strip_exchange(gwaoi_strip_comm* comm, void* stream, int left_peer, int right_peer, const uint32_t* d_left,
+                         const uint32_t* d_right, const uint32_t* d_counts, uint32_t cap, uint32_t* d_left_in,
+                         uint32_t* d_right_in, uint32_t* d_counts_in);
 
 #ifdef __cplusplus
 }
