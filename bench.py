@@ -16,7 +16,10 @@ Other workloads (--workload; the JSON line names the one measured):
   gametick one GoWorld game tick per step at config-2 scale: client position records ingested on the GPU,
            the AOI tick, and the sync fan-out into per-gate packet bodies (include/gwaoi_sync.h)
   strips   config 4: ONE world of 2M entities per GPU (16M, L = 140,000 at 8 GPUs) cut into X-strips,
-           halo records exchanged with the neighbour GPUs every tick (torch.distributed = RCCL/xGMI)
+           halo records exchanged with the neighbour GPUs every tick by gwaoi_strip_exchange (RCCL
+           p2p over xGMI inside libgwaoi, on the strip's stream)
+  strips_skew  config 5 in strips: the same world, 10% of the entities in Gaussian hotspots, strip
+           edges at the x-quantiles of the entities
 
 Prints ONE JSON line on rank 0. Also reports: p50/p99 tick latency with events left in HBM and with
 events delivered to host memory (PCIe-inclusive, never `value`), the sweep kernel's roofline, and
@@ -430,6 +433,7 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
         step(t, None)
     eng.set_timing(True)
     eng.reset_stats()
+    sy.reset_stats()
     sync_all()
     lat = []
     t0 = time.perf_counter()
@@ -438,6 +442,7 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
     sync_all()
     elapsed = allmax(time.perf_counter() - t0)
     st = eng.stats()
+    ss = sy.stats()
     eng.close()
     if rank != 0:
         return None
@@ -447,13 +452,31 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
     moved = float(a[:, 5].mean())
     ticks = max(1, st["ticks"])
     rec_grid = st["grid_records"] / ticks
-    # algorithmic bytes: fan-out = records written (48 B) + per entity state read once (flag 1, gate 2,
-    # EntityID 16, x y z yaw 16) + the grid records walked once (32 B); ingest = payload read (32 B) +
-    # hash probe (16 B key + 4 B slot) + the staged Moved (12 B) + flag/y/yaw written (9 B)
-    b_fan = 48.0 * recs + 35.0 * n + 32.0 * rec_grid
+    # Device time per stage (hipEvents on the manager's stream, gwaoi_sync_get_stats) and algorithmic
+    # bytes per launch (DESIGN.md "Sync fan-out"):
+    #  write walk (k_fan_tile<true>): grid record read (x z slot 16 B + seq 4 B + scanned count 4 B) per
+    #    record walked + per collected entity flag/gate 3 B, EntityID/Y/yaw 24 B read, info 32 B written
+    #    + 8 B per pair written + the client sub-grid records (16 B) staged once;
+    #  gate partition (k_gate_hist + k_gate_scatter): per record the pair (8 B) and its gate (1 B), the
+    #    receiver's ClientID (16 B) and the entity's info (32 B) gathered, the 48-B record written;
+    #  ingest: payload read (32 B) + hash probe (16 B key + 4 B slot) + staged Moved (12 B) + flag/y/yaw (9 B).
+    nc = max(1, ss["collects"])
+    ents = ss["entities"] / nc
+    n_client = float(has_client.sum())
+    d_write = ss["ms_write"] / nc
+    d_gate = ss["ms_gate"] / nc
+    d_cg = ss["ms_client_grid"] / nc
+    d_count = ss["ms_count"] / nc
+    d_ing = ss["ms_ingest"] / max(1, ss["ingests"])
+    b_write = 24.0 * rec_grid + 59.0 * ents + 8.0 * recs + 16.0 * n_client
+    b_gate = (8.0 + 1.0 + 16.0 + 32.0 + 48.0) * recs
     b_ing = (32.0 + 20.0 + 12.0 + 9.0) * n
-    fan_gbs = b_fan / (ms[2] * 1e-3) / 1e9
-    ing_gbs = b_ing / (ms[0] * 1e-3) / 1e9
+    gbs = lambda b, d: b / (d * 1e-3) / 1e9 if d > 0 else 0.0
+    stages = {"write_walk": (d_write, b_write, "k_fan_tile<true>"),
+              "gate_partition": (d_gate, b_gate, "k_gate_hist + k_gate_scatter")}
+    dom = max(stages, key=lambda k: stages[k][0])
+    dd, db, dk = stages[dom]
+    ach = gbs(db, dd)
     return {
         "metric": "GoWorld game tick (client position ingest + AOI tick + sync fan-out) entity-updates/s at 1M "
                   "entities per Space",
@@ -484,32 +507,62 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
         "sync_records_per_tick": recs,
         "sync_bytes_per_tick": 48.0 * recs,
         "events_per_tick": st["events"] / ticks,
+        "device_stage_ms": {"ingest": d_ing, "client_grid": d_cg, "count_walk": d_count, "write_walk": d_write,
+                            "gate_partition": d_gate},
         "roofline": {
-            "bound": "hbm", "kernel": "collect_sync (whole call, host wall time incl. 2 syncs)",
-            "achieved": fan_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": fan_gbs / HBM_PEAK_GBS,
-            "traffic": None, "algorithmic_bytes_per_launch": b_fan,
-            "ingest": {"achieved": ing_gbs, "frac": ing_gbs / HBM_PEAK_GBS, "algorithmic_bytes": b_ing},
+            "bound": "hbm", "kernel": dk, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": db,
+            "avg_launch_ms": dd, "timing": "hipEvents on the manager's stream (gwaoi_sync_get_stats)",
+            "stages": {k: {"kernel": v[2], "ms": v[0], "algorithmic_bytes": v[1], "achieved": gbs(v[1], v[0]),
+                           "frac": gbs(v[1], v[0]) / HBM_PEAK_GBS} for k, v in stages.items()}
+                      | {"ingest": {"ms": d_ing, "algorithmic_bytes": b_ing, "achieved": gbs(b_ing, d_ing),
+                                    "frac": gbs(b_ing, d_ing) / HBM_PEAK_GBS}},
         },
         "cpu_baseline": None,
     }
 
 
 def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
-    """config 4: one world of per_gpu * world entities (density of config 2) in X-strips, one per rank."""
+    """config 4: one world of per_gpu * world entities (density of config 2) in X-strips, one per rank.
+    strips_skew (config 5 in strips): the same world with 10% of the entities in Gaussian hotspots
+    (sigma 55, ~1,560 entities each: peak ~100x the mean density) and the strip edges at the
+    x-quantiles of the entities. On GPUs the halo exchange is gwaoi_strip_exchange (RCCL p2p inside
+    libgwaoi, enqueued on the strip's stream: StripNode.tick_rccl); via_cpu (several ranks on one GPU,
+    gloo) keeps the host-driven exchange."""
+    import numpy as np
     import torch
-    from goworld_amd.strips import StripLayout, StripNode, exchange_dist
+    from goworld_amd.strips import StripComm, StripLayout, StripNode, exchange_dist
 
     n = args.per_gpu * world
     L = float(math.sqrt(n / DENSITY))
     W, K = args.warmup, args.steps
-    lay = StripLayout(world, L, args.dist, 1.0)
+    skew = None
+    seed = args.seed_strips
     t_setup = time.perf_counter()
-    nd = StripNode(lay, rank, n, device=dev, seed=args.seed_strips)
+    if args.workload == "strips_skew":
+        from goworld_amd.engine import DeviceBuffer, wl_init_spaces
+        seed = args.seed_strips + 0x50
+        skew = (max(1, round(n / 15625)), 55.0, 10)
+        bx, bz = DeviceBuffer(4 * n, dev), DeviceBuffer(4 * n, dev)
+        wl_init_spaces(dev, bx.ptr, bz.ptr, n, 1, seed, L, *skew)
+        lay = StripLayout.from_quantiles(world, bx.download(np.float32, n), L, args.dist, 1.0)
+        bx.free()
+        bz.free()
+    else:
+        lay = StripLayout(world, L, args.dist, 1.0)
+    nd = StripNode(lay, rank, n, device=dev, seed=seed, skew=skew)
+    comm = None
+    if not via_cpu:
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        comm = StripComm.from_dist(rank, world, dev) if world > 1 else StripComm(StripComm.make_id(), 1, 0, dev)
     ev0 = nd.start()
     log(f"[rank {rank}] strips setup {time.perf_counter() - t_setup:.1f}s: world {n} entities, L={L:.0f}, "
         f"{nd.last_ops} in this region, {int(ev0.count)} owned enter pairs")
 
     def tick(t):
+        if comm is not None:
+            ev = nd.tick_rccl(t, comm)
+            return ev, 0  # halo counts are read from the device after the run
         lo, ro = nd.prepare(t)
         if world > 1:
             li, ri = exchange_dist(lo, ro, rank, world, via_cpu=via_cpu)
@@ -534,7 +587,11 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
     sync_all()
     elapsed = allmax(time.perf_counter() - t0)
     st = nd.eng.stats()
+    if comm is not None:  # the last tick's halo sizes (the RCCL path keeps them on the device)
+        sent = int(nd.counts[:2].sum().item()) * K
     nd.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         import torch.distributed as dist
         tot = torch.tensor([evs, sent], dtype=torch.float64, device="cpu" if via_cpu else torch.device("cuda", dev))
@@ -543,6 +600,12 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
     if rank != 0:
         return None
     ticks = max(1, st["ticks"])
+    sweep_ms = st["ms_sweep"] / ticks
+    ops_t = ops / K
+    ev0_t = st["events"] / ticks
+    rec_t = st["grid_records"] / ticks
+    b_sweep = 32.0 * rec_t + 4.0 * st["grid_cells"] / ticks + 4.0 * ops_t + 16.0 * ev0_t
+    ach = b_sweep / (sweep_ms * 1e-3) / 1e9 if sweep_ms > 0 else 0.0
     return {
         "metric": METRIC,
         "value": n * K / elapsed,
@@ -557,11 +620,18 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
         "dtype": "f32",
         "data": DATA,
         "config": {
-            "workload": f"config 4: one open world of {n} entities ({args.per_gpu} per GPU), L={L:.0f}, D={args.dist}, "
-                        f"X-strips over {world} GPU(s), halo {lay.halo:.1f} exchanged with the neighbours each tick",
-            "entities_total": n, "world_L": L, "aoi_dist": args.dist, "seed": hex(args.seed_strips),
-            "parallelism": f"{world} X-strips, halo exchange over torch.distributed "
-                           f"({'gloo via host' if via_cpu else 'RCCL/xGMI'})" if world > 1 else "1 GPU (one strip)",
+            "workload": (f"config 4: one open world of {n} entities ({args.per_gpu} per GPU), L={L:.0f}, D={args.dist}, "
+                         f"X-strips over {world} GPU(s), halo {lay.halo:.1f} exchanged with the neighbours each tick"
+                         if skew is None else
+                         f"config 5 in strips: one open world of {n} entities ({args.per_gpu} per GPU), L={L:.0f}, "
+                         f"D={args.dist}, 10% in {skew[0]} Gaussian hotspots (sigma {skew[1]:.0f}), X-strips at the "
+                         f"x-quantiles over {world} GPU(s), halo {lay.halo:.1f}"),
+            "entities_total": n, "world_L": L, "aoi_dist": args.dist, "seed": hex(seed),
+            "strip_edges": lay.edges,
+            "parallelism": (f"{world} X-strips, halo exchange " +
+                            ("over torch.distributed (gloo via host)" if via_cpu else
+                             "by gwaoi_strip_exchange (RCCL p2p over xGMI, on the strip's stream)"))
+                           if world > 1 else "1 GPU (one strip)",
         },
         "p50_tick_ms": percentile(lat, 50) * 1e3,
         "p99_tick_ms": percentile(lat, 99) * 1e3,
@@ -569,7 +639,13 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
         "halo_records_per_tick": sent / K,
         "rank0_ops_per_tick": ops / K,
         "stage_ms_rank0": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
-        "roofline": None,
+        "roofline": {
+            "bound": "hbm", "kernel": "k_sweep (rank 0's strip)", "achieved": ach, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": b_sweep,
+            "avg_launch_ms": sweep_ms, "grid_records_per_tick": rec_t, "movers_per_tick": ops_t,
+            "timing": "hipEvents around the sweep launch (gwaoi_get_stats)",
+            "halo_bytes_per_tick": 16.0 * sent / K,
+        },
         "cpu_baseline": None,
     }
 
@@ -579,7 +655,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=["config2", "config3", "skew", "skew50", "strips", "gametick"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "config3", "skew", "skew50", "strips", "strips_skew", "gametick"], default="config2")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--L", type=float, default=35000.0)
     ap.add_argument("--dist", type=float, default=100.0)
@@ -642,7 +718,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    if args.workload == "strips":
+    if args.workload in ("strips", "strips_skew"):
         result = run_strips(args, rank, world, dev, sync_all, allmax, via_cpu=(backend == "gloo"))
     elif args.workload == "gametick":
         result = run_gametick(args, rank, world, dev, sync_all, allmax)

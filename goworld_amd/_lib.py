@@ -56,6 +56,7 @@ STRIP_SYMBOLS = (
 SYNC_SYMBOLS = (
     "gwaoi_sync_enable", "gwaoi_sync_get_tables", "gwaoi_sync_set_entities", "gwaoi_sync_set_clients",
     "gwaoi_sync_set_syncing", "gwaoi_sync_mark", "gwaoi_collect_sync", "gwaoi_ingest_positions",
+    "gwaoi_sync_get_stats", "gwaoi_sync_reset_stats",
 )
 GWAOI_SYNC_OWN_CLIENT = 0x01
 GWAOI_SYNC_NEIGHBOR_CLIENTS = 0x02
@@ -82,6 +83,14 @@ class SyncOut(ctypes.Structure):
 class IngestResult(ctypes.Structure):
     _fields_ = [("n_records", ctypes.c_uint32), ("n_moved", ctypes.c_uint32), ("n_unknown", ctypes.c_uint32),
                 ("n_rejected", ctypes.c_uint32), ("n_passes", ctypes.c_uint32), ("n_nonfinite", ctypes.c_uint32)]
+
+
+class SyncStats(ctypes.Structure):
+    """gwaoi_sync_stats (include/gwaoi_sync.h): per-stage device time of collect/ingest."""
+    _fields_ = [("collects", ctypes.c_uint64), ("ms_client_grid", ctypes.c_double), ("ms_count", ctypes.c_double),
+                ("ms_write", ctypes.c_double), ("ms_gate", ctypes.c_double), ("records", ctypes.c_uint64),
+                ("entities", ctypes.c_uint64), ("ingests", ctypes.c_uint64), ("ms_ingest", ctypes.c_double),
+                ("ingest_records", ctypes.c_uint64)]
 
 
 class StripGeom(ctypes.Structure):
@@ -220,6 +229,8 @@ def load(path: str = SO_PATH):
         "gwaoi_wl_pack_ingest": ([ctypes.c_int, vp, vp, vp, u32, u32, vp], ctypes.c_int),
         "gwaoi_sync_enable": ([vp, u32], ctypes.c_int),
         "gwaoi_sync_get_tables": ([vp, ctypes.POINTER(SyncTables)], ctypes.c_int),
+        "gwaoi_sync_get_stats": ([vp, ctypes.POINTER(SyncStats)], ctypes.c_int),
+        "gwaoi_sync_reset_stats": ([vp], ctypes.c_int),
         "gwaoi_sync_set_entities": ([vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_sync_set_clients": ([vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_sync_set_syncing": ([vp, vp, vp, u32], ctypes.c_int),

@@ -254,6 +254,7 @@ struct MgrView {
   SyncState** sync;          // the manager's sync state slot (owned by the manager)
   bool pending;              // ops staged and not yet run
   uint64_t index_limit;      // largest uint32-indexed output accepted (2^32 - 1; lowered by a test hook)
+  bool timing;               // gwaoi_set_timing: the sync calls time their stages with hipEvents too
 };
 }  // namespace gw
 struct gwaoi_mgr;

@@ -968,6 +968,7 @@ int mgr_view(gwaoi_mgr* m, MgrView* out) {
   out->sync = &m->sync;
   out->pending = m->n_ops || m->dv_n;
   out->index_limit = m->index_limit;
+  out->timing = m->timing;
   return GWAOI_OK;
 }
 

@@ -656,6 +656,9 @@ struct SyncState {
   uint32_t* op_slot = nullptr;
   float* op_x = nullptr;
   float* op_z = nullptr;
+  // stage timing (gwaoi_set_timing)
+  hipEvent_t tev[6] = {};
+  gwaoi_sync_stats stats = {};
 };
 
 void sync_free(SyncState* s) {
@@ -668,6 +671,8 @@ void sync_free(SyncState* s) {
     if (q) hipFree(q);
   if (s->h_out) hipHostFree(s->h_out);
   if (s->h_small) hipHostFree(s->h_small);
+  for (hipEvent_t e : s->tev)
+    if (e) hipEventDestroy(e);
   delete s;
 }
 
@@ -901,6 +906,12 @@ int gwaoi_sync_enable(gwaoi_mgr* m, uint32_t n_gates) {
   s->is_dirty.assign(s->hcap, 0);
   s->h_mark.assign(C, 0);
   s->dirty_all = false;  // device table already empty
+  for (hipEvent_t& e : s->tev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      gw::set_error("sync_enable: hipEventCreate failed");
+      gw::sync_free(s);
+      return GWAOI_ERR_HIP;
+    }
   *v.sync = s;
   return GWAOI_OK;
 }
@@ -1188,6 +1199,7 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   cg.ccid = s->ccid;
   const uint32_t fan_blocks = std::min<uint32_t>(gw::blocks_for((uint64_t)bound + 1), 8192);
   SRCHK(gw::ensure_scan(s, std::max(bound, v.ncells) + 1));
+  if (v.timing) SCHK(hipEventRecord(s->tev[0], st));
   hipLaunchKernelGGL(gw::k_cg_flag, dim3(fan_blocks), dim3(gw::kSy), 0, st, cg);
   gw::launch_scan(s->scan, s->cpos, bound + 1, st);
   hipLaunchKernelGGL(gw::k_cg_build, dim3(fan_blocks), dim3(gw::kSy), 0, st, cg);
@@ -1216,8 +1228,10 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   SCHK(hipMemsetAsync(s->cnt, 0, ((size_t)bound + 1) * 4, st));
   const uint32_t ntiles = v.ntiles;
   if (!ntiles) return GWAOI_OK;
+  if (v.timing) SCHK(hipEventRecord(s->tev[1], st));
   hipLaunchKernelGGL(gw::k_fan_tile<false>, dim3(ntiles), dim3(gw::kSy), 0, st, f);
   gw::launch_scan(s->scan, s->cnt, bound + 1, st);
+  if (v.timing) SCHK(hipEventRecord(s->tev[2], st));
   SCHK(hipMemcpyAsync(s->h_small, s->cnt + bound, 4, hipMemcpyDeviceToHost, st));
   // [4] entities collected, [6..7] the 64-bit pair total
   SCHK(hipMemcpyAsync(s->h_small + 4, s->ictr + 8, 16, hipMemcpyDeviceToHost, st));
@@ -1242,7 +1256,9 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   SRCHK(gw::dgrow(&s->pairs, &s->pairs_cap, M));
   f.off = s->cnt;
   f.pairs = s->pairs;
+  if (v.timing) SCHK(hipEventRecord(s->tev[3], st));
   hipLaunchKernelGGL(gw::k_fan_tile<true>, dim3(ntiles), dim3(gw::kSy), 0, st, f);
+  if (v.timing) SCHK(hipEventRecord(s->tev[4], st));
 
   gw::GateArgs g = {};
   g.pairs = s->pairs;
@@ -1265,6 +1281,7 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   gw::launch_scan(s->scan, s->ghist, (uint32_t)hn, st);
   hipLaunchKernelGGL(gw::k_gate_scatter, dim3(g.nchunks), dim3(gw::kSy), 0, st, g);
   hipLaunchKernelGGL(gw::k_gate_offsets, dim3(1), dim3(GWAOI_SYNC_MAX_GATES + 64), 0, st, g);
+  if (v.timing) SCHK(hipEventRecord(s->tev[5], st));
   SCHK(hipGetLastError());
   SCHK(hipMemcpyAsync(s->h_small + 8, s->d_goff, (s->n_gates + 1) * 4, hipMemcpyDeviceToHost, st));
   const uint64_t bytes = (uint64_t)M * GWAOI_SYNC_RECORD_BYTES;
@@ -1288,6 +1305,20 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   for (uint32_t k = 0; k <= s->n_gates; ++k) s->goff64[k] = s->h_small[8 + k];
   out->n_records = M;
   out->d_records = (const uint8_t*)s->out;
+  if (v.timing) {  // the stream was synchronised above: every event is complete
+    float t01, t12, t34, t45;
+    SCHK(hipEventElapsedTime(&t01, s->tev[0], s->tev[1]));
+    SCHK(hipEventElapsedTime(&t12, s->tev[1], s->tev[2]));
+    SCHK(hipEventElapsedTime(&t34, s->tev[3], s->tev[4]));
+    SCHK(hipEventElapsedTime(&t45, s->tev[4], s->tev[5]));
+    s->stats.collects++;
+    s->stats.ms_client_grid += t01;
+    s->stats.ms_count += t12;
+    s->stats.ms_write += t34;
+    s->stats.ms_gate += t45;
+    s->stats.records += M;
+    s->stats.entities += out->n_entities;
+  }
   return GWAOI_OK;
 }
 
@@ -1357,8 +1388,10 @@ int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes,
   a.op_x = s->op_x;
   a.op_z = s->op_z;
   SCHK(hipMemsetAsync(s->ictr, 0, 16, st));
+  if (v.timing) SCHK(hipEventRecord(s->tev[0], st));
   hipLaunchKernelGGL(gw::k_ing_resolve, dim3(nb), dim3(gw::kSy), 0, st, a);
   uint32_t seg = 0, passes = 0, moved = 0;
+  float ing_ms = 0.f;
   for (;;) {
     const uint32_t nseg = gw::blocks_for(n - seg);
     a.seg = seg;
@@ -1369,18 +1402,30 @@ int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes,
     hipLaunchKernelGGL(gw::k_fill_u32, dim3(1), dim3(64), 0, st, s->bcnt + nseg, 0u, 1u);
     gw::launch_scan(s->scan, s->bcnt, nseg + 1, st);
     hipLaunchKernelGGL(gw::k_ing_emit, dim3(nseg), dim3(gw::kSy), 0, st, a);
+    if (v.timing) SCHK(hipEventRecord(s->tev[1], st));
     SCHK(hipGetLastError());
     const uint32_t bound = std::min<uint32_t>(n - seg, s->cap);
     SRCHK(gw::mgr_stage_moves_device_n(m, s->op_slot, s->op_x, s->op_z, s->bcnt + nseg, bound));
     SCHK(hipMemcpyAsync(s->h_small, s->ictr, 16, hipMemcpyDeviceToHost, st));
     SCHK(hipMemcpyAsync(s->h_small + 4, s->bcnt + nseg, 4, hipMemcpyDeviceToHost, st));
     SCHK(hipStreamSynchronize(st));
+    if (v.timing) {
+      float t;
+      SCHK(hipEventElapsedTime(&t, s->tev[0], s->tev[1]));
+      ing_ms += t;
+    }
     ++passes;
     moved += s->h_small[4];
     const uint32_t cut = std::min(s->h_small[0], n);
     if (cut >= n) break;
     SRCHK(gw::mgr_flush(m));  // run this batch now; the next starts at the repeat
     seg = cut;
+    if (v.timing) SCHK(hipEventRecord(s->tev[0], st));
+  }
+  if (v.timing) {
+    s->stats.ingests++;
+    s->stats.ms_ingest += ing_ms;
+    s->stats.ingest_records += n;
   }
   if (out) {
     out->n_moved = moved;
@@ -1389,6 +1434,26 @@ int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes,
     out->n_passes = passes;
     out->n_nonfinite = s->h_small[3];
   }
+  return GWAOI_OK;
+}
+
+int gwaoi_sync_get_stats(gwaoi_mgr* m, gwaoi_sync_stats* out) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (!out) {
+    gw::set_error("sync_get_stats: null output");
+    return GWAOI_ERR_INVALID;
+  }
+  *out = s->stats;
+  return GWAOI_OK;
+}
+
+int gwaoi_sync_reset_stats(gwaoi_mgr* m) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  s->stats = gwaoi_sync_stats{};
   return GWAOI_OK;
 }
 

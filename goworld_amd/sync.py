@@ -48,6 +48,16 @@ class EntitySync:
         check(self._L.gwaoi_sync_get_tables(self.eng.handle, ctypes.byref(t)))
         return t
 
+    def stats(self) -> dict:
+        """Per-stage device time (ms, summed) of the collect/ingest calls made while the engine's timing
+        was on (Engine.set_timing)."""
+        st = _lib.SyncStats()
+        check(self._L.gwaoi_sync_get_stats(self.eng.handle, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in _lib.SyncStats._fields_}
+
+    def reset_stats(self):
+        check(self._L.gwaoi_sync_reset_stats(self.eng.handle))
+
     @staticmethod
     def _ids(ids, n) -> np.ndarray:
         a = np.ascontiguousarray(np.asarray(ids, dtype=np.uint8).reshape(n, 16))

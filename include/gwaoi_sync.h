@@ -95,6 +95,23 @@ typedef struct {
  * entities and of neighbours is deterministic but unspecified (the reference's is Go map order). */
 int gwaoi_collect_sync(gwaoi_mgr* mgr, uint32_t opts, gwaoi_sync_out* out);
 
+/* Per-stage device time of the sync calls (hipEvents on the manager's stream), accumulated while the
+ * manager's timing is on (gwaoi_set_timing). */
+typedef struct {
+  uint64_t collects;         /* gwaoi_collect_sync calls timed */
+  double ms_client_grid;     /* client sub-grid build (k_cg_flag, scan, k_cg_build) */
+  double ms_count;           /* fan-out count walk + scan (k_fan_tile<false>) */
+  double ms_write;           /* fan-out write walk (k_fan_tile<true>): pairs + per-entity info */
+  double ms_gate;            /* gate partition: k_gate_hist, scan, k_gate_scatter, k_gate_offsets */
+  uint64_t records;          /* 48-B records written */
+  uint64_t entities;         /* entities collected */
+  uint64_t ingests;          /* gwaoi_ingest_positions calls timed */
+  double ms_ingest;          /* decode + resolve + cut + compaction into the Moved batch */
+  uint64_t ingest_records;   /* records decoded */
+} gwaoi_sync_stats;
+int gwaoi_sync_get_stats(gwaoi_mgr* mgr, gwaoi_sync_stats* out);
+int gwaoi_sync_reset_stats(gwaoi_mgr* mgr);
+
 /* ---- 2. position ingest ---- */
 #define GWAOI_INGEST_HOST_PAYLOAD 0x1u /* payload is host memory (copied to the device first) */
 typedef struct {

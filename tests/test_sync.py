@@ -170,6 +170,27 @@ def test_collect_sync_parity(gpu, oracle_lib, n, L, dist, n_gates, seed):
 
 
 @pytest.mark.gpu
+def test_collect_stage_timing(gpu, oracle_lib):
+    """gwaoi_sync_get_stats: with the manager's timing on, each collect adds its stages' device time and
+    its record/entity counts; timing does not change the records."""
+    from goworld_amd.sync import EntitySync
+    n = 3000
+    eng, orc, x, z = world(oracle_lib, n, 1600.0, 100.0, 21)
+    sy = EntitySync(eng, 4)
+    st = fill_sync(sy, np.random.default_rng(21), n, 4)
+    eng.set_timing(True)
+    sy.reset_stats()
+    check_collect(sy, orc, st, x, z, 4, keep=True)
+    s = sy.stats()
+    assert s["collects"] == 1 and s["records"] == sy.last.n_records > 0
+    assert s["entities"] == sy.last.n_entities
+    for k in ("ms_client_grid", "ms_count", "ms_write", "ms_gate"):
+        assert s[k] > 0.0, k
+    sy.reset_stats()
+    assert sy.stats()["collects"] == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cpd", [1.0, 10.0])
 def test_collect_cell_sizes(gpu, oracle_lib, cpd):
     """Coarse cells (small LDS halo) and fine cells (halo beyond the LDS region: global-table walk)."""
