@@ -74,14 +74,24 @@ __device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t
   }
 }
 
+// q = n / d for 0 <= n < 2^20, 1 <= d < 2^11 (region cell indices): float reciprocal, then one
+// correction step each way (exact; avoids the ~30-instruction integer division sequence)
+__device__ __forceinline__ int small_div(int n, int d) {
+  int q = (int)(((float)n + 0.5f) * (1.0f / (float)d));
+  q -= (q * d > n) ? 1 : 0;
+  q += ((q + 1) * d <= n) ? 1 : 0;
+  return q;
+}
+
 // Stage the records of a tile's region (cells [cx0, cx0 + W) x [cz0, cz0 + ncell / W), row-major) into
 // LDS in row-major cell order, so the cells [x0, x1] of region row r are ONE contiguous LDS range
 // [cst[r W + x0], cst[r W + x1 + 1]). load(q) gives the staged form of global record q. Every thread of
 // the block calls it; it ends with a barrier. Returns false (block-uniform, nothing staged) when the
 // region holds more than `cap` records. red: kThreads / 64 words of LDS scratch.
-template <int kThreads, int kMaxCells, class Load>
+#if GW_STAGE_V1  // A/B knob: the per-cell staging loop (one dependent load chain per cell and record)
+template <int kThreads, int kMaxCells, int kMaxRecs, class Load>
 __device__ bool stage_region(const Geom& g, const uint32_t* __restrict__ cs, int cx0, int cz0, int W, int ncell,
-                             uint16_t* cst, uint4* out, uint32_t cap, uint32_t* red, uint32_t* tot_sh, Load&& load) {
+                             uint16_t* cst, uint4* out, uint32_t* red, uint32_t* tot_sh, Load&& load) {
   constexpr int kPer = (kMaxCells + kThreads - 1) / kThreads;
   const int c0 = threadIdx.x * kPer, c1 = min(c0 + kPer, ncell);
   uint32_t sum = 0;
@@ -101,7 +111,7 @@ __device__ bool stage_region(const Geom& g, const uint32_t* __restrict__ cs, int
   if (threadIdx.x == kThreads - 1) *tot_sh = inc;
   __syncthreads();
   const uint32_t tot = *tot_sh;
-  const bool fits = tot <= cap;
+  const bool fits = tot <= (uint32_t)kMaxRecs;
   if (fits) {
     uint32_t p = inc - sum;
     for (int i = c0; i < c1; ++i) {
@@ -114,5 +124,78 @@ __device__ bool stage_region(const Geom& g, const uint32_t* __restrict__ cs, int
   __syncthreads();
   return fits;
 }
+#else
+// Each thread takes kPer consecutive cells; every cell-start load is issued up front, and the
+// records are then gathered by a flat pass (thread per staged record, its loads issued together), so
+// the staging costs a few memory round trips instead of one per cell and per record.
+template <int kThreads, int kMaxCells, int kMaxRecs, class Load>
+__device__ bool stage_region(const Geom& g, const uint32_t* __restrict__ cs, int cx0, int cz0, int W, int ncell,
+                             uint16_t* cst, uint4* out, uint32_t* red, uint32_t* tot_sh, Load&& load) {
+  constexpr int kPer = (kMaxCells + kThreads - 1) / kThreads;
+  constexpr int kIters = (kMaxRecs + kThreads - 1) / kThreads;
+  const int c0 = threadIdx.x * kPer;
+  uint32_t s0[kPer], n[kPer];
+  uint32_t sum = 0;
+  const int rr0 = small_div(c0, W), col0 = c0 - rr0 * W;
+  {
+    int rr = rr0, col = col0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      s0[k] = 0;
+      n[k] = 0;
+      if (c0 + k < ncell) {
+        const uint32_t key = cell_key(g, cx0 + col, cz0 + rr);
+        s0[k] = cs[key];
+        n[k] = cs[key + 1] - s0[k];
+      }
+      sum += n[k];
+      if (++col == W) col = 0, ++rr;
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  uint32_t inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
+  }
+  if (lane == 63) red[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) inc += red[w];
+  if (threadIdx.x == kThreads - 1) *tot_sh = inc;
+  __syncthreads();
+  const uint32_t tot = *tot_sh;
+  const bool fits = tot <= (uint32_t)kMaxRecs;
+  if (!fits) return false;  // block-uniform
+  uint32_t p = inc - sum;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    if (c0 + k < ncell) cst[c0 + k] = (uint16_t)p;
+    for (uint32_t q = 0; q < n[k]; ++q) out[p + q].x = s0[k] + q;  // source map, gathered below
+    p += n[k];
+  }
+  if (threadIdx.x == 0) cst[ncell] = (uint16_t)tot;
+  __syncthreads();
+  uint32_t src[kIters];
+#pragma unroll
+  for (int k = 0; k < kIters; ++k) {
+    const uint32_t i = threadIdx.x + k * kThreads;
+    src[k] = i < tot ? out[i].x : 0u;
+  }
+  uint4 v[kIters];
+#pragma unroll
+  for (int k = 0; k < kIters; ++k) {
+    const uint32_t i = threadIdx.x + k * kThreads;
+    if (i < tot) v[k] = load(src[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kIters; ++k) {
+    const uint32_t i = threadIdx.x + k * kThreads;
+    if (i < tot) out[i] = v[k];
+  }
+  __syncthreads();
+  return true;
+}
+
+#endif
 
 }  // namespace gw

@@ -173,6 +173,9 @@ struct RelArgs {
   uint32_t* cols;
   uint32_t ntiles;          // tiles of the grid (one block each)
   unsigned long long* total64;  // count pass: sum of the row lengths in 64 bits (uint32 overflow guard)
+  uint32_t* maxlen;         // count pass: longest row
+  uint32_t* slab;           // count pass, optional: the rows by grid record, interleaved (k_row_sort_slab)
+  uint32_t slab_s;          // entries per row kept in the slab (rows longer than this: not kept)
 };
 
 // Scan scratch (the chunk sums of launch_scan), owned by the stream's manager.
@@ -225,7 +228,13 @@ struct OrderArgs {
 void launch_order(const OrderArgs& o, hipStream_t st);
 void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_t st);
 void launch_relation(const RelArgs& a, hipStream_t st);
+// Rows of cols (filled by the fill pass) sorted in place.
 void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, uint32_t* tmp, hipStream_t st);
+// Rows from the count pass's slab (every row <= slab_s) into cols, sorted. fix: room for one entry per
+// record; *nfix zeroed beforehand.
+void launch_row_sort_slab(const Rec* rec, const uint32_t* nrec, uint32_t rec_bound, const uint32_t* row_ptr,
+                          const uint32_t* slab, uint32_t slab_s, uint32_t* cols, uint32_t* tmp, uint4* fix,
+                          uint32_t* nfix, hipStream_t st);
 void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st);
 void launch_wl_init_spaces(float* x, float* z, uint32_t n_per, uint32_t nspaces, uint64_t seed0, float L,
                            uint32_t nhot, float sigma, uint32_t hot_every, hipStream_t st);

@@ -964,14 +964,6 @@ constexpr uint32_t kCoreBit = 0x80000000u;  // staging map: the record lies in t
 
 __device__ __forceinline__ bool is_walker(const SweepArgs& a, const uint4 ra);
 
-// q = n / d for 0 <= n < 2^20, 1 <= d < 2^11 (region cell indices): float reciprocal, then one
-// correction step each way (exact; avoids the ~30-instruction integer division sequence)
-__device__ __forceinline__ int small_div(int n, int d) {
-  int q = (int)(((float)n + 0.5f) * (1.0f / (float)d));
-  q -= (q * d > n) ? 1 : 0;
-  q += ((q + 1) * d <= n) ? 1 : 0;
-  return q;
-}
 
 // Stage the region of tile (tcx, tcz: the tile's first column / row inside the region). Per cell
 // (kCellsPerThread consecutive cells per thread, every cell-start load issued up front): counts, a
@@ -1856,13 +1848,14 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
   const int cz0 = max(tz * kTile - R, 0), cz1 = min(tz * kTile + kTile - 1 + R, g.ncz - 1);
   const int W = cx1 - cx0 + 1, ncell = W * (cz1 - cz0 + 1);
   const bool lds = R > 0 && ncell <= kSweepRegCells &&
-                   stage_region<kBlock, kSweepRegCells>(g, a.g.cs, cx0, cz0, W, ncell, cst, rl, kRelLdsRecs, red,
-                                                        &tot_sh, [&](uint32_t q) {
+                   stage_region<kBlock, kSweepRegCells, kRelLdsRecs>(g, a.g.cs, cx0, cz0, W, ncell, cst, rl, red,
+                                                                     &tot_sh, [&](uint32_t q) {
                                                           const Rec r = a.g.rec[q];
                                                           return make_uint4(r.a.x, r.a.y, r.b.w, r.a.z);
                                                         });
   const float D = g.D;
   unsigned long long rsum = 0;  // count pass: this thread's row lengths
+  uint32_t rmax = 0;            // count pass: this thread's longest row
   for (uint32_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
     const uint4 ma = a.g.rec[j].a;
     if (ma.z & REC_GHOST) continue;
@@ -1872,12 +1865,19 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
     const CellBox B = qbox(g, sx, sz);
     uint32_t n = 0;
     uint32_t w = a.row_ptr ? a.row_ptr[s] : 0u;
+    // slab output, interleaved by record: entry k of grid record j at
+    // slab[(j / 64) * slab_s * 64 + k * 64 + j % 64], so the lanes of a wave (consecutive j) that find
+    // their k-th neighbour together store into one 256-B run
+    uint32_t* const srow = a.slab ? a.slab + (size_t)(j >> 6) * a.slab_s * 64 + (j & 63u) : nullptr;
     auto judge = [&](uint32_t rz, uint32_t qo, float ox, float oz) {
       const uint32_t o = rz & REC_SLOT;
       if ((rz & REC_GHOST) || o == s) return;
       const bool in = (qo > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz);
       if (in) {
         if (a.row_ptr) a.cols[w++] = o;
+#ifndef GW_ABL_NOSLAB  // ablation (timing only): the walk without the slab stores
+        if (srow && n < a.slab_s) srow[(size_t)n * 64] = o;
+#endif
         ++n;
       }
     };
@@ -1898,11 +1898,13 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
         });
       }
     }
-    if (!a.row_ptr) a.row_cnt[s] = n, rsum += n;
+    if (!a.row_ptr) a.row_cnt[s] = n, rsum += n, rmax = max(rmax, n);
   }
   if (!a.row_ptr) {  // one 64-bit atomic per wave: the host checks the total before it sizes cols
     for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o, 64);
+    for (int o = 32; o > 0; o >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o, 64));
     if ((threadIdx.x & 63) == 0 && rsum) atomicAdd(a.total64, rsum);
+    if ((threadIdx.x & 63) == 0 && rmax) atomicMax(a.maxlen, rmax);
   }
 }
 
@@ -1910,61 +1912,193 @@ void launch_relation(const RelArgs& a, hipStream_t st) {
   if (a.ntiles) hipLaunchKernelGGL(k_relation, dim3(a.ntiles), dim3(kBlock), 0, st, a);
 }
 
-// Neighbours of each row in ascending slot order. One block = 256 consecutive rows, whose entries are
-// ONE contiguous range of cols: staged in LDS with coalesced loads, then every entry is ranked inside
-// its row by a scan of the row in LDS (lanes of one row read the same words: broadcasts) and stored at
-// its final place. Blocks whose range or longest row is too large take the segmented sort of
+// Neighbours of each row in ascending slot order. A wave takes 64 consecutive rows (a contiguous
+// range of cols): each row is loaded with one coalesced load (lanes over its entries) into a per-wave
+// LDS tile that holds entry k of row r at k * 65 + r (the padding makes both the row-wise writes and
+// the lane-per-row reads conflict-free); each lane then sorts its row in registers with a fixed
+// bitonic network (32 or 64 wide, by the wave's longest row; padded with ~0), and the rows go back
+// out the way they came in. A row is a SET of slots (each entity has one main record, ghosts are
+// skipped), so keys are distinct. A block holding a row longer than 64 takes the segmented sort of
 // k_slice_sort (registers / wave / LDS bitonic chunks merged by rank).
-constexpr uint32_t kRowLds = 10240;     // 40 KB of staged entries (a 1M config-2 block holds ~8.3k)
-constexpr uint32_t kRowRankMax = 512;   // longest row ranked by the LDS scan (cost grows as len^2)
+// (Measured before, config 2: ranking each entry by a scan of its row in LDS, 0.43 ms; insertion
+// sort in LDS, 0.88 ms; the network over unpadded LDS rows, 0.18 ms, bank conflicts.)
+constexpr uint32_t kRowNetMax = 64;  // longest row sorted by the register network
+constexpr int kRowPitch = 65;
+
+// Ascending sort of N registers by Batcher's odd-even merge network for any N (comparators past N
+// dropped): 191 / 305 / 384 / 543 compare-exchanges for N = 32 / 40 / 48 / 64 (bitonic 64: 672).
+template <int N>
+__device__ __forceinline__ void net_sort(uint32_t (&r)[N]) {
+#pragma unroll
+  for (int p = 1; p < N; p <<= 1) {
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+      for (int j = k % p; j + k < N; j += 2 * k) {
+#pragma unroll
+        for (int i = 0; i < k && i + j + k < N; ++i) {
+          if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            const uint32_t x = r[i + j], y = r[i + j + k];
+            r[i + j] = min(x, y);
+            r[i + j + k] = max(x, y);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void sort_row_net(uint32_t* ww, int lane, uint32_t len) {
+  uint32_t r[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) r[k] = (uint32_t)k < len ? ww[k * kRowPitch + lane] : 0xffffffffu;
+  net_sort<N>(r);
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    if ((uint32_t)k < len) ww[k * kRowPitch + lane] = r[k];
+}
+
 __global__ void __launch_bounds__(kBlock) k_row_sort(const uint32_t* __restrict__ row_ptr, uint32_t cap,
                                                      uint32_t* __restrict__ cols, uint32_t* __restrict__ tmp) {
-  __shared__ uint32_t v[kRowLds];  // also the fallback's bitonic chunk (kBigChunk <= kRowLds)
-  __shared__ uint8_t rid[kRowLds];  // row (thread) of each staged entry
-  __shared__ uint32_t ro[kBlock + 1];
+  __shared__ uint32_t w[kBlock / 64][64 * kRowPitch];  // also the fallback's bitonic chunk
   __shared__ SegSmem ss;
-  static_assert(kBigChunk <= kRowLds && kBlock <= 256, "fallback chunk aliases v; row ids fit a byte");
-  const uint32_t s0 = blockIdx.x * kBlock, s = s0 + threadIdx.x;
+  static_assert((kBlock / 64) * 64 * kRowPitch >= (int)kBigChunk, "fallback chunk aliases w");
+  const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t b = s < cap ? row_ptr[s] : 0u, len = s < cap ? row_ptr[s + 1] - b : 0u;
-  const uint32_t b0 = row_ptr[s0], e0 = row_ptr[min(s0 + (uint32_t)kBlock, cap)];
-  const uint32_t n = e0 - b0;
-  const bool long_row = __syncthreads_or(len > kRowRankMax) != 0;
+  const bool long_row = __syncthreads_or(len > kRowNetMax) != 0;
 #ifdef GW_RS_FALLBACK  // A/B knob: every block takes the segmented sort
   if (true) {
 #else
-  if (n > kRowLds || long_row) {  // block-uniform
+  if (long_row) {  // block-uniform
 #endif
-    seg_sort(cols, tmp, b, len, v, ss.bigq, &ss.nbig);
+    seg_sort(cols, tmp, b, len, &w[0][0], ss.bigq, &ss.nbig);
     return;
   }
-  ro[threadIdx.x] = (s < cap ? b : e0) - b0;
-  if (threadIdx.x == 0) ro[kBlock] = n;
-  for (uint32_t i = 0; i < len; ++i) rid[b - b0 + i] = (uint8_t)threadIdx.x;
-  for (uint32_t i = threadIdx.x; i < n; i += kBlock) v[i] = cols[b0 + i];
+  const int lane = threadIdx.x & 63;
+  uint32_t* ww = w[threadIdx.x >> 6];
+  for (int r = 0; r < 64; ++r) {  // row r of the wave: lanes over its entries
+    const uint32_t lr = (uint32_t)__builtin_amdgcn_readlane((int)len, r);
+    const uint32_t br = (uint32_t)__builtin_amdgcn_readlane((int)b, r);
+    if ((uint32_t)lane < lr) ww[lane * kRowPitch + r] = cols[br + lane];
+  }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
-    const uint32_t r = rid[i];
-    const uint32_t rs = ro[r], re = ro[r + 1];
-    const uint32_t key = v[i];
-    // rank = entries of the row with a smaller key. A row is a SET of slots (each entity has one main
-    // record, ghosts are skipped), so keys are distinct and no tie-break is needed. (Reading the row
-    // 16 B at a time with masked ends measured slower: 0.91 -> 1.15 ms per 1M view.)
-    uint32_t pos = rs;
-#ifdef GW_RS_NORANK  // A/B knob: skip the ranking (measures the rest of the kernel)
-    pos = i;
-    if (0)
-#endif
-#pragma unroll 8
-      for (uint32_t j = rs; j < re; ++j) {
-        const uint32_t k = v[j];
-        pos += k < key ? 1u : 0u;
-      }
-    cols[b0 + pos] = key;
+  uint32_t wmax = len;
+  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
+  if (wmax <= 32u) {  // wave-uniform
+    sort_row_net<32>(ww, lane, len);
+  } else if (wmax <= 48u) {
+    sort_row_net<48>(ww, lane, len);
+  } else {
+    sort_row_net<64>(ww, lane, len);
+  }
+  __syncthreads();
+  for (int r = 0; r < 64; ++r) {
+    const uint32_t lr = (uint32_t)__builtin_amdgcn_readlane((int)len, r);
+    const uint32_t br = (uint32_t)__builtin_amdgcn_readlane((int)b, r);
+    if ((uint32_t)lane < lr) cols[br + lane] = ww[lane * kRowPitch + r];
+  }
+}
+
+// The slab path: rows straight from the count pass's interleaved slab, in grid-record order (a wave =
+// 64 consecutive records = one 64-wide column group of the slab, so entry k of all 64 rows is one
+// coalesced load into lane = row registers), sorted by the register network, then out through the
+// padded LDS tile one row at a time to cols[row_ptr[slot] ...]. Rows longer than 64 (every row is at
+// most slab_s) are listed in fix[] and finished by k_row_fix.
+template <int N>
+__device__ __forceinline__ void slab_row_net(const uint32_t* __restrict__ col, uint32_t* ww, int lane, uint32_t len) {
+  uint32_t r[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) r[k] = (uint32_t)k < len ? col[(size_t)k * 64] : 0xffffffffu;
+  net_sort<N>(r);
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    if ((uint32_t)k < len) ww[k * kRowPitch + lane] = r[k];
+}
+
+__global__ void __launch_bounds__(kBlock) k_row_sort_slab(const Rec* __restrict__ rec, const uint32_t* __restrict__ nrec_p,
+                                                          const uint32_t* __restrict__ row_ptr,
+                                                          const uint32_t* __restrict__ slab, uint32_t S,
+                                                          uint32_t* __restrict__ cols, uint4* __restrict__ fix,
+                                                          uint32_t* __restrict__ nfix) {
+  __shared__ uint32_t w[kBlock / 64][64 * kRowPitch];
+  const uint32_t nrec = *nrec_p;
+  const uint32_t jw = blockIdx.x * kBlock + (threadIdx.x & ~63u);  // the wave's first record
+  if (jw >= nrec) return;  // wave-uniform; no block barrier below
+  const int lane = threadIdx.x & 63;
+  const uint32_t j = jw + (uint32_t)lane;
+  uint32_t b = 0, len = 0;
+  if (j < nrec) {
+    const uint32_t z = rec[j].a.z;
+    if (!(z & REC_GHOST)) {
+      const uint32_t s = z & REC_SLOT;
+      b = row_ptr[s];
+      len = row_ptr[s + 1] - b;
+    }
+  }
+  if (len > kRowNetMax) {  // rare: k_row_fix
+    fix[atomicAdd(nfix, 1u)] = make_uint4(b, len, j, 0u);
+    len = 0;
+  }
+  uint32_t wmax = len;
+  for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
+  uint32_t* ww = w[threadIdx.x >> 6];
+  const uint32_t* col = slab + (size_t)(j >> 6) * S * 64 + (j & 63u);
+  if (wmax <= 32u) {  // wave-uniform
+    slab_row_net<32>(col, ww, lane, len);
+  } else if (wmax <= 40u) {
+    slab_row_net<40>(col, ww, lane, len);
+  } else if (wmax <= 48u) {
+    slab_row_net<48>(col, ww, lane, len);
+  } else {
+    slab_row_net<64>(col, ww, lane, len);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  for (int r = 0; r < 64; ++r) {
+    const uint32_t lr = (uint32_t)__builtin_amdgcn_readlane((int)len, r);
+    const uint32_t br = (uint32_t)__builtin_amdgcn_readlane((int)b, r);
+    if ((uint32_t)lane < lr) cols[br + lane] = ww[lane * kRowPitch + r];
   }
 }
 
 void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, uint32_t* tmp, hipStream_t st) {
   hipLaunchKernelGGL(k_row_sort, dim3((cap + kBlock - 1) / kBlock), dim3(kBlock), 0, st, row_ptr, cap, cols, tmp);
+}
+
+// The rows k_row_sort_slab listed (longer than its network, at most slab_s <= 128): one wave per row,
+// two entries per lane, each ranked by a pass over the row (keys are distinct), stored at its rank.
+// A fixed grid walks the list (its length is read on the device).
+__global__ void __launch_bounds__(kBlock) k_row_fix(const uint32_t* __restrict__ slab, uint32_t S,
+                                                    const uint4* __restrict__ fix, const uint32_t* __restrict__ nfix,
+                                                    uint32_t* __restrict__ cols) {
+  const uint32_t nf = *nfix;
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (kBlock / 64);
+  for (uint32_t q = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); q < nf; q += nw) {  // wave-uniform
+    const uint4 f = fix[q];
+    const uint32_t b = f.x, len = min(f.y, 128u);
+    const uint32_t* col = slab + (size_t)(f.z >> 6) * S * 64 + (f.z & 63u);
+    const uint32_t e0 = (uint32_t)lane < len ? col[(size_t)lane * 64] : 0xffffffffu;
+    const uint32_t e1 = (uint32_t)lane + 64u < len ? col[(size_t)(lane + 64) * 64] : 0xffffffffu;
+    uint32_t r0 = 0, r1 = 0;
+    for (uint32_t t = 0; t < len; ++t) {
+      const uint32_t v = t < 64u ? (uint32_t)__shfl((int)e0, (int)t, 64) : (uint32_t)__shfl((int)e1, (int)(t - 64u), 64);
+      r0 += v < e0 ? 1u : 0u;
+      r1 += v < e1 ? 1u : 0u;
+    }
+    if ((uint32_t)lane < len) cols[b + r0] = e0;
+    if ((uint32_t)lane + 64u < len) cols[b + r1] = e1;
+  }
+}
+
+void launch_row_sort_slab(const Rec* rec, const uint32_t* nrec, uint32_t rec_bound, const uint32_t* row_ptr,
+                          const uint32_t* slab, uint32_t slab_s, uint32_t* cols, uint32_t* tmp, uint4* fix,
+                          uint32_t* nfix, hipStream_t st) {
+  hipLaunchKernelGGL(k_row_sort_slab, dim3((rec_bound + kBlock - 1) / kBlock), dim3(kBlock), 0, st, rec, nrec, row_ptr,
+                     slab, slab_s, cols, fix, nfix);
+  hipLaunchKernelGGL(k_row_fix, dim3(64), dim3(kBlock), 0, st, slab, slab_s, fix, nfix, cols);
 }
 
 // ---------------------------------------------------------------------------------------------

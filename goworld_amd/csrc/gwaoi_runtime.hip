@@ -147,7 +147,10 @@ struct gwaoi_mgr {
   // relation view (gwaoi_relation_device): CSR in HBM, allocated on first use, grown on demand
   uint32_t *rel_rp = nullptr, *rel_cols = nullptr, *rel_tmp = nullptr;
   uint64_t rel_cap = 0;
-  unsigned long long* rel_tot = nullptr;  // device: the count pass's 64-bit entry total
+  unsigned long long* rel_tot = nullptr;  // device: [0] the count pass's 64-bit entry total, [1] longest row
+  uint32_t* rel_slab = nullptr;           // count pass output: the rows by grid record (k_row_sort_slab)
+  bool rel_no_slab = false;               // no room for the slab: the two-walk path
+  uint4* rel_fix = nullptr;               // rows longer than the slab sort's network (2 x cap entries)
   uint64_t index_limit = 0xFFFFFFFFull;   // uint32-indexed outputs (relation view, fan-out) fail above it
   float *d_op_x = nullptr, *d_op_z = nullptr;
   uint8_t* d_op_kind = nullptr;
@@ -758,7 +761,7 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot};
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot, m->rel_slab, m->rel_fix};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
@@ -1286,7 +1289,21 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   }
   hipStream_t st = m->stream;
   if (!m->rel_rp) RCHK(dalloc(&m->rel_rp, (size_t)m->cap + 1));
-  if (!m->rel_tot) RCHK(dalloc(&m->rel_tot, 1));
+  if (!m->rel_tot) RCHK(dalloc(&m->rel_tot, 3));  // [0] entries, [1] longest row, [2] rows to fix
+  // The count pass also writes every row of up to kSlabS entries into a slab (by grid record, 2 x cap
+  // records), when that fits the budget; the rows then go from the slab to cols sorted, with no second
+  // walk. A longer row (crowds) sends the call down the two-walk path: fill pass, sort in place.
+  constexpr uint32_t kSlabS = 128;
+  constexpr uint64_t kSlabBudget = 4ull << 30;  // bytes
+  const uint64_t slab_words = ((2ull * m->cap + 63) / 64) * 64 * kSlabS;
+  if (!m->rel_slab && !m->rel_no_slab) {
+    if (slab_words * 4 > kSlabBudget || dalloc(&m->rel_slab, (size_t)slab_words) != GWAOI_OK ||
+        dalloc(&m->rel_fix, 2 * (size_t)m->cap) != GWAOI_OK) {
+      if (m->rel_slab) hipFree(m->rel_slab);
+      m->rel_slab = nullptr;
+      m->rel_no_slab = true;
+    }
+  }
   const Grid& g = m->grid[m->cur];
   gw::RelArgs a;
   a.g = {g.rec, g.cs, g.d_geom, g.d_tile_space};
@@ -1300,13 +1317,18 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   a.cols = nullptr;
   a.ntiles = g.ncells ? g.ntiles : 0u;
   a.total64 = m->rel_tot;
+  a.maxlen = reinterpret_cast<uint32_t*>(m->rel_tot + 1);
+  a.slab = m->rel_slab;
+  a.slab_s = a.slab ? kSlabS : 0u;
   // count pass, scan, then the row lengths' total is the one value the host must know (allocation)
   HIPCHK(hipMemsetAsync(m->rel_rp, 0, ((size_t)m->cap + 1) * sizeof(uint32_t), st));
-  HIPCHK(hipMemsetAsync(m->rel_tot, 0, sizeof(unsigned long long), st));
+  HIPCHK(hipMemsetAsync(m->rel_tot, 0, 3 * sizeof(unsigned long long), st));
   gw::launch_relation(a, st);
-  unsigned long long total64 = 0;
-  HIPCHK(hipMemcpyAsync(&total64, m->rel_tot, sizeof total64, hipMemcpyDeviceToHost, st));
+  unsigned long long tot[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(tot, m->rel_tot, sizeof tot, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  const unsigned long long total64 = tot[0];
+  const uint32_t maxlen = (uint32_t)tot[1];
   if (total64 > m->index_limit) {  // row_ptr is uint32: a scan past 2^32 - 1 would wrap
     set_err("relation_device: %llu directed entries exceed the view's uint32 row offsets (limit %llu)",
             (unsigned long long)total64, (unsigned long long)m->index_limit);
@@ -1324,10 +1346,19 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
     RCHK(dalloc(&m->rel_tmp, want));
     m->rel_cap = want;
   }
-  a.row_ptr = m->rel_rp;
-  a.cols = m->rel_cols;
-  gw::launch_relation(a, st);
-  gw::launch_row_sort(m->rel_rp, m->cap, m->rel_cols, m->rel_tmp, st);
+  if (total == 0) {
+    // empty relation: row_ptr is all zeros, nothing to sort
+  } else if (a.slab && maxlen <= a.slab_s) {
+    gw::launch_row_sort_slab(g.rec, g.cs + g.ncells, 2 * m->cap, m->rel_rp, a.slab, a.slab_s, m->rel_cols,
+                             m->rel_tmp, m->rel_fix, reinterpret_cast<uint32_t*>(m->rel_tot + 2), st);
+  } else {  // a row longer than the slab keeps: the fill pass walks again
+    a.row_ptr = m->rel_rp;
+    a.cols = m->rel_cols;
+    a.slab = nullptr;
+    a.slab_s = 0;
+    gw::launch_relation(a, st);
+    gw::launch_row_sort(m->rel_rp, m->cap, m->rel_cols, m->rel_tmp, st);
+  }
   HIPCHK(hipGetLastError());
   out->row_ptr = m->rel_rp;
   out->cols = m->rel_cols;

@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
   const int W = cx1 - cx0 + 1, Hh = cz1 - cz0 + 1;
   const int ncell = W * Hh;
   const bool lds = R > 0 && ncell <= kFanRegCells &&
-                   stage_region<kSy, kFanRegCells>(g, a.ccs, cx0, cz0, W, ncell, cst, crl, kFanLdsRecs, red, &tot_sh,
+                   stage_region<kSy, kFanRegCells, kFanLdsRecs>(g, a.ccs, cx0, cz0, W, ncell, cst, crl, red, &tot_sh,
                                                    [&](uint32_t q) {
                                                      const uint4 c = a.crec[q];
                                                      return make_uint4(c.x, c.y, c.z, q);

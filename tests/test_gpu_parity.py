@@ -259,6 +259,34 @@ def test_empty_and_tiny(gpu, po):
     assert eng.last.n_subticks == 2
 
 
+@pytest.mark.parametrize("L", [5000.0, 3500.0, 2400.0])
+def test_relation_view_paths(gpu, po, L):
+    """gwaoi_relation_device at three densities (20,000 entities, D = 100): mean row ~32 (slab rows
+    sorted by the 32/64 register networks), ~65 (rows over 64 listed and finished by k_row_fix) and
+    ~140 (rows longer than the slab keeps: the fill pass and the in-place sort). Rows equal oracle
+    (ii)'s, in ascending order, before and after a tick of moves."""
+    from goworld_amd.engine import Engine
+    n, seed = 20000, 0x5EED0AA1
+    x, z = po.workload_init(seed, n, L)
+    eng = Engine(100.0, n, bounds=(0, 0, L, L))
+    orc = po.GridOracle(100.0, n, (0, 0, L, L))
+    slots = np.arange(n, dtype=np.uint32)
+    orc.bulk_enter(slots, x, z)
+    H.gpu_tick(eng, [(H.ENTER, i, float(x[i]), float(z[i])) for i in range(n)])
+    for t in range(3):
+        if t == 2:
+            po.workload_step(seed, 1, x, z, L, 1.0)
+            orc.moved_batch(slots, x, z)
+            orc.take_events()
+            eng.stage_moves(slots, x, z)
+            eng.tick()
+        rg, ro = eng.relation(), orc.relation()
+        assert np.array_equal(rg[0], ro[0]), f"call {t}: row lengths"
+        assert np.array_equal(rg[1], ro[1]), f"call {t}: rows"
+    lens = np.diff(ro[0])
+    assert lens.max() > {5000.0: 40, 3500.0: 64, 2400.0: 128}[L]
+
+
 @pytest.mark.slow
 def test_config2_full_size_two_ticks(gpu, po):
     """SURVEY.md §8(d) config 2 at full size: N=1,000,000, L=35,000, D=100, seed 0x5EED0002; the
