@@ -74,6 +74,28 @@ __device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t
   }
 }
 
+// A Space's geometry as block-uniform values: every field read through readfirstlane, so the
+// compiler keeps them (and what is derived from them) in scalar registers. The loads themselves are
+// vector loads (the kernels also store to global memory, so the compiler does not use the scalar
+// cache for them), and without this the fields stay in VGPRs.
+__device__ __forceinline__ Geom uniform_geom(const Geom* p) {
+  const Geom v = *p;
+  Geom g;
+  g.x0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x0)));
+  g.z0 = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.z0)));
+  g.inv_c = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.inv_c)));
+  g.D = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.D)));
+  g.ncx = __builtin_amdgcn_readfirstlane(v.ncx);
+  g.ncz = __builtin_amdgcn_readfirstlane(v.ncz);
+  g.ntx = __builtin_amdgcn_readfirstlane(v.ntx);
+  g.ntz = __builtin_amdgcn_readfirstlane(v.ntz);
+  g.base = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.base);
+  g.tile_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.tile_base);
+  g.reach = __builtin_amdgcn_readfirstlane(v.reach);
+  g.pad = 0;
+  return g;
+}
+
 // q = n / d for 0 <= n < 2^20, 1 <= d < 2^11 (region cell indices): float reciprocal, then one
 // correction step each way (exact; avoids the ~30-instruction integer division sequence)
 __device__ __forceinline__ int small_div(int n, int d) {

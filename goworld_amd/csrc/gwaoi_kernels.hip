@@ -561,8 +561,11 @@ struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint2 rm[kCap];      // {r | G, seq_start | A}: op rank (kNoRank: no op) and the validity mode (lds_record)
   uint32_t rslot[kCap];  // slot (read only when an event is emitted); while staging: grid index | kCoreBit
 };
-// three blocks per CU (160 KiB of LDS)
-static_assert(sizeof(SweepSmem) <= 163840 / 3 - 512, "sweep LDS budget: 3 blocks per CU");
+// 24 waves per CU (160 KiB of LDS): three 512-thread blocks, or four 384-thread blocks
+#ifndef GW_SWEEP_BLOCKS_PER_CU
+#define GW_SWEEP_BLOCKS_PER_CU 3
+#endif
+static_assert(sizeof(SweepSmem) <= 163840 / GW_SWEEP_BLOCKS_PER_CU - 512, "sweep LDS budget per block");
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
 uint32_t sweep_block() { return kSweepBlock; }
@@ -1190,14 +1193,18 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_walker(a, a.g.rec[j].a);
     if (!__syncthreads_or(mine)) return;  // nothing queued: the caller's barrier follows
   }
-  const uint32_t sp = a.g.tile_space[t];
-  const Geom g = a.g.geom[sp];
+  // block-uniform: a scalar index, so the Space's geometry comes in with scalar loads
+  const uint32_t sp = __builtin_amdgcn_readfirstlane(a.g.tile_space[t]);
+  const Geom g = uniform_geom(&a.g.geom[sp]);
   bool lds = a.use_lds && g.reach > 0;
   Region R;
   int tcx = 0, tcz = 0;
   if (lds) {
     const uint32_t tl = t - g.tile_base;
-    const int tz = (int)(tl / (uint32_t)g.ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)g.ntx);
+    // the division runs on the VALU: pin the (block-uniform) tile coordinates, and with them the region
+    // bounds, to scalar registers (in VGPRs they were spilled once per mover)
+    const int tz = __builtin_amdgcn_readfirstlane((int)(tl / (uint32_t)g.ntx));
+    const int tx = __builtin_amdgcn_readfirstlane((int)(tl - (uint32_t)tz * (uint32_t)g.ntx));
     R.zr0 = max(0, tz * kTile - g.reach);
     R.zr1 = min(g.ncz - 1, tz * kTile + kTile - 1 + g.reach);
     R.xr0 = max(0, tx * kTile - g.reach);

@@ -220,8 +220,8 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
   __shared__ uint32_t tot_sh;
   __shared__ uint2 lpairs[kWrite ? kFanLdsPairs : 1];
   const uint32_t t = blockIdx.x;
-  const uint32_t sp = a.g.tile_space[t];
-  const Geom g = a.g.geom[sp];
+  const uint32_t sp = __builtin_amdgcn_readfirstlane(a.g.tile_space[t]);
+  const Geom g = uniform_geom(&a.g.geom[sp]);
   const int lt = (int)(t - g.tile_base);
   const int tx = lt % g.ntx, tz = lt / g.ntx;
   const uint32_t k0 = g.base + ((uint32_t)lt << kTileCellShift);
