@@ -185,49 +185,55 @@ __global__ void __launch_bounds__(kSBlock) k_strip_count(const uint8_t* flags, u
   if (threadIdx.x == 0) blk[blockIdx.x] = tot;
 }
 
+// One block per chunk of kSChunk ids (the chunk's op count scanned beforehand by k_strip_count), in
+// kSItems rounds of one id per thread: every load and store of a round covers consecutive ids or
+// consecutive op slots (a ballot ranks a wave's ops, four wave totals in LDS place the waves).
+// (Sixteen consecutive ids per thread made every access a 16-element stride: 137 us at 2M ids.)
 __global__ void __launch_bounds__(kSBlock) k_strip_emit(gwaoi_strip_geom g, uint8_t* flags, float* sx, float* sz,
                                                         const float* ex, const float* ez, const uint32_t* blk,
                                                         uint32_t* ids, float* ox, float* oz, uint8_t* kinds) {
-  const uint32_t i0 = blockIdx.x * kSChunk + threadIdx.x * kSItems;
-  uint8_t f[kSItems];
-  load_flags16(flags, g.n, i0, f);
-  uint32_t c = 0;
+  __shared__ uint32_t wsum[2][kSBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t pos = blk[blockIdx.x];
+#pragma unroll 1
+  for (int r = 0; r < kSItems; ++r) {
+    const uint32_t i = blockIdx.x * kSChunk + (uint32_t)r * kSBlock + threadIdx.x;
+    const uint8_t f = i < g.n ? flags[i] : (uint8_t)0;
+    const bool op = has_op(f);
+    const unsigned long long m = __ballot(op);
+    if (lane == 0) wsum[r & 1][w] = (uint32_t)__popcll(m);
+    __syncthreads();  // one barrier per round: the two wsum buffers alternate
+    uint32_t off = 0, tot = 0;
 #pragma unroll
-  for (int k = 0; k < kSItems; ++k) c += has_op(f[k]) ? 1u : 0u;
-  uint32_t tot;
-  uint32_t pos = blk[blockIdx.x] + block_scan_s(c, &tot);
-  uint8_t nf[kSItems];
-#pragma unroll
-  for (int k = 0; k < kSItems; ++k) {
-    const uint32_t i = i0 + k;
-    nf[k] = 0;
-    if (!has_op(f[k])) continue;
-    const bool p = f[k] & GWAOI_STRIP_PRESENT, e = f[k] & GWAOI_STRIP_END;
-    uint8_t kind = p ? (e ? GWAOI_OP_MOVE : GWAOI_OP_LEAVE) : GWAOI_OP_ENTER;
-    if (!(f[k] & GWAOI_STRIP_OWNED)) kind |= GWAOI_OP_SILENT;
-    float x = 0.f, z = 0.f;
-    if (e) {
-      x = ex[i];
-      z = ez[i];
-      sx[i] = x;
-      sz[i] = z;
-      nf[k] = GWAOI_STRIP_PRESENT | (in_range(x, g.xa, g.xb) ? GWAOI_STRIP_OWNED : 0);
+    for (int k = 0; k < kSBlock / 64; ++k) {
+      const uint32_t v = wsum[r & 1][k];
+      off += k < w ? v : 0u;
+      tot += v;
     }
-    ids[pos] = i;
-    ox[pos] = x;
-    oz[pos] = z;
-    kinds[pos] = kind;
-    ++pos;
-  }
-  if (i0 + kSItems <= g.n) {
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < kSItems; ++k) w[k >> 2] |= (uint32_t)nf[k] << (8 * (k & 3));
-    *reinterpret_cast<uint4*>(flags + i0) = make_uint4(w[0], w[1], w[2], w[3]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < kSItems; ++k)
-      if (i0 + k < g.n) flags[i0 + k] = nf[k];
+    if (op) {
+      const uint32_t q = pos + off + (uint32_t)__popcll(m & below);
+      const bool p = f & GWAOI_STRIP_PRESENT, e = f & GWAOI_STRIP_END;
+      uint8_t kind = p ? (e ? GWAOI_OP_MOVE : GWAOI_OP_LEAVE) : GWAOI_OP_ENTER;
+      if (!(f & GWAOI_STRIP_OWNED)) kind |= GWAOI_OP_SILENT;
+      float x = 0.f, z = 0.f;
+      uint8_t nf = 0;
+      if (e) {
+        x = ex[i];
+        z = ez[i];
+        sx[i] = x;
+        sz[i] = z;
+        nf = GWAOI_STRIP_PRESENT | (in_range(x, g.xa, g.xb) ? GWAOI_STRIP_OWNED : 0);
+      }
+      ids[q] = i;
+      ox[q] = x;
+      oz[q] = z;
+      kinds[q] = kind;
+      flags[i] = nf;
+    } else if (i < g.n && f) {
+      flags[i] = 0;
+    }
+    pos += tot;
   }
 }
 
