@@ -30,7 +30,7 @@ ABI_SYMBOLS = (
     "gwaoi_enter_space", "gwaoi_stage_enters", "gwaoi_leave", "gwaoi_moved", "gwaoi_stage_moves", "gwaoi_stage_moves_device",
     "gwaoi_stage_ops_device",
     "gwaoi_stage_ops_device_spaces",
-    "gwaoi_stage_ops_device_n", "gwaoi_adopt_device_state",
+    "gwaoi_stage_ops_device_n", "gwaoi_adopt_device_state", "gwaoi_set_population_hint",
     "gwaoi_tick", "gwaoi_tick_ex", "gwaoi_count", "gwaoi_export_relation", "gwaoi_relation_device", "gwaoi_set_timing",
     "gwaoi_get_stats", "gwaoi_reset_stats", "gwaoi_version", "gwaoi_last_error",
 )
@@ -186,6 +186,7 @@ def load(path: str = SO_PATH):
         "gwaoi_stage_ops_device_spaces": ([vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_stage_ops_device_n": ([vp, vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_adopt_device_state": ([vp], ctypes.c_int),
+        "gwaoi_set_population_hint": ([vp, u32, u32], ctypes.c_int),
         "gwaoi_tick": ([vp, ctypes.POINTER(Events)], ctypes.c_int),
         "gwaoi_tick_ex": ([vp, u32, ctypes.POINTER(Events)], ctypes.c_int),
         "gwaoi_count": ([vp, u32p, u32p], ctypes.c_int),

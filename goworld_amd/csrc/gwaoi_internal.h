@@ -119,15 +119,23 @@ struct BinArgs {
   Rec* rec;
   // tile-bucketed build (launch_bin_tiles): per-(tile, slot chunk) histogram, bucket buffers
   uint32_t ntiles, nblk;
+  uint32_t chunk;             // slots per block: kBinChunk, larger for big capacities (nblk <= ~256)
   uint32_t* thist;            // [ntiles * nblk + 1]
   const uint32_t* tile_space;  // tile -> space
   Rec* trec;                  // records bucketed by tile (the other grid's buffer: unused this pass)
   const uint8_t* op_kind;     // the pass's op kinds (null: all moves), for tile_walk
   uint32_t* tile_walk;        // [ntiles] out: 1 = the tile holds a reported mover (k_sweep skips the rest)
 };
-// Slots per block of the tile-bucketed build, and the largest tile count its LDS histogram holds
-// (larger grids use the cell-atomic build).
+// Slots per block of the tile-bucketed build (at least; a capacity over 256 chunks gets larger
+// chunks, so the tile x chunk histogram stays ~256 x tiles), and the largest tile count its LDS
+// histogram holds (larger grids use the cell-atomic build).
 constexpr uint32_t kBinChunk = 4096;
+constexpr uint32_t kBinMaxBlocks = 256;
+inline uint32_t bin_chunk(uint32_t cap) {
+  const uint64_t per = ((uint64_t)cap + kBinMaxBlocks - 1) / kBinMaxBlocks;
+  const uint64_t c = (per + kBinChunk - 1) / kBinChunk * kBinChunk;
+  return (uint32_t)(c > kBinChunk ? c : kBinChunk);
+}
 constexpr uint32_t kMaxLdsTiles = 12288;
 
 struct SweepArgs {

@@ -329,11 +329,7 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
   extern __shared__ uint32_t th[];
   for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) th[i] = 0u;
   __syncthreads();
-  const uint32_t s0 = blockIdx.x * kBinChunk;
-#pragma unroll
-  for (int k = 0; k < kBinItems; ++k) {
-    const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
-    if (s >= a.cap) break;
+  auto body = [&](uint32_t s) {
     const SlotState t = slot_state(a, s);
     uint32_t k1 = kNoKey, k0 = kNoKey;
     if (t.p_end || t.p_start) {
@@ -347,6 +343,18 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
       reinterpret_cast<uint2*>(a.local_of)[s] = make_uint2(l1, l0);
     }
     reinterpret_cast<uint2*>(a.key_of)[s] = make_uint2(k1, k0);
+  };
+  const uint32_t s0 = blockIdx.x * a.chunk;
+  if (a.chunk == kBinChunk) {  // the common size: unrolled, every item's loads in flight together
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) {
+      const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
+      if (s >= a.cap) break;
+      body(s);
+    }
+  } else {
+    const uint32_t s1 = min(s0 + a.chunk, a.cap);
+    for (uint32_t s = s0 + threadIdx.x; s < s1; s += kBinThreads) body(s);
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) a.thist[i * a.nblk + blockIdx.x] = th[i];
@@ -354,14 +362,10 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
 }
 
 __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
-  const uint32_t s0 = blockIdx.x * kBinChunk;
-#pragma unroll
-  for (int k = 0; k < kBinItems; ++k) {
-    const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
-    if (s >= a.cap) break;
+  auto body = [&](uint32_t s) {
     const uint2 kk = reinterpret_cast<const uint2*>(a.key_of)[s];
     const uint32_t k1 = kk.x, k0 = kk.y;
-    if (k1 == kNoKey && k0 == kNoKey) continue;
+    if (k1 == kNoKey && k0 == kNoKey) return;
     const uint2 ll = reinterpret_cast<const uint2*>(a.local_of)[s];
     const SlotState t = slot_state(a, s);
     const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
@@ -374,6 +378,18 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
       const uint32_t j = a.thist[(k0 >> kTileCellShift) * a.nblk + blockIdx.x] + ll.y;
       a.trec[j] = Rec{make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq), rb};
     }
+  };
+  const uint32_t s0 = blockIdx.x * a.chunk;
+  if (a.chunk == kBinChunk) {
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) {
+      const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
+      if (s >= a.cap) break;
+      body(s);
+    }
+  } else {
+    const uint32_t s1 = min(s0 + a.chunk, a.cap);
+    for (uint32_t s = s0 + threadIdx.x; s < s1; s += kBinThreads) body(s);
   }
 }
 

@@ -79,6 +79,7 @@ int halloc(T** p, size_t n) {
 struct SpaceHost {
   gwaoi_space_desc desc;
   bool auto_extent;
+  uint32_t pop_hint = 0;  // gwaoi_set_population_hint (0: capacity / nspaces)
   // auto-extent tracking (host-staged coordinates)
   float seen_minx, seen_minz, seen_maxx, seen_maxz;
   bool seen_any;
@@ -242,7 +243,7 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
       // then holds proportionally fewer candidates. Density is planned from the capacity share over
       // the Space's declared extent.
       const double area = ((double)x1 - x0) * ((double)z1 - z0);
-      const double pop = (double)m->cap / std::max<uint32_t>(1, m->nspaces);
+      const double pop = sh.pop_hint ? (double)sh.pop_hint : (double)m->cap / std::max<uint32_t>(1, m->nspaces);
       const double cr = std::sqrt(kCellOccupancy * area / std::max(1.0, pop));
       if (cr < 0.75 * c) c = std::max(cr, (double)sh.desc.dist / 16.0);
     }
@@ -395,6 +396,7 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_
   b.rec = g.rec;
   b.ntiles = g.ntiles;
   b.nblk = m->nblk;
+  b.chunk = gw::bin_chunk(m->cap);
   b.thist = m->thist;
   b.tile_space = g.d_tile_space;
   b.trec = m->grid[gi ^ 1].rec;  // the other grid's records are not read by this pass
@@ -847,7 +849,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->d_op_z, C));
   chk(dalloc(&m->d_op_kind, C));
   chk(dalloc(&m->rank_cnt, C + 1));
-  m->nblk = (capacity + gw::kBinChunk - 1) / gw::kBinChunk;
+  m->nblk = (capacity + gw::bin_chunk(capacity) - 1) / gw::bin_chunk(capacity);
   const uint64_t max_tiles = m->max_cells / gw::kTileCells + 1;
   const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
   chk(dalloc(&m->thist, thist_n));
@@ -1537,6 +1539,17 @@ int gwaoi_debug_read_stamps(void* host, size_t bytes) {
   const int r = gw::read_stamps(host, bytes);
   if (r) set_err("debug_read_stamps: library not built with GW_STAMPS=1");
   return r;
+}
+
+int gwaoi_set_population_hint(gwaoi_mgr* m, uint32_t space, uint32_t expected) {
+  RCHK(check_mgr(m));
+  if (space >= m->nspaces) {
+    set_err("set_population_hint: space %u >= %u", space, m->nspaces);
+    return GWAOI_ERR_INVALID;
+  }
+  m->spaces[space].pop_hint = expected;
+  m->geom_dirty = true;
+  return GWAOI_OK;
 }
 
 int gwaoi_debug_set_index_limit(gwaoi_mgr* m, uint64_t limit) {

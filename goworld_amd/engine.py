@@ -106,6 +106,10 @@ class Engine:
         """Host-staged calls are accepted again after mixed device batches (gwaoi_adopt_device_state)."""
         check(self._L.gwaoi_adopt_device_state(self._h))
 
+    def set_population_hint(self, space: int, expected: int):
+        """About `expected` entities present in Space `space`: plans its cell size (gwaoi_set_population_hint)."""
+        check(self._L.gwaoi_set_population_hint(self._h, int(space), int(expected)))
+
     def set_stream(self, stream_ptr: int):
         check(self._L.gwaoi_set_stream(self._h, ctypes.c_void_p(stream_ptr)))
 

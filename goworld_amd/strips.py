@@ -44,6 +44,7 @@ class StripLayout:
         if margin is None:
             margin = max(1.0, (self.L + self.dist) * 2.0 ** -16)
         self.halo = float(f32(self.dist + self.max_step + margin))
+        self.uniform = edges is None  # equal widths (else: explicit edges, e.g. x-quantiles)
         if edges is None:
             edges = [rank * self.L / self.world for rank in range(1, self.world)]
         if len(edges) != self.world - 1:
@@ -137,6 +138,12 @@ class StripNode:
         hi = min(self.g.rb, layout.L)
         self.eng = Engine(layout.dist, capacity=n, device=device, bounds=(lo, 0.0, hi, layout.L))
         self.eng.set_stream(self.stream.cuda_stream)
+        # the slot space is the whole world's id range; the region holds about its share of the entities
+        # (equal widths: by area; quantile strips: an equal count), which is what the cell size is
+        # planned from
+        own_w = max(1e-9, min(self.g.xb, layout.L) - max(self.g.xa, 0.0))  # owned strip width
+        share = n * (hi - lo) / layout.L if layout.uniform else n / layout.world * (hi - lo) / own_w
+        self.eng.set_population_hint(0, max(1, min(n, int(share * 1.05))))
         self.tick_no = 0
 
     # ---- raw kernel calls ----

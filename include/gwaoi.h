@@ -139,6 +139,13 @@ int gwaoi_stage_ops_device_n(gwaoi_mgr* mgr, const uint32_t* d_slots, const floa
  * be staged. Auto-extent Spaces do not see the adopted coordinates (give restored Spaces extents). */
 int gwaoi_adopt_device_state(gwaoi_mgr* mgr);
 
+/* Planning hint: about `expected` entities will be present in Space `space` (default: capacity / number
+ * of Spaces). The cell size of a Space with a declared extent is planned from its density; a manager
+ * whose slot space is larger than its population (an X-strip rank whose slots are the whole world's
+ * ids, include/gwaoi_strips.h) should say so, or its cells come out too fine for the LDS sweep.
+ * Correctness never depends on it; takes effect at the next pass. 0 restores the default. */
+int gwaoi_set_population_hint(gwaoi_mgr* mgr, uint32_t space, uint32_t expected);
+
 /* Apply every staged op; blocks until the events are on the host (or in device memory, see flags). */
 #define GWAOI_TICK_DEVICE_EVENTS 1u /* leave events in device memory (no D2H copy) */
 int gwaoi_tick(gwaoi_mgr* mgr, gwaoi_events* out);

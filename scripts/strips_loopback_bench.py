@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Per-strip pipeline cost of a W-strip world on ONE GPU (loopback exchange): what each rank of a
+W-GPU strips run would pay per tick, stage by stage (hipEvents). Used to see how the per-rank tick
+grows with the world size (the manager's slot space is the whole world's id range).
+usage: strips_loopback_bench.py [world=8] [per_gpu=2000000] [ticks=20]"""
+import json
+import math
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: F401  (one HIP runtime per process)
+
+from goworld_amd.strips import LoopbackExchange, StripLayout, StripNode  # noqa: E402
+
+world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+per = int(sys.argv[2]) if len(sys.argv) > 2 else 2_000_000
+ticks = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+n = per * world
+L = math.sqrt(n / (1_000_000 / 35000.0 ** 2))
+lay = StripLayout(world, L, 100.0, 1.0)
+t0 = time.perf_counter()
+nodes = [StripNode(lay, r, n, device=0, seed=0x5EED0004) for r in range(world)]
+for nd in nodes:
+    nd.start(host_events=False)
+print(f"setup {time.perf_counter() - t0:.1f}s, world {n}, L {L:.0f}", file=sys.stderr, flush=True)
+for t in range(1, 4):
+    ins = LoopbackExchange.exchange([nd.prepare(t) for nd in nodes])
+    for nd, i in zip(nodes, ins):
+        nd.finish(*i)
+for nd in nodes:
+    nd.eng.set_timing(True)
+    nd.eng.reset_stats()
+torch.cuda.synchronize()
+for t in range(4, 4 + ticks):
+    ins = LoopbackExchange.exchange([nd.prepare(t) for nd in nodes])
+    for nd, i in zip(nodes, ins):
+        nd.finish(*i)
+torch.cuda.synchronize()
+rows = []
+for nd in nodes:
+    st = nd.eng.stats()
+    k = max(1, st["ticks"])
+    rows.append({key: round(st[key] / k, 4) for key in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")})
+    rows[-1]["ops"] = nd.last_ops
+    nd.close()
+print(json.dumps({"world": world, "per_gpu": per, "ticks": ticks, "per_strip": rows}))
