@@ -48,7 +48,7 @@ STRIP_SYMBOLS = (
     "gwaoi_strip_init_walk", "gwaoi_strip_walk", "gwaoi_strip_ingest", "gwaoi_strip_select",
     "gwaoi_strip_absorb", "gwaoi_strip_emit", "gwaoi_strip_scratch_words", "gwaoi_strip_init_skew",
     "gwaoi_strip_absorb_n", "gwaoi_strip_comm_id", "gwaoi_strip_comm_init", "gwaoi_strip_comm_destroy",
-    "gwaoi_strip_exchange",
+    "gwaoi_strip_exchange", "gwaoi_strip_local_init", "gwaoi_strip_emit_local", "gwaoi_strip_translate_events",
 )
 
 
@@ -221,6 +221,10 @@ def load(path: str = SO_PATH):
         "gwaoi_strip_absorb": ([vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_strip_emit": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "gwaoi_strip_scratch_words": ([u32], ctypes.c_size_t),
+        "gwaoi_strip_local_init": ([vp, u32, u32, vp, vp, vp], ctypes.c_int),
+        "gwaoi_strip_emit_local": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp],
+                                   ctypes.c_int),
+        "gwaoi_strip_translate_events": ([vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_strip_init_skew": ([vp, vp, vp, vp, vp, u64, f32, u32, f32, u32], ctypes.c_int),
         "gwaoi_strip_absorb_n": ([vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_strip_comm_id": ([vp], ctypes.c_int),

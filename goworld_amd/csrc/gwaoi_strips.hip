@@ -118,33 +118,57 @@ __global__ void __launch_bounds__(kSBlock) k_strip_ingest(gwaoi_strip_geom g, ui
   flags[i] |= GWAOI_STRIP_END;
 }
 
+// One block per kSelChunk ids, kSelItems rounds of one id per thread (coalesced flag reads); a
+// thread remembers its selected rounds in two bit masks, the block scans the per-thread counts and
+// reserves its range of each list with ONE atomic per list, then writes. (One wave-aggregated atomic
+// per wave with a selection serialised on the two counters when the world's ids are spread over many
+// strips: 270 us for a 16M-id world at 8 strips.)
+constexpr int kSelItems = 64;
+constexpr uint32_t kSelChunk = kSBlock * kSelItems;
 __global__ void __launch_bounds__(kSBlock) k_strip_select(gwaoi_strip_geom g, const uint8_t* flags, const float* sx,
                                                           const float* ex, const float* ez, uint4* left,
                                                           uint4* right, uint32_t cap, uint32_t* counts,
                                                           uint32_t* err) {
-  const uint32_t i = blockIdx.x * kSBlock + threadIdx.x;
-  bool sl = false, sr = false;
-  float x1 = 0.f, z1 = 0.f;
-  if (i < g.n) {
+  __shared__ uint32_t base_sh[2];
+  const uint32_t c0 = blockIdx.x * kSelChunk + threadIdx.x;
+  unsigned long long ml = 0, mr = 0;
+#pragma unroll 4
+  for (int r = 0; r < kSelItems; ++r) {
+    const uint32_t i = c0 + (uint32_t)r * kSBlock;
+    if (i >= g.n) break;
     const uint8_t f = flags[i];
     if ((f & GWAOI_STRIP_OWNED) && (f & GWAOI_STRIP_END)) {
-      const float x0 = sx[i];
-      x1 = ex[i];
-      z1 = ez[i];
-      sl = g.has_left && (x0 < g.left_hi || x1 < g.left_hi);
-      sr = g.has_right && (x0 >= g.right_lo || x1 >= g.right_lo);
+      const float x0 = sx[i], x1 = ex[i];
+      if (g.has_left && (x0 < g.left_hi || x1 < g.left_hi)) ml |= 1ull << r;
+      if (g.has_right && (x0 >= g.right_lo || x1 >= g.right_lo)) mr |= 1ull << r;
     }
   }
-  const uint4 rec = make_uint4(i, __float_as_uint(x1), __float_as_uint(z1), 0u);
-  const uint32_t pl = wave_append_s(&counts[0], sl);
-  const uint32_t pr = wave_append_s(&counts[1], sr);
-  if (sl) {
-    if (pl < cap) left[pl] = rec;
-    else atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
+  uint32_t totl, totr;
+  uint32_t pl = block_scan_s((uint32_t)__popcll(ml), &totl);
+  uint32_t pr = block_scan_s((uint32_t)__popcll(mr), &totr);
+  if (threadIdx.x == 0) {
+    base_sh[0] = totl ? atomicAdd(&counts[0], totl) : 0u;
+    base_sh[1] = totr ? atomicAdd(&counts[1], totr) : 0u;
   }
-  if (sr) {
-    if (pr < cap) right[pr] = rec;
-    else atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
+  __syncthreads();
+  pl += base_sh[0];
+  pr += base_sh[1];
+  unsigned long long m = ml | mr;
+  while (m) {
+    const int r = __ffsll((long long)m) - 1;
+    m &= m - 1ull;
+    const uint32_t i = c0 + (uint32_t)r * kSBlock;
+    const uint4 rec = make_uint4(i, __float_as_uint(ex[i]), __float_as_uint(ez[i]), 0u);
+    if ((ml >> r) & 1ull) {
+      if (pl < cap) left[pl] = rec;
+      else atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
+      ++pl;
+    }
+    if ((mr >> r) & 1ull) {
+      if (pr < cap) right[pr] = rec;
+      else atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
+      ++pr;
+    }
   }
 }
 
@@ -237,6 +261,111 @@ __global__ void __launch_bounds__(kSBlock) k_strip_emit(gwaoi_strip_geom g, uint
   }
 }
 
+// ---- local slots ----
+__global__ void __launch_bounds__(kSBlock) k_local_init(uint32_t n, uint32_t cap_l, uint32_t* g2l, uint32_t* fq,
+                                                        uint32_t* ctr) {
+  const uint32_t i = blockIdx.x * kSBlock + threadIdx.x;
+  if (i < n) g2l[i] = GWAOI_STRIP_NO_SLOT;
+  if (i < cap_l) fq[i] = i;
+  if (i == 0) {
+    ctr[0] = 0u;
+    ctr[1] = cap_l;
+    ctr[2] = 0u;
+    ctr[3] = 0u;
+  }
+}
+
+// the previous tick's Leave slots back into the free ring (one block; the count is on the device)
+__global__ void __launch_bounds__(1024) k_local_release(uint32_t* fq, const uint32_t* pend, uint32_t mask, uint32_t* ctr) {
+  const uint32_t np = ctr[2], tail = ctr[1];
+  for (uint32_t k = threadIdx.x; k < np; k += 1024) fq[(tail + k) & mask] = pend[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ctr[1] = tail + np;
+    ctr[2] = 0u;
+  }
+}
+
+// k_strip_emit, with the manager's slot of each op mapped: an Enter takes the next free slot of the
+// ring, a Move keeps its slot, a Leave queues its slot in pend (released at the next emit).
+__global__ void __launch_bounds__(kSBlock) k_strip_emit_local(gwaoi_strip_geom g, uint8_t* flags, float* sx, float* sz,
+                                                              const float* ex, const float* ez, const uint32_t* blk,
+                                                              uint32_t* slots, float* ox, float* oz, uint8_t* kinds,
+                                                              uint32_t* g2l, uint32_t* l2g, const uint32_t* fq,
+                                                              uint32_t* pend, uint32_t mask, uint32_t* ctr) {
+  __shared__ uint32_t wsum[2][kSBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const uint32_t tail = ctr[1];  // releases happened before this kernel; allocations must stay below
+  uint32_t pos = blk[blockIdx.x];
+#pragma unroll 1
+  for (int r = 0; r < kSItems; ++r) {
+    const uint32_t i = blockIdx.x * kSChunk + (uint32_t)r * kSBlock + threadIdx.x;
+    const uint8_t f = i < g.n ? flags[i] : (uint8_t)0;
+    const bool op = has_op(f);
+    const bool p = f & GWAOI_STRIP_PRESENT, e = f & GWAOI_STRIP_END;
+    const unsigned long long m = __ballot(op);
+    if (lane == 0) wsum[r & 1][w] = (uint32_t)__popcll(m);
+    const uint32_t ka = wave_append_s(&ctr[0], op && !p);        // Enter: allocation index
+    const uint32_t kl = wave_append_s(&ctr[2], op && p && !e);   // Leave: pending index
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSBlock / 64; ++k) {
+      const uint32_t v = wsum[r & 1][k];
+      off += k < w ? v : 0u;
+      tot += v;
+    }
+    if (op) {
+      const uint32_t q = pos + off + (uint32_t)__popcll(m & below);
+      uint8_t kind = p ? (e ? GWAOI_OP_MOVE : GWAOI_OP_LEAVE) : GWAOI_OP_ENTER;
+      if (!(f & GWAOI_STRIP_OWNED)) kind |= GWAOI_OP_SILENT;
+      uint32_t l;
+      if (!p) {
+        if ((int)(tail - ka) <= 0) {  // ring empty: more entities than cap_l
+          atomicOr(&ctr[3], GWAOI_STRIP_ERR_SLOTS);
+          l = 0u;
+        } else {
+          l = fq[ka & mask];
+          g2l[i] = l;
+          l2g[l] = i;
+        }
+      } else {
+        l = g2l[i];
+        if (!e) {
+          pend[kl] = l;
+          g2l[i] = GWAOI_STRIP_NO_SLOT;
+        }
+      }
+      float x = 0.f, z = 0.f;
+      uint8_t nf = 0;
+      if (e) {
+        x = ex[i];
+        z = ez[i];
+        sx[i] = x;
+        sz[i] = z;
+        nf = GWAOI_STRIP_PRESENT | (in_range(x, g.xa, g.xb) ? GWAOI_STRIP_OWNED : 0);
+      }
+      slots[q] = l;
+      ox[q] = x;
+      oz[q] = z;
+      kinds[q] = kind;
+      flags[i] = nf;
+    } else if (i < g.n && f) {
+      flags[i] = 0;
+    }
+    pos += tot;
+  }
+}
+
+__global__ void __launch_bounds__(kSBlock) k_translate(const uint32_t* l2g, uint32_t* ev, uint32_t n) {
+  const uint32_t k = blockIdx.x * kSBlock + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t m = ev[2 * k], o = ev[2 * k + 1];
+  ev[2 * k] = l2g[m];
+  ev[2 * k + 1] = l2g[o & 0x7FFFFFFFu] | (o & 0x80000000u);
+}
+
 inline dim3 blocks_for(uint32_t n) { return dim3((n + kSBlock - 1) / kSBlock); }
 inline uint32_t emit_blocks(uint32_t n) { return (n + kSChunk - 1) / kSChunk; }
 
@@ -278,7 +407,8 @@ int gwaoi_strip_select(void* stream, const gwaoi_strip_geom* g, const uint8_t* f
   if (!g || !flags || !sx || !ex || !ez || !d_left || !d_right || !d_counts || !d_err) return GWAOI_ERR_INVALID;
   if (hipMemsetAsync(d_counts, 0, 2 * sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return GWAOI_ERR_HIP;
   if (g->n)
-    hipLaunchKernelGGL(gw::k_strip_select, gw::blocks_for(g->n), dim3(gw::kSBlock), 0, (hipStream_t)stream, *g, flags,
+    hipLaunchKernelGGL(gw::k_strip_select, dim3((g->n + gw::kSelChunk - 1) / gw::kSelChunk), dim3(gw::kSBlock), 0,
+                       (hipStream_t)stream, *g, flags,
                        sx, ex, ez, reinterpret_cast<uint4*>(d_left), reinterpret_cast<uint4*>(d_right), cap, d_counts,
                        d_err);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
@@ -334,6 +464,47 @@ int gwaoi_strip_emit(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, fl
   }
   if (hipMemcpyAsync(d_n_ops, blk + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
     return GWAOI_ERR_HIP;
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_local_init(void* stream, uint32_t n, uint32_t cap_l, uint32_t* g2l, uint32_t* fq, uint32_t* ctr) {
+  if (!g2l || !fq || !ctr || !cap_l || (cap_l & (cap_l - 1))) return GWAOI_ERR_INVALID;
+  const uint32_t m = n > cap_l ? n : cap_l;
+  hipLaunchKernelGGL(gw::k_local_init, gw::blocks_for(m), dim3(gw::kSBlock), 0, (hipStream_t)stream, n, cap_l, g2l, fq,
+                     ctr);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_emit_local(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* sx, float* sz,
+                           const float* ex, const float* ez, uint32_t* d_slots, float* d_x, float* d_z,
+                           uint8_t* d_kinds, uint32_t* d_scratch, uint32_t* d_n_ops, uint32_t* g2l, uint32_t* l2g,
+                           uint32_t* fq, uint32_t* pend, uint32_t cap_l, uint32_t* ctr) {
+  if (!g || !flags || !sx || !sz || !ex || !ez || !d_slots || !d_x || !d_z || !d_kinds || !d_scratch || !d_n_ops ||
+      !g2l || !l2g || !fq || !pend || !ctr || !cap_l || (cap_l & (cap_l - 1)))
+    return GWAOI_ERR_INVALID;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t nb = gw::emit_blocks(g->n);
+  uint32_t* blk = d_scratch;  // [nb + 1]
+  gw::ScanCtx sc;
+  sc.status = d_scratch + nb + 1;
+  if (hipMemsetAsync(blk + nb, 0, sizeof(uint32_t), st) != hipSuccess) return GWAOI_ERR_HIP;
+  hipLaunchKernelGGL(gw::k_local_release, dim3(1), dim3(1024), 0, st, fq, (const uint32_t*)pend, cap_l - 1, ctr);
+  if (nb) {
+    hipLaunchKernelGGL(gw::k_strip_count, dim3(nb), dim3(gw::kSBlock), 0, st, flags, g->n, blk);
+    gw::launch_scan(sc, blk, nb + 1, st);
+    hipLaunchKernelGGL(gw::k_strip_emit_local, dim3(nb), dim3(gw::kSBlock), 0, st, *g, flags, sx, sz, ex, ez,
+                       (const uint32_t*)blk, d_slots, d_x, d_z, d_kinds, g2l, l2g, (const uint32_t*)fq, pend,
+                       cap_l - 1, ctr);
+  }
+  if (hipMemcpyAsync(d_n_ops, blk + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return GWAOI_ERR_HIP;
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_translate_events(void* stream, const uint32_t* l2g, uint32_t* d_events, uint32_t n) {
+  if (!l2g || (n && !d_events)) return GWAOI_ERR_INVALID;
+  if (n)
+    hipLaunchKernelGGL(gw::k_translate, gw::blocks_for(n), dim3(gw::kSBlock), 0, (hipStream_t)stream, l2g, d_events, n);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 

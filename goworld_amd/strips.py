@@ -106,8 +106,10 @@ class StripNode:
     """The strip of GPU `rank`: per-id state, the region's gwaoi manager, the per-tick kernels."""
 
     def __init__(self, layout: StripLayout, rank: int, n: int, device: int = 0, seed: int = 0x5EED0004,
-                 halo_cap: Optional[int] = None, skew: Optional[Tuple[int, float, int]] = None):
-        """skew = (nhot, sigma, hot_every): the skewed-crowd placement of config 5 instead of uniform."""
+                 halo_cap: Optional[int] = None, skew: Optional[Tuple[int, float, int]] = None,
+                 local_slots: bool = True):
+        """skew = (nhot, sigma, hot_every): the skewed-crowd placement of config 5 instead of uniform.
+        local_slots: the manager sees local slots (gwaoi_strip_emit_local); False: slot = global id."""
         self.layout, self.rank, self.n, self.seed = layout, int(rank), int(n), int(seed)
         self.skew = skew
         self.g = layout.geom(rank, n)
@@ -136,13 +138,30 @@ class StripNode:
         torch.cuda.synchronize(dev)  # the buffers above were zeroed on the current stream
         lo = max(self.g.ra, 0.0)
         hi = min(self.g.rb, layout.L)
-        self.eng = Engine(layout.dist, capacity=n, device=device, bounds=(lo, 0.0, hi, layout.L))
-        self.eng.set_stream(self.stream.cuda_stream)
-        # the slot space is the whole world's id range; the region holds about its share of the entities
-        # (equal widths: by area; quantile strips: an equal count), which is what the cell size is
-        # planned from
+        # the region holds about its share of the world's entities (equal widths: by area; quantile
+        # strips: an equal count)
         own_w = max(1e-9, min(self.g.xb, layout.L) - max(self.g.xa, 0.0))  # owned strip width
         share = n * (hi - lo) / layout.L if layout.uniform else n / layout.world * (hi - lo) / own_w
+        # Local slots (include/gwaoi_strips.h): the manager indexes the region's entities by a slot of
+        # its own, so its per-pass work follows the region's population, not the world's id range.
+        # cap_l: a power of two with room for crowds drifting in (1.5x the share + 8k), at most n.
+        want = min(n, int(share * 1.5) + 8192) if local_slots else n
+        self.cap_l = 1 << max(0, (max(1, want) - 1).bit_length())
+        self.local = bool(local_slots)
+        if self.local:
+            self.g2l = torch.empty(n, dtype=i32, device=dev)
+            self.l2g = torch.zeros(self.cap_l, dtype=i32, device=dev)
+            self.fq = torch.empty(self.cap_l, dtype=i32, device=dev)
+            self.pend = torch.empty(self.cap_l, dtype=i32, device=dev)
+            self.lctr = torch.zeros(4, dtype=i32, device=dev)
+            self.h_lctr = torch.zeros(4, dtype=i32).pin_memory()
+            torch.cuda.synchronize(dev)
+            check(self._L.gwaoi_strip_local_init(ctypes.c_void_p(0), n, self.cap_l, _ptr(self.g2l), _ptr(self.fq),
+                                                 _ptr(self.lctr)))
+            torch.cuda.synchronize(dev)
+        self.eng = Engine(layout.dist, capacity=self.cap_l if self.local else n, device=device,
+                          bounds=(lo, 0.0, hi, layout.L))
+        self.eng.set_stream(self.stream.cuda_stream)
         self.eng.set_population_hint(0, max(1, min(n, int(share * 1.05))))
         self.tick_no = 0
 
@@ -160,19 +179,52 @@ class StripNode:
         """The op list goes to the manager with its count in device memory (no host round trip);
         n_bound bounds it: entities present at the start + records received this tick."""
         L = self._L
-        check(L.gwaoi_strip_emit(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz), _ptr(self.ex),
-                                 _ptr(self.ez), _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds),
-                                 _ptr(self.scratch), ctypes.c_void_p(self.counts.data_ptr() + 8)))
+        common = (self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz), _ptr(self.ex), _ptr(self.ez),
+                  _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds), _ptr(self.scratch),
+                  ctypes.c_void_p(self.counts.data_ptr() + 8))
+        if self.local:
+            check(L.gwaoi_strip_emit_local(*common, _ptr(self.g2l), _ptr(self.l2g), _ptr(self.fq), _ptr(self.pend),
+                                           self.cap_l, _ptr(self.lctr)))
+            self.h_lctr.copy_(self.lctr, non_blocking=True)
+        else:
+            check(L.gwaoi_strip_emit(*common))
         self.h_counts.copy_(self.counts, non_blocking=True)  # stream-ordered before the tick's kernels
-        n_bound = max(1, min(self.n, int(n_bound)))
+        n_bound = max(1, min(self.cap_l if self.local else self.n, int(n_bound)))
         self.eng.stage_ops_device(self.ids.data_ptr(), self.ox.data_ptr(), self.oz.data_ptr(),
                                   self.kinds.data_ptr(), n_bound, d_count=self.counts.data_ptr() + 8)
-        ev = self.eng.tick() if host_events else self.eng.tick_device()
+        if host_events and self.local:
+            dev_ev = self.eng.tick_device()
+            ev = self._events_to_host(dev_ev)
+        else:
+            ev = self.eng.tick() if host_events else self.eng.tick_device()
         c = self.h_counts  # complete: the tick waited for every kernel after the copy
-        if int(c[3]):
-            raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, f"strip {self.rank}: protocol check failed (flags {int(c[3])})")
+        if int(c[3]) or (self.local and int(self.h_lctr[3])):
+            raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, f"strip {self.rank}: protocol check failed (flags "
+                                  f"{int(c[3]) | (int(self.h_lctr[3]) if self.local else 0)})")
         self.last_ops = int(c[2])
         return ev
+
+    def _events_to_host(self, ev) -> np.ndarray:
+        """Device events of a local-slot tick -> (n, 2) global ids in the canonical order of one manager
+        over the world: op (= global id) order, Leave before Enter, other id ascending."""
+        n = int(ev.count)
+        if n == 0:
+            return np.zeros((0, 2), dtype=np.uint32)
+        evp = ctypes.cast(ev.events, ctypes.c_void_p)  # device pointer (GWAOI_TICK_DEVICE_EVENTS)
+        check(self._L.gwaoi_strip_translate_events(self._s(), _ptr(self.l2g), evp, n))
+        self.stream.synchronize()
+        host = np.empty(2 * n, dtype=np.uint32)
+        check(self._L.gwaoi_dev_dtoh(self.eng.device, host.ctypes.data_as(ctypes.c_void_p), evp,
+                                     8 * n))
+        a = host.reshape(n, 2)
+        return a[np.lexsort((a[:, 1] & 0x7FFFFFFF, a[:, 1] >> 31, a[:, 0]))]
+
+    def last_op_ids(self) -> np.ndarray:
+        """Global ids of the last tick's op list (the manager saw local slots when local_slots)."""
+        ids = self.ids[: self.last_ops].cpu().numpy().view(np.uint32)
+        if self.local:  # a Leave's slot is only recycled at the next emit: l2g still names it
+            return self.l2g.cpu().numpy().view(np.uint32)[ids]
+        return ids
 
     # ---- protocol ----
     def start(self, host_events: bool = False):

@@ -46,6 +46,7 @@ extern "C" {
 #define GWAOI_STRIP_ERR_STEP 1u     /* an owned entity moved further than max_step in one tick */
 #define GWAOI_STRIP_ERR_NOT_OWNED 2u /* ingest named an entity this GPU does not own */
 #define GWAOI_STRIP_ERR_OVERFLOW 4u  /* a select list exceeded its capacity */
+#define GWAOI_STRIP_ERR_SLOTS 8u     /* local slots: the region holds more entities than cap_l */
 
 typedef struct {
   uint32_t n;       /* global entity count: ids 0..n-1 */
@@ -80,6 +81,25 @@ int gwaoi_strip_emit(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, fl
                      const float* ez, uint32_t* d_ids, float* d_x, float* d_z, uint8_t* d_kinds, uint32_t* d_scratch,
                      uint32_t* d_n_ops);
 size_t gwaoi_strip_scratch_words(uint32_t n);
+
+/* ---- local slots ----
+ * The rank's manager can index its entities by a LOCAL slot instead of the global id, so its per-pass
+ * work (op apply, grid build) follows the rank's population, not the world's id range (a 16M-id world
+ * on 8 GPUs: ~2M present per rank). The op list stays in global id order (that order is what makes
+ * the merged events equal one manager's), only the slot the manager sees changes. State (device):
+ * g2l[n] (global id -> local slot, GWAOI_STRIP_NO_SLOT = none), l2g[cap_l], a ring of free slots
+ * fq[cap_l] (cap_l a power of two), pend[cap_l] (slots of this tick's Leaves, returned to the ring at
+ * the next emit, after the caller has translated the tick's events with l2g) and ctr[4] =
+ * {allocations, releases, pending, error bits}. */
+#define GWAOI_STRIP_NO_SLOT 0xFFFFFFFFu
+int gwaoi_strip_local_init(void* stream, uint32_t n, uint32_t cap_l, uint32_t* g2l, uint32_t* fq, uint32_t* ctr);
+/* gwaoi_strip_emit with d_slots = local slots: Enter ops take a free slot, Leave ops queue theirs. */
+int gwaoi_strip_emit_local(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* sx, float* sz,
+                           const float* ex, const float* ez, uint32_t* d_slots, float* d_x, float* d_z,
+                           uint8_t* d_kinds, uint32_t* d_scratch, uint32_t* d_n_ops, uint32_t* g2l, uint32_t* l2g,
+                           uint32_t* fq, uint32_t* pend, uint32_t cap_l, uint32_t* ctr);
+/* Events {mover, other | flags} of a tick from local slots to global ids, in place (n pairs). */
+int gwaoi_strip_translate_events(void* stream, const uint32_t* l2g, uint32_t* d_events, uint32_t n);
 
 /* Skewed-crowd variant of gwaoi_strip_init_walk (gww_skew_init_coord). */
 int gwaoi_strip_init_skew(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* ex, float* ez,

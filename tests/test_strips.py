@@ -92,16 +92,17 @@ def test_cpu_gloo_world(oracle_lib, tmp_path, world):
 # ------------------------------------------------------------------------------------------------ GPU
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [1, 3, 4])
-def test_gpu_strips_loopback(gpu, oracle_lib, world):
+@pytest.mark.parametrize("world,local", [(1, True), (3, True), (4, True), (3, False)])
+def test_gpu_strips_loopback(gpu, oracle_lib, world, local):
     """HIP strip kernels + one libgwaoi manager per strip, all on cuda:0; every step's op list equals
-    the CPU restatement's and the merged events equal one manager over the whole world."""
+    the CPU restatement's and the merged events equal one manager over the whole world. local: the
+    managers index their entities by local slot (gwaoi_strip_emit_local), events translated back."""
     from goworld_amd.strips import LoopbackExchange, StripNode
     po = oracle_lib
     n, Lw = 12000, 3800.0
     want = SC.global_events(po, n, Lw, D, SEED, TICKS)
     lay = _layout(world, Lw)
-    nodes = [StripNode(lay, r, n, device=0, seed=SEED) for r in range(world)]
+    nodes = [StripNode(lay, r, n, device=0, seed=SEED, local_slots=local) for r in range(world)]
     cpu = [SC.CPUStripNode(lay, r, n, po, SEED) for r in range(world)]
     got = [SC.merge_sorted([nd.start(host_events=True) for nd in nodes])]
     for c in cpu:
@@ -122,7 +123,7 @@ def test_gpu_strips_loopback(gpu, oracle_lib, world):
             c.absorb(*ci)
             ids, kinds = c.ops()
             e = nd.finish(*i, host_events=True)
-            gids = nd.ids[: nd.last_ops].cpu().numpy().view(np.uint32)
+            gids = nd.last_op_ids()
             extra, miss = np.setdiff1d(gids, ids), np.setdiff1d(ids, gids)
             assert len(extra) == 0 and len(miss) == 0, (
                 f"tick {t} rank {nd.rank}: gpu-only ops {extra[:8]} (kinds "
