@@ -186,6 +186,27 @@ struct RelArgs {
   uint32_t slab_s;          // entries per row kept in the slab (rows longer than this: not kept)
 };
 
+// Incremental relation view (gwaoi_relation_device after a tick whose events are all in ev_out).
+struct RelDeltaArgs {
+  const uint2* ev;        // the tick's events {mover, other | ENTER}
+  uint32_t nev;
+  uint32_t cap;
+  const uint32_t* rp_old;  // [cap + 1] the view before the tick
+  const uint32_t* cols_old;
+  uint32_t* dn;            // [cap + 1] changes per row (zeroed), then their exclusive scan
+  uint32_t* dcur;          // [cap] fill cursors (zeroed)
+  uint32_t* dch;           // [2 nev] changes by row: col | ENTER
+  uint32_t* dchrow;        // [2 nev] the row of each change
+  uint32_t* rp_new;        // [cap + 1]
+  uint32_t* cols_new;
+  uint64_t cols_cap;       // entries cols_new holds (every store is bounded by it)
+  uint32_t* flag;          // set: the update cannot be done (a row's changes exceed the sort's LDS)
+  int32_t* psum;           // [2 nev] rows with many changes: inclusive prefix of the signs of the sorted list
+  uint32_t* longrows;      // rows with more than kRdShort changes (sorted by k_rd_sort_long)
+  uint32_t* nlong;         // their count (zeroed)
+  uint32_t long_cap;
+};
+
 // Scan scratch (the chunk sums of launch_scan), owned by the stream's manager.
 struct ScanCtx {
   uint32_t* status = nullptr;  // scan_part_words(max n) words
@@ -243,6 +264,10 @@ void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, uint
 void launch_row_sort_slab(const Rec* rec, const uint32_t* nrec, uint32_t rec_bound, const uint32_t* row_ptr,
                           const uint32_t* slab, uint32_t slab_s, uint32_t* cols, uint32_t* tmp, uint4* fix,
                           uint32_t* nfix, hipStream_t st);
+// Incremental view: count the changes per row (dn), then (after the caller scans dn) fill, new row
+// lengths, scan, and place old and new entries.
+void launch_rel_delta_count(const RelDeltaArgs& a, hipStream_t st);
+void launch_rel_delta_apply(const RelDeltaArgs& a, ScanCtx& sc, hipStream_t st);
 void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st);
 void launch_wl_init_spaces(float* x, float* z, uint32_t n_per, uint32_t nspaces, uint64_t seed0, float L,
                            uint32_t nhot, float sigma, uint32_t hot_every, hipStream_t st);

@@ -710,7 +710,8 @@ __device__ __forceinline__ void walk_cells(const Walk& w, SegF&& segf) {
 // `lo <= p && p <= hi` on float32 (a NaN coordinate compares false, as in Go).
 struct Judge {
   float lx1, hx1, lz1, hz1;  // m's new box
-  float mx0, mz0, D;
+  float mx0, mz0, mx1, mz1, D;
+  float eps;                 // judge_lds: distances within eps of D take the exact test
   bool v0, v1;               // m present before / after its op
   uint32_t base, rank, q, q0;
 };
@@ -719,7 +720,13 @@ __device__ __forceinline__ Judge make_judge(const Mover& m, uint32_t base) {
   Judge j;
   const float D = m.D;
   j.lx1 = m.mx1 - D, j.hx1 = m.mx1 + D, j.lz1 = m.mz1 - D, j.hz1 = m.mz1 + D;
-  j.mx0 = m.mx0, j.mz0 = m.mz0, j.D = D;
+  j.mx0 = m.mx0, j.mz0 = m.mz0, j.mx1 = m.mx1, j.mz1 = m.mz1, j.D = D;
+  // Every bound fl(c +- D) is within 2^-23 (|c| + D) of c +- D and fl(t - c) within 2^-24 |t - c| of
+  // t - c; candidates whose box could be decided differently lie within 2D + a cell of the mover, so
+  // |c| <= max|m| + 3D. A Chebyshev distance farther than eps from D is therefore decided exactly by
+  // the symmetric test (the rest, ~1e-4 of the candidates, by the exact one).
+  j.eps = (fmaxf(fmaxf(fabsf(m.mx0), fabsf(m.mz0)), fmaxf(fabsf(m.mx1), fabsf(m.mz1))) + 4.0f * D) *
+          4.76837158203125e-07f;  // 2^-21
   j.v0 = m.valid0;
   j.v1 = m.valid1;
   j.base = base, j.rank = m.rank, j.q = m.q, j.q0 = m.q0;
@@ -766,19 +773,31 @@ __device__ __forceinline__ void lds_record(const uint4 ra, const uint4 rb, uint3
   rslot = ra.z & REC_SLOT;
 }
 
-// judge() on the LDS form
+// judge() on the LDS form. Both box tests first as Chebyshev distances (|dx|, |dz| <= D: symmetric,
+// no centre/test-point selection, no bound arithmetic); a distance within J.eps of D, where float
+// rounding of the bounds could matter, is re-decided by judge()'s exact asymmetric tests.
 __device__ __forceinline__ int judge_lds(const Judge& J, const uint4 rp, const uint2 rm) {
-  const uint32_t r = rm.x & ~kTopBit, seq0 = rm.y & ~kTopBit;
+  const uint32_t r = rm.x & ~kTopBit;
   const bool ae = r < J.rank;  // acted earlier in this pass
   const bool valid = (r != J.rank) & (!(rm.x & kTopBit) | !ae) & (!(rm.y & kTopBit) | ae);
   const float px = __uint_as_float(ae ? rp.z : rp.x);
   const float pz = __uint_as_float(ae ? rp.w : rp.y);
-  const bool useo = ae | (seq0 > J.q0);  // o's box (o acted last) or m's old box
-  const float cx = useo ? px : J.mx0, cz = useo ? pz : J.mz0;  // box centre
-  const float tx = useo ? J.mx0 : px, tz = useo ? J.mz0 : pz;  // point tested
   const float D = J.D;
-  const bool before = J.v0 & (tx >= cx - D) & (tx <= cx + D) & (tz >= cz - D) & (tz <= cz + D);
-  const bool after = J.v1 & (px >= J.lx1) & (px <= J.hx1) & (pz >= J.lz1) & (pz <= J.hz1);
+  const float b = fmaxf(fabsf(px - J.mx0), fabsf(pz - J.mz0));
+  const float f = fmaxf(fabsf(px - J.mx1), fabsf(pz - J.mz1));
+  bool before = J.v0 & (b <= D);
+  bool after = J.v1 & (f <= D);
+#ifndef GW_JUDGE_EXACT  // A/B knob: 1 = the exact tests for every candidate
+#define GW_JUDGE_EXACT 0
+#endif
+  if (GW_JUDGE_EXACT || __builtin_expect((fabsf(b - D) <= J.eps) | (fabsf(f - D) <= J.eps), 0)) {
+    const uint32_t seq0 = rm.y & ~kTopBit;
+    const bool useo = ae | (seq0 > J.q0);  // o's box (o acted last) or m's old box
+    const float cx = useo ? px : J.mx0, cz = useo ? pz : J.mz0;  // box centre
+    const float tx = useo ? J.mx0 : px, tz = useo ? J.mz0 : pz;  // point tested
+    before = J.v0 & (tx >= cx - D) & (tx <= cx + D) & (tz >= cz - D) & (tz <= cz + D);
+    after = J.v1 & (px >= J.lx1) & (px <= J.hx1) & (pz >= J.lz1) & (pz <= J.hz1);
+  }
   return (valid & (before != after)) ? (after ? 2 : 1) : 0;
 }
 
@@ -864,58 +883,98 @@ __device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const 
   return true;
 }
 
-// Queue events of a wave into the block's LDS queue: one LDS atomic per call for the whole wave (a
-// ballot, the leader's add, a shuffle). Every lane of the wave that reached the call passes `has`;
-// queue overflow spills to ev_tmp with one global atomic per wave.
-__device__ __forceinline__ void emit_wave(const SweepArgs& a, SweepSmem& sm, bool has, const uint4 rec) {
-#if GW_ABL_NOEMIT  // ablation (timing only): events counted, not queued
-  return;
-#endif
-  const uint32_t li = wave_append(&sm.n, has);
-  const bool spill = has && li >= (uint32_t)kEvLds;
-  if (has && !spill) sm.ev[li] = rec;
-  const uint32_t gi = wave_append(&a.ctr[CTR_EVENTS], spill);
-  if (spill && gi < a.ev_cap) a.ev_tmp[gi] = rec;
+// Judge candidates b..b+63 of one stream (idx(k) = LDS record index of candidate k): the hot loop
+// only records which candidates raise an event and of which kind (bit k - b of two per-lane masks).
+// No atomic, branch or LDS write sits in the candidate loop itself. (32-candidate chunks with 32-bit
+// masks: the register allocator spills 5x more in this kernel, measured slower.)
+template <class IdxF>
+__device__ __forceinline__ void judge_chunk(const SweepSmem& sm, const Judge& J, uint32_t b, uint32_t total,
+                                            IdxF&& idx, unsigned long long& hit, unsigned long long& ent) {
+  const uint32_t n = b < total ? min(total - b, 64u) : 0u;
+  hit = 0;
+  ent = 0;
+  uint32_t k = 0;
+  for (; k + 1 < n; k += 2) {  // two candidates per iteration: both LDS reads in flight
+    const uint32_t j0 = idx(b + k), j1 = idx(b + k + 1);
+    const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
+    const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
+    const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
+    hit |= ((unsigned long long)(e0 != 0) << k) | ((unsigned long long)(e1 != 0) << (k + 1));
+    ent |= ((unsigned long long)(e0 == 2) << k) | ((unsigned long long)(e1 == 2) << (k + 1));
+  }
+  if (k < n) {
+    const uint32_t j0 = idx(b + k);
+    const int e0 = judge_lds(J, sm.rp[j0], sm.rm[j0]);
+    hit |= (unsigned long long)(e0 != 0) << k;
+    ent |= (unsigned long long)(e0 == 2) << k;
+  }
 }
 
-// Judge candidates 0..total-1 of one stream (idx(k) = LDS record index of candidate k), 64 at a time:
-// the hot loop only records which candidates raise an event and of which kind (bit k of two per-lane
-// masks); the events are then queued a round at a time, every lane with a set bit at once
-// (emit_wave). No atomic, branch or LDS write sits in the candidate loop itself. (32-candidate chunks
-// with 32-bit masks: the register allocator spills 5x more in this kernel, measured slower.)
+// Queue the events marked in two mask pairs (hA/eA: candidates ia(bit), hB/eB: ib(bit)) for every
+// lane of the wave at once: each lane's event count c, the wave's exclusive prefix and total by one
+// ballot per bit of c (no LDS round trip), ONE LDS atomic per wave for the queue range, one global
+// atomic per wave when the range runs past the queue; then each lane writes its own events in mask
+// order (its `local` numbering). Every lane that reached the call takes part (the masks of a lane
+// without events are zero).
+template <class IdxA, class IdxB>
+__device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, const Mover& m, unsigned long long hA,
+                                           unsigned long long eA, IdxA&& ia, unsigned long long hB,
+                                           unsigned long long eB, IdxB&& ib, uint32_t& local, uint32_t& nent) {
+  const uint32_t c = (uint32_t)(__popcll(hA) + __popcll(hB));
+#if GW_ABL_NOEMIT  // ablation (timing only): events counted, not queued
+  nent += (uint32_t)(__popcll(eA) + __popcll(eB));
+  local += c;
+  return;
+#endif
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t pre = 0, tot = 0;
+  for (int bit = 0; __any((c >> bit) != 0u); ++bit) {  // wave-uniform: the bits of the largest count
+    const unsigned long long mb = __ballot((c >> bit) & 1u);
+    pre += (uint32_t)__popcll(mb & below) << bit;
+    tot += (uint32_t)__popcll(mb) << bit;
+  }
+  if (tot == 0u) return;  // wave-uniform
+  const int leader = __ffsll((long long)__ballot(1)) - 1;
+  uint32_t q0 = 0;
+  if (lane == leader) q0 = atomicAdd(&sm.n, tot);
+  q0 = __builtin_amdgcn_readfirstlane(q0);  // the first active lane is the leader
+  const uint32_t qs = max(q0, (uint32_t)kEvLds);  // first queue position that spills
+  uint32_t g0 = 0;
+  if (q0 + tot > qs) {  // wave-uniform
+    if (lane == leader) g0 = atomicAdd(&a.ctr[CTR_EVENTS], q0 + tot - qs);
+    g0 = __builtin_amdgcn_readfirstlane(g0);
+  }
+  uint32_t p = q0 + pre;
+  auto put = [&](unsigned long long& h, unsigned long long e, auto&& idx) {
+    while (h) {
+      const int bit = __ffsll((long long)h) - 1;
+      const bool enter = (e >> bit) & 1ull;
+      const uint4 rec = make_uint4(m.rank, local++, m.slot, sm.rslot[idx((uint32_t)bit)] | (enter ? 0x80000000u : 0u));
+      nent += enter ? 1u : 0u;
+      if (p < (uint32_t)kEvLds) {
+        sm.ev[p] = rec;
+      } else {
+        const uint32_t gi = g0 + (p - qs);
+        if (gi < a.ev_cap) a.ev_tmp[gi] = rec;
+      }
+      ++p;
+      h &= h - 1ull;
+    }
+  };
+  put(hA, eA, ia);
+  put(hB, eB, ib);
+}
+
+// Judge candidates 0..total-1 of one stream, 64 at a time, queueing each chunk's events.
 template <class IdxF>
 __device__ __forceinline__ void judge_stream(const SweepArgs& a, SweepSmem& sm, const Judge& J, const Mover& m,
                                              uint32_t total, IdxF&& idx, uint32_t& local, uint32_t& nent) {
   for (uint32_t b = 0; __any(b < total); b += 64) {
-    const uint32_t n = b < total ? min(total - b, 64u) : 0u;
-    unsigned long long hit = 0, ent = 0;
-    uint32_t k = 0;
-    for (; k + 1 < n; k += 2) {  // two candidates per iteration: both LDS reads in flight
-      const uint32_t j0 = idx(b + k), j1 = idx(b + k + 1);
-      const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
-      const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
-      const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
-      hit |= ((unsigned long long)(e0 != 0) << k) | ((unsigned long long)(e1 != 0) << (k + 1));
-      ent |= ((unsigned long long)(e0 == 2) << k) | ((unsigned long long)(e1 == 2) << (k + 1));
-    }
-    if (k < n) {
-      const uint32_t j0 = idx(b + k);
-      const int e0 = judge_lds(J, sm.rp[j0], sm.rm[j0]);
-      hit |= (unsigned long long)(e0 != 0) << k;
-      ent |= (unsigned long long)(e0 == 2) << k;
-    }
-    while (__any(hit != 0)) {
-      const bool has = hit != 0;
-      uint4 rec = make_uint4(0, 0, 0, 0);
-      if (has) {
-        const int bit = __ffsll((long long)hit) - 1;
-        const bool enter = (ent >> bit) & 1ull;
-        rec = make_uint4(m.rank, local++, m.slot, sm.rslot[idx(b + (uint32_t)bit)] | (enter ? 0x80000000u : 0u));
-        nent += enter ? 1u : 0u;
-        hit &= hit - 1ull;
-      }
-      emit_wave(a, sm, has, rec);
-    }
+    unsigned long long hit, ent;
+    judge_chunk(sm, J, b, total, idx, hit, ent);
+    emit_masks(a, sm, m, hit, ent, [&](uint32_t k) { return idx(b + k); }, 0ull, 0ull,
+               [&](uint32_t k) { return k; }, local, nent);
   }
 }
 
@@ -926,9 +985,17 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
   RingStream Rs, Cs;
   if (ring_plan(w, R, sm, Rs, Cs)) {
     // row stream: LDS record indices directly; column stream: through the column-major index
-    judge_stream(a, sm, J, m, Rs.total, [&](uint32_t k) { return stream_at(Rs, k); }, local, nent);
-    judge_stream(a, sm, J, m, Cs.total, [&](uint32_t k) { return (uint32_t)sm.cidx[stream_at(Cs, k)]; }, local,
-                 nent);
+    auto ri = [&](uint32_t k) { return stream_at(Rs, k); };
+    auto ci = [&](uint32_t k) { return (uint32_t)sm.cidx[stream_at(Cs, k)]; };
+    if (__all(Rs.total <= 64u && Cs.total <= 64u)) {  // the usual ring: both streams in one chunk, one emission
+      unsigned long long hR, eR, hC, eC;
+      judge_chunk(sm, J, 0, Rs.total, ri, hR, eR);
+      judge_chunk(sm, J, 0, Cs.total, ci, hC, eC);
+      emit_masks(a, sm, m, hR, eR, ri, hC, eC, ci, local, nent);
+      return local;
+    }
+    judge_stream(a, sm, J, m, Rs.total, ri, local, nent);
+    judge_stream(a, sm, J, m, Cs.total, ci, local, nent);
     return local;
   }
   walk_cells(w, [&](int r, int c0, int c1) {
@@ -1297,6 +1364,8 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     GW_STAMP(13, __builtin_amdgcn_s_memrealtime());  // movers ordered: the walk starts
 #endif
     if (a.use_lds != 2) {  // 2: ablation (timing only), staging and ordering without the walk
+      // (one wave per mover for a tile's few movers beyond a full round: measured 110 -> 123 us; the
+      // planner sizes tiles below one round instead, compute_geometry)
       for (uint32_t r = 0; r * kSweepBlock < nm; ++r) {
         const uint32_t p = r * kSweepBlock + ((r & 1u) ? (uint32_t)(kSweepBlock - 1) - threadIdx.x : threadIdx.x);
         if (p >= nm) continue;
@@ -2122,6 +2191,246 @@ void launch_row_sort_slab(const Rec* rec, const uint32_t* nrec, uint32_t rec_bou
   hipLaunchKernelGGL(k_row_sort_slab, dim3((rec_bound + kBlock - 1) / kBlock), dim3(kBlock), 0, st, rec, nrec, row_ptr,
                      slab, slab_s, cols, fix, nfix);
   hipLaunchKernelGGL(k_row_fix, dim3(64), dim3(kBlock), 0, st, slab, slab_s, fix, nfix, cols);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Relation view, incremental: the view after a tick = the view before it + the tick's pair events
+// (every pass of the tick, in ev_out). N is symmetric, so event (m, o, +-) changes rows m and o; the
+// net change of (row, col) over the tick is the sum of its signs, in {-1, 0, +1} (the events are
+// exactly the relation's changes, in sequence: transient enter/leave pairs cancel). Entries are
+// placed by rank arithmetic: an old entry v at index i of row r goes to ns[r] + i + (sum of the signs
+// of r's changes with col < v), and is dropped when the signs of col == v sum to -1; a col whose
+// signs sum to +1 is written once at ns[r] + #(old entries < col) + (sum of the signs of the changes
+// < col). A row with at most kRdShort changes is scanned linearly (unsorted); a longer one (a mover
+// crossing a crowd) is sorted in LDS with the prefix of its signs, then searched.
+constexpr uint32_t kRdShort = 32;
+constexpr uint32_t kRdLongMax = 4096;  // longest change list sorted in LDS (longer: the view is rebuilt)
+
+__global__ void __launch_bounds__(kBlock) k_rd_count(RelDeltaArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.nev) return;
+  const uint2 e = a.ev[i];
+  atomicAdd(&a.dn[e.x], 1u);
+  atomicAdd(&a.dn[e.y & 0x7FFFFFFFu], 1u);
+}
+
+__global__ void __launch_bounds__(kBlock) k_rd_fill(RelDeltaArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.nev) return;
+  const uint2 e = a.ev[i];
+  const uint32_t sg = e.y & 0x80000000u, o = e.y & 0x7FFFFFFFu;
+  const uint32_t p = a.dn[e.x] + atomicAdd(&a.dcur[e.x], 1u);
+  a.dch[p] = o | sg;
+  a.dchrow[p] = e.x;
+  const uint32_t q = a.dn[o] + atomicAdd(&a.dcur[o], 1u);
+  a.dch[q] = e.x | sg;
+  a.dchrow[q] = o;
+}
+
+// new row lengths (rp_new, scanned by the caller; rp_new[cap] = 0); rows with many changes listed
+__global__ void __launch_bounds__(kBlock) k_rd_len(RelDeltaArgs a) {
+  const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+  if (r == 0) a.rp_new[a.cap] = 0u;
+  if (r >= a.cap) return;
+  const uint32_t cs = a.dn[r], ce = a.dn[r + 1];
+  int s = 0;
+  for (uint32_t k = cs; k < ce; ++k) s += (a.dch[k] >> 31) ? 1 : -1;
+  if (ce - cs > kRdLongMax) {
+    atomicOr(a.flag, 1u);
+  } else if (ce - cs > kRdShort) {
+    const uint32_t li = atomicAdd(a.nlong, 1u);  // every listed index < long_cap is written
+    if (li < a.long_cap) a.longrows[li] = r;
+    else atomicOr(a.flag, 1u);
+  }
+  a.rp_new[r] = (uint32_t)((int)(a.rp_old[r + 1] - a.rp_old[r]) + s);
+}
+
+// One block per listed row (grid-stride): its changes sorted by col in LDS (bitonic over key
+// col * 2 + ENTER, padded to a power of two), written back in place, with the inclusive prefix of
+// their signs in psum.
+__global__ void __launch_bounds__(kBlock) k_rd_sort_long(RelDeltaArgs a) {
+  __shared__ uint32_t key[kRdLongMax];
+  if (*a.flag) return;  // set by k_rd_len (earlier in the stream): the update is abandoned
+  const uint32_t nl = min(*a.nlong, a.long_cap);
+  for (uint32_t li = blockIdx.x; li < nl; li += gridDim.x) {
+    const uint32_t r = a.longrows[li];
+    const uint32_t cs = a.dn[r], n = a.dn[r + 1] - cs;  // kRdShort < n <= kRdLongMax
+    uint32_t np = 64;
+    while (np < n) np <<= 1;
+    for (uint32_t k = threadIdx.x; k < np; k += kBlock) {
+      const uint32_t c = k < n ? a.dch[cs + k] : 0xFFFFFFFFu;
+      key[k] = k < n ? ((c & 0x7FFFFFFFu) << 1) | (c >> 31) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (uint32_t size = 2; size <= np; size <<= 1) {
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t k = threadIdx.x; k < np; k += kBlock) {
+          const uint32_t l = k ^ stride;
+          if (l > k) {
+            const uint32_t x = key[k], y = key[l];
+            const bool up = (k & size) == 0;
+            if ((x > y) == up) {
+              key[k] = y;
+              key[l] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // inclusive prefix of the signs: kRdLongMax / kBlock consecutive entries per thread
+    constexpr uint32_t kPer = kRdLongMax / kBlock;
+    const uint32_t k0 = threadIdx.x * kPer;
+    int loc = 0;
+    for (uint32_t q = 0; q < kPer; ++q)
+      if (k0 + q < n) loc += (key[k0 + q] & 1u) ? 1 : -1;
+    uint32_t total;
+    int run = (int)block_excl_scan((uint32_t)loc, &total);
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const uint32_t k = k0 + q;
+      if (k < n) {
+        const uint32_t kk = key[k];
+        run += (kk & 1u) ? 1 : -1;
+        a.dch[cs + k] = (kk >> 1) | (kk << 31);
+        a.psum[cs + k] = run;
+      }
+    }
+    __syncthreads();  // key[] is reused by the next row
+  }
+}
+
+// sorted change list [cs, ce) of a long row: (sum of signs of cols < v, sum of signs of cols == v)
+__device__ __forceinline__ int2 rd_long_sums(const RelDeltaArgs& a, uint32_t cs, uint32_t ce, uint32_t v) {
+  uint32_t lo = cs, hi = ce;
+  while (lo < hi) {  // first col >= v
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((a.dch[mid] & 0x7FFFFFFFu) < v) lo = mid + 1;
+    else hi = mid;
+  }
+  uint32_t lo2 = lo, hi2 = ce;
+  while (lo2 < hi2) {  // first col > v
+    const uint32_t mid = (lo2 + hi2) >> 1;
+    if ((a.dch[mid] & 0x7FFFFFFFu) <= v) lo2 = mid + 1;
+    else hi2 = mid;
+  }
+  const int below = lo > cs ? a.psum[lo - 1] : 0;
+  const int upto = lo2 > cs ? a.psum[lo2 - 1] : 0;
+  return make_int2(below, upto - below);
+}
+
+// Old entries to their new places: a wave takes 64 consecutive rows (one contiguous range of the old
+// cols) and walks it 64 entries at a time, coalesced both ways; each lane finds its entry's row among
+// the few rows the chunk touches (a wave-uniform loop over readlanes, no LDS).
+__global__ void __launch_bounds__(kBlock) k_rd_merge(RelDeltaArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t r0 = ((blockIdx.x * kBlock + threadIdx.x) >> 6) * 64u;
+  if (r0 >= a.cap || *a.flag) return;  // wave-uniform
+  const uint32_t nr = min(64u, a.cap - r0);
+  uint32_t os = 0, ns = 0, cs = 0, ce = 0;
+  if ((uint32_t)lane < nr) {
+    const uint32_t r = r0 + lane;
+    os = a.rp_old[r];
+    ns = a.rp_new[r];
+    cs = a.dn[r];
+    ce = a.dn[r + 1];
+  }
+  const uint32_t G0 = __builtin_amdgcn_readfirstlane(os);
+  const uint32_t G1 = __builtin_amdgcn_readfirstlane(a.rp_old[r0 + nr]);
+  uint32_t L0 = 0;  // first row the chunk touches (wave-uniform)
+  for (uint32_t b = G0; b < G1; b += 64) {
+    const uint32_t e = b + lane;
+    const bool act = e < G1;
+    const uint32_t v = act ? a.cols_old[e] : 0u;
+    const uint32_t cend = min(b + 64u, G1);
+    uint32_t ri = L0, mos = 0, mns = 0, mcs = 0, mce = 0;
+    for (uint32_t L = L0; L < nr; ++L) {
+      const uint32_t osL = __builtin_amdgcn_readlane(os, L);
+      if (osL >= cend) break;  // wave-uniform
+      const uint32_t nsL = __builtin_amdgcn_readlane(ns, L), csL = __builtin_amdgcn_readlane(cs, L),
+                     ceL = __builtin_amdgcn_readlane(ce, L);
+      const bool in = e >= osL;  // the last such row holds e (an empty row shares its start with the next)
+      ri = in ? L : ri;
+      mos = in ? osL : mos;
+      mns = in ? nsL : mns;
+      mcs = in ? csL : mcs;
+      mce = in ? ceL : mce;
+    }
+    if (act) {
+      int sl = 0, se = 0;
+      if (mce - mcs <= kRdShort) {
+        for (uint32_t k = mcs; k < mce; ++k) {
+          const uint32_t c = a.dch[k], col = c & 0x7FFFFFFFu;
+          const int sg = (c >> 31) ? 1 : -1;
+          sl += col < v ? sg : 0;
+          se += col == v ? sg : 0;
+        }
+      } else if (mce - mcs <= kRdLongMax) {
+        const int2 ss = rd_long_sums(a, mcs, mce, v);
+        sl = ss.x;
+        se = ss.y;
+      }
+      const uint32_t o = mns + (e - mos) + (uint32_t)sl;
+      if (se >= 0 && o < a.cols_cap) a.cols_new[o] = v;  // (the bound holds for a consistent event stream)
+    }
+    L0 = __builtin_amdgcn_readlane(ri, 63);
+  }
+}
+
+// New entries: one thread per change. A short row's col is written by its first ENTER change, a long
+// (sorted) row's by the first change of its run of equal cols, when its signs sum to +1.
+__global__ void __launch_bounds__(kBlock) k_rd_adds(RelDeltaArgs a) {
+  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= 2u * a.nev || *a.flag) return;
+  const uint32_t c = a.dch[j];
+  const uint32_t r = a.dchrow[j], col = c & 0x7FFFFFFFu;
+  const uint32_t cs = a.dn[r], ce = a.dn[r + 1];
+  int sl = 0, se = 0;
+  if (ce - cs <= kRdShort) {
+    if (!(c >> 31)) return;
+    bool first = true;
+    for (uint32_t k = cs; k < ce; ++k) {
+      const uint32_t c2 = a.dch[k], col2 = c2 & 0x7FFFFFFFu;
+      const int sg = (c2 >> 31) ? 1 : -1;
+      sl += col2 < col ? sg : 0;
+      se += col2 == col ? sg : 0;
+      first = first && !(col2 == col && (c2 >> 31) && k < j);
+    }
+    if (!first) return;
+  } else {
+    if (ce - cs > kRdLongMax) return;  // flagged by k_rd_len
+    if (j > cs && (a.dch[j - 1] & 0x7FFFFFFFu) == col) return;
+    const int2 ss = rd_long_sums(a, cs, ce, col);
+    sl = ss.x;
+    se = ss.y;
+  }
+  if (se <= 0) return;
+  uint32_t lo = a.rp_old[r], hi = a.rp_old[r + 1];
+  const uint32_t os = lo;
+  while (lo < hi) {  // old entries < col
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.cols_old[mid] < col) lo = mid + 1;
+    else hi = mid;
+  }
+  const uint32_t o = a.rp_new[r] + (lo - os) + (uint32_t)sl;
+  if (o < a.cols_cap) a.cols_new[o] = col;
+}
+
+void launch_rel_delta_count(const RelDeltaArgs& a, hipStream_t st) {
+  const uint32_t nb = (a.nev + kBlock - 1) / kBlock;
+  if (nb) hipLaunchKernelGGL(k_rd_count, dim3(nb), dim3(kBlock), 0, st, a);
+}
+
+void launch_rel_delta_apply(const RelDeltaArgs& a, ScanCtx& sc, hipStream_t st) {
+  // dn holds the scanned change offsets on entry
+  const uint32_t nb = (a.nev + kBlock - 1) / kBlock;
+  if (nb) hipLaunchKernelGGL(k_rd_fill, dim3(nb), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(k_rd_len, dim3((a.cap + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(k_rd_sort_long, dim3(512), dim3(kBlock), 0, st, a);
+  launch_scan(sc, a.rp_new, a.cap + 1, st);
+  const uint32_t waves = (a.cap + 63) / 64;
+  hipLaunchKernelGGL(k_rd_merge, dim3((waves + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, a);
+  const uint32_t nb2 = (2 * a.nev + kBlock - 1) / kBlock;
+  if (nb2) hipLaunchKernelGGL(k_rd_adds, dim3(nb2), dim3(kBlock), 0, st, a);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -47,7 +47,7 @@ void set_err(const char* fmt, ...) {
 
 constexpr uint32_t kSeqLimit = 0x7ff00000u;  // renormalise seqs before they pass this
 #ifndef GW_CELLS_PER_SLOT
-#define GW_CELLS_PER_SLOT 2  // grid cell budget per slot of capacity (cells beyond it coarsen the grid)
+#define GW_CELLS_PER_SLOT 3  // grid cell budget per slot of capacity (cells beyond it coarsen the grid)
 #endif
 
 template <class T>
@@ -147,7 +147,15 @@ struct gwaoi_mgr {
   uint32_t *d_op_slot = nullptr, *d_op_space = nullptr, *d_leaves = nullptr, *d_dense = nullptr;
   // relation view (gwaoi_relation_device): CSR in HBM, allocated on first use, grown on demand
   uint32_t *rel_rp = nullptr, *rel_cols = nullptr, *rel_tmp = nullptr;
-  uint64_t rel_cap = 0;
+  uint64_t rel_cap = 0, rel_tmp_cap = 0;  // capacities of rel_cols / rel_tmp (swapped by the incremental path)
+  // incremental view (relation_delta): the view is valid for the state after pass `rel_passes`
+  uint32_t *rel_rp2 = nullptr, *rel_dn = nullptr, *rel_dcur = nullptr, *rel_dch = nullptr, *rel_flag = nullptr;
+  uint64_t rel_dch_cap = 0;  // changes rel_dch (and its row array behind it) hold
+  bool rel_valid = false;
+  uint64_t rel_passes = 0, rel_nnz = 0;
+  int rel_mode = 0;  // 0: incremental when possible, 1: always rebuild from the grid (gwaoi_debug_set_relation_mode)
+  uint64_t rel_stat_incr = 0, rel_stat_full = 0;
+  int rel_why = 0;  // why the last view was rebuilt (gwaoi_debug_set_relation_mode)
   unsigned long long* rel_tot = nullptr;  // device: [0] the count pass's 64-bit entry total, [1] longest row
   uint32_t* rel_slab = nullptr;           // count pass output: the rows by grid record (k_row_sort_slab)
   bool rel_no_slab = false;               // no room for the slab: the two-walk path
@@ -189,6 +197,9 @@ struct gwaoi_mgr {
   uint64_t tick_events = 0, tick_enter = 0;  // accumulated over the passes since the last tick
   uint32_t tick_passes = 0, tick_ops = 0;
   bool acc_open = false;                      // a pass ran since the last gwaoi_tick
+  uint64_t passes_run = 0;   // pipeline passes completed by this manager
+  uint64_t acc_base = 0;     // passes_run when the event accumulation (ev_out) was opened
+  bool acc_silent = false;   // a pass of the accumulation may have applied SILENT ops (not in ev_out)
 
   gw::SyncState* sync = nullptr;  // sync fan-out / ingest state (gwaoi_sync.hip), on demand
 
@@ -225,6 +236,7 @@ void space_extent(const SpaceHost& sh, float* x0, float* z0, float* x1, float* z
 }
 
 constexpr double kCellOccupancy = 0.5;  // planned entities per cell (config 2: 1M in 35,000^2, cells of 25)
+constexpr double kTileMovers = 440.0;   // planned entities per 32 x 32-cell tile (k_sweep: 512 threads)
 
 void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
   out.resize(m->nspaces);
@@ -245,7 +257,19 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
       const double area = ((double)x1 - x0) * ((double)z1 - z0);
       const double pop = sh.pop_hint ? (double)sh.pop_hint : (double)m->cap / std::max<uint32_t>(1, m->nspaces);
       const double cr = std::sqrt(kCellOccupancy * area / std::max(1.0, pop));
-      if (cr < 0.75 * c) c = std::max(cr, (double)sh.desc.dist / 16.0);
+      if (cr < 0.75 * c) {
+        c = std::max(cr, (double)sh.desc.dist / 16.0);
+      } else {
+        // Tile fill: the sweep walks a tile's movers one per thread of a kSweepBlock-thread block, so
+        // a 32 x 32-cell tile of a uniform crowd should hold a little less than one round of them
+        // (the count per tile is Poisson-like: +-sqrt). At config 2 (D 100) this is cells of 22.95
+        // instead of 25: 441 movers per tile instead of 522, of which two thirds of the tiles needed a
+        // second round; k_sweep 110 -> 98 us. Only for Spaces many tiles wide (a small Space's tiles
+        // are mostly partial: its cell count, not its tile fill, sets the cost).
+        const double ct = std::sqrt(kTileMovers * area / std::max(1.0, pop)) / gw::kTile;
+        const double w = std::min((double)x1 - x0, (double)z1 - z0);
+        if (ct < c && w >= 8.0 * gw::kTile * c) c = std::max(ct, (double)sh.desc.dist / 7.0);
+      }
     }
     if (!(c > 0)) c = 1.0;
     // tiles of kTile x kTile cells; cell counts padded to whole tiles
@@ -506,7 +530,10 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   if (!m->acc_open) {
     reset_tick(m);
     m->acc_open = true;
+    m->acc_base = m->passes_run;
+    m->acc_silent = false;
   }
+  if (dev && m->dv_kind) m->acc_silent = true;  // a mixed device batch may hold SILENT ops
   if ((uint64_t)m->next_seq + n_ops >= kSeqLimit) RCHK(renormalise(m));
   const uint32_t base = m->next_seq;
   m->next_seq += n_ops;
@@ -663,6 +690,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     break;
   }
   m->cur = ng;
+  m->passes_run++;
   m->grid[og].cs_zeroed = tile_build(m->grid[og]) ? 0u : m->grid[og].ncells + 1;
   m->ctr_sel ^= 1;
   m->ctr = m->ctr_buf + m->ctr_sel * gw::CTR_N;
@@ -763,7 +791,8 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot, m->rel_slab, m->rel_fix};
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot, m->rel_slab, m->rel_fix,
+                   m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
@@ -1277,6 +1306,87 @@ int gwaoi_count(const gwaoi_mgr* m, uint32_t* n_present, uint32_t* n_staged) {
   return GWAOI_OK;
 }
 
+namespace {
+
+// The view after the current accumulation's passes, from the view before them and their events
+// (the replay sink maintained from the events instead of rebuilt from positions).
+// Returns GWAOI_OK with *done = false when the events do not allow it (a row with too many
+// changes): the caller rebuilds from the grid. Costs one small read-back (the flag).
+int relation_delta(gwaoi_mgr* m, bool* done) {
+  *done = false;
+  hipStream_t st = m->stream;
+  const uint64_t nev = m->tick_events;
+  const uint64_t bound = m->rel_nnz + 2 * nev;  // every event an ENTER: the most the view can grow to
+  m->rel_why = 6;
+  if (bound > m->index_limit) return GWAOI_OK;
+  const size_t n1 = (size_t)m->cap + 1;
+  if (!m->rel_rp2) RCHK(dalloc(&m->rel_rp2, n1));
+  if (!m->rel_dn) RCHK(dalloc(&m->rel_dn, n1));
+  if (!m->rel_dcur) RCHK(dalloc(&m->rel_dcur, n1));
+  if (!m->rel_flag) RCHK(dalloc(&m->rel_flag, 2));  // [0] flag, [1] long rows
+  if (2 * nev > m->rel_dch_cap) {
+    if (m->rel_dch) hipFree(m->rel_dch);
+    m->rel_dch = nullptr;
+    m->rel_dch_cap = 0;
+    const uint64_t want = 2 * nev + nev / 2 + 4096;
+    // changes, their rows, the sign prefixes of long rows, the long rows (at most want / 32 of them)
+    RCHK(dalloc(&m->rel_dch, 3 * want + want / 32 + 1));
+    m->rel_dch_cap = want;
+  }
+  if (bound > m->rel_tmp_cap) {
+    if (m->rel_tmp) hipFree(m->rel_tmp);
+    m->rel_tmp = nullptr;
+    m->rel_tmp_cap = 0;
+    const uint64_t want = bound + m->rel_nnz / 4 + 1024;
+    RCHK(dalloc(&m->rel_tmp, want));
+    m->rel_tmp_cap = want;
+  }
+  gw::RelDeltaArgs a;
+  a.ev = m->ev_out;
+  a.nev = (uint32_t)nev;
+  a.cap = m->cap;
+  a.rp_old = m->rel_rp;
+  a.cols_old = m->rel_cols;
+  a.dn = m->rel_dn;
+  a.dcur = m->rel_dcur;
+  a.dch = m->rel_dch;
+  a.dchrow = m->rel_dch + m->rel_dch_cap;
+  a.rp_new = m->rel_rp2;
+  a.cols_new = m->rel_tmp;
+  a.cols_cap = m->rel_tmp_cap;
+  a.flag = m->rel_flag;
+  a.psum = reinterpret_cast<int32_t*>(m->rel_dch + 2 * m->rel_dch_cap);
+  a.longrows = m->rel_dch + 3 * m->rel_dch_cap;
+  a.nlong = m->rel_flag + 1;
+  a.long_cap = (uint32_t)(m->rel_dch_cap / 32 + 1);
+  HIPCHK(hipMemsetAsync(m->rel_dn, 0, n1 * sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(m->rel_dcur, 0, n1 * sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(m->rel_flag, 0, 2 * sizeof(uint32_t), st));
+  gw::launch_rel_delta_count(a, st);
+  gw::launch_scan(m->scan, m->rel_dn, m->cap + 1, st);
+  gw::launch_rel_delta_apply(a, m->scan, st);
+  HIPCHK(hipGetLastError());
+  uint32_t flag = 0, nnz_new = 0;
+  HIPCHK(hipMemcpyAsync(&flag, m->rel_flag, sizeof flag, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(&nnz_new, m->rel_rp2 + m->cap, sizeof nnz_new, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  m->rel_why = 7;
+  if (flag) return GWAOI_OK;
+  m->rel_why = 8;
+  // the events are exactly the relation's changes: the new size is the old one plus twice the net
+  // enters (a mismatch would mean a broken event stream: rebuild rather than trust it)
+  const int64_t expect = (int64_t)m->rel_nnz + 2 * ((int64_t)m->tick_enter - (int64_t)(nev - m->tick_enter));
+  if (expect != (int64_t)nnz_new) return GWAOI_OK;
+  std::swap(m->rel_rp, m->rel_rp2);
+  std::swap(m->rel_cols, m->rel_tmp);
+  std::swap(m->rel_cap, m->rel_tmp_cap);
+  m->rel_nnz = nnz_new;
+  *done = true;
+  return GWAOI_OK;
+}
+
+}  // namespace
+
 int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   RCHK(check_mgr(m));
   if (!out) {
@@ -1284,11 +1394,45 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
     return GWAOI_ERR_INVALID;
   }
   RCHK(set_dev(m));
+  bool flushed = false;
   if (m->n_ops || m->dv_n) {
     RCHK(run_pass(m, false));
-    m->acc_open = false;  // events of the flushed batch are discarded (documented in gwaoi.h)
-    reset_tick(m);
+    flushed = true;
   }
+  // events of a batch flushed here are discarded (documented in gwaoi.h), after the view used them
+  struct Discard {
+    gwaoi_mgr* m;
+    bool on;
+    ~Discard() {
+      if (on) {
+        m->acc_open = false;
+        reset_tick(m);
+      }
+    }
+  } discard{m, flushed};
+  if (m->rel_valid && m->rel_mode == 0 && m->rel_passes == m->passes_run) {  // nothing ran since the view
+    out->row_ptr = m->rel_rp;
+    out->cols = m->rel_cols;
+    out->nnz = m->rel_nnz;
+    return GWAOI_OK;
+  }
+  // Incremental when every pass since the view is in the open accumulation, none applied SILENT ops,
+  // and the events are not many against the relation (the update copies the whole view once).
+  m->rel_why = !m->rel_valid ? 1 : m->rel_mode ? 2 : m->acc_base != m->rel_passes ? 3 : m->acc_silent ? 4
+               : m->tick_events > m->rel_nnz / 2 + 65536 ? 5 : 0;
+  if (m->rel_why == 0) {
+    bool done = false;
+    RCHK(relation_delta(m, &done));
+    if (done) {
+      m->rel_passes = m->passes_run;
+      m->rel_stat_incr++;
+      out->row_ptr = m->rel_rp;
+      out->cols = m->rel_cols;
+      out->nnz = m->rel_nnz;
+      return GWAOI_OK;
+    }
+  }
+  m->rel_valid = false;
   hipStream_t st = m->stream;
   if (!m->rel_rp) RCHK(dalloc(&m->rel_rp, (size_t)m->cap + 1));
   if (!m->rel_tot) RCHK(dalloc(&m->rel_tot, 3));  // [0] entries, [1] longest row, [2] rows to fix
@@ -1338,15 +1482,20 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   }
   gw::launch_scan(m->scan, m->rel_rp, m->cap + 1, st);
   const uint32_t total = (uint32_t)total64;
+  const uint64_t want = (uint64_t)total + total / 4 + 1024;
   if (total > m->rel_cap) {
     if (m->rel_cols) hipFree(m->rel_cols);
-    if (m->rel_tmp) hipFree(m->rel_tmp);
-    m->rel_cols = m->rel_tmp = nullptr;
+    m->rel_cols = nullptr;
     m->rel_cap = 0;
-    const uint64_t want = (uint64_t)total + total / 4 + 1024;
     RCHK(dalloc(&m->rel_cols, want));
-    RCHK(dalloc(&m->rel_tmp, want));
     m->rel_cap = want;
+  }
+  if (total > m->rel_tmp_cap) {
+    if (m->rel_tmp) hipFree(m->rel_tmp);
+    m->rel_tmp = nullptr;
+    m->rel_tmp_cap = 0;
+    RCHK(dalloc(&m->rel_tmp, want));
+    m->rel_tmp_cap = want;
   }
   if (total == 0) {
     // empty relation: row_ptr is all zeros, nothing to sort
@@ -1362,9 +1511,24 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
     gw::launch_row_sort(m->rel_rp, m->cap, m->rel_cols, m->rel_tmp, st);
   }
   HIPCHK(hipGetLastError());
+  m->rel_valid = true;
+  m->rel_passes = m->passes_run;
+  m->rel_nnz = total;
+  m->rel_stat_full++;
   out->row_ptr = m->rel_rp;
   out->cols = m->rel_cols;
   out->nnz = total;
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_relation_mode(gwaoi_mgr* m, int mode, uint64_t* n_incremental, uint64_t* n_full,
+                                  int* last_rebuild_reason) {
+  RCHK(check_mgr(m));
+  if (mode < -1 || mode > 1) return GWAOI_ERR_INVALID;
+  if (mode >= 0) m->rel_mode = mode;
+  if (n_incremental) *n_incremental = m->rel_stat_incr;
+  if (n_full) *n_full = m->rel_stat_full;
+  if (last_rebuild_reason) *last_rebuild_reason = m->rel_why;
   return GWAOI_OK;
 }
 

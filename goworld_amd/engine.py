@@ -184,6 +184,15 @@ class Engine:
     def debug_set_next_seq(self, v: int):
         check(self._L.gwaoi_debug_set_next_seq(self._h, v))
 
+    def debug_relation_mode(self, mode: int = -1):
+        """Relation view path: 0 = incremental from the tick's events when possible, 1 = always rebuilt
+        from the grid, -1 = unchanged. Returns (views built incrementally, views rebuilt, reason code of
+        the last rebuild: include/gwaoi_tools.h)."""
+        ni, nf, why = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_int(0)
+        check(self._L.gwaoi_debug_set_relation_mode(self._h, mode, ctypes.byref(ni), ctypes.byref(nf),
+                                                    ctypes.byref(why)))
+        return ni.value, nf.value, why.value
+
     def debug_set_sweep_lds(self, on: bool):
         check(self._L.gwaoi_debug_set_sweep_lds(self._h, 1 if on else 0))
 

@@ -55,6 +55,13 @@ int gwaoi_debug_read_stamps(void* host, size_t bytes);
  * (gwaoi_collect_sync) accept before failing with GWAOI_ERR_NOMEM (default and maximum 2^32 - 1: their
  * offsets are uint32). Lowering it exercises the overflow guard without a 2^32-entry workload. */
 int gwaoi_debug_set_index_limit(struct gwaoi_mgr* mgr, uint64_t limit);
+/* Relation view mode: 0 = update the view from the tick's events when it allows (default), 1 = rebuild
+ * it from the grid on every call (even with no pass since the last one: timing); -1 leaves the mode.
+ * Reports how many views each path has built, and why the last rebuild was not an update (1 no view
+ * yet, 2 mode 1, 3 passes ran outside the event accumulation, 4 SILENT ops, 5 too many events, 6 size
+ * bound, 7 a row with too many changes, 8 inconsistent size). */
+int gwaoi_debug_set_relation_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* n_incremental, uint64_t* n_full,
+                                  int* last_rebuild_reason);
 /* Diagnostics: resident sweep workgroups per CU (HIP occupancy API) and the sweep's LDS bytes. */
 int gwaoi_debug_sweep_occupancy(int device, int* blocks_per_cu, int* lds_bytes);
 

@@ -287,6 +287,33 @@ def test_relation_view_paths(gpu, po, L):
     assert lens.max() > {5000.0: 40, 3500.0: 64, 2400.0: 128}[L]
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_relation_incremental_from_events(gpu, po, seed):
+    """gwaoi_relation_device kept up to date from each tick's events (k_rd_*: rows changed by rank
+    arithmetic over the tick's changes, no rebuild from the grid) equals the view rebuilt from the grid
+    (mode 1, a second manager fed the same calls) and oracle (i)'s neighbour sets after EVERY tick, over
+    Enter/Leave/Moved mixes with repeated slots (sub-passes: one tick's events span several passes),
+    teleports and leaves. Snapped positions crowd lattice points: rows with more than 32 changes in a
+    tick take the sorted path (k_rd_sort_long + binary searches)."""
+    case = H.case_random_ops(seed=2000 + seed, n=[300, 1000, 2000, 800][seed], nticks=12,
+                             ops_per_tick=[200, 300, 400, 900][seed], world=[300.0, 1000.0, 400.0, 60.0][seed],
+                             dist=[50.0, 100.0, 25.0, 10.0][seed], snap=seed % 2 == 0)
+    eng, ref = engine(case), engine(case)
+    ref.debug_relation_mode(1)
+    orc = po.XZListOracle(case["dist"], case["cap"])
+    for t, ops in enumerate(case["ticks"]):
+        want = H.oracle_tick(orc, ops)
+        assert_same(H.gpu_tick(eng, ops), want, f"{case['name']} tick {t}")
+        H.gpu_tick(ref, ops)
+        ra, rb, ro = eng.relation(), ref.relation(), orc.relation()
+        assert np.array_equal(ra[0], ro[0]) and np.array_equal(ra[1], ro[1]), f"tick {t}: incremental vs oracle"
+        assert np.array_equal(rb[0], ro[0]) and np.array_equal(rb[1], ro[1]), f"tick {t}: rebuilt vs oracle"
+    n_inc, n_full, why = eng.debug_relation_mode()
+    assert n_inc + n_full == len(case["ticks"])
+    assert n_inc >= len(case["ticks"]) // 2, (n_inc, n_full, why)
+    assert ref.debug_relation_mode()[0] == 0
+
+
 @pytest.mark.slow
 def test_config2_full_size_two_ticks(gpu, po):
     """SURVEY.md §8(d) config 2 at full size: N=1,000,000, L=35,000, D=100, seed 0x5EED0002; the
@@ -312,6 +339,10 @@ def test_config2_full_size_two_ticks(gpu, po):
         got = eng.tick()
         assert_same(got, want, f"1M tick {t}")
         assert len(got) > 10000
+        # the view updated from the tick's 325k events equals oracle (ii)'s relation
+        rg, ro = eng.relation(), orc.relation()
+        assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1]), f"1M tick {t}: relation"
+    assert eng.debug_relation_mode()[0] == 2, eng.debug_relation_mode()  # both moving ticks: updated
 
 
 def test_skewed_crowd_dense_path(gpu, po):
