@@ -733,6 +733,9 @@ __device__ __forceinline__ Judge make_judge(const Mover& m, uint32_t base) {
   return j;
 }
 
+#ifndef GW_JUDGE_EXACT  // A/B knob: 1 = the exact tests for every candidate
+#define GW_JUDGE_EXACT 0
+#endif
 // 0: no event; otherwise 1 = LEAVE, 2 = ENTER
 __device__ __forceinline__ int judge(const Judge& J, const uint4 ra, const uint4 rb) {
   const uint32_t opq = ra.w;
@@ -742,12 +745,19 @@ __device__ __forceinline__ int judge(const Judge& J, const uint4 ra, const uint4
   const bool valid = (opq != J.q) & (ghost ? !ae : (ae | (!hasg & (seq0 != 0u))));
   const float px = ae ? __uint_as_float(ra.x) : __uint_as_float(rb.x);
   const float pz = ae ? __uint_as_float(ra.y) : __uint_as_float(rb.y);
-  const bool useo = ae | (seq0 > J.q0);  // o's box (o acted last) or m's old box
-  const float cx = useo ? px : J.mx0, cz = useo ? pz : J.mz0;  // box centre
-  const float tx = useo ? J.mx0 : px, tz = useo ? J.mz0 : pz;  // point tested
   const float D = J.D;
-  const bool before = J.v0 & (tx >= cx - D) & (tx <= cx + D) & (tz >= cz - D) & (tz <= cz + D);
-  const bool after = J.v1 & (px >= J.lx1) & (px <= J.hx1) & (pz >= J.lz1) & (pz <= J.hz1);
+  // Chebyshev distances first; the exact asymmetric tests only near the bound (cf. make_judge)
+  const float b = fmaxf(fabsf(px - J.mx0), fabsf(pz - J.mz0));
+  const float f = fmaxf(fabsf(px - J.mx1), fabsf(pz - J.mz1));
+  bool before = J.v0 & (b <= D);
+  bool after = J.v1 & (f <= D);
+  if (GW_JUDGE_EXACT || __builtin_expect((int)(fabsf(b - D) <= J.eps) | (int)(fabsf(f - D) <= J.eps), 0)) {
+    const bool useo = ae | (seq0 > J.q0);  // o's box (o acted last) or m's old box
+    const float cx = useo ? px : J.mx0, cz = useo ? pz : J.mz0;  // box centre
+    const float tx = useo ? J.mx0 : px, tz = useo ? J.mz0 : pz;  // point tested
+    before = J.v0 & (tx >= cx - D) & (tx <= cx + D) & (tz >= cz - D) & (tz <= cz + D);
+    after = J.v1 & (px >= J.lx1) & (px <= J.hx1) & (pz >= J.lz1) & (pz <= J.hz1);
+  }
   return (valid & (before != after)) ? (after ? 2 : 1) : 0;
 }
 
@@ -787,10 +797,7 @@ __device__ __forceinline__ int judge_lds(const Judge& J, const uint4 rp, const u
   const float f = fmaxf(fabsf(px - J.mx1), fabsf(pz - J.mz1));
   bool before = J.v0 & (b <= D);
   bool after = J.v1 & (f <= D);
-#ifndef GW_JUDGE_EXACT  // A/B knob: 1 = the exact tests for every candidate
-#define GW_JUDGE_EXACT 0
-#endif
-  if (GW_JUDGE_EXACT || __builtin_expect((fabsf(b - D) <= J.eps) | (fabsf(f - D) <= J.eps), 0)) {
+  if (GW_JUDGE_EXACT || __builtin_expect((int)(fabsf(b - D) <= J.eps) | (int)(fabsf(f - D) <= J.eps), 0)) {
     const uint32_t seq0 = rm.y & ~kTopBit;
     const bool useo = ae | (seq0 > J.q0);  // o's box (o acted last) or m's old box
     const float cx = useo ? px : J.mx0, cz = useo ? pz : J.mz0;  // box centre
@@ -1592,17 +1599,66 @@ k_sweep_dense(SweepArgs a) {
     uint32_t local = 0;      // wave-uniform
     uint32_t pk = 0, pe = 0;  // this lane's cell-key range [pk, pe) (one tile part of one row segment)
     int np = 0;               // parts collected (wave-uniform)
+    // one chunk's events: numbered by a ballot prefix on top of the wave-uniform running count,
+    // slots from the wave's current chunk of ev_tmp (a fresh one reserved when it fills up)
+    auto emit_round = [&](int ev, uint32_t other) {
+      const unsigned long long em = __ballot(ev != 0);
+      if (!em) return;
+      const uint32_t cnt = (uint32_t)__popcll(em);
+      const uint32_t pre = (uint32_t)__popcll(em & below);
+      uint32_t gi = cur + pre;
+      if (cnt > left) {  // this chunk fills up: the rest goes to a fresh one
+        uint32_t nb = 0;
+        if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
+        nb = __shfl(nb, 0, 64);
+        if (pre >= left) gi = nb + (pre - left);
+        cur = nb + (cnt - left);
+        left = kEvChunk - (cnt - left);
+      } else {
+        cur += cnt;
+        left -= cnt;
+      }
+      if (ev) {
+        if (gi < a.ev_cap)
+          a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
+        nent += ev == 2 ? 1u : 0u;
+      }
+      local += cnt;
+    };
     auto flush = [&]() {
-      // one round trip for every part's record range, then the candidates 64 at a time
+      // one round trip for every part's record range, then the candidates 128 at a time (two loads in
+      // flight per lane). Candidate k belongs to the first part whose inclusive prefix exceeds k (a
+      // binary search over the lanes' prefixes; GW_DENSE_SEARCH=1: a wave-uniform readlane loop from the
+      // previous chunk's last part).
       uint32_t rs = 0, rl = 0;
       if (lane < np) {
         rs = a.g.cs[pk];
         rl = a.g.cs[pe] - rs;
       }
       const uint32_t incl = wave_incl_scan(rl);
-      const uint32_t total = __shfl(incl, 63, 64);
-      for (uint32_t b = 0; b < total; b += 64) {
-        const uint32_t k = b + lane;
+      const uint32_t excl = incl - rl;
+      const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+      int pcur = 0;  // wave-uniform
+#ifndef GW_DENSE_SEARCH
+#define GW_DENSE_SEARCH 0  // candidate -> part: 0 binary search over the lanes' prefixes, 1 readlane loop
+#endif
+      auto locate = [&](uint32_t k, uint32_t cend) -> uint32_t {  // record index of candidate k
+#if GW_DENSE_SEARCH
+        uint32_t base = 0, off = 0;
+        int p = pcur;
+        for (int q = pcur; q < np; ++q) {
+          const uint32_t ex = __builtin_amdgcn_readlane(excl, q);
+          if (ex >= cend) break;  // wave-uniform
+          const uint32_t rsq = __builtin_amdgcn_readlane(rs, q);
+          const bool in = k >= ex;
+          p = in ? q : p;
+          base = in ? rsq : base;
+          off = in ? ex : off;
+        }
+        pcur = __builtin_amdgcn_readlane(p, 63);
+        return base + (k - off);
+#else
+        (void)cend;
         int lo = 0, hi = 63;  // first lane whose inclusive prefix exceeds k
 #pragma unroll
         for (int st = 0; st < 6; ++st) {
@@ -1610,36 +1666,19 @@ k_sweep_dense(SweepArgs a) {
           if (__shfl(incl, mid, 64) > k) hi = mid;
           else lo = mid + 1;
         }
-        const uint32_t jj = __shfl(rs, lo, 64) + (k - (__shfl(incl, lo, 64) - __shfl(rl, lo, 64)));
-        int ev = 0;
-        uint32_t other = 0;
-        if (k < total) {
-          const uint4 ra = a.g.rec[jj].a;
-          ev = judge(J, ra, a.g.rec[jj].b);
-          other = ra.z & REC_SLOT;
-        }
-        const unsigned long long em = __ballot(ev != 0);
-        if (!em) continue;
-        const uint32_t cnt = (uint32_t)__popcll(em);
-        const uint32_t pre = (uint32_t)__popcll(em & below);
-        uint32_t gi = cur + pre;
-        if (cnt > left) {  // this chunk fills up: the rest goes to a fresh one
-          uint32_t nb = 0;
-          if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
-          nb = __shfl(nb, 0, 64);
-          if (pre >= left) gi = nb + (pre - left);
-          cur = nb + (cnt - left);
-          left = kEvChunk - (cnt - left);
-        } else {
-          cur += cnt;
-          left -= cnt;
-        }
-        if (ev) {
-          if (gi < a.ev_cap)
-            a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
-          nent += ev == 2 ? 1u : 0u;
-        }
-        local += cnt;
+        return __shfl(rs, lo, 64) + (k - __shfl(excl, lo, 64));
+#endif
+      };
+      for (uint32_t b = 0; b < total; b += 128) {
+        const uint32_t kA = b + lane, kB = b + 64 + lane;
+        const uint32_t jA = locate(kA, min(b + 64, total));
+        const bool hasB = b + 64 < total;  // wave-uniform
+        const uint32_t jB = hasB ? locate(kB, min(b + 128, total)) : 0u;
+        uint4 aA = make_uint4(0, 0, 0, 0), bA = aA, aB = aA, bB = aA;
+        if (kA < total) aA = a.g.rec[jA].a, bA = a.g.rec[jA].b;
+        if (hasB && kB < total) aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
+        emit_round(kA < total ? judge(J, aA, bA) : 0, aA.z & REC_SLOT);
+        if (hasB) emit_round(kB < total ? judge(J, aB, bB) : 0, aB.z & REC_SLOT);
       }
       np = 0;
     };
@@ -2319,10 +2358,45 @@ __device__ __forceinline__ int2 rd_long_sums(const RelDeltaArgs& a, uint32_t cs,
 }
 
 // Old entries to their new places: a wave takes 64 consecutive rows (one contiguous range of the old
-// cols) and walks it 64 entries at a time, coalesced both ways; each lane finds its entry's row among
-// the few rows the chunk touches (a wave-uniform loop over readlanes, no LDS).
+// cols, ~2,080 entries at config 2) and walks it 64 entries at a time; each lane finds its entry's row
+// among the few rows the chunk touches (a wave-uniform loop over readlanes). The group's old entries
+// are loaded into registers first (one chunk per register, every load in flight at once) and its
+// change lists (one contiguous range of dch, ~42 changes, with the sign prefixes of long rows) into
+// the wave's LDS: the walk then reads no global memory and its stores never wait (gfx9 counts stores
+// and loads on one vmcnt, so a global load in the walk waits for every store before it: 121 us at
+// config 2 that way; staging the entries in LDS instead cost occupancy, 145 us).
+template <bool B>
+struct BoolTag {
+  static constexpr bool value = B;
+};
+constexpr uint32_t kRdWaveCh = 256;    // changes of a 64-row group staged in LDS (+ their sign prefixes)
+// staged sorted list of a long row, indices relative to the group: (signs < v, signs == v)
+__device__ __forceinline__ int2 rd_long_sums_lds(const uint32_t* ch, const int32_t* ps, uint32_t cs, uint32_t ce,
+                                                 uint32_t v) {
+  uint32_t lo = cs, hi = ce;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((ch[mid] & 0x7FFFFFFFu) < v) lo = mid + 1;
+    else hi = mid;
+  }
+  uint32_t lo2 = lo, hi2 = ce;
+  while (lo2 < hi2) {
+    const uint32_t mid = (lo2 + hi2) >> 1;
+    if ((ch[mid] & 0x7FFFFFFFu) <= v) lo2 = mid + 1;
+    else hi2 = mid;
+  }
+  const int below = lo > cs ? ps[lo - 1] : 0;
+  const int upto = lo2 > cs ? ps[lo2 - 1] : 0;
+  return make_int2(below, upto - below);
+}
+
+constexpr int kRdRegChunks = 36;  // chunks of a group held in registers (config 2: 33 +- 1)
 __global__ void __launch_bounds__(kBlock) k_rd_merge(RelDeltaArgs a) {
+  __shared__ uint32_t chs_all[kBlock / 64][kRdWaveCh];
+  __shared__ int32_t pss_all[kBlock / 64][kRdWaveCh];
   const int lane = threadIdx.x & 63;
+  uint32_t* chs = chs_all[threadIdx.x >> 6];
+  int32_t* pss = pss_all[threadIdx.x >> 6];
   const uint32_t r0 = ((blockIdx.x * kBlock + threadIdx.x) >> 6) * 64u;
   if (r0 >= a.cap || *a.flag) return;  // wave-uniform
   const uint32_t nr = min(64u, a.cap - r0);
@@ -2336,11 +2410,17 @@ __global__ void __launch_bounds__(kBlock) k_rd_merge(RelDeltaArgs a) {
   }
   const uint32_t G0 = __builtin_amdgcn_readfirstlane(os);
   const uint32_t G1 = __builtin_amdgcn_readfirstlane(a.rp_old[r0 + nr]);
+  const uint32_t C0 = __builtin_amdgcn_readfirstlane(cs);
+  const uint32_t C1 = __builtin_amdgcn_readfirstlane(a.dn[r0 + nr]);
+  // registers: the group's old entries, all loads issued at once, one chunk per register
+  const bool staged = C1 - C0 <= kRdWaveCh && G1 - G0 <= (uint32_t)kRdRegChunks * 64u;  // wave-uniform
   uint32_t L0 = 0;  // first row the chunk touches (wave-uniform)
-  for (uint32_t b = G0; b < G1; b += 64) {
+  // one chunk: entries b + lane (value v); the row of each among the rows the chunk touches, its
+  // offset from the row's changes, the store
+  auto chunk = [&](uint32_t b, uint32_t v, auto tag) {
+    constexpr bool kStaged = decltype(tag)::value;
     const uint32_t e = b + lane;
     const bool act = e < G1;
-    const uint32_t v = act ? a.cols_old[e] : 0u;
     const uint32_t cend = min(b + 64u, G1);
     uint32_t ri = L0, mos = 0, mns = 0, mcs = 0, mce = 0;
     for (uint32_t L = L0; L < nr; ++L) {
@@ -2357,14 +2437,21 @@ __global__ void __launch_bounds__(kBlock) k_rd_merge(RelDeltaArgs a) {
     }
     if (act) {
       int sl = 0, se = 0;
-      if (mce - mcs <= kRdShort) {
-        for (uint32_t k = mcs; k < mce; ++k) {
-          const uint32_t c = a.dch[k], col = c & 0x7FFFFFFFu;
-          const int sg = (c >> 31) ? 1 : -1;
-          sl += col < v ? sg : 0;
-          se += col == v ? sg : 0;
-        }
-      } else if (mce - mcs <= kRdLongMax) {
+      auto scan = [&](uint32_t c) {
+        const uint32_t col = c & 0x7FFFFFFFu;
+        const int sg = (c >> 31) ? 1 : -1;
+        sl += col < v ? sg : 0;
+        se += col == v ? sg : 0;
+      };
+      if (kStaged && mce - mcs <= kRdShort) {
+        for (uint32_t k = mcs - C0; k < mce - C0; ++k) scan(chs[k]);
+      } else if (kStaged) {  // a long (sorted) row of a staged group (<= kRdWaveCh changes)
+        const int2 ss = rd_long_sums_lds(chs, pss, mcs - C0, mce - C0, v);
+        sl = ss.x;
+        se = ss.y;
+      } else if (mce - mcs <= kRdShort) {
+        for (uint32_t k = mcs; k < mce; ++k) scan(a.dch[k]);
+      } else if (mce - mcs <= kRdLongMax) {  // a long (sorted) row: binary searches in global memory
         const int2 ss = rd_long_sums(a, mcs, mce, v);
         sl = ss.x;
         se = ss.y;
@@ -2373,6 +2460,30 @@ __global__ void __launch_bounds__(kBlock) k_rd_merge(RelDeltaArgs a) {
       if (se >= 0 && o < a.cols_cap) a.cols_new[o] = v;  // (the bound holds for a consistent event stream)
     }
     L0 = __builtin_amdgcn_readlane(ri, 63);
+  };
+  if (staged) {
+    uint32_t vv[kRdRegChunks];
+#pragma unroll
+    for (int i = 0; i < kRdRegChunks; ++i) {
+      const uint32_t e = G0 + (uint32_t)i * 64u + lane;
+      vv[i] = e < G1 ? a.cols_old[e] : 0u;
+    }
+    for (uint32_t k = lane; k < C1 - C0; k += 64) chs[k] = a.dch[C0 + k];
+    for (uint32_t k = lane; k < C1 - C0; k += 64) pss[k] = a.psum[C0 + k];  // (meaningful for long rows)
+    // every load complete before the first store: the walk's uses of vv then wait on nothing (a wait
+    // for one of them after stores were issued would be vmcnt(0), i.e. for the stores too)
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < kRdRegChunks; ++i) {
+      const uint32_t b = G0 + (uint32_t)i * 64u;
+      if (b >= G1) break;  // wave-uniform
+      chunk(b, vv[i], BoolTag<true>{});
+    }
+  } else {
+    for (uint32_t b = G0; b < G1; b += 64) chunk(b, b + lane < G1 ? a.cols_old[b + lane] : 0u, BoolTag<false>{});
   }
 }
 
