@@ -236,7 +236,10 @@ void space_extent(const SpaceHost& sh, float* x0, float* z0, float* x1, float* z
 }
 
 constexpr double kCellOccupancy = 0.5;  // planned entities per cell (config 2: 1M in 35,000^2, cells of 25)
-constexpr double kTileMovers = 440.0;   // planned entities per 32 x 32-cell tile (k_sweep: 512 threads)
+#ifndef GW_TILE_MOVERS
+#define GW_TILE_MOVERS 440.0
+#endif
+constexpr double kTileMovers = GW_TILE_MOVERS;  // planned entities per 32 x 32-cell tile (k_sweep: 512 threads)
 
 void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
   out.resize(m->nspaces);

@@ -79,6 +79,19 @@ def test_config3_512_spaces_vs_oracle_per_space(gpu, oracle_lib):
         got = eng.tick()
         assert np.array_equal(got, want), f"tick {t}: " + H.fmt_diff(got, want)
         assert len(got) > 1000
+        # the relation view, updated from the tick's events (the enter tick's view was rebuilt: its
+        # device batch could hold SILENT ops), equals the 512 per-Space oracles' neighbour sets
+        rp, cols = eng.relation()
+        wrp, wcols, base = [np.zeros(1, np.int64)], [], 0
+        for s in range(S):
+            orp, ocols = orcs[s].relation()
+            wrp.append(orp[1:].astype(np.int64) + base)
+            wcols.append(ocols.astype(np.int64) + s * N)
+            base += len(ocols)
+        assert np.array_equal(rp.astype(np.int64), np.concatenate(wrp)), f"tick {t}: relation rows"
+        assert np.array_equal(cols.astype(np.int64), np.concatenate(wcols)), f"tick {t}: relation cols"
+    n_inc, n_full, why = eng.debug_relation_mode()
+    assert n_inc == 2 and n_full == 1, (n_inc, n_full, why)  # ticks 2, 3 updated; tick 1's view rebuilt
     eng.close()
 
 
