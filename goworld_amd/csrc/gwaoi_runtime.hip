@@ -815,8 +815,10 @@ void free_all(gwaoi_mgr* m) {
 
 int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capacity, int device,
                 gwaoi_mgr** out) {
-  if (!out || !spaces || !nspaces || !capacity || capacity > 0x7fffffffu) {
-    set_err("gwaoi_create: invalid argument");
+  // slots live in a grid record's 30-bit slot field, and op ranks (< capacity) below the sweep's
+  // kNoRank (2^30 - 1)
+  if (!out || !spaces || !nspaces || !capacity || capacity > 0x3fffffffu) {
+    set_err("gwaoi_create: invalid argument (capacity must be 1 .. 2^30 - 1)");
     return GWAOI_ERR_INVALID;
   }
   *out = nullptr;

@@ -77,7 +77,8 @@ typedef struct {
   float max_x, max_z;         /* are clamped into edge cells (only slower). min >= max => auto extent. */
 } gwaoi_space_desc;
 
-/* Replaces aoi.NewXZListAOIManager(aoidist) (Space.go:105) for one Space. capacity = max slot + 1. */
+/* Replaces aoi.NewXZListAOIManager(aoidist) (Space.go:105) for one Space. capacity = max slot + 1
+ * (1 .. 2^30 - 1). */
 int gwaoi_create(float dist, uint32_t capacity, int device, gwaoi_mgr** out);
 /* Many Spaces in one manager (one pipeline pass per tick for all of them). */
 int gwaoi_create_spaces(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capacity, int device,
