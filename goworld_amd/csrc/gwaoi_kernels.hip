@@ -923,6 +923,9 @@ __device__ __forceinline__ void judge_chunk(const SweepSmem& sm, const Judge& J,
 // atomic per wave when the range runs past the queue; then each lane writes its own events in mask
 // order (its `local` numbering). Every lane that reached the call takes part (the masks of a lane
 // without events are zero).
+#ifndef GW_EV_LIDX
+#define GW_EV_LIDX 0
+#endif
 template <class IdxA, class IdxB>
 __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, const Mover& m, unsigned long long hA,
                                            unsigned long long eA, IdxA&& ia, unsigned long long hB,
@@ -957,14 +960,17 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, co
     while (h) {
       const int bit = __ffsll((long long)h) - 1;
       const bool enter = (e >> bit) & 1ull;
-      const uint4 rec = make_uint4(m.rank, local++, m.slot, sm.rslot[idx((uint32_t)bit)] | (enter ? 0x80000000u : 0u));
+      const uint32_t j = idx((uint32_t)bit), eb = enter ? 0x80000000u : 0u;
       nent += enter ? 1u : 0u;
       if (p < (uint32_t)kEvLds) {
-        sm.ev[p] = rec;
+        // GW_EV_LIDX: the queue holds the candidate's LDS record index; the block's flush turns it into
+        // the slot (one coalesced pass instead of a dependent LDS read per event in this loop)
+        sm.ev[p] = make_uint4(m.rank, local, m.slot, (GW_EV_LIDX ? j : sm.rslot[j]) | eb);
       } else {
         const uint32_t gi = g0 + (p - qs);
-        if (gi < a.ev_cap) a.ev_tmp[gi] = rec;
+        if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local, m.slot, sm.rslot[j] | eb);
       }
+      ++local;
       ++p;
       h &= h - 1ull;
     }
@@ -985,6 +991,9 @@ __device__ __forceinline__ void judge_stream(const SweepArgs& a, SweepSmem& sm, 
   }
 }
 
+#ifndef GW_RING_MERGE
+#define GW_RING_MERGE 0
+#endif
 __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Walk& w,
                                               const Region& R, const Geom& g, uint32_t& nent) {
   const Judge J = make_judge(m, a.base);
@@ -994,6 +1003,20 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     // row stream: LDS record indices directly; column stream: through the column-major index
     auto ri = [&](uint32_t k) { return stream_at(Rs, k); };
     auto ci = [&](uint32_t k) { return (uint32_t)sm.cidx[stream_at(Cs, k)]; };
+#if GW_RING_MERGE
+    // both streams as ONE stream (row candidates, then column candidates): a wave's judge loop runs
+    // max over lanes of (rows + columns) instead of max(rows) + max(columns)
+    const uint32_t nr = Rs.total, tot = Rs.total + Cs.total;
+    auto bi = [&](uint32_t k) { return k < nr ? stream_at(Rs, k) : (uint32_t)sm.cidx[stream_at(Cs, k - nr)]; };
+    if (__all(tot <= 64u)) {
+      unsigned long long h, e;
+      judge_chunk(sm, J, 0, tot, bi, h, e);
+      emit_masks(a, sm, m, h, e, bi, 0ull, 0ull, [&](uint32_t k) { return k; }, local, nent);
+      return local;
+    }
+    judge_stream(a, sm, J, m, tot, bi, local, nent);
+    return local;
+#endif
     if (__all(Rs.total <= 64u && Cs.total <= 64u)) {  // the usual ring: both streams in one chunk, one emission
       unsigned long long hR, eR, hC, eC;
       judge_chunk(sm, J, 0, Rs.total, ri, hR, eR);
@@ -1404,7 +1427,9 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nq; i += kSweepBlock) {
     const uint32_t gi = sm.base + i;
-    if (gi < a.ev_cap) a.ev_tmp[gi] = sm.ev[i];
+    uint4 e = sm.ev[i];
+    if (GW_EV_LIDX && lds) e.w = sm.rslot[e.w & ~kTopBit] | (e.w & kTopBit);  // block-uniform: LDS path events
+    if (gi < a.ev_cap) a.ev_tmp[gi] = e;
   }
   GW_STAMP(4, __builtin_amdgcn_s_memrealtime());
 }
@@ -1555,6 +1580,37 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
     a.rank_cnt[i] = sweep_global(a, q, m, g, nent);
+  }
+  if (nent) atomicAdd(&q.enter, nent);
+  __syncthreads();
+  const uint32_t nq = min(q.n, (uint32_t)kEvLds);
+  if (threadIdx.x == 0) {
+    q.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+    if (q.enter) atomicAdd(&a.ctr[CTR_ENTER], q.enter);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
+    const uint32_t gi = q.base + i;
+    if (gi < a.ev_cap) a.ev_tmp[gi] = q.ev[i];
+  }
+}
+
+// A/B (GW_DENSE_FLAT=1): the dense list one THREAD per mover (sweep_global), instead of one wave.
+__global__ void __launch_bounds__(kBlock) k_sweep_dense_flat(SweepArgs a) {
+  __shared__ FlatQ q;
+  uint32_t nent = 0;
+  if (threadIdx.x == 0) {
+    q.n = 0;
+    q.enter = 0;
+  }
+  __syncthreads();
+  const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
+  for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < nd; t += gridDim.x * kBlock) {
+    const uint32_t s = a.dense[t];
+    const Geom g = a.g.geom[a.space_of[s]];
+    const Mover m = slot_mover(a, s, g.D);
+    const uint32_t cnt = sweep_global(a, q, m, g, nent);
+    if (cnt) a.rank_cnt[m.rank] = cnt;
   }
   if (nent) atomicAdd(&q.enter, nent);
   __syncthreads();
@@ -1738,7 +1794,12 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
                        st, a);
   // the dense list's length is on the device: a fixed grid that exits at once when it is empty (a
   // small one when the previous pass had none; the kernel is grid-stride, any grid is correct)
-  if (a.dense)
+#ifndef GW_DENSE_FLAT
+#define GW_DENSE_FLAT 0
+#endif
+  if (a.dense && GW_DENSE_FLAT)
+    hipLaunchKernelGGL(k_sweep_dense_flat, dim3(a.dense_hint ? 256 * GW_DENSE_FLAT : 16), dim3(kBlock), 0, st, a);
+  else if (a.dense)
     hipLaunchKernelGGL(k_sweep_dense, dim3(a.dense_hint ? kDenseGrid : 64), dim3(kDenseBlock), 0, st, a);
 }
 
