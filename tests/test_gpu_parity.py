@@ -317,7 +317,7 @@ def test_relation_incremental_from_events(gpu, po, seed):
 @pytest.mark.slow
 def test_config2_full_size_two_ticks(gpu, po):
     """SURVEY.md §8(d) config 2 at full size: N=1,000,000, L=35,000, D=100, seed 0x5EED0002; the
-    bulk enter tick and two all-moving ticks against oracle (ii)."""
+    bulk enter tick (relation and every ENTER event) and four all-moving ticks against oracle (ii)."""
     from goworld_amd.engine import Engine
     n, L, seed = 1_000_000, 35000.0, 0x5EED0002
     x, z = po.workload_init(seed, n, L)
@@ -330,7 +330,14 @@ def test_config2_full_size_two_ticks(gpu, po):
     rg, ro = eng.relation(), orc.relation()
     assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1])
     assert len(ev0) == len(ro[1]) // 2  # one ENTER per pair, raised by the later Enter
-    for t in (1, 2):
+    # the enter tick's events exactly: Enters run in slot order, so pair {a < b} raises ENTER(b, a)
+    # (mover b, other a) once; every event of the tick is such an ENTER, rows and columns ascending
+    rp, cols = ro
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(rp.astype(np.int64)))
+    keep = cols.astype(np.int64) < rows
+    want0 = np.stack([rows[keep].astype(np.uint32), cols[keep].astype(np.uint32) | np.uint32(H.EV_ENTER)], axis=1)
+    assert ev0.dtype == want0.dtype and np.array_equal(ev0, want0), "1M enter tick: " + H.fmt_diff(ev0[:100000], want0[:100000])
+    for t in (1, 2, 3, 4):
         po.workload_step(seed, t, x, z, L, 1.0)
         orc.moved_batch(slots, x, z)
         ev = orc.take_events()
@@ -342,7 +349,7 @@ def test_config2_full_size_two_ticks(gpu, po):
         # the view updated from the tick's 325k events equals oracle (ii)'s relation
         rg, ro = eng.relation(), orc.relation()
         assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1]), f"1M tick {t}: relation"
-    assert eng.debug_relation_mode()[0] == 2, eng.debug_relation_mode()  # both moving ticks: updated
+    assert eng.debug_relation_mode()[0] == 4, eng.debug_relation_mode()  # every moving tick: updated
 
 
 def test_skewed_crowd_dense_path(gpu, po):
