@@ -129,8 +129,14 @@ struct BinArgs {
 // Slots per block of the tile-bucketed build (at least; a capacity over 256 chunks gets larger
 // chunks, so the tile x chunk histogram stays ~256 x tiles), and the largest tile count its LDS
 // histogram holds (larger grids use the cell-atomic build).
-constexpr uint32_t kBinChunk = 4096;
-constexpr uint32_t kBinMaxBlocks = 256;
+#ifndef GW_BIN_CHUNK
+#define GW_BIN_CHUNK 4096
+#endif
+#ifndef GW_BIN_MAX_BLOCKS
+#define GW_BIN_MAX_BLOCKS 256
+#endif
+constexpr uint32_t kBinChunk = GW_BIN_CHUNK;
+constexpr uint32_t kBinMaxBlocks = GW_BIN_MAX_BLOCKS;
 inline uint32_t bin_chunk(uint32_t cap) {
   const uint64_t per = ((uint64_t)cap + kBinMaxBlocks - 1) / kBinMaxBlocks;
   const uint64_t c = (per + kBinChunk - 1) / kBinChunk * kBinChunk;
