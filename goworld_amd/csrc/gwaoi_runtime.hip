@@ -275,6 +275,16 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
       }
     }
     if (!(c > 0)) c = 1.0;
+#ifndef GW_DENSE_CELL_DIV
+#define GW_DENSE_CELL_DIV 0  // A/B: k > 0 gives a Space whose LDS region cannot fit cells of D / k
+#endif
+    if (GW_DENSE_CELL_DIV > 0 && m->cell_side <= 0) {
+      // its movers all take the dense walk, whose cost follows the candidates of its ring (ring width
+      // ~ one cell), not the region: finer cells thin the ring
+      const int rch = (int)std::ceil((double)sh.desc.dist * (1.0 + 1e-5) / c) + 1;
+      if ((gw::kTile + 2 * rch) * (gw::kTile + 2 * rch) > gw::kSweepRegCells)
+        c = std::min(c, (double)sh.desc.dist / GW_DENSE_CELL_DIV);
+    }
     // tiles of kTile x kTile cells; cell counts padded to whole tiles
     auto dims = [&](double cc, int64_t* tx, int64_t* tz) {
       const int64_t nx = (int64_t)(((double)x1 - x0) / cc) + 1, nz = (int64_t)(((double)z1 - z0) / cc) + 1;
