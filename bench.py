@@ -87,6 +87,58 @@ def cpu_baseline(n, L, dist, seed, target_s):
             "cpu": _cpu_model(), "nproc": os.cpu_count()}
 
 
+def cpu_baseline_spaces(n_per, L, dist, seed0, nspaces, target_s, threads=16):
+    """Config 3 on the CPU (one worker per Space, across the cores): oracle (i), one
+    XZListAOIManager restatement per Space (C; ctypes drops the GIL), bulk-loaded at tick 0, then one
+    all-moving tick of Moved() in slot order per Space, Spaces handed to `threads` workers until about
+    `target_s` of wall time has passed. Rate = updates of the finished Spaces / wall time."""
+    import threading
+
+    import numpy as np
+    from oracle import pyoracle
+    pyoracle.build()
+    lock = threading.Lock()
+    state = {"next": 0, "done": 0, "events": 0}
+    stop = time.perf_counter() + target_s
+
+    def worker():
+        while True:
+            with lock:
+                s = state["next"]
+                if s >= nspaces or time.perf_counter() > stop:
+                    return
+                state["next"] = s + 1
+            x, z = pyoracle.workload_init(seed0 + s, n_per, L)
+            orc = pyoracle.XZListOracle(dist, n_per)
+            slots = np.arange(n_per, dtype=np.uint32)
+            orc.bulk_enter(slots, x, z)
+            orc.set_record(True)
+            pyoracle.workload_step(seed0 + s, 1, x, z, L, 1.0)
+            orc.moved_batch(slots, x, z)
+            ne = len(orc.take_events())
+            orc.close()
+            with lock:
+                state["done"] += 1
+                state["events"] += ne
+
+    # untimed warm-up of the library (build, first load)
+    pyoracle.XZListOracle(dist, 8).close()
+    ts = [threading.Thread(target=worker) for _ in range(threads)]
+    t = time.perf_counter()
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join()
+    wall = time.perf_counter() - t
+    m = state["done"] * n_per
+    return {"value": m / wall, "unit": "entity-updates/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (i) go-aoi XZListAOIManager restatement (C), one manager per Space, {threads} worker "
+                      f"threads: {state['done']} of {nspaces} Spaces x {n_per} (L={L:g}, D={dist:g}, seeds "
+                      f"{seed0:#x}+s), each bulk-loaded then one all-moving tick of Moved(); {m} updates in "
+                      f"{wall:.2f}s wall (bulk loads inside the wall time, a small share), {state['events']} pair events",
+            "cpu": _cpu_model(), "nproc": os.cpu_count()}
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -745,10 +797,16 @@ def main():
     else:
         result = run_spaces(args, rank, world, dev, sync_all, allmax)
 
-    # ---- CPU baseline (rank 0, N=1, config 2 only) ----
+    # ---- CPU baseline (rank 0, N=1: config 2, and config 3 per Space) ----
     if rank == 0 and world == 1 and args.workload == "config2" and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args.n, args.L, args.dist, args.seed, args.cpu_baseline_seconds)
+        except Exception as e:  # reported, never fatal to the GPU line
+            result["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and args.workload == "config3" and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline_spaces(2000, 1600.0, 100.0, 0x5EED0003, args.spaces,
+                                                         args.cpu_baseline_seconds)
         except Exception as e:  # reported, never fatal to the GPU line
             result["cpu_baseline"] = {"error": repr(e)}
     if world > 1:
