@@ -89,40 +89,47 @@ def cpu_baseline(n, L, dist, seed, target_s):
 
 def cpu_baseline_spaces(n_per, L, dist, seed0, nspaces, target_s, threads=16):
     """Config 3 on the CPU (one worker per Space, across the cores): oracle (i), one
-    XZListAOIManager restatement per Space (C; ctypes drops the GIL), bulk-loaded at tick 0, then one
-    all-moving tick of Moved() in slot order per Space, Spaces handed to `threads` workers until about
-    `target_s` of wall time has passed. Rate = updates of the finished Spaces / wall time."""
+    XZListAOIManager restatement per Space (C; ctypes drops the GIL), bulk-loaded at tick 0, then `nt`
+    all-moving ticks of Moved() in slot order, Spaces handed to `threads` workers. `nt` is sized from
+    one calibration tick so the pool runs about `target_s`. Rate = updates / wall time of the pool."""
     import threading
 
     import numpy as np
     from oracle import pyoracle
     pyoracle.build()
+
+    def space_run(s, nt):
+        x, z = pyoracle.workload_init(seed0 + s, n_per, L)
+        orc = pyoracle.XZListOracle(dist, n_per)
+        slots = np.arange(n_per, dtype=np.uint32)
+        orc.bulk_enter(slots, x, z)
+        orc.set_record(True)
+        ne = 0
+        t = time.perf_counter()
+        for k in range(1, nt + 1):
+            pyoracle.workload_step(seed0 + s, k, x, z, L, 1.0)
+            orc.moved_batch(slots, x, z)
+            ne += len(orc.take_events())
+        dt = time.perf_counter() - t
+        orc.close()
+        return ne, dt
+
+    _, t_one = space_run(0, 1)  # calibration (and library warm-up), untimed
+    nt = int(min(1000, max(1, target_s * threads / max(1e-9, nspaces * t_one))))
     lock = threading.Lock()
-    state = {"next": 0, "done": 0, "events": 0}
-    stop = time.perf_counter() + target_s
+    state = {"next": 0, "events": 0}
 
     def worker():
         while True:
             with lock:
                 s = state["next"]
-                if s >= nspaces or time.perf_counter() > stop:
+                if s >= nspaces:
                     return
                 state["next"] = s + 1
-            x, z = pyoracle.workload_init(seed0 + s, n_per, L)
-            orc = pyoracle.XZListOracle(dist, n_per)
-            slots = np.arange(n_per, dtype=np.uint32)
-            orc.bulk_enter(slots, x, z)
-            orc.set_record(True)
-            pyoracle.workload_step(seed0 + s, 1, x, z, L, 1.0)
-            orc.moved_batch(slots, x, z)
-            ne = len(orc.take_events())
-            orc.close()
+            ne, _ = space_run(s, nt)
             with lock:
-                state["done"] += 1
                 state["events"] += ne
 
-    # untimed warm-up of the library (build, first load)
-    pyoracle.XZListOracle(dist, 8).close()
     ts = [threading.Thread(target=worker) for _ in range(threads)]
     t = time.perf_counter()
     for th in ts:
@@ -130,12 +137,12 @@ def cpu_baseline_spaces(n_per, L, dist, seed0, nspaces, target_s, threads=16):
     for th in ts:
         th.join()
     wall = time.perf_counter() - t
-    m = state["done"] * n_per
+    m = nspaces * n_per * nt
     return {"value": m / wall, "unit": "entity-updates/s", "cores": threads, "kind": "port",
             "sample": f"oracle (i) go-aoi XZListAOIManager restatement (C), one manager per Space, {threads} worker "
-                      f"threads: {state['done']} of {nspaces} Spaces x {n_per} (L={L:g}, D={dist:g}, seeds "
-                      f"{seed0:#x}+s), each bulk-loaded then one all-moving tick of Moved(); {m} updates in "
-                      f"{wall:.2f}s wall (bulk loads inside the wall time, a small share), {state['events']} pair events",
+                      f"threads: {nspaces} Spaces x {n_per} (L={L:g}, D={dist:g}, seeds {seed0:#x}+s), each "
+                      f"bulk-loaded then {nt} all-moving ticks of Moved(); {m} updates in {wall:.2f}s wall "
+                      f"(bulk loads inside the wall time), {state['events']} pair events",
             "cpu": _cpu_model(), "nproc": os.cpu_count()}
 
 
