@@ -1294,6 +1294,9 @@ __device__ __forceinline__ Mover lds_mover(const SweepSmem& sm, uint32_t i, uint
   return m;
 }
 
+#ifndef GW_EV_RESERVE
+#define GW_EV_RESERVE 0
+#endif
 // One work item of k_sweep: a tile. Stage its region (which lists the tile's movers); walk them, one
 // thread per mover, consecutive rounds of the block in alternating direction (a tile holds ~520
 // movers for 512 threads). The block's LDS event queue is flushed with one global atomic at the end.
@@ -1332,7 +1335,13 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     tcz = tz * kTile - R.zr0;
     lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= 3 * kTile;
   }
+  // GW_EV_RESERVE: an LDS-path block reserves its event-queue range (kEvLds slots) before staging, so
+  // the returning global atomic overlaps the staging loads instead of sitting between the walk and the
+  // flush; the flush then writes its events and marks the rest of the range as holes (k_place skips them)
+  const bool reserved = GW_EV_RESERVE && lds;  // block-uniform
+  uint32_t resv = 0;                           // thread 0: first reserved slot
   if (lds) {
+    if (reserved && threadIdx.x == 0) resv = atomicAdd(&a.ctr[CTR_EVENTS], (uint32_t)kEvLds);
     GW_STAMP(1, __builtin_amdgcn_s_memrealtime());
     const uint32_t nst = stage(a, g, R, tcx, tcz, sm);
     lds = nst <= (uint32_t)kCap;  // block-uniform
@@ -1424,14 +1433,20 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
   GW_STAMP(3, __builtin_amdgcn_s_memrealtime());
   const uint32_t nq = min(sm.n, (uint32_t)kEvLds);
   if (threadIdx.x == 0) {
-    sm.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+    if (reserved) {
+      sm.base = resv;
+      if (nq < (uint32_t)kEvLds) atomicAdd(&a.ctr[CTR_HOLES], (uint32_t)kEvLds - nq);
+    } else {
+      sm.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+    }
     if (sm.enter) atomicAdd(&a.ctr[CTR_ENTER], sm.enter);
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nq; i += kSweepBlock) {
+  const uint32_t nw = reserved ? (uint32_t)kEvLds : nq;
+  for (uint32_t i = threadIdx.x; i < nw; i += kSweepBlock) {
     const uint32_t gi = sm.base + i;
-    uint4 e = sm.ev[i];
-    if (GW_EV_LIDX && lds) e.w = sm.rslot[e.w & ~kTopBit] | (e.w & kTopBit);  // block-uniform: LDS path events
+    uint4 e = i < nq ? sm.ev[i] : make_uint4(kEvHole, 0u, 0u, 0u);
+    if (GW_EV_LIDX && lds && i < nq) e.w = sm.rslot[e.w & ~kTopBit] | (e.w & kTopBit);  // LDS path events
     if (gi < a.ev_cap) a.ev_tmp[gi] = e;
   }
   GW_STAMP(4, __builtin_amdgcn_s_memrealtime());
