@@ -220,3 +220,31 @@ def test_replay_tool_tracks_the_relation(po):
     bad = np.ascontiguousarray(ev[-1:])  # replaying the last change of a pair again is inconsistent
     assert rs.replay(bad.ctypes.data, 1) == 4
     rs.close()
+
+
+def test_config3_cpu_baseline_sample(po):
+    """bench.py's config-3 CPU baseline (one oracle (i) manager per Space, a worker
+    pool): a bounded sample reports a rate, the threads used and every Space walked the same number of
+    ticks; its pair events equal one sequential replay of those ticks."""
+    import re
+
+    import numpy as np
+
+    import bench
+    r = bench.cpu_baseline_spaces(500, 800.0, 100.0, 0x5EED0003, 3, 0.05, threads=2)
+    assert r["value"] > 0 and r["cores"] == 2 and r["kind"] == "port"
+    m = re.search(r"then (\d+) all-moving ticks.*?(\d+) pair events", r["sample"])
+    nt, nev = int(m.group(1)), int(m.group(2))
+    want = 0
+    for s in range(3):
+        x, z = po.workload_init(0x5EED0003 + s, 500, 800.0)
+        orc = po.XZListOracle(100.0, 500)
+        slots = np.arange(500, dtype=np.uint32)
+        orc.bulk_enter(slots, x, z)
+        orc.set_record(True)
+        for k in range(1, nt + 1):
+            po.workload_step(0x5EED0003 + s, k, x, z, 800.0, 1.0)
+            orc.moved_batch(slots, x, z)
+            want += len(orc.take_events())
+        orc.close()
+    assert nev == want
