@@ -551,7 +551,7 @@ void launch_bin_tiles(const BinArgs& a, ScanCtx& sc, hipStream_t st) {
 #endif
 constexpr int kSweepBlock = GW_SWEEP_BLOCK;  // 8 waves: a config-2 tile holds ~520 movers (one round, a few twice)
 #ifndef GW_EV_LDS
-#define GW_EV_LDS 192
+#define GW_EV_LDS 256
 #endif
 constexpr int kEvLds = GW_EV_LDS;      // events staged per block before spilling to global atomics
 constexpr int kRegCells = kSweepRegCells;  // max cells of a staged region (48 x 48)
