@@ -1613,37 +1613,6 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
   }
 }
 
-// A/B (GW_DENSE_FLAT=1): the dense list one THREAD per mover (sweep_global), instead of one wave.
-__global__ void __launch_bounds__(kBlock) k_sweep_dense_flat(SweepArgs a) {
-  __shared__ FlatQ q;
-  uint32_t nent = 0;
-  if (threadIdx.x == 0) {
-    q.n = 0;
-    q.enter = 0;
-  }
-  __syncthreads();
-  const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
-  for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < nd; t += gridDim.x * kBlock) {
-    const uint32_t s = a.dense[t];
-    const Geom g = a.g.geom[a.space_of[s]];
-    const Mover m = slot_mover(a, s, g.D);
-    const uint32_t cnt = sweep_global(a, q, m, g, nent);
-    if (cnt) a.rank_cnt[m.rank] = cnt;
-  }
-  if (nent) atomicAdd(&q.enter, nent);
-  __syncthreads();
-  const uint32_t nq = min(q.n, (uint32_t)kEvLds);
-  if (threadIdx.x == 0) {
-    q.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
-    if (q.enter) atomicAdd(&a.ctr[CTR_ENTER], q.enter);
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
-    const uint32_t gi = q.base + i;
-    if (gi < a.ev_cap) a.ev_tmp[gi] = q.ev[i];
-  }
-}
-
 // Dense movers: one WAVE per mover (grid-stride over the list k_sweep built). The walk is the same
 // row walk as sweep_global, but its cell ranges are collected one per lane, and the concatenated
 // candidate stream is judged 64 at a time (each lane finds its range by a binary search over the
@@ -1798,161 +1767,6 @@ k_sweep_dense(SweepArgs a) {
   if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
 }
 
-// Dense movers, v2 (GW_DENSE_V2, default): the same wave-per-mover walk with fewer dependent memory
-// round trips per mover, which is what a uniform large-D mover (ring of ~50-100 candidates) pays for:
-//  - software-pipelined mover list: the next mover's slot and Space (and the slot after it) are loaded
-//    while the current mover walks, so a mover starts with ONE round trip (Space geometry + slot
-//    state) instead of three (list -> space_of -> geometry);
-//  - one lane per ROW (64 rows per block) with both of the row's segments, and two parts per lane per
-//    flush (128 per flush): a D = 400 ring (35 rows, ~72 tile parts) is one cell-start round trip and
-//    one candidate round trip, instead of three of each over 32-row blocks of 64 parts.
-__device__ __forceinline__ int first_above(uint32_t incl, uint32_t k) {  // first lane whose incl > k
-  int lo = 0, hi = 63;
-#pragma unroll
-  for (int st = 0; st < 6; ++st) {
-    const int mid = (lo + hi) >> 1;
-    if (__shfl(incl, mid, 64) > k) hi = mid;
-    else lo = mid + 1;
-  }
-  return lo;
-}
-
-__global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_DENSE_WPE)))
-k_sweep_dense2(SweepArgs a) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = (blockIdx.x * kDenseBlock + threadIdx.x) >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
-  const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
-  const unsigned long long below = (1ull << lane) - 1ull;
-  uint32_t nent = 0;
-  uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
-  if (wave >= nd) return;  // wave-uniform; no barrier in this kernel
-  // list indices clamped to the last entry: the prefetch loads are unconditional (no branch around
-  // them, so the waits the compiler inserts stay per register)
-  const uint32_t dl = nd - 1;
-  uint32_t d = wave;
-  uint32_t s_c = a.dense[d];                       // this mover's slot
-  uint32_t s_n = a.dense[min(d + nwaves, dl)];     // the next one's
-  uint32_t sp_c = a.space_of[s_c];                 // this mover's Space
-  for (; d < nd; d += nwaves) {
-    // prefetch (consumed by the next iteration): the next mover's Space, the slot after it
-    const uint32_t sp_n = a.space_of[s_n];
-    const uint32_t s_nn = a.dense[min(d + 2 * nwaves, dl)];
-    const Geom g = a.g.geom[sp_c];
-    const Mover m = slot_mover(a, s_c, g.D);
-    const Judge J = make_judge(m, a.base);
-    uint32_t local = 0;  // wave-uniform
-    auto emit_round = [&](int ev, uint32_t other) {
-      const unsigned long long em = __ballot(ev != 0);
-      if (!em) return;
-      const uint32_t cnt = (uint32_t)__popcll(em);
-      const uint32_t pre = (uint32_t)__popcll(em & below);
-      uint32_t gi = cur + pre;
-      if (cnt > left) {
-        uint32_t nb = 0;
-        if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
-        nb = __shfl(nb, 0, 64);
-        if (pre >= left) gi = nb + (pre - left);
-        cur = nb + (cnt - left);
-        left = kEvChunk - (cnt - left);
-      } else {
-        cur += cnt;
-        left -= cnt;
-      }
-      if (ev) {
-        if (gi < a.ev_cap)
-          a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
-        nent += ev == 2 ? 1u : 0u;
-      }
-      local += cnt;
-    };
-    const Walk w = make_walk(m, g);
-    const int h = w.z1 - w.z0 + 1;
-    for (int rb = 0; rb < h; rb += 64) {
-      const int r = w.z0 + rb + lane;
-      int a0, a1, b0, b1;
-      walk_row(w, rb + lane < h ? r : w.z1 + 1, a0, a1, b0, b1);
-      const uint32_t na = a0 <= a1 ? (uint32_t)((a1 >> kTileShift) - (a0 >> kTileShift) + 1) : 0u;
-      const uint32_t nb = b0 <= b1 ? (uint32_t)((b1 >> kTileShift) - (b0 >> kTileShift) + 1) : 0u;
-      const uint32_t pincl = wave_incl_scan(na + nb);
-      const uint32_t T = __builtin_amdgcn_readlane(pincl, 63);
-      for (uint32_t pb = 0; pb < T; pb += 128) {
-        // part pb + half * 64 + lane: its owner lane (row), segment and tile -> a cell-key range
-        auto part = [&](uint32_t p, uint32_t& pk, uint32_t& pe) {
-          pk = pe = 0;
-          const int lo = first_above(pincl, p);
-          const uint32_t q = p - (__shfl(pincl, lo, 64) - __shfl(na + nb, lo, 64));
-          // every shuffle by every lane, then select: a shuffle inside a divergent branch reads 0 from a
-          // source lane that is off in that branch
-          const uint32_t nal = __shfl(na, lo, 64);
-          const int xa0 = __shfl(a0, lo, 64), xa1 = __shfl(a1, lo, 64);
-          const int xb0 = __shfl(b0, lo, 64), xb1 = __shfl(b1, lo, 64);
-          const int sr = __shfl(r, lo, 64);
-          const bool sa = q < nal;
-          const int sc0 = sa ? xa0 : xb0, sc1 = sa ? xa1 : xb1;
-          if (p >= T) return;
-          const int tx = (sc0 >> kTileShift) + (int)(sa ? q : q - nal);
-          const int plo = max(sc0, tx << kTileShift), phi = min(sc1, (tx << kTileShift) + kTile - 1);
-          pk = g.base + ((uint32_t)((sr >> kTileShift) * g.ntx) << kTileCellShift) +
-               (uint32_t)((sr & (kTile - 1)) << kTileShift) + ((uint32_t)tx << kTileCellShift) +
-               (uint32_t)(plo & (kTile - 1));
-          pe = pk + (uint32_t)(phi - plo) + 1;
-        };
-        uint32_t pk0, pe0, pk1, pe1;
-        part(pb + lane, pk0, pe0);
-        part(pb + 64 + lane, pk1, pe1);
-        // every part's record range in one round trip; the candidate stream = parts in order
-        uint32_t rs0 = 0, rl0 = 0, rs1 = 0, rl1 = 0;
-        if (pe0 > pk0) {
-          rs0 = a.g.cs[pk0];
-          rl0 = a.g.cs[pe0] - rs0;
-        }
-        if (pe1 > pk1) {
-          rs1 = a.g.cs[pk1];
-          rl1 = a.g.cs[pe1] - rs1;
-        }
-        const uint32_t i0 = wave_incl_scan(rl0);
-        const uint32_t t0 = __builtin_amdgcn_readlane(i0, 63);
-        const uint32_t i1 = wave_incl_scan(rl1) + t0;
-        const uint32_t total = __builtin_amdgcn_readlane(i1, 63);
-        const uint32_t o0 = rs0 - (i0 - rl0), o1 = rs1 - (i1 - rl1);  // record index = k + offset
-        auto locate = [&](uint32_t k) -> uint32_t {
-          const bool hi = k >= t0;
-          int lo = 0, up = 63;
-#pragma unroll
-          for (int st = 0; st < 6; ++st) {
-            const int mid = (lo + up) >> 1;
-            const uint32_t v0 = __shfl(i0, mid, 64), v1 = __shfl(i1, mid, 64);
-            if ((hi ? v1 : v0) > k) up = mid;
-            else lo = mid + 1;
-          }
-          const uint32_t f0 = __shfl(o0, lo, 64), f1 = __shfl(o1, lo, 64);
-          return k + (hi ? f1 : f0);
-        };
-        for (uint32_t b = 0; b < total; b += 128) {
-          const uint32_t kA = b + lane, kB = b + 64 + lane;
-          const uint32_t jA = locate(kA);
-          const bool hasB = b + 64 < total;  // wave-uniform
-          const uint32_t jB = hasB ? locate(kB) : 0u;
-          uint4 aA = make_uint4(0, 0, 0, 0), bA = aA, aB = aA, bB = aA;
-          if (kA < total) aA = a.g.rec[jA].a, bA = a.g.rec[jA].b;
-          if (hasB && kB < total) aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
-          emit_round(kA < total ? judge(J, aA, bA) : 0, aA.z & REC_SLOT);
-          if (hasB) emit_round(kB < total ? judge(J, aB, bB) : 0, aB.z & REC_SLOT);
-        }
-      }
-    }
-    if (lane == 0 && local) a.rank_cnt[m.rank] = local;
-    s_c = s_n;
-    s_n = s_nn;
-    sp_c = sp_n;
-  }
-  for (uint32_t i = lane; i < left; i += 64)
-    if (cur + i < a.ev_cap) a.ev_tmp[cur + i] = make_uint4(kEvHole, 0u, 0u, 0u);
-  if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
-  const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);
-  if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
-}
-
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
   if (a.use_lds == 0) {
     const uint32_t n = a.n_rec + (a.n_leaves_dev ? a.n_ops : a.n_leaves);
@@ -1967,17 +1781,7 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
                        st, a);
   // the dense list's length is on the device: a fixed grid that exits at once when it is empty (a
   // small one when the previous pass had none; the kernel is grid-stride, any grid is correct)
-#ifndef GW_DENSE_FLAT
-#define GW_DENSE_FLAT 0
-#endif
-  if (a.dense && GW_DENSE_FLAT)
-    hipLaunchKernelGGL(k_sweep_dense_flat, dim3(a.dense_hint ? 256 * GW_DENSE_FLAT : 16), dim3(kBlock), 0, st, a);
-#ifndef GW_DENSE_V2
-#define GW_DENSE_V2 0  // A/B: measured slower (skew 3.13 -> 3.22, skew50 6.75 -> 7.46 ms of sweep)
-#endif
-  else if (a.dense && GW_DENSE_V2)
-    hipLaunchKernelGGL(k_sweep_dense2, dim3(a.dense_hint ? kDenseGrid : 64), dim3(kDenseBlock), 0, st, a);
-  else if (a.dense)
+  if (a.dense)
     hipLaunchKernelGGL(k_sweep_dense, dim3(a.dense_hint ? kDenseGrid : 64), dim3(kDenseBlock), 0, st, a);
 }
 
