@@ -1624,7 +1624,10 @@ constexpr int kDenseBlock = 256;
 #define GW_DENSE_WPE 6
 #endif
 constexpr int kDenseGrid = 256 * GW_DENSE_WPE;  // GW_DENSE_WPE waves per SIMD: every wave resident
-constexpr uint32_t kEvChunk = 128;    // event slots a wave reserves at a time (one returning atomic
+#ifndef GW_EV_CHUNK
+#define GW_EV_CHUNK 128
+#endif
+constexpr uint32_t kEvChunk = GW_EV_CHUNK;  // event slots a wave reserves at a time (one returning atomic
                                       // on the shared counter each: ~11 ns apiece when serialised)
 
 __global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_DENSE_WPE)))
