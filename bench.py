@@ -729,6 +729,42 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
     }
 
 
+def self_launch_command(argv, env, gpus, port):
+    """The child command that starts `gpus` ranks of this script, or None when no launch is needed.
+
+    `bench.py --gpus N` (N > 1) started WITHOUT a launcher (no WORLD_SIZE in the environment) starts
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>` as a CHILD process and
+    relays rank 0's JSON line. The decision is taken before anything touches the GPU: the parent never
+    initialises HIP (no torch.cuda call, no libgwaoi load), so it never has to exec over a live device."""
+    if gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(cmd):
+    """Run the launcher as a child; relay the JSON line(s) rank 0 prints; exit with the child's status."""
+    import subprocess
+    log("launching " + " ".join(cmd[1:5]) + " ... (one rank per GPU)")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:  # rank 0 prints exactly one JSON line; anything else is relayed to stderr
+        if line.lstrip().startswith("{"):
+            print(line.rstrip("\n"), flush=True)
+        else:
+            log(line.rstrip("\n"))
+    rc = p.wait()
+    if rc != 0:
+        log(f"launcher exited with status {rc}")
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -755,9 +791,16 @@ def main():
     ap.add_argument("--dists", default=None, help="skew workloads: comma list of per-Space D (A/B)")
     ap.add_argument("--cell-side", type=float, default=None, help="absolute cell side for every Space (A/B)")
     ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch + rendezvous + barrier only, no GPU work (CPU test of the multi-rank plumbing)")
     ap.add_argument("--stamps", default=None, help="diagnostic GW_STAMPS build: dump the last sweep's per-block "
                                                    "phase timestamps to this .npy file")
     args = ap.parse_args()
+
+    # N > 1 without an external launcher: start the ranks as a child before any GPU call
+    cmd = self_launch_command(sys.argv[1:], os.environ, args.gpus, _free_port() if args.gpus > 1 else 0)
+    if cmd is not None:
+        sys.exit(_self_launch(cmd))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -781,10 +824,11 @@ def main():
         torch.cuda.set_device(dev)
 
     from goworld_amd import _lib
-    L_ = _lib.load()
+    L_ = None if args.dry_run else _lib.load()
 
     def sync_all():
-        _lib.check(L_.gwaoi_dev_sync(dev))
+        if not args.dry_run:
+            _lib.check(L_.gwaoi_dev_sync(dev))
         if have_cuda:
             torch.cuda.synchronize()
         if world > 1:
@@ -797,7 +841,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    if args.workload in ("strips", "strips_skew"):
+    if args.dry_run:
+        sync_all()
+        result = {"dry_run": True, "n_gpus": world, "devices": ndev, "backend": backend,
+                  "elapsed": allmax(0.001 * (rank + 1))}
+    elif args.workload in ("strips", "strips_skew"):
         result = run_strips(args, rank, world, dev, sync_all, allmax, via_cpu=(backend == "gloo"))
     elif args.workload == "gametick":
         result = run_gametick(args, rank, world, dev, sync_all, allmax)
@@ -820,6 +868,8 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
+        if have_cuda and 0 < ndev < world:  # functional runs only: several ranks time-share one GPU
+            result["ranks_share_devices"] = f"{world} ranks on {ndev} device(s)"
         print(json.dumps(result), flush=True)
 
 

@@ -28,11 +28,12 @@ GWAOI_OP_MOVE, GWAOI_OP_ENTER, GWAOI_OP_LEAVE, GWAOI_OP_SILENT = 0, 1, 2, 0x80
 ABI_SYMBOLS = (
     "gwaoi_create", "gwaoi_create_spaces", "gwaoi_destroy", "gwaoi_set_stream", "gwaoi_enter",
     "gwaoi_enter_space", "gwaoi_stage_enters", "gwaoi_leave", "gwaoi_moved", "gwaoi_stage_moves", "gwaoi_stage_moves_device",
+    "gwaoi_stage_buffers", "gwaoi_stage_moves_pinned",
     "gwaoi_stage_ops_device",
     "gwaoi_stage_ops_device_spaces",
     "gwaoi_stage_ops_device_n", "gwaoi_adopt_device_state", "gwaoi_set_population_hint",
     "gwaoi_tick", "gwaoi_tick_ex", "gwaoi_count", "gwaoi_export_relation", "gwaoi_relation_device", "gwaoi_set_timing",
-    "gwaoi_get_stats", "gwaoi_reset_stats", "gwaoi_version", "gwaoi_last_error",
+    "gwaoi_get_stats", "gwaoi_reset_stats", "gwaoi_version", "gwaoi_last_error", "gwaoi_abi_version",
 )
 TOOL_SYMBOLS = (
     "gwaoi_device_count", "gwaoi_dev_malloc", "gwaoi_dev_free", "gwaoi_dev_htod", "gwaoi_dev_dtoh",
@@ -183,6 +184,9 @@ def load(path: str = SO_PATH):
         "gwaoi_moved": ([vp, u32, f32, f32], ctypes.c_int),
         "gwaoi_stage_moves": ([vp, u32p, f32p, f32p, u32], ctypes.c_int),
         "gwaoi_stage_moves_device": ([vp, vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_stage_buffers": ([vp, ctypes.POINTER(u32p), ctypes.POINTER(f32p), ctypes.POINTER(f32p),
+                                 ctypes.POINTER(u32)], ctypes.c_int),
+        "gwaoi_stage_moves_pinned": ([vp, u32], ctypes.c_int),
         "gwaoi_stage_ops_device": ([vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_stage_ops_device_spaces": ([vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_stage_ops_device_n": ([vp, vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
@@ -197,6 +201,7 @@ def load(path: str = SO_PATH):
         "gwaoi_get_stats": ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
         "gwaoi_reset_stats": ([vp], ctypes.c_int),
         "gwaoi_version": ([], ctypes.c_char_p),
+        "gwaoi_abi_version": ([], ctypes.c_int),
         "gwaoi_last_error": ([], ctypes.c_char_p),
         "gwaoi_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "gwaoi_dev_malloc": ([ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)], ctypes.c_int),
@@ -229,7 +234,7 @@ def load(path: str = SO_PATH):
                                    ctypes.c_int),
         "gwaoi_strip_translate_events": ([vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_strip_init_skew": ([vp, vp, vp, vp, vp, u64, f32, u32, f32, u32], ctypes.c_int),
-        "gwaoi_strip_absorb_n": ([vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
+        "gwaoi_strip_absorb_n": ([vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),
         "gwaoi_strip_comm_id": ([vp], ctypes.c_int),
         "gwaoi_strip_comm_init": ([vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
         "gwaoi_strip_comm_destroy": ([vp], ctypes.c_int),

@@ -11,7 +11,9 @@ vendored, names as used by goworld):
     func NewXZListAOIManager(aoidist Coord) AOIManager                              # Space.go:105
 
 Differences, all by design of the tick-batched engine (DESIGN.md "Boundary"):
-  * Moved() only stages; callbacks of staged moves fire at Flush(), which GoWorld calls once per
+  * Moved() only writes the call into the manager's pinned staging arrays (gwaoi_stage_buffers); the
+    batch goes to the GPU in ONE gwaoi_stage_moves_pinned before the next Enter/Leave and at Flush(),
+    as the cgo wrapper does. Callbacks of staged moves fire at Flush(), which GoWorld calls once per
     game tick before CollectEntitySyncInfos (GameService.go:185-191). With sync_enter_leave=True
     (default) Enter() and Leave() flush immediately, so their callbacks fire inside the call as in
     the reference (Space.enter runs user hooks right after aoiMgr.Enter, Space.go:211-217).
@@ -85,6 +87,15 @@ class GPUAOIManager(AOIManager):
         self._released: List[int] = []
         self.sync_enter_leave = sync_enter_leave
         self.last_events = None
+        self._ms, self._mx, self._mz = self._eng.stage_buffers()  # pinned, library-owned
+        self._nmv = 0  # Moved calls written and not yet pushed
+
+    def _push_moves(self) -> None:
+        """One gwaoi_stage_moves_pinned for the Moved calls written since the last push (validated on the
+        device; a slot moved twice splits into sub-passes there)."""
+        if self._nmv:
+            n, self._nmv = self._nmv, 0
+            self._eng.stage_moves_pinned(n)
 
     @property
     def engine(self) -> Engine:
@@ -96,6 +107,7 @@ class GPUAOIManager(AOIManager):
         if not self._free:
             raise _lib.GwaoiError(_lib.GWAOI_ERR_NOMEM, "Enter: manager capacity exhausted")
         slot = self._free.pop()
+        self._push_moves()  # Moved calls made before this Enter come first
         self._eng.enter(slot, x, y)
         aoi._slot, aoi._mgr = slot, self
         aoi.x, aoi.y = float(x), float(y)
@@ -106,6 +118,7 @@ class GPUAOIManager(AOIManager):
     def Leave(self, aoi: AOI) -> None:
         if aoi._mgr is not self:
             raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, "Leave: AOI not in this manager")
+        self._push_moves()
         self._eng.leave(aoi._slot)
         self._released.append(aoi._slot)
         aoi._mgr = None
@@ -115,11 +128,16 @@ class GPUAOIManager(AOIManager):
     def Moved(self, aoi: AOI, x: Coord, y: Coord) -> None:
         if aoi._mgr is not self:
             raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, "Moved: AOI not in this manager")
-        self._eng.moved(aoi._slot, x, y)
+        k = self._nmv
+        self._ms[k], self._mx[k], self._mz[k] = aoi._slot, x, y
+        self._nmv = k + 1
+        if self._nmv == len(self._ms):
+            self._push_moves()
         aoi.x, aoi.y = float(x), float(y)
 
     def Flush(self) -> int:
         """Run the tick and replay its events into the callbacks; returns the number of pair events."""
+        self._push_moves()
         ev = self._eng.tick()
         self.last_events = ev
         by = self._by_slot
@@ -139,6 +157,7 @@ class GPUAOIManager(AOIManager):
         return len(ev)
 
     def close(self):
+        self._ms = self._mx = self._mz = None
         self._eng.close()
 
 

@@ -34,6 +34,18 @@ struct gwaoi_strip_comm {
     }                                                                                   \
   } while (0)
 
+// Inside an open ncclGroupStart: on a failure the group is closed before returning, so RCCL is never
+// left in group state (a later collective on this thread would otherwise be folded into the dead group).
+#define NCHK_GROUP(x)                                                                   \
+  do {                                                                                  \
+    ncclResult_t r_ = (x);                                                              \
+    if (r_ != ncclSuccess) {                                                            \
+      gw::set_error("%s:%d %s: %s", __FILE__, __LINE__, #x, ncclGetErrorString(r_));   \
+      (void)ncclGroupEnd();                                                             \
+      return GWAOI_ERR_HIP;                                                             \
+    }                                                                                   \
+  } while (0)
+
 extern "C" {
 
 int gwaoi_strip_comm_id(uint8_t* id) {
@@ -99,16 +111,16 @@ int gwaoi_strip_exchange(gwaoi_strip_comm* c, void* stream, int left_peer, int r
   const size_t words = (size_t)cap * 4;  // records are 4 x uint32
   NCHK(ncclGroupStart());
   if (left_peer >= 0) {  // sends and receives to one peer match in issue order: count, then records
-    NCHK(ncclSend(d_counts, 1, ncclUint32, left_peer, c->comm, st));
-    NCHK(ncclRecv(d_counts_in, 1, ncclUint32, left_peer, c->comm, st));
-    NCHK(ncclSend(d_left, words, ncclUint32, left_peer, c->comm, st));
-    NCHK(ncclRecv(d_left_in, words, ncclUint32, left_peer, c->comm, st));
+    NCHK_GROUP(ncclSend(d_counts, 1, ncclUint32, left_peer, c->comm, st));
+    NCHK_GROUP(ncclRecv(d_counts_in, 1, ncclUint32, left_peer, c->comm, st));
+    NCHK_GROUP(ncclSend(d_left, words, ncclUint32, left_peer, c->comm, st));
+    NCHK_GROUP(ncclRecv(d_left_in, words, ncclUint32, left_peer, c->comm, st));
   }
   if (right_peer >= 0) {
-    NCHK(ncclSend(d_counts + 1, 1, ncclUint32, right_peer, c->comm, st));
-    NCHK(ncclRecv(d_counts_in + 1, 1, ncclUint32, right_peer, c->comm, st));
-    NCHK(ncclSend(d_right, words, ncclUint32, right_peer, c->comm, st));
-    NCHK(ncclRecv(d_right_in, words, ncclUint32, right_peer, c->comm, st));
+    NCHK_GROUP(ncclSend(d_counts + 1, 1, ncclUint32, right_peer, c->comm, st));
+    NCHK_GROUP(ncclRecv(d_counts_in + 1, 1, ncclUint32, right_peer, c->comm, st));
+    NCHK_GROUP(ncclSend(d_right, words, ncclUint32, right_peer, c->comm, st));
+    NCHK_GROUP(ncclRecv(d_right_in, words, ncclUint32, right_peer, c->comm, st));
   }
   NCHK(ncclGroupEnd());
   return GWAOI_OK;

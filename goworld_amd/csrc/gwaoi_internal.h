@@ -20,9 +20,7 @@ __host__ __device__ __forceinline__ bool finite_bits(uint32_t b) { return (b & 0
 // Counters block in device memory.
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
        CTR_DENSE = 7, CTR_HOLES = 8, CTR_NOPS = 9,  // ops of the pass (device-counted batches)
-       CTR_TQ = 32,          // k_sweep's per-XCD tile queues (persistent blocks): queue q at CTR_TQ + q * CTR_QSTRIDE,
-       CTR_QSTRIDE = 32,     // one 128-B line each (a returning atomic serialises per line)
-       CTR_N = 32 + 8 * 32 };
+       CTR_N = 32 };
 constexpr int kPubWords = 16;  // counters [0, 16) are what the host reads after a pass
 // CTR_EVENTS counts SLOTS of ev_tmp; k_sweep_dense reserves them in per-wave chunks and marks the
 // unused tail of its last chunk as holes (x == kEvHole), counted in CTR_HOLES. Events = slots - holes.
@@ -282,6 +280,26 @@ void launch_wl_step_spaces(const float* xp, const float* zp, float* xo, float* z
 void launch_wl_step(const float* xp, const float* zp, float* xo, float* zo, uint32_t n, uint64_t seed,
                     uint64_t tick, float L, float s, hipStream_t st);
 void launch_iota(uint32_t* d, uint32_t n, hipStream_t st);
+
+// Pinned host staging (gwaoi_stage_moves_pinned): validation and repeat detection of a Moved batch
+// already copied to the device, without touching the manager's state.
+struct PinCheckArgs {
+  const uint32_t* slot;
+  const float* x;
+  const float* z;
+  uint32_t seg, n;             // ops [seg, n) of the batch
+  uint32_t cap;
+  int validate;                // 1: slot present + finite coordinates (the first call of a batch)
+  const uint32_t* seq;         // 0 = absent
+  const uint32_t* space_of;
+  unsigned long long* first;   // [cap]: (id << 32 | ~first op index) of the last call naming the slot
+  uint32_t id;                 // this call's id (> every id stored before)
+  const float4* ext;           // per Space {gx0, gz0, gx1, gz1} of auto-extent Spaces (null: none)
+  uint32_t* seen;              // per Space 4 order keys: min x, min z, max x, max z of coordinates beyond ext
+  uint32_t* out;               // [0] error bits, [1] first repeat (n: none), [2] first bad op, [3] beyond ext
+};
+void launch_pin_check(const PinCheckArgs& a, bool reset_seen, uint32_t nspaces, hipStream_t st);
+float ord_float(uint32_t k);
 
 // ---- manager view for the callers either side of the path (gwaoi_sync.hip) ----
 struct SyncState;  // gwaoi_sync.hip

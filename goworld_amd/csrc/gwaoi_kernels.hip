@@ -24,6 +24,9 @@
 // preserved), compared inclusively — bit-exact with Go float32 arithmetic.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstring>
+
 #include "gwaoi_device.h"
 #include "gwaoi_internal.h"
 #include "gwaoi_workload.h"
@@ -562,20 +565,15 @@ constexpr int kCap = GW_CAP;  // max records staged (config 2: ~1030 +- 32 in a 
 constexpr int kMaxRows = 48;
 constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
-constexpr int kKeyBins = 128;  // mover sort keys: candidate count (clamped), kKeyBins - 1 = row walk
-#ifndef GW_SWEEP_SORT
-#define GW_SWEEP_SORT 0  // 1: order a tile's movers by candidate count (A/B: no gain measured, 6 us/block)
-#endif
 struct SweepSmem {  // dynamic LDS (16-B aligned carve)
   uint32_t n, enter, base, item;
-  uint32_t qk, nmv, pad1, pad2;  // qk: tile queues this block has found empty; nmv: movers in mv
-  uint32_t ws[16];              // block-scan scratch
-  uint32_t hist[kKeyBins];      // movers per sort key, then (scanned) each key's first position in mv
+  uint32_t nmv, pad0, pad1, pad2;  // nmv: movers in mv
+  uint32_t ws[16];                 // block-scan scratch
   uint4 ev[kEvLds];             // event queue
   uint16_t lcs[kRegCells + 8];  // row-major: LDS start of each region cell (+ total)
   uint16_t ccs[kRegCells + 8];  // column-major: start in cidx of each region cell (+ total)
   uint16_t cidx[kCap];          // column-major order of the staged records (LDS record indices)
-  uint16_t mv[kCap];            // the tile's movers (LDS record indices), heaviest candidate stream first
+  uint16_t mv[kCap];            // the tile's movers (LDS record indices)
   uint4 rp[kCap];      // staged record, LDS form: {x_start, z_start, x_end, z_end} (float bits)
   uint2 rm[kCap];      // {r | G, seq_start | A}: op rank (kNoRank: no op) and the validity mode (lds_record)
   uint32_t rslot[kCap];  // slot (read only when an event is emitted); while staging: grid index | kCoreBit
@@ -926,9 +924,6 @@ __device__ __forceinline__ void judge_chunk(const SweepSmem& sm, const Judge& J,
 // atomic per wave when the range runs past the queue; then each lane writes its own events in mask
 // order (its `local` numbering). Every lane that reached the call takes part (the masks of a lane
 // without events are zero).
-#ifndef GW_EV_LIDX
-#define GW_EV_LIDX 0
-#endif
 template <class IdxA, class IdxB>
 __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, const Mover& m, unsigned long long hA,
                                            unsigned long long eA, IdxA&& ia, unsigned long long hB,
@@ -966,9 +961,7 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, co
       const uint32_t j = idx((uint32_t)bit), eb = enter ? 0x80000000u : 0u;
       nent += enter ? 1u : 0u;
       if (p < (uint32_t)kEvLds) {
-        // GW_EV_LIDX: the queue holds the candidate's LDS record index; the block's flush turns it into
-        // the slot (one coalesced pass instead of a dependent LDS read per event in this loop)
-        sm.ev[p] = make_uint4(m.rank, local, m.slot, (GW_EV_LIDX ? j : sm.rslot[j]) | eb);
+        sm.ev[p] = make_uint4(m.rank, local, m.slot, sm.rslot[j] | eb);
       } else {
         const uint32_t gi = g0 + (p - qs);
         if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local, m.slot, sm.rslot[j] | eb);
@@ -994,9 +987,6 @@ __device__ __forceinline__ void judge_stream(const SweepArgs& a, SweepSmem& sm, 
   }
 }
 
-#ifndef GW_RING_MERGE
-#define GW_RING_MERGE 0
-#endif
 __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Walk& w,
                                               const Region& R, const Geom& g, uint32_t& nent) {
   const Judge J = make_judge(m, a.base);
@@ -1006,20 +996,6 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     // row stream: LDS record indices directly; column stream: through the column-major index
     auto ri = [&](uint32_t k) { return stream_at(Rs, k); };
     auto ci = [&](uint32_t k) { return (uint32_t)sm.cidx[stream_at(Cs, k)]; };
-#if GW_RING_MERGE
-    // both streams as ONE stream (row candidates, then column candidates): a wave's judge loop runs
-    // max over lanes of (rows + columns) instead of max(rows) + max(columns)
-    const uint32_t nr = Rs.total, tot = Rs.total + Cs.total;
-    auto bi = [&](uint32_t k) { return k < nr ? stream_at(Rs, k) : (uint32_t)sm.cidx[stream_at(Cs, k - nr)]; };
-    if (__all(tot <= 64u)) {
-      unsigned long long h, e;
-      judge_chunk(sm, J, 0, tot, bi, h, e);
-      emit_masks(a, sm, m, h, e, bi, 0ull, 0ull, [&](uint32_t k) { return k; }, local, nent);
-      return local;
-    }
-    judge_stream(a, sm, J, m, tot, bi, local, nent);
-    return local;
-#endif
     if (__all(Rs.total <= 64u && Cs.total <= 64u)) {  // the usual ring: both streams in one chunk, one emission
       unsigned long long hR, eR, hC, eC;
       judge_chunk(sm, J, 0, Rs.total, ri, hR, eR);
@@ -1140,7 +1116,6 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
     sm.lcs[R.ncells] = (uint16_t)total;
     sm.nmv = 0;
   }
-  if (threadIdx.x < kKeyBins) sm.hist[threadIdx.x] = 0u;
   __syncthreads();
   GW_STAMP(9, __builtin_amdgcn_s_memrealtime());  // row-major table and source map written
   // column-major cell starts (cell counts from the row-major table; cell (rr, cc) is column-major
@@ -1262,9 +1237,6 @@ __device__ __forceinline__ Mover leaver(const SweepArgs& a, uint32_t i, float D)
 // b % 8), each with its own L2. Give XCD x a contiguous run of tiles, visited in order, so the halo a
 // tile shares with its predecessor is still in that XCD's L2. A bijection on [0, n).
 constexpr uint32_t kXcds = 8;
-#ifndef GW_SWEEP_PERSIST
-#define GW_SWEEP_PERSIST 0  // 1: persistent blocks over per-XCD tile queues (spills SGPRs today: 1 block per CU)
-#endif
 
 __device__ __forceinline__ bool is_mover(const uint4 ra, uint32_t base, uint32_t n_ops) {
   return !(ra.z & REC_GHOST) && (ra.w - base) < n_ops;
@@ -1294,13 +1266,9 @@ __device__ __forceinline__ Mover lds_mover(const SweepSmem& sm, uint32_t i, uint
   return m;
 }
 
-#ifndef GW_EV_RESERVE
-#define GW_EV_RESERVE 0
-#endif
 // One work item of k_sweep: a tile. Stage its region (which lists the tile's movers); walk them, one
 // thread per mover, consecutive rounds of the block in alternating direction (a tile holds ~520
 // movers for 512 threads). The block's LDS event queue is flushed with one global atomic at the end.
-// (GW_SWEEP_SORT=1 orders the movers by candidate-stream length first: measured no faster.)
 __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, const uint32_t item) {
   uint32_t nent = 0;  // enter events of this thread's movers
   const uint32_t t = item;
@@ -1335,13 +1303,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     tcz = tz * kTile - R.zr0;
     lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= 3 * kTile;
   }
-  // GW_EV_RESERVE: an LDS-path block reserves its event-queue range (kEvLds slots) before staging, so
-  // the returning global atomic overlaps the staging loads instead of sitting between the walk and the
-  // flush; the flush then writes its events and marks the rest of the range as holes (k_place skips them)
-  const bool reserved = GW_EV_RESERVE && lds;  // block-uniform
-  uint32_t resv = 0;                           // thread 0: first reserved slot
   if (lds) {
-    if (reserved && threadIdx.x == 0) resv = atomicAdd(&a.ctr[CTR_EVENTS], (uint32_t)kEvLds);
     GW_STAMP(1, __builtin_amdgcn_s_memrealtime());
     const uint32_t nst = stage(a, g, R, tcx, tcz, sm);
     lds = nst <= (uint32_t)kCap;  // block-uniform
@@ -1368,43 +1330,6 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     }
   } else {
     const uint32_t nm = sm.nmv;
-#if GW_SWEEP_SORT  // A/B: order the movers by candidate count (the lanes of a wave then walk similar streams)
-    // sort key: the mover's candidate count (ring streams), or the top key for a row walk. Per mover
-    // slot of this thread: key << 22 | rank inside the key << 11 | LDS record index (kCap < 2^11).
-    static_assert(kCap < 2048 && kKeyBins <= 1024, "packed mover sort entry");
-    uint32_t ent[kStageIters];
-#pragma unroll
-    for (int k = 0; k < kStageIters; ++k) {
-      const uint32_t p = threadIdx.x + k * kSweepBlock;
-      ent[k] = 0;
-      if (p < nm) {
-        const uint32_t i = sm.mv[p];
-        const Mover m = lds_mover(sm, i, a.base, g.D);
-        const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
-        uint32_t key = kKeyBins - 1u;  // row walks, and movers that leave the region (k_sweep_dense)
-        RingStream Rs, Cs;
-        if (R.holds(A1) && (!m.valid0 || R.holds(A0)) && ring_plan(make_walk(m, g, A0, A1), R, sm, Rs, Cs))
-          key = min(Rs.total + Cs.total, (uint32_t)kKeyBins - 2u);
-        ent[k] = key << 22 | atomicAdd(&sm.hist[key], 1u) << 11 | i;
-      }
-    }
-    __syncthreads();
-    GW_STAMP(12, __builtin_amdgcn_s_memrealtime());  // sort keys counted
-    if (threadIdx.x < 64) {  // descending exclusive scan of the key histogram: key kKeyBins-1 first
-      const uint32_t b0 = kKeyBins - 1 - 2 * threadIdx.x, b1 = b0 - 1;
-      const uint32_t h0 = sm.hist[b0], h1 = sm.hist[b1];
-      const uint32_t ex = wave_incl_scan(h0 + h1) - (h0 + h1);
-      sm.hist[b0] = ex;
-      sm.hist[b1] = ex + h0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kStageIters; ++k)
-      if (threadIdx.x + k * kSweepBlock < nm)
-        sm.mv[sm.hist[ent[k] >> 22] + ((ent[k] >> 11) & 2047u)] = (uint16_t)(ent[k] & 2047u);
-    __syncthreads();
-    GW_STAMP(13, __builtin_amdgcn_s_memrealtime());  // movers ordered: the walk starts
-#endif
     if (a.use_lds != 2) {  // 2: ablation (timing only), staging and ordering without the walk
       // (one wave per mover for a tile's few movers beyond a full round: measured 110 -> 123 us; the
       // planner sizes tiles below one round instead, compute_geometry)
@@ -1433,21 +1358,13 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
   GW_STAMP(3, __builtin_amdgcn_s_memrealtime());
   const uint32_t nq = min(sm.n, (uint32_t)kEvLds);
   if (threadIdx.x == 0) {
-    if (reserved) {
-      sm.base = resv;
-      if (nq < (uint32_t)kEvLds) atomicAdd(&a.ctr[CTR_HOLES], (uint32_t)kEvLds - nq);
-    } else {
-      sm.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
-    }
+    sm.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
     if (sm.enter) atomicAdd(&a.ctr[CTR_ENTER], sm.enter);
   }
   __syncthreads();
-  const uint32_t nw = reserved ? (uint32_t)kEvLds : nq;
-  for (uint32_t i = threadIdx.x; i < nw; i += kSweepBlock) {
+  for (uint32_t i = threadIdx.x; i < nq; i += kSweepBlock) {
     const uint32_t gi = sm.base + i;
-    uint4 e = i < nq ? sm.ev[i] : make_uint4(kEvHole, 0u, 0u, 0u);
-    if (GW_EV_LIDX && lds && i < nq) e.w = sm.rslot[e.w & ~kTopBit] | (e.w & kTopBit);  // LDS path events
-    if (gi < a.ev_cap) a.ev_tmp[gi] = e;
+    if (gi < a.ev_cap) a.ev_tmp[gi] = sm.ev[i];
   }
   GW_STAMP(4, __builtin_amdgcn_s_memrealtime());
 }
@@ -1459,10 +1376,7 @@ __global__ void __launch_bounds__(kSweepBlock) __attribute__((amdgpu_waves_per_e
 k_sweep(SweepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   SweepSmem& sm = *reinterpret_cast<SweepSmem*>(smem_raw);
-  // Persistent blocks (2 per CU) pull tiles from per-XCD queues (queue x = the x-th contiguous
-  // eighth of the tiles, so neighbouring tiles, which share halo records, run on one XCD's L2; an
-  // XCD whose queue is empty steals from the next). Leaves run in k_sweep_leaves.
-#if !GW_SWEEP_PERSIST  // one block per item, tiles mapped XCD-aware by block index (A/B reference)
+  // one block per tile, tiles mapped XCD-aware by block index
   if (threadIdx.x == 0) {
     const uint32_t xcd = blockIdx.x % kXcds;
     const uint32_t per = a.ntiles / kXcds, rem = a.ntiles % kXcds;
@@ -1474,32 +1388,6 @@ k_sweep(SweepArgs a) {
   __syncthreads();
   GW_STAMP(0, __builtin_amdgcn_s_memrealtime());
   sweep_item(a, sm, __builtin_amdgcn_readfirstlane(sm.item));
-  return;
-#endif
-  if (threadIdx.x == 0) sm.qk = 0;
-  for (;;) {
-    if (threadIdx.x == 0) {
-      const uint32_t xcd = blockIdx.x % kXcds;
-      const uint32_t per = a.ntiles / kXcds, rem = a.ntiles % kXcds;
-      uint32_t item = ~0u, k = sm.qk;
-      for (; k < kXcds && item == ~0u; ++k) {
-        const uint32_t q = (xcd + k) % kXcds;
-        const uint32_t i = atomicAdd(&a.ctr[CTR_TQ + q * CTR_QSTRIDE], 1u);
-        if (i < per + (q < rem ? 1u : 0u)) item = q * per + min(q, rem) + i;
-      }
-      sm.qk = item == ~0u ? k : k - 1;
-      sm.item = item;
-      sm.n = 0;
-      sm.enter = 0;
-    }
-    __syncthreads();
-    // block-uniform: keep it (and the tile geometry derived from it) in scalar registers
-    const uint32_t item = __builtin_amdgcn_readfirstlane(sm.item);
-    if (item == ~0u) break;
-    GW_STAMP(0, __builtin_amdgcn_s_memrealtime());
-    sweep_item(a, sm, item);
-    __syncthreads();  // the next item reuses the LDS
-  }
 }
 
 int read_stamps(void* host, size_t bytes) {
@@ -1518,21 +1406,9 @@ int sweep_occupancy(int* blocks) {
                                                       sizeof(SweepSmem)) == hipSuccess ? 0 : -3;
 }
 
-#if GW_SWEEP_PERSIST
-static uint32_t g_sweep_slots = 512;  // resident k_sweep blocks on the whole chip
-#else
-static uint32_t g_sweep_slots = ~0u;
-#endif
-
 void sweep_init() {
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)sizeof(SweepSmem));
-  int blocks = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(&k_sweep), kSweepBlock,
-                                                   sizeof(SweepSmem)) == hipSuccess &&
-      hipGetDevice(&dev) == hipSuccess &&
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && blocks > 0 && cus > 0)
-    g_sweep_slots = GW_SWEEP_PERSIST ? (uint32_t)(blocks * cus) : ~0u;
 }
 
 // Flat variant (use_lds == 0): one thread per record in key (tile-major) order, 256-thread blocks
@@ -1674,8 +1550,7 @@ k_sweep_dense(SweepArgs a) {
     auto flush = [&]() {
       // one round trip for every part's record range, then the candidates 128 at a time (two loads in
       // flight per lane). Candidate k belongs to the first part whose inclusive prefix exceeds k (a
-      // binary search over the lanes' prefixes; GW_DENSE_SEARCH=1: a wave-uniform readlane loop from the
-      // previous chunk's last part).
+      // binary search over the lanes' prefixes).
       uint32_t rs = 0, rl = 0;
       if (lane < np) {
         rs = a.g.cs[pk];
@@ -1684,27 +1559,7 @@ k_sweep_dense(SweepArgs a) {
       const uint32_t incl = wave_incl_scan(rl);
       const uint32_t excl = incl - rl;
       const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-      int pcur = 0;  // wave-uniform
-#ifndef GW_DENSE_SEARCH
-#define GW_DENSE_SEARCH 0  // candidate -> part: 0 binary search over the lanes' prefixes, 1 readlane loop
-#endif
-      auto locate = [&](uint32_t k, uint32_t cend) -> uint32_t {  // record index of candidate k
-#if GW_DENSE_SEARCH
-        uint32_t base = 0, off = 0;
-        int p = pcur;
-        for (int q = pcur; q < np; ++q) {
-          const uint32_t ex = __builtin_amdgcn_readlane(excl, q);
-          if (ex >= cend) break;  // wave-uniform
-          const uint32_t rsq = __builtin_amdgcn_readlane(rs, q);
-          const bool in = k >= ex;
-          p = in ? q : p;
-          base = in ? rsq : base;
-          off = in ? ex : off;
-        }
-        pcur = __builtin_amdgcn_readlane(p, 63);
-        return base + (k - off);
-#else
-        (void)cend;
+      auto locate = [&](uint32_t k) -> uint32_t {  // record index of candidate k
         int lo = 0, hi = 63;  // first lane whose inclusive prefix exceeds k
 #pragma unroll
         for (int st = 0; st < 6; ++st) {
@@ -1713,13 +1568,12 @@ k_sweep_dense(SweepArgs a) {
           else lo = mid + 1;
         }
         return __shfl(rs, lo, 64) + (k - __shfl(excl, lo, 64));
-#endif
       };
       for (uint32_t b = 0; b < total; b += 128) {
         const uint32_t kA = b + lane, kB = b + 64 + lane;
-        const uint32_t jA = locate(kA, min(b + 64, total));
+        const uint32_t jA = locate(kA);
         const bool hasB = b + 64 < total;  // wave-uniform
-        const uint32_t jB = hasB ? locate(kB, min(b + 128, total)) : 0u;
+        const uint32_t jB = hasB ? locate(kB) : 0u;
         uint4 aA = make_uint4(0, 0, 0, 0), bA = aA, aB = aA, bB = aA;
         if (kA < total) aA = a.g.rec[jA].a, bA = a.g.rec[jA].b;
         if (hasB && kB < total) aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
@@ -1776,9 +1630,7 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
     if (n) hipLaunchKernelGGL(k_sweep_flat, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
     return;
   }
-  // persistent: one block per resident slot, tiles pulled from the queues (CTR_TQ)
-  if (a.ntiles)
-    hipLaunchKernelGGL(k_sweep, dim3(std::min(a.ntiles, g_sweep_slots)), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
+  if (a.ntiles) hipLaunchKernelGGL(k_sweep, dim3(a.ntiles), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
   if (a.leave_blocks)
     hipLaunchKernelGGL(k_sweep_leaves, dim3(a.leave_blocks * ((kSweepBlock + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        st, a);
@@ -2665,6 +2517,102 @@ void launch_wl_step(const float* xp, const float* zp, float* xo, float* zo, uint
 }
 void launch_iota(uint32_t* d, uint32_t n, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_iota, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, d, n);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pinned host staging (gwaoi_stage_moves_pinned): the cgo wrapper writes one tick's Moved calls into
+// library-owned pinned arrays; after one DMA copy the GPU validates the batch (what gwaoi_stage_moves
+// did on one host thread) and finds where a slot repeats (the sub-pass rule of host staging). Neither
+// kernel changes the manager's state, so a refused batch leaves it untouched (all-or-nothing).
+//   first[s] (64 bit, never reset): max over this call's ops naming s of (id << 32 | ~i), so the
+//   first op naming s in call `id` is ~low32 when high32 == id.
+__device__ __forceinline__ uint32_t ord_key(float f) {  // order-preserving float -> uint32
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+__global__ void __launch_bounds__(kBlock) k_pin_check(PinCheckArgs a) {
+  const uint32_t i = a.seg + blockIdx.x * kBlock + threadIdx.x;
+  uint32_t err = 0, bad = 0xFFFFFFFFu;
+  bool out_ext = false;
+  if (i < a.n) {
+    const uint32_t s = a.slot[i];
+    const float x = a.x[i], z = a.z[i];
+    if (s >= a.cap) {
+      err |= ERR_BAD_SLOT;
+    } else {
+      if (a.validate && a.seq[s] == 0u) err |= ERR_ABSENT_SLOT;
+      atomicMax(&a.first[s], (unsigned long long)a.id << 32 | (unsigned long long)(~i));
+      if (a.ext) {  // auto-extent Spaces: coordinates beyond the current grid extent (rare) are reported
+        const uint32_t sp = a.space_of[s];
+        const float4 e = a.ext[sp];
+        if (!(x >= e.x && x <= e.z && z >= e.y && z <= e.w) && finite_bits(__float_as_uint(x)) &&
+            finite_bits(__float_as_uint(z))) {
+          out_ext = true;
+          atomicMin(&a.seen[4 * sp + 0], ord_key(x));
+          atomicMin(&a.seen[4 * sp + 1], ord_key(z));
+          atomicMax(&a.seen[4 * sp + 2], ord_key(x));
+          atomicMax(&a.seen[4 * sp + 3], ord_key(z));
+        }
+      }
+    }
+    if (a.validate && !(finite_bits(__float_as_uint(x)) && finite_bits(__float_as_uint(z)))) err |= ERR_BAD_COORD;
+    if (err) bad = i;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    err |= (uint32_t)__shfl_xor(err, o, 64);
+    bad = min(bad, (uint32_t)__shfl_xor(bad, o, 64));
+  }
+  const bool anyx = __any(out_ext);
+  if ((threadIdx.x & 63) == 0) {
+    if (err) {
+      atomicOr(&a.out[0], err);
+      atomicMin(&a.out[2], bad);
+    }
+    if (anyx) atomicOr(&a.out[3], 1u);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_pin_cut(PinCheckArgs a) {
+  const uint32_t i = a.seg + blockIdx.x * kBlock + threadIdx.x;
+  uint32_t c = 0xFFFFFFFFu;
+  if (i < a.n) {
+    const uint32_t s = a.slot[i];
+    if (s < a.cap) {
+      const unsigned long long v = a.first[s];
+      if ((uint32_t)(v >> 32) == a.id && ~(uint32_t)v != i) c = i;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) c = min(c, (uint32_t)__shfl_xor(c, o, 64));
+  if ((threadIdx.x & 63) == 0 && c != 0xFFFFFFFFu) atomicMin(&a.out[1], c);
+}
+
+__global__ void k_pin_init(uint32_t* out, uint32_t n, uint32_t* seen, uint32_t nseen) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) {
+    out[0] = 0u;
+    out[1] = n;
+    out[2] = 0xFFFFFFFFu;
+    out[3] = 0u;
+  }
+  if (seen && t < nseen) seen[t] = (t & 2u) ? 0u : 0xFFFFFFFFu;  // [min x, min z, max x, max z] per Space
+}
+
+void launch_pin_check(const PinCheckArgs& a, bool reset_seen, uint32_t nspaces, hipStream_t st) {
+  const uint32_t nseen = reset_seen && a.seen ? 4u * nspaces : 0u;
+  hipLaunchKernelGGL(k_pin_init, dim3((std::max(nseen, 1u) + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a.out, a.n,
+                     nseen ? a.seen : (uint32_t*)nullptr, nseen);
+  const uint32_t m = a.n - a.seg;
+  if (!m) return;
+  hipLaunchKernelGGL(k_pin_check, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(k_pin_cut, dim3((m + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+}
+
+float ord_float(uint32_t k) {  // inverse of ord_key (host)
+  const uint32_t b = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+  float f;
+  std::memcpy(&f, &b, 4);
+  return f;
 }
 
 }  // namespace gw

@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <new>
 #include <string>
 #include <utility>
@@ -202,6 +203,18 @@ struct gwaoi_mgr {
   bool acc_silent = false;   // a pass of the accumulation may have applied SILENT ops (not in ev_out)
 
   gw::SyncState* sync = nullptr;  // sync fan-out / ingest state (gwaoi_sync.hip), on demand
+
+  // pinned host staging (gwaoi_stage_buffers / gwaoi_stage_moves_pinned), allocated on first use
+  uint32_t* h_pin_slot = nullptr;
+  float *h_pin_x = nullptr, *h_pin_z = nullptr;
+  unsigned long long* d_pin_first = nullptr;  // [cap] repeat detection (k_pin_check)
+  uint32_t pin_id = 0;
+  uint32_t* d_pin_out = nullptr;   // [4]
+  uint32_t* h_pin_out = nullptr;   // [4 + 4 nspaces]: out, then the per-Space beyond-extent keys
+  uint32_t* d_pin_seen = nullptr;  // [4 nspaces]
+  float4* d_pin_ext = nullptr;     // [nspaces]
+  float4* h_pin_ext = nullptr;
+  bool pin_seen_dirty = true;
 
   // timing
   bool timing = false;
@@ -614,7 +627,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_DENSE, 0, 2 * sizeof(uint32_t), st));  // + CTR_HOLES
-      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_TQ, 0, (gw::CTR_N - gw::CTR_TQ) * sizeof(uint32_t), st));
     }
     gw::SweepArgs s;
     const Grid& G = m->grid[ng];
@@ -805,7 +817,8 @@ void free_all(gwaoi_mgr* m) {
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out,
                    m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot, m->rel_slab, m->rel_fix,
-                   m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag};
+                   m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
+                   m->d_pin_seen, m->d_pin_ext};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
@@ -815,7 +828,7 @@ void free_all(gwaoi_mgr* m) {
       if (p) hipFree(p);
   }
   void* hptrs[] = {m->h_op_slot, m->h_op_x, m->h_op_z, m->h_op_kind, m->h_op_space, m->h_leaves, m->h_ctr,
-                   m->h_ev, m->h_pub};
+                   m->h_ev, m->h_pub, m->h_pin_slot, m->h_pin_x, m->h_pin_z, m->h_pin_out, m->h_pin_ext};
   for (void* p : hptrs)
     if (p) hipHostFree(p);
   for (auto& e : m->tev)
@@ -1039,7 +1052,8 @@ int mgr_stage_moves_device_n(gwaoi_mgr* m, const uint32_t* d_slots, const float*
 
 extern "C" {
 
-const char* gwaoi_version(void) { return "gwaoi 0.1.0 (gfx950)"; }
+const char* gwaoi_version(void) { return "gwaoi 0.3.0 (gfx950, abi 2)"; }
+int gwaoi_abi_version(void) { return GWAOI_ABI_VERSION; }
 const char* gwaoi_last_error(void) { return g_err.c_str(); }
 
 int gwaoi_create(float dist, uint32_t capacity, int device, gwaoi_mgr** out) {
@@ -1212,6 +1226,126 @@ int gwaoi_stage_moves(gwaoi_mgr* m, const uint32_t* slots, const float* x, const
     m->n_ops += k;
     i = e;
     if (i < n) RCHK(run_pass(m, true));  // slots[i] already has an op in this batch
+  }
+  return GWAOI_OK;
+}
+
+int gwaoi_stage_buffers(gwaoi_mgr* m, uint32_t** slots, float** x, float** z, uint32_t* capacity) {
+  RCHK(check_mgr(m));
+  if (!slots || !x || !z) {
+    set_err("stage_buffers: null output");
+    return GWAOI_ERR_INVALID;
+  }
+  RCHK(set_dev(m));
+  if (!m->h_pin_slot) {
+    const uint32_t ns = m->nspaces;
+    int r = halloc(&m->h_pin_slot, m->cap);
+    if (!r) r = halloc(&m->h_pin_x, m->cap);
+    if (!r) r = halloc(&m->h_pin_z, m->cap);
+    if (!r) r = halloc(&m->h_pin_out, 4 + 4 * (size_t)ns);
+    if (!r) r = halloc(&m->h_pin_ext, ns);
+    if (!r) r = dalloc(&m->d_pin_first, m->cap);
+    if (!r) r = dalloc(&m->d_pin_out, 4);
+    if (!r) r = dalloc(&m->d_pin_seen, 4 * (size_t)ns);
+    if (!r) r = dalloc(&m->d_pin_ext, ns);
+    if (r) return r;  // freed with the manager
+    HIPCHK(hipMemsetAsync(m->d_pin_first, 0, (size_t)m->cap * sizeof(unsigned long long), m->stream));
+    m->pin_id = 0;
+    m->pin_seen_dirty = true;
+  }
+  *slots = m->h_pin_slot;
+  *x = m->h_pin_x;
+  *z = m->h_pin_z;
+  if (capacity) *capacity = m->cap;
+  return GWAOI_OK;
+}
+
+// The Moved batch in the pinned buffers: one DMA copy, then k_pin_check validates it on the GPU and
+// finds the first repeated slot; nothing changes unless the whole batch is acceptable. Runs of the
+// batch without a repeat are staged as device batches (all but the last run as sub-passes now).
+int gwaoi_stage_moves_pinned(gwaoi_mgr* m, uint32_t n) {
+  RCHK(check_mgr(m));
+  RCHK(host_staging_ok(m));
+  if (!m->h_pin_slot) {
+    set_err("stage_moves_pinned: no staging buffers (call gwaoi_stage_buffers first)");
+    return GWAOI_ERR_STATE;
+  }
+  if (n > m->cap) {
+    set_err("stage_moves_pinned: %u moves > capacity %u", n, m->cap);
+    return GWAOI_ERR_INVALID;
+  }
+  if (!n) return GWAOI_OK;
+  RCHK(set_dev(m));
+  if (m->n_ops || m->dv_n) RCHK(run_pass(m, true));  // ops staged earlier come first
+  hipStream_t st = m->stream;
+  HIPCHK(hipMemcpyAsync(m->d_op_slot, m->h_pin_slot, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(m->d_op_x, m->h_pin_x, (size_t)n * sizeof(float), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(m->d_op_z, m->h_pin_z, (size_t)n * sizeof(float), hipMemcpyHostToDevice, st));
+  bool any_auto = false;
+  for (const SpaceHost& sh : m->spaces) any_auto |= sh.auto_extent;
+  if (any_auto) {  // the extent each auto-extent Space's grid covers (beyond it: reported, geometry redone)
+    const float inf = std::numeric_limits<float>::infinity();
+    for (uint32_t sp = 0; sp < m->nspaces; ++sp) {
+      const SpaceHost& sh = m->spaces[sp];
+      m->h_pin_ext[sp] = sh.auto_extent ? (sh.seen_any ? make_float4(sh.gx0, sh.gz0, sh.gx1, sh.gz1)
+                                                       : make_float4(inf, inf, -inf, -inf))  // nothing seen yet
+                                        : make_float4(-inf, -inf, inf, inf);
+    }
+    HIPCHK(hipMemcpyAsync(m->d_pin_ext, m->h_pin_ext, m->nspaces * sizeof(float4), hipMemcpyHostToDevice, st));
+  }
+  gw::PinCheckArgs a;
+  a.slot = m->d_op_slot;
+  a.x = m->d_op_x;
+  a.z = m->d_op_z;
+  a.n = n;
+  a.cap = m->cap;
+  a.seq = m->seq;
+  a.space_of = m->space_of;
+  a.first = m->d_pin_first;
+  a.ext = any_auto ? m->d_pin_ext : nullptr;
+  a.seen = m->d_pin_seen;
+  a.out = m->d_pin_out;
+  uint32_t seg = 0;
+  for (int validate = 1;; validate = 0) {
+    if (++m->pin_id == 0) {  // ids wrapped: forget every stored id
+      HIPCHK(hipMemsetAsync(m->d_pin_first, 0, (size_t)m->cap * sizeof(unsigned long long), st));
+      m->pin_id = 1;
+    }
+    a.seg = seg;
+    a.id = m->pin_id;
+    a.validate = validate;
+    gw::launch_pin_check(a, validate && m->pin_seen_dirty, m->nspaces, st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(m->h_pin_out, m->d_pin_out, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const uint32_t* o = m->h_pin_out;
+    if (validate && o[0]) {
+      set_err("stage_moves_pinned: entry %u refused (flags 0x%x: 2=slot not in a Space, 4=slot >= capacity, "
+              "64=non-finite coordinate); nothing staged",
+              o[2], o[0]);
+      return (o[0] & (gw::ERR_BAD_SLOT | gw::ERR_BAD_COORD)) ? GWAOI_ERR_INVALID : GWAOI_ERR_STATE;
+    }
+    if (validate) {
+      m->pin_seen_dirty = o[3] != 0;
+      if (o[3]) {  // coordinates beyond an auto-extent Space's grid: widen what it has seen
+        uint32_t* k = m->h_pin_out + 4;
+        HIPCHK(hipMemcpyAsync(k, m->d_pin_seen, 4 * sizeof(uint32_t) * m->nspaces, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (uint32_t sp = 0; sp < m->nspaces; ++sp) {
+          if (!m->spaces[sp].auto_extent || k[4 * sp] > k[4 * sp + 2]) continue;  // none beyond
+          note_coord(m, sp, gw::ord_float(k[4 * sp]), gw::ord_float(k[4 * sp + 1]));
+          note_coord(m, sp, gw::ord_float(k[4 * sp + 2]), gw::ord_float(k[4 * sp + 3]));
+        }
+      }
+    }
+    const uint32_t cut = std::min(o[1], n);
+    m->dv_slot = m->d_op_slot + seg;
+    m->dv_x = m->d_op_x + seg;
+    m->dv_z = m->d_op_z + seg;
+    m->dv_n = cut - seg;
+    if (cut >= n) break;
+    RCHK(run_pass(m, true));  // op `cut` repeats a slot of this run: the run is a sub-pass
+    seg = cut;
   }
   return GWAOI_OK;
 }

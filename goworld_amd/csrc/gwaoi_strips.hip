@@ -173,9 +173,15 @@ __global__ void __launch_bounds__(kSBlock) k_strip_select(gwaoi_strip_geom g, co
 }
 
 __global__ void __launch_bounds__(kSBlock) k_strip_absorb(uint8_t* flags, float* ex, float* ez, const uint4* recs,
-                                                          uint32_t n, const uint32_t* d_n) {
+                                                          uint32_t n, const uint32_t* d_n, uint32_t* err) {
   const uint32_t k = blockIdx.x * kSBlock + threadIdx.x;
-  if (d_n) n = min(n, *d_n);  // received count (device): the launch covers the message's capacity
+  if (d_n) {  // received count (device): the launch covers the message's capacity
+    const uint32_t got = *d_n;
+    // a sender past its capacity kept counting: the list was cut, so this rank's AOI would miss halo
+    // entities. The sender flags its own overflow; the receiver fails its protocol check as well.
+    if (got > n && k == 0 && err) atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
+    n = min(n, got);
+  }
   if (k >= n) return;
   const uint4 r = recs[k];
   ex[r.x] = __uint_as_float(r.y);
@@ -198,15 +204,26 @@ __device__ __forceinline__ void load_flags16(const uint8_t* flags, uint32_t n, u
 
 __device__ __forceinline__ bool has_op(uint8_t f) { return (f & (GWAOI_STRIP_PRESENT | GWAOI_STRIP_END)) != 0; }
 
-__global__ void __launch_bounds__(kSBlock) k_strip_count(const uint8_t* flags, uint32_t n, uint32_t* blk) {
+__device__ __forceinline__ bool is_enter(uint8_t f) { return (f & (GWAOI_STRIP_PRESENT | GWAOI_STRIP_END)) == GWAOI_STRIP_END; }
+
+// ops per chunk (blk) and, for local slots, the tick's Enter count (enters: one atomic per block)
+__global__ void __launch_bounds__(kSBlock) k_strip_count(const uint8_t* flags, uint32_t n, uint32_t* blk,
+                                                         uint32_t* enters) {
   uint8_t f[kSItems];
   load_flags16(flags, n, blockIdx.x * kSChunk + threadIdx.x * kSItems, f);
-  uint32_t c = 0;
+  uint32_t c = 0, ce = 0;
 #pragma unroll
-  for (int k = 0; k < kSItems; ++k) c += has_op(f[k]) ? 1u : 0u;
-  uint32_t tot;
+  for (int k = 0; k < kSItems; ++k) {
+    c += has_op(f[k]) ? 1u : 0u;
+    ce += is_enter(f[k]) ? 1u : 0u;
+  }
+  uint32_t tot, tote = 0;
   block_scan_s(c, &tot);
-  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+  if (enters) block_scan_s(ce, &tote);  // grid-uniform branch
+  if (threadIdx.x == 0) {
+    blk[blockIdx.x] = tot;
+    if (tote) atomicAdd(enters, tote);
+  }
 }
 
 // One block per chunk of kSChunk ids (the chunk's op count scanned beforehand by k_strip_count), in
@@ -275,14 +292,19 @@ __global__ void __launch_bounds__(kSBlock) k_local_init(uint32_t n, uint32_t cap
   }
 }
 
-// the previous tick's Leave slots back into the free ring (one block; the count is on the device)
-__global__ void __launch_bounds__(1024) k_local_release(uint32_t* fq, const uint32_t* pend, uint32_t mask, uint32_t* ctr) {
+// the previous tick's Leave slots back into the free ring (one block; the count is on the device).
+// sc[0] = free slots after the release (what this tick's Enters may take), sc[1] = 0 (k_strip_count
+// adds the tick's Enters there).
+__global__ void __launch_bounds__(1024) k_local_release(uint32_t* fq, const uint32_t* pend, uint32_t mask, uint32_t* ctr,
+                                                        uint32_t* sc) {
   const uint32_t np = ctr[2], tail = ctr[1];
   for (uint32_t k = threadIdx.x; k < np; k += 1024) fq[(tail + k) & mask] = pend[k];
   __syncthreads();
   if (threadIdx.x == 0) {
     ctr[1] = tail + np;
     ctr[2] = 0u;
+    sc[0] = tail + np - ctr[0];
+    sc[1] = 0u;
   }
 }
 
@@ -292,11 +314,21 @@ __global__ void __launch_bounds__(kSBlock) k_strip_emit_local(gwaoi_strip_geom g
                                                               const float* ex, const float* ez, const uint32_t* blk,
                                                               uint32_t* slots, float* ox, float* oz, uint8_t* kinds,
                                                               uint32_t* g2l, uint32_t* l2g, const uint32_t* fq,
-                                                              uint32_t* pend, uint32_t mask, uint32_t* ctr) {
+                                                              uint32_t* pend, uint32_t mask, uint32_t* ctr,
+                                                              const uint32_t* sc, uint32_t nb, uint32_t* n_ops) {
   __shared__ uint32_t wsum[2][kSBlock / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long below = (1ull << lane) - 1ull;
   const uint32_t tail = ctr[1];  // releases happened before this kernel; allocations must stay below
+  // More Enters than free slots (a crowd drifting into the region past cap_l): the tick emits NOTHING
+  // (zero ops, state not advanced), so the manager runs an empty pass and stays usable, and the error
+  // bit names the cause. Decided from counts complete before this kernel (grid-uniform).
+  const bool fits = sc[1] <= sc[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *n_ops = fits ? blk[nb] : 0u;
+    if (!fits) atomicOr(&ctr[3], GWAOI_STRIP_ERR_SLOTS);
+  }
+  if (!fits) return;
   uint32_t pos = blk[blockIdx.x];
 #pragma unroll 1
   for (int r = 0; r < kSItems; ++r) {
@@ -322,7 +354,7 @@ __global__ void __launch_bounds__(kSBlock) k_strip_emit_local(gwaoi_strip_geom g
       if (!(f & GWAOI_STRIP_OWNED)) kind |= GWAOI_OP_SILENT;
       uint32_t l;
       if (!p) {
-        if ((int)(tail - ka) <= 0) {  // ring empty: more entities than cap_l
+        if ((int)(tail - ka) <= 0) {  // ring empty (excluded by the check above; kept as a guard)
           atomicOr(&ctr[3], GWAOI_STRIP_ERR_SLOTS);
           l = 0u;
         } else {
@@ -418,16 +450,16 @@ int gwaoi_strip_absorb(void* stream, uint8_t* flags, float* ex, float* ez, const
   if (!flags || !ex || !ez || (n && !d_recs)) return GWAOI_ERR_INVALID;
   if (n)
     hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n), dim3(gw::kSBlock), 0, (hipStream_t)stream, flags, ex, ez,
-                       reinterpret_cast<const uint4*>(d_recs), n, (const uint32_t*)nullptr);
+                       reinterpret_cast<const uint4*>(d_recs), n, (const uint32_t*)nullptr, (uint32_t*)nullptr);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 
 int gwaoi_strip_absorb_n(void* stream, uint8_t* flags, float* ex, float* ez, const uint32_t* d_recs, const uint32_t* d_n,
-                         uint32_t n_max) {
+                         uint32_t n_max, uint32_t* d_err) {
   if (!flags || !ex || !ez || !d_n || (n_max && !d_recs)) return GWAOI_ERR_INVALID;
-  if (n_max)
-    hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n_max), dim3(gw::kSBlock), 0, (hipStream_t)stream, flags, ex,
-                       ez, reinterpret_cast<const uint4*>(d_recs), n_max, d_n);
+  // one block at least: the overflow check runs even for a zero-capacity message
+  hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n_max ? n_max : 1u), dim3(gw::kSBlock), 0, (hipStream_t)stream,
+                     flags, ex, ez, reinterpret_cast<const uint4*>(d_recs), n_max, d_n, d_err);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 
@@ -457,7 +489,7 @@ int gwaoi_strip_emit(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, fl
   sc.status = d_scratch + nb + 1;
   if (hipMemsetAsync(blk + nb, 0, sizeof(uint32_t), st) != hipSuccess) return GWAOI_ERR_HIP;
   if (nb) {
-    hipLaunchKernelGGL(gw::k_strip_count, dim3(nb), dim3(gw::kSBlock), 0, st, flags, g->n, blk);
+    hipLaunchKernelGGL(gw::k_strip_count, dim3(nb), dim3(gw::kSBlock), 0, st, flags, g->n, blk, (uint32_t*)nullptr);
     gw::launch_scan(sc, blk, nb + 1, st);
     hipLaunchKernelGGL(gw::k_strip_emit, dim3(nb), dim3(gw::kSBlock), 0, st, *g, flags, sx, sz, ex, ez,
                        (const uint32_t*)blk, d_ids, d_x, d_z, d_kinds);
@@ -488,16 +520,18 @@ int gwaoi_strip_emit_local(void* stream, const gwaoi_strip_geom* g, uint8_t* fla
   gw::ScanCtx sc;
   sc.status = d_scratch + nb + 1;
   if (hipMemsetAsync(blk + nb, 0, sizeof(uint32_t), st) != hipSuccess) return GWAOI_ERR_HIP;
-  hipLaunchKernelGGL(gw::k_local_release, dim3(1), dim3(1024), 0, st, fq, (const uint32_t*)pend, cap_l - 1, ctr);
+  uint32_t* spare = d_scratch + nb + 1 + gw::scan_part_words(nb + 1);  // 4 words (gwaoi_strip_scratch_words)
+  hipLaunchKernelGGL(gw::k_local_release, dim3(1), dim3(1024), 0, st, fq, (const uint32_t*)pend, cap_l - 1, ctr, spare);
   if (nb) {
-    hipLaunchKernelGGL(gw::k_strip_count, dim3(nb), dim3(gw::kSBlock), 0, st, flags, g->n, blk);
+    hipLaunchKernelGGL(gw::k_strip_count, dim3(nb), dim3(gw::kSBlock), 0, st, flags, g->n, blk, spare + 1);
     gw::launch_scan(sc, blk, nb + 1, st);
+    // writes *d_n_ops (0 when the Enters do not fit the free slots)
     hipLaunchKernelGGL(gw::k_strip_emit_local, dim3(nb), dim3(gw::kSBlock), 0, st, *g, flags, sx, sz, ex, ez,
                        (const uint32_t*)blk, d_slots, d_x, d_z, d_kinds, g2l, l2g, (const uint32_t*)fq, pend,
-                       cap_l - 1, ctr);
-  }
-  if (hipMemcpyAsync(d_n_ops, blk + nb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st) != hipSuccess)
+                       cap_l - 1, ctr, (const uint32_t*)spare, nb, d_n_ops);
+  } else if (hipMemsetAsync(d_n_ops, 0, sizeof(uint32_t), st) != hipSuccess) {
     return GWAOI_ERR_HIP;
+  }
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 

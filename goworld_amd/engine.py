@@ -47,6 +47,7 @@ class Engine:
 
     # ---- lifecycle ----
     def close(self):
+        self._pin = None  # views of memory the manager owns
         if getattr(self, "_h", None) and self._h.value:
             self._L.gwaoi_destroy(self._h)
             self._h = ctypes.c_void_p()
@@ -88,6 +89,23 @@ class Engine:
         xa = np.ascontiguousarray(x, dtype=np.float32)
         za = np.ascontiguousarray(z, dtype=np.float32)
         check(self._L.gwaoi_stage_moves(self._h, _u32p(s), _f32p(xa), _f32p(za), len(s)))
+
+    def stage_buffers(self):
+        """The manager's pinned staging arrays (gwaoi_stage_buffers) as numpy views: (slots, x, z), each
+        of `capacity` entries. Write n moves into their heads, then stage_moves_pinned(n)."""
+        if getattr(self, "_pin", None) is None:
+            ps, px, pz = ctypes.POINTER(ctypes.c_uint32)(), ctypes.POINTER(ctypes.c_float)(), ctypes.POINTER(ctypes.c_float)()
+            cap = ctypes.c_uint32(0)
+            check(self._L.gwaoi_stage_buffers(self._h, ctypes.byref(ps), ctypes.byref(px), ctypes.byref(pz),
+                                              ctypes.byref(cap)))
+            n = int(cap.value)
+            self._pin = (np.ctypeslib.as_array(ps, shape=(n,)), np.ctypeslib.as_array(px, shape=(n,)),
+                         np.ctypeslib.as_array(pz, shape=(n,)))
+        return self._pin
+
+    def stage_moves_pinned(self, n: int):
+        """The first n entries of the pinned staging arrays as n Moved calls (validated on the device)."""
+        check(self._L.gwaoi_stage_moves_pinned(self._h, int(n)))
 
     def stage_moves_device(self, d_slots: int, d_x: int, d_z: int, n: int):
         check(self._L.gwaoi_stage_moves_device(self._h, ctypes.c_void_p(d_slots), ctypes.c_void_p(d_x),

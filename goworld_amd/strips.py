@@ -29,6 +29,7 @@ from ._lib import check
 from .engine import Engine
 
 f32 = np.float32
+STRIP_ERR_SLOTS = 8  # GWAOI_STRIP_ERR_SLOTS (include/gwaoi_strips.h)
 
 
 class StripLayout:
@@ -107,7 +108,7 @@ class StripNode:
 
     def __init__(self, layout: StripLayout, rank: int, n: int, device: int = 0, seed: int = 0x5EED0004,
                  halo_cap: Optional[int] = None, skew: Optional[Tuple[int, float, int]] = None,
-                 local_slots: bool = True):
+                 local_slots: bool = True, cap_l: Optional[int] = None):
         """skew = (nhot, sigma, hot_every): the skewed-crowd placement of config 5 instead of uniform.
         local_slots: the manager sees local slots (gwaoi_strip_emit_local); False: slot = global id."""
         self.layout, self.rank, self.n, self.seed = layout, int(rank), int(n), int(seed)
@@ -146,6 +147,8 @@ class StripNode:
         # its own, so its per-pass work follows the region's population, not the world's id range.
         # cap_l: a power of two with room for crowds drifting in (1.5x the share + 8k), at most n.
         want = min(n, int(share * 1.5) + 8192) if local_slots else n
+        if cap_l is not None:  # explicit (tests: a region that overflows its slots)
+            want = int(cap_l)
         self.cap_l = 1 << max(0, (max(1, want) - 1).bit_length())
         self.local = bool(local_slots)
         if self.local:
@@ -199,8 +202,11 @@ class StripNode:
             ev = self.eng.tick() if host_events else self.eng.tick_device()
         c = self.h_counts  # complete: the tick waited for every kernel after the copy
         if int(c[3]) or (self.local and int(self.h_lctr[3])):
+            flags = int(c[3]) | (int(self.h_lctr[3]) if self.local else 0)
+            why = " (the region holds more entities than its local slots, cap_l = %d: nothing of this tick was " \
+                  "applied)" % self.cap_l if flags & STRIP_ERR_SLOTS else ""
             raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, f"strip {self.rank}: protocol check failed (flags "
-                                  f"{int(c[3]) | (int(self.h_lctr[3]) if self.local else 0)})")
+                                  f"{flags}){why}")
         self.last_ops = int(c[2])
         return ev
 
@@ -323,7 +329,7 @@ class StripNode:
                 if peers[k] >= 0:
                     check(L.gwaoi_strip_absorb_n(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
                                                  _ptr(recs), ctypes.c_void_p(self.counts_in.data_ptr() + 4 * k),
-                                                 self.cap))
+                                                 self.cap, self._err()))
             self.tick_no = t
             return self._emit_and_tick(host_events, self.eng.count()[0] + 2 * self.cap)
 

@@ -102,6 +102,17 @@ int gwaoi_leave(gwaoi_mgr* mgr, uint32_t slot);
 int gwaoi_moved(gwaoi_mgr* mgr, uint32_t slot, float x, float z);
 /* n Moved calls in array order (GameService.HandleSyncPositionYawFromClient loop, GameService.go:398-410). */
 int gwaoi_stage_moves(gwaoi_mgr* mgr, const uint32_t* slots, const float* x, const float* z, uint32_t n);
+/* Zero-copy variant for the cgo wrapper's per-tick flush (replaces the copy-in of gwaoi_stage_moves).
+ * gwaoi_stage_buffers returns three library-owned pinned host arrays of `*capacity` entries (allocated on
+ * the first call, owned by the manager, the same arrays every call); the caller writes n Moved calls
+ * into them (Go: unsafe.Slice over the C pointers) and calls gwaoi_stage_moves_pinned(mgr, n). That
+ * call copies the arrays to the device once and validates them THERE (slot range, slot in a Space,
+ * finite coordinates: GWAOI_ERR_INVALID / GWAOI_ERR_STATE with nothing staged, as gwaoi_stage_moves);
+ * a slot that repeats splits the batch into sub-passes on the device's report, exactly as
+ * gwaoi_stage_moves does. Ops staged before it run first. When it returns, the buffers may be
+ * rewritten. */
+int gwaoi_stage_buffers(gwaoi_mgr* mgr, uint32_t** slots, float** x, float** z, uint32_t* capacity);
+int gwaoi_stage_moves_pinned(gwaoi_mgr* mgr, uint32_t n);
 /* Same, from DEVICE arrays (inputs resident in HBM). Must be the only ops of the batch; slots must be
  * distinct and present — checked on the device, reported by gwaoi_tick as GWAOI_ERR_DEVICE_CHECK
  * (the manager is then unusable and must be destroyed). The arrays must stay valid until gwaoi_tick. */
@@ -195,6 +206,13 @@ int gwaoi_reset_stats(gwaoi_mgr* mgr);
 
 /* Library version string and the thread-local message of the last failing call. */
 const char* gwaoi_version(void);
+/* ABI revision of the headers the library was built from. A binding compiled against these headers
+ * checks gwaoi_abi_version() == GWAOI_ABI_VERSION once at start-up: a struct that grew
+ * (e.g. gwaoi_ingest_result.n_nonfinite, ABI 2) would otherwise be written past its end.
+ *   1: round-1 surface;  2: gwaoi_ingest_result.n_nonfinite, gwaoi_strip_absorb_n's d_err,
+ *   gwaoi_stage_buffers / gwaoi_stage_moves_pinned, gwaoi_export_relation_delta. */
+#define GWAOI_ABI_VERSION 2
+int gwaoi_abi_version(void);
 const char* gwaoi_last_error(void);
 
 #ifdef __cplusplus

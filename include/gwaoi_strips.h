@@ -93,7 +93,9 @@ size_t gwaoi_strip_scratch_words(uint32_t n);
  * {allocations, releases, pending, error bits}. */
 #define GWAOI_STRIP_NO_SLOT 0xFFFFFFFFu
 int gwaoi_strip_local_init(void* stream, uint32_t n, uint32_t cap_l, uint32_t* g2l, uint32_t* fq, uint32_t* ctr);
-/* gwaoi_strip_emit with d_slots = local slots: Enter ops take a free slot, Leave ops queue theirs. */
+/* gwaoi_strip_emit with d_slots = local slots: Enter ops take a free slot, Leave ops queue theirs. When
+ * the tick's Enters exceed the free slots, nothing is emitted (*d_n_ops = 0, state not advanced, the
+ * manager's pass is empty and it stays usable) and ctr[3] gets GWAOI_STRIP_ERR_SLOTS. */
 int gwaoi_strip_emit_local(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* sx, float* sz,
                            const float* ex, const float* ez, uint32_t* d_slots, float* d_x, float* d_z,
                            uint8_t* d_kinds, uint32_t* d_scratch, uint32_t* d_n_ops, uint32_t* g2l, uint32_t* l2g,
@@ -104,9 +106,11 @@ int gwaoi_strip_translate_events(void* stream, const uint32_t* l2g, uint32_t* d_
 /* Skewed-crowd variant of gwaoi_strip_init_walk (gww_skew_init_coord). */
 int gwaoi_strip_init_skew(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, float* ex, float* ez,
                           uint64_t seed, float L, uint32_t nhot, float sigma, uint32_t hot_every);
-/* gwaoi_strip_absorb with the record count in device memory (min(*d_n, n_max) records). */
+/* gwaoi_strip_absorb with the record count in device memory (min(*d_n, n_max) records). A count above
+ * n_max (the sender's list was cut at its capacity) sets GWAOI_STRIP_ERR_OVERFLOW in *d_err (if not
+ * NULL), so the receiving rank fails its protocol check too. (ABI 2: d_err added.) */
 int gwaoi_strip_absorb_n(void* stream, uint8_t* flags, float* ex, float* ez, const uint32_t* d_recs,
-                         const uint32_t* d_n, uint32_t n_max);
+                         const uint32_t* d_n, uint32_t n_max, uint32_t* d_err);
 
 /* ---- the halo exchange over RCCL (xGMI), device-resident end to end ----
  * One communicator per strip world, one rank per GPU. Rank 0 makes the id; the caller hands the 128

@@ -5,8 +5,10 @@
  *
  *   Enter      -> gwaoi_enter, then Flush (SyncEnterLeave: the callbacks fire inside Space.enter,
  *                 /root/reference/engine/entity/Space.go:211-217)
- *   Moved      -> appended to host slices; Flush stages them with ONE gwaoi_stage_moves call
- *   Flush      -> gwaoi_stage_moves + gwaoi_tick, events replayed in order
+ *   Moved      -> written into the manager's pinned staging arrays (gwaoi_stage_buffers); Flush pushes
+ *                 them with ONE gwaoi_stage_moves_pinned call (validated on the device). The scenario
+ *                 runs a second time with host slices and ONE gwaoi_stage_moves call (the copy-in path).
+ *   Flush      -> push the pending moves + gwaoi_tick, events replayed in order
  *   Leave      -> pending moves first (call order), gwaoi_leave, then Flush
  *
  * Every tick's events are checked against a brute-force sequential model of the reference
@@ -67,9 +69,12 @@ static void model_op(int kind, int m, float x, float z) { /* kind: 0 move, 1 ent
 }
 
 static gwaoi_mgr* mgr;
-static uint32_t pend_slot[4 * CAP];
-static float pend_x[4 * CAP], pend_z[4 * CAP];
+static uint32_t host_slot[4 * CAP];
+static float host_x[4 * CAP], host_z[4 * CAP];
+static uint32_t *pend_slot, pin_cap;
+static float *pend_x, *pend_z;
 static uint32_t npend;
+static int pinned;
 static int failures;
 
 #define CHK(call)                                                                        \
@@ -81,9 +86,14 @@ static int failures;
     }                                                                                    \
   } while (0)
 
-static void flush(const char* what) {
-  if (npend) CHK(gwaoi_stage_moves(mgr, pend_slot, pend_x, pend_z, npend));
+static void push(void) {
+  if (npend && pinned) CHK(gwaoi_stage_moves_pinned(mgr, npend));
+  if (npend && !pinned) CHK(gwaoi_stage_moves(mgr, pend_slot, pend_x, pend_z, npend));
   npend = 0;
+}
+
+static void flush(const char* what) {
+  push();
   gwaoi_events ev;
   CHK(gwaoi_tick(mgr, &ev));
   int ok = ev.count == nwant && ev.n_enter + ev.n_leave == ev.count;
@@ -103,6 +113,7 @@ static void enter(uint32_t s, float x, float z) {
 }
 
 static void moved(uint32_t s, float x, float z) { /* staged on the host side, like the Go wrapper */
+  if (npend == pin_cap) push();
   pend_slot[npend] = s;
   pend_x[npend] = x;
   pend_z[npend] = z;
@@ -111,20 +122,24 @@ static void moved(uint32_t s, float x, float z) { /* staged on the host side, li
 }
 
 static void leave(uint32_t s) {
-  if (npend) CHK(gwaoi_stage_moves(mgr, pend_slot, pend_x, pend_z, npend)); /* keep the call order */
-  npend = 0;
+  push(); /* keep the call order */
   CHK(gwaoi_leave(mgr, s));
   model_op(2, (int)s, 0.f, 0.f);
   flush("leave");
 }
 
-int main(void) {
-  int ndev = 0;
-  if (gwaoi_device_count(&ndev) != GWAOI_OK || ndev < 1) {
-    fprintf(stderr, "abi_smoke: no HIP device\n");
-    return 3;
-  }
+static void scenario(int use_pinned) {
+  memset(present, 0, sizeof present);
+  memset(rel, 0, sizeof rel);
+  nwant = npend = 0;
+  pinned = use_pinned;
   CHK(gwaoi_create(D, CAP, 0, &mgr));
+  if (pinned) {
+    CHK(gwaoi_stage_buffers(mgr, &pend_slot, &pend_x, &pend_z, &pin_cap));
+    if (pin_cap != CAP) ++failures, fprintf(stderr, "staging capacity %u\n", pin_cap);
+  } else {
+    pend_slot = host_slot, pend_x = host_x, pend_z = host_z, pin_cap = 4 * CAP;
+  }
   /* MySpace.OnSpaceCreated: 10 monsters at the origin (examples/test_game/MySpace.go:27-34) */
   for (uint32_t s = 0; s < 10; ++s) enter(s, 0.f, 0.f);
   /* a crowd on a coarse lattice: exact-D offsets and ties */
@@ -145,6 +160,12 @@ int main(void) {
   moved(4, 100.0f, 0.0f);
   leave(5); /* flushes moved(4) first */
   enter(3, 0.f, 0.f);
+  if (pinned) { /* a refused pinned batch stages nothing (slot 80 is not in a Space) */
+    pend_slot[0] = 0, pend_x[0] = 0.f, pend_z[0] = 0.f;
+    pend_slot[1] = 80, pend_x[1] = 1.f, pend_z[1] = 1.f;
+    if (gwaoi_stage_moves_pinned(mgr, 2) != GWAOI_ERR_STATE) ++failures, fprintf(stderr, "pinned absent accepted\n");
+    flush("refused batch");
+  }
   /* misuse is reported, not crashed on: Enter twice, Moved/Leave of an absent slot, NaN */
   if (gwaoi_enter(mgr, 0, 1.f, 1.f) != GWAOI_ERR_STATE) ++failures, fprintf(stderr, "enter twice accepted\n");
   if (gwaoi_moved(mgr, 80, 1.f, 1.f) != GWAOI_ERR_STATE) ++failures, fprintf(stderr, "moved of absent accepted\n");
@@ -155,6 +176,20 @@ int main(void) {
   CHK(gwaoi_count(mgr, &npres, &nst));
   if (npres != 59 || nst != 0) ++failures, fprintf(stderr, "count %u staged %u\n", npres, nst);
   CHK(gwaoi_destroy(mgr));
+}
+
+int main(void) {
+  int ndev = 0;
+  if (gwaoi_device_count(&ndev) != GWAOI_OK || ndev < 1) {
+    fprintf(stderr, "abi_smoke: no HIP device\n");
+    return 3;
+  }
+  if (gwaoi_abi_version() != GWAOI_ABI_VERSION) {
+    fprintf(stderr, "abi_smoke: library ABI %d, headers %d\n", gwaoi_abi_version(), GWAOI_ABI_VERSION);
+    return 4;
+  }
+  scenario(1);
+  scenario(0);
   if (failures) {
     fprintf(stderr, "abi_smoke: %d failure(s)\n", failures);
     return 1;

@@ -90,6 +90,35 @@ def gpu_tick(eng, ops) -> np.ndarray:
     return eng.tick()
 
 
+def gpu_tick_pinned(eng, ops) -> np.ndarray:
+    """The cgo wrapper's batching: Moved calls are written into the manager's pinned
+    staging arrays and pushed with ONE gwaoi_stage_moves_pinned before the next Enter/Leave and at the
+    flush; a slot moved twice stays in the batch (the device splits it into sub-passes)."""
+    ps, px, pz = eng.stage_buffers()
+    k = 0
+
+    def push():
+        nonlocal k
+        if k:
+            eng.stage_moves_pinned(k)
+            k = 0
+
+    for kind, slot, x, z in ops:
+        if kind == MOVE:
+            ps[k], px[k], pz[k] = slot, x, z
+            k += 1
+            if k == len(ps):
+                push()
+            continue
+        push()
+        if kind == ENTER:
+            eng.enter(slot, x, z)
+        else:
+            eng.leave(slot)
+    push()
+    return eng.tick()
+
+
 def fmt_diff(a: np.ndarray, b: np.ndarray, limit=10) -> str:
     sa = set(map(tuple, a.tolist()))
     sb = set(map(tuple, b.tolist()))

@@ -333,3 +333,51 @@ def test_strip_tick_rccl_single_rank_matches(gpu):
     comm.close()
     a.close()
     b.close()
+
+
+def test_strip_local_slots_exhausted_keeps_manager_usable(gpu):
+    """a region with more entities than its local slots (cap_l) used to emit Enters of slot 0
+    when the free ring ran dry, which failed the manager's device check and left it unusable with the
+    real cause hidden. Now the tick emits nothing, the error names GWAOI_STRIP_ERR_SLOTS, and the
+    manager still runs passes."""
+    import torch
+    from goworld_amd import _lib
+    from goworld_amd.strips import StripLayout, StripNode
+    n, L = 20_000, 4000.0
+    lay = StripLayout(1, L, 100.0, 1.0)
+    nd = StripNode(lay, 0, n, device=0, seed=0x5EED0078, cap_l=1024)
+    assert nd.cap_l == 1024
+    with pytest.raises(_lib.GwaoiError) as ei:
+        nd.start(host_events=True)
+    assert "cap_l = 1024" in str(ei.value) and "flags 8" in str(ei.value)
+    assert nd.eng.count()[0] == 0  # nothing applied
+    ev = nd.eng.tick()  # the manager is not poisoned: an empty pass runs
+    assert int(ev.count) == 0
+    torch.cuda.synchronize()
+    nd.close()
+
+
+def test_strip_absorb_n_flags_a_cut_list(gpu):
+    """a received count above the message capacity (the sender's list was cut) sets
+    GWAOI_STRIP_ERR_OVERFLOW on the receiving rank too; a count within capacity sets nothing."""
+    import ctypes
+
+    import torch
+    from goworld_amd import _lib
+    L_ = _lib.load()
+    dev = torch.device("cuda", 0)
+    n, cap = 64, 16
+    flags = torch.zeros(n, dtype=torch.uint8, device=dev)
+    ex, ez = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    recs = torch.zeros((cap, 4), dtype=torch.int32, device=dev)
+    recs[:, 0] = torch.arange(cap, dtype=torch.int32, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    for got, want_err in ((cap, 0), (cap + 5, 4)):
+        cnt = torch.tensor([got], dtype=torch.int32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        flags.zero_()
+        _lib.check(L_.gwaoi_strip_absorb_n(st, p(flags), p(ex), p(ez), p(recs), p(cnt), cap, p(err)))
+        torch.cuda.synchronize(dev)
+        assert int(err.item()) == want_err
+        assert int((flags != 0).sum().item()) == cap  # min(count, cap) records absorbed

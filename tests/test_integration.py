@@ -118,6 +118,32 @@ def test_gpu_aoi_manager_replays_into_entity_sets(gpu, oracle_lib, sync_enter_le
 
 
 @pytest.mark.gpu
+def test_moved_twice_in_one_tick_replays(gpu):
+    """The mirror batches Moved like the Go wrapper (one gwaoi_stage_moves_pinned per flush). A slot
+    moved twice in one tick splits the batch into two sub-passes on the device: b walks into a's box
+    and out again, so the tick replays ENTER then LEAVE of the pair (both callbacks each) and the sets
+    end empty, exactly as two sequential go-aoi Moved calls."""
+    from goworld_amd.aoi import NewXZListAOIManager
+    mgr = NewXZListAOIManager(100.0, capacity=8)
+    a, b, c = Entity(0), Entity(1), Entity(2)
+    mgr.Enter(a.aoi, 0.0, 0.0)
+    mgr.Enter(b.aoi, 150.0, 0.0)
+    mgr.Enter(c.aoi, 400.0, 0.0)
+    mgr.Flush()
+    assert not a.interested_in and not b.interested_in
+    mgr.Moved(b.aoi, 50.0, 0.0)
+    mgr.Moved(c.aoi, 390.0, 0.0)
+    mgr.Moved(b.aoi, 150.0, 0.0)  # repeats b: the device cuts the batch here
+    assert mgr.Flush() == 2
+    ev = mgr.last_events.tolist()
+    sa, sb = a.aoi._slot, b.aoi._slot
+    assert ev == [[sb, sa | 0x80000000], [sb, sa]]
+    assert a.enter_calls == b.enter_calls == 1 and a.leave_calls == b.leave_calls == 1
+    assert not a.interested_in and not b.interested_in and not a.interested_by
+    mgr.close()
+
+
+@pytest.mark.gpu
 def test_slot_reuse_waits_for_replay(gpu):
     """Leave then Enter of another entity in one batched tick: the new entity must not get the leaver's
     slot before the leaver's LEAVE events were replayed (they name that slot)."""
