@@ -306,19 +306,37 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             rs = None
     if HS:
         eng.adopt_device_state()  # the restore was a device batch: host staging from here on
+    # the cgo wrapper's path: Moved calls written into the manager's pinned staging arrays as the client
+    # packets arrive (here: the tick's positions copied in, untimed), then ONE gwaoi_stage_moves_pinned
+    # (one DMA copy, validation and repeat detection on the GPU). The last `copyin` ticks use the
+    # copy-in gwaoi_stage_moves (host validation) from plain host arrays instead, for comparison.
     slots_h = np.arange(n, dtype=np.uint32)
     xh = np.empty(n, np.float32)
     zh = np.empty(n, np.float32)
+    pin_s = pin_x = pin_z = None
+    if HS:
+        pin_s, pin_x, pin_z = eng.stage_buffers()
+        pin_s[:n] = slots_h
+    copyin = min(10, HS // 2)
+    stage_ci = []
     for t in range(W + K + H + 1, T):
-        _lib.check(L_.gwaoi_dev_dtoh(dev, xh.ctypes.data, ctypes.c_void_p(px(t)), 4 * n))  # untimed
-        _lib.check(L_.gwaoi_dev_dtoh(dev, zh.ctypes.data, ctypes.c_void_p(pz(t)), 4 * n))
+        use_pin = t < T - copyin
+        dx, dz = (pin_x, pin_z) if use_pin else (xh, zh)
+        _lib.check(L_.gwaoi_dev_dtoh(dev, dx.ctypes.data, ctypes.c_void_p(px(t)), 4 * n))  # untimed
+        _lib.check(L_.gwaoi_dev_dtoh(dev, dz.ctypes.data, ctypes.c_void_p(pz(t)), 4 * n))
         ts = time.perf_counter()
-        eng.stage_moves(slots_h, xh, zh)
+        if use_pin:
+            eng.stage_moves_pinned(n)
+        else:
+            eng.stage_moves(slots_h, xh, zh)
         t1 = time.perf_counter()
         ev = eng.tick_raw()
         te = time.perf_counter()
-        lat_hs.append(te - ts)
-        stage_hs.append(t1 - ts)
+        if use_pin:
+            lat_hs.append(te - ts)
+            stage_hs.append(t1 - ts)
+        else:
+            stage_ci.append(t1 - ts)
         if rs is not None and ev.count:
             tr = time.perf_counter()
             replay_bad += rs.replay(ctypes.cast(ev.events, ctypes.c_void_p).value, int(ev.count))
@@ -328,7 +346,8 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
 
     # relation size for the SURVEY §8(d) formula (directed entries |S|)
     nnz = None
-    rel_ms = rel_upd_ms = rel_upd_n = None
+    rel_ms = rel_upd_ms = rel_upd_n = rel_delta_ms = rel_delta_n = rel_export_ms = rel_apply_ms = None
+    dr_bad = None
     if args.workload in ("config2", "config3"):  # config 5's relation runs to billions of entries
         # the relation as a device-resident CSR (SURVEY 8(f)3 view), timed host-side incl. its syncs:
         # rebuilt from the grid (mode 1, every call), then kept up to date from each tick's events
@@ -344,18 +363,48 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         rel_ms = sorted(reps)[len(reps) // 2] * 1e3
         eng.debug_relation_mode(0)
         n_inc0 = eng.debug_relation_mode()[0]
-        reps = []
+        reps, dreps, dlen, areps = [], [], [], []
+        dr = None
+        try:  # the consumer by delta on the host: per-slot sorted neighbour arrays (tools/delta_rows.c)
+            from tools.replay import DeltaRows
+            dr = DeltaRows(*eng.relation())
+        except Exception as e:  # a bench aid: report, never fail the GPU line
+            log(f"[rank {rank}] delta rows unavailable: {e!r}")
+        dr_bad = 0
         for j in range(10):  # more ticks of the walk, into snapshot slots 0/1 (their ticks are over)
             a, b = (T - 1) if j == 0 else (j - 1) % 2, j % 2
             wl_step_spaces(dev, px(a), pz(a), px(b), pz(b), n_per, nsp, seed0, T + j, L, 1.0)
             tick_dev(b)
             L_.gwaoi_dev_sync(dev)
+            # the consumer by delta: the tick's net relation changes, computed from its events in HBM
+            # and copied to the host (gwaoi_export_relation_delta)
+            t0 = time.perf_counter()
+            dl = eng.relation_delta(cap=4 * n)
+            dreps.append(time.perf_counter() - t0)
+            dlen.append(len(dl))
+            if dr is not None:
+                t0 = time.perf_counter()
+                dr_bad += dr.apply(dl)
+                areps.append(time.perf_counter() - t0)
             t0 = time.perf_counter()
             eng.relation_device()
             L_.gwaoi_dev_sync(dev)
             reps.append(time.perf_counter() - t0)
         rel_upd_ms = sorted(reps)[len(reps) // 2] * 1e3
+        rel_delta_ms = sorted(dreps)[len(dreps) // 2] * 1e3
+        rel_delta_n = float(np.mean(dlen))
+        rel_apply_ms = sorted(areps)[len(areps) // 2] * 1e3 if areps else None
+        if dr is not None:
+            dr_bad += dr.diff(*eng.relation())  # the patched arrays must equal the relation now
+            dr.close()
         rel_upd_n = eng.debug_relation_mode()[0] - n_inc0
+        # the whole relation copied to the host (gwaoi_export_relation: row_ptr + cols, ~130 MB at 1M)
+        reps = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            eng.relation()
+            reps.append(time.perf_counter() - t0)
+        rel_export_ms = sorted(reps)[1] * 1e3
     eng.close()
     if rank != 0:
         return None
@@ -403,15 +452,29 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         "p50_tick_ms_host_staged": percentile(lat_hs, 50) * 1e3 if lat_hs else None,
         "p99_tick_ms_host_staged": percentile(lat_hs, 99) * 1e3 if lat_hs else None,
         "host_stage_ms": percentile(stage_hs, 50) * 1e3 if stage_hs else None,
+        "host_stage_copyin_ms": percentile(stage_ci, 50) * 1e3 if stage_ci else None,
         "replay_ms": percentile(replay_s, 50) * 1e3 if replay_s else None,
         "replay_note": ("events replayed into per-entity InterestedIn/InterestedBy hash sets in C, 4 set ops per "
-                        "pair event (tools/replay_sets.c); host_staged = gwaoi_stage_moves(host arrays) -> events "
-                        f"in pinned host memory, {len(lat_hs)} ticks" + (f"; {replay_bad} inconsistent set ops"
+                        "pair event (tools/replay_sets.c); host_staged = gwaoi_stage_moves_pinned (the positions "
+                        "written into the manager's pinned staging arrays; one DMA copy, validated on the GPU) -> "
+                        f"events in pinned host memory, {len(lat_hs)} ticks; host_stage_copyin_ms = the copy-in "
+                        f"gwaoi_stage_moves (host validation), {len(stage_ci)} ticks" + (f"; {replay_bad} inconsistent set ops"
                                                                           if replay_s else "")) if lat_hs else None,
         "events_per_tick": ev_per_tick,
         "relation_directed_entries": nnz,
         "relation_view_ms": rel_ms,
         "relation_update_ms": rel_upd_ms,
+        "relation_delta_ms": rel_delta_ms,
+        "relation_delta_entries": rel_delta_n,
+        "relation_export_ms": rel_export_ms,
+        "relation_delta_apply_ms": rel_apply_ms,
+        "relation_delta_inconsistent": dr_bad,
+        "relation_consumer_note": None if rel_delta_ms is None else
+        "relation_delta_ms = gwaoi_export_relation_delta (net changes of the tick from its events in HBM, "
+        "O(events), into host memory); relation_delta_apply_ms = those entries patched into per-slot sorted "
+        "neighbour arrays on the host (tools/delta_rows.c, the Go Sets consumer; relation_delta_inconsistent = "
+        "bad entries + rows differing from the relation afterwards, 0 expected); relation_export_ms = "
+        "gwaoi_export_relation (the whole CSR to the host)",
         "relation_update_note": None if rel_upd_ms is None else
         f"view updated from each tick's events (k_rd_*), {rel_upd_n}/10 ticks incremental; "
         "relation_view_ms = rebuilt from the grid",

@@ -32,7 +32,7 @@ ABI_SYMBOLS = (
     "gwaoi_stage_ops_device",
     "gwaoi_stage_ops_device_spaces",
     "gwaoi_stage_ops_device_n", "gwaoi_adopt_device_state", "gwaoi_set_population_hint",
-    "gwaoi_tick", "gwaoi_tick_ex", "gwaoi_count", "gwaoi_export_relation", "gwaoi_relation_device", "gwaoi_set_timing",
+    "gwaoi_tick", "gwaoi_tick_ex", "gwaoi_count", "gwaoi_export_relation", "gwaoi_export_relation_delta", "gwaoi_relation_device", "gwaoi_set_timing",
     "gwaoi_get_stats", "gwaoi_reset_stats", "gwaoi_version", "gwaoi_last_error", "gwaoi_abi_version",
 )
 TOOL_SYMBOLS = (
@@ -156,6 +156,9 @@ class Stats(ctypes.Structure):
 _lib = None
 
 
+ABI_VERSION = 2  # GWAOI_ABI_VERSION of include/gwaoi.h that these ctypes structs and signatures follow
+
+
 def load(path: str = SO_PATH):
     """Load libgwaoi.so (raises if it is missing: build it with `python -m goworld_amd.build`)."""
     global _lib
@@ -200,6 +203,7 @@ def load(path: str = SO_PATH):
         "gwaoi_set_timing": ([vp, ctypes.c_int], ctypes.c_int),
         "gwaoi_get_stats": ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
         "gwaoi_reset_stats": ([vp], ctypes.c_int),
+        "gwaoi_export_relation_delta": ([vp, vp, u64, ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_version": ([], ctypes.c_char_p),
         "gwaoi_abi_version": ([], ctypes.c_int),
         "gwaoi_last_error": ([], ctypes.c_char_p),
@@ -257,6 +261,8 @@ def load(path: str = SO_PATH):
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    if L.gwaoi_abi_version() != ABI_VERSION:  # structs of another ABI would be read or written out of shape
+        raise ImportError(f"libgwaoi.so has ABI {L.gwaoi_abi_version()}, this binding expects {ABI_VERSION}: rebuild it")
     _lib = L
     return L
 

@@ -211,6 +211,19 @@ struct RelDeltaArgs {
   uint32_t long_cap;
 };
 
+// Relation delta export: net changes of the relation over one tick's events (k_dx_*).
+struct DeltaExportArgs {
+  const uint2* ev;               // the tick's events {mover, other | ENTER}
+  uint32_t nev;
+  uint32_t mask;                 // hash table slots - 1 (slots >= 2 nev, a power of two)
+  unsigned long long* keys;      // [slots] unordered pair (min << 32 | max); ~0 = empty
+  uint32_t* cnt;                 // [slots] events of the pair (zeroed)
+  uint32_t* last;                // [slots] largest event index of the pair (zeroed)
+  uint32_t* slot_of;             // [nev]
+  uint32_t* flags;               // [nev + 1] kept, then their exclusive scan
+  uint2* out;                    // [2 nev] {row, col | ENTER (added) or col (removed)}
+};
+
 // Scan scratch (the chunk sums of launch_scan), owned by the stream's manager.
 struct ScanCtx {
   uint32_t* status = nullptr;  // scan_part_words(max n) words
@@ -272,6 +285,7 @@ void launch_row_sort_slab(const Rec* rec, const uint32_t* nrec, uint32_t rec_bou
 // lengths, scan, and place old and new entries.
 void launch_rel_delta_count(const RelDeltaArgs& a, hipStream_t st);
 void launch_rel_delta_apply(const RelDeltaArgs& a, ScanCtx& sc, hipStream_t st);
+void launch_delta_export(const DeltaExportArgs& a, ScanCtx& sc, hipStream_t st);  // count: flags[nev] (x2)
 void launch_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L, hipStream_t st);
 void launch_wl_init_spaces(float* x, float* z, uint32_t n_per, uint32_t nspaces, uint64_t seed0, float L,
                            uint32_t nhot, float sigma, uint32_t hot_every, hipStream_t st);

@@ -2443,6 +2443,66 @@ void launch_rel_delta_apply(const RelDeltaArgs& a, ScanCtx& sc, hipStream_t st) 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Relation delta export (gwaoi_export_relation_delta): the NET changes of the relation over the last
+// tick, from its events alone, O(events) with no sort. A pair's events alternate ENTER / LEAVE in
+// sequence, so the pair changed iff it has an odd number of events, and the kind of its LAST event is
+// the change. Pairs are grouped through an open-addressing hash table keyed by the unordered pair
+// (min, max); per slot: the event count and the largest event index. The event that is its pair's
+// last one, with an odd count, emits the change in both directions, at its place in event order
+// (flags -> scan -> emit), so the output is deterministic.
+__device__ __forceinline__ uint32_t dx_hash(unsigned long long k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  return (uint32_t)k;
+}
+
+__global__ void __launch_bounds__(kBlock) k_dx_insert(DeltaExportArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.nev) return;
+  const uint2 e = a.ev[i];
+  const uint32_t m = e.x, o = e.y & 0x7FFFFFFFu;
+  const unsigned long long key = (unsigned long long)min(m, o) << 32 | max(m, o);
+  uint32_t h = dx_hash(key) & a.mask;
+  for (;;) {  // the table has at least 2 x nev slots: a free one is always found
+    const unsigned long long prev = atomicCAS(&a.keys[h], ~0ull, key);
+    if (prev == ~0ull || prev == key) break;
+    h = (h + 1) & a.mask;
+  }
+  atomicAdd(&a.cnt[h], 1u);
+  atomicMax(&a.last[h], i);
+  a.slot_of[i] = h;
+}
+
+__global__ void __launch_bounds__(kBlock) k_dx_flag(DeltaExportArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i == 0) a.flags[a.nev] = 0u;  // the scan's total
+  if (i >= a.nev) return;
+  const uint32_t h = a.slot_of[i];
+  a.flags[i] = ((a.cnt[h] & 1u) && a.last[h] == i) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(kBlock) k_dx_emit(DeltaExportArgs a) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.nev) return;
+  const uint32_t p = a.flags[i];
+  if (a.flags[i + 1] == p) return;  // not kept (flags scanned: kept iff the offset steps)
+  const uint2 e = a.ev[i];
+  const uint32_t m = e.x, o = e.y & 0x7FFFFFFFu, sg = e.y & 0x80000000u;
+  a.out[2 * p] = make_uint2(m, o | sg);
+  a.out[2 * p + 1] = make_uint2(o, m | sg);
+}
+
+void launch_delta_export(const DeltaExportArgs& a, ScanCtx& sc, hipStream_t st) {
+  const uint32_t nb = (a.nev + kBlock - 1) / kBlock;
+  if (!nb) return;
+  hipLaunchKernelGGL(k_dx_insert, dim3(nb), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(k_dx_flag, dim3(nb), dim3(kBlock), 0, st, a);
+  launch_scan(sc, a.flags, a.nev + 1, st);
+  hipLaunchKernelGGL(k_dx_emit, dim3(nb), dim3(kBlock), 0, st, a);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Workload generator (bench/test tooling), bit-identical to include/gwaoi_workload.h on the host.
 __global__ void __launch_bounds__(kBlock) k_wl_init(float* x, float* z, uint32_t n, uint64_t seed, float L) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;

@@ -216,6 +216,15 @@ struct gwaoi_mgr {
   float4* h_pin_ext = nullptr;
   bool pin_seen_dirty = true;
 
+  // relation delta export (gwaoi_export_relation_delta): the last tick's events are still in ev_out
+  bool dx_ready = false;         // set by gwaoi_tick, cleared when the next accumulation opens
+  bool dx_silent = false;        // that tick applied SILENT ops (their pairs are not in the events)
+  uint64_t dx_events = 0;
+  unsigned long long* dx_keys = nullptr;
+  uint32_t *dx_cnt = nullptr, *dx_last = nullptr, *dx_slot = nullptr, *dx_flags = nullptr, *dx_part = nullptr;
+  uint2* dx_out = nullptr;
+  uint64_t dx_slots = 0, dx_cap = 0;  // hash slots; events the per-event buffers hold
+
   // timing
   bool timing = false;
   hipEvent_t tev[5] = {};
@@ -556,6 +565,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   if (!m->acc_open) {
     reset_tick(m);
     m->acc_open = true;
+    m->dx_ready = false;  // ev_out is about to be overwritten
     m->acc_base = m->passes_run;
     m->acc_silent = false;
   }
@@ -818,7 +828,8 @@ void free_all(gwaoi_mgr* m) {
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out,
                    m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
-                   m->d_pin_seen, m->d_pin_ext};
+                   m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
+                   m->dx_part, m->dx_out};
   for (void* p : dptrs)
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
@@ -1435,6 +1446,9 @@ int gwaoi_tick_ex(gwaoi_mgr* m, uint32_t flags, gwaoi_events* out) {
   if (r) return r;
   if (!m->acc_open) reset_tick(m);  // nothing ran since the last tick
   m->acc_open = false;
+  m->dx_ready = true;
+  m->dx_silent = m->acc_silent;
+  m->dx_events = m->tick_events;
   if (out) {
     out->events = copy ? m->h_ev : (const gwaoi_event*)m->ev_out;
     out->count = m->tick_events;
@@ -1702,6 +1716,83 @@ int gwaoi_export_relation(gwaoi_mgr* m, uint32_t* row_ptr, uint32_t* cols, uint6
   if (e != hipSuccess) {
     set_err("export_relation: %s", hipGetErrorString(e));
     return GWAOI_ERR_HIP;
+  }
+  return GWAOI_OK;
+}
+
+int gwaoi_export_relation_delta(gwaoi_mgr* m, gwaoi_event* out, uint64_t cap, uint64_t* n) {
+  RCHK(check_mgr(m));
+  if (!n || (cap && !out)) {
+    set_err("export_relation_delta: null argument");
+    return GWAOI_ERR_INVALID;
+  }
+  *n = 0;
+  if (!m->dx_ready) {
+    set_err("export_relation_delta: no tick to export (call it after gwaoi_tick, before the next pass runs)");
+    return GWAOI_ERR_STATE;
+  }
+  if (m->dx_silent) {
+    set_err("export_relation_delta: the tick applied SILENT ops, whose pairs are not in its events");
+    return GWAOI_ERR_STATE;
+  }
+  const uint64_t nev = m->dx_events;
+  if (!nev) return GWAOI_OK;
+  if (nev > 0x7FFFFFFFull) {
+    set_err("export_relation_delta: %llu events exceed the export's uint32 indices", (unsigned long long)nev);
+    return GWAOI_ERR_NOMEM;
+  }
+  RCHK(set_dev(m));
+  hipStream_t st = m->stream;
+  uint64_t slots = 1024;
+  while (slots < 2 * nev) slots <<= 1;
+  if (slots > m->dx_slots) {
+    for (void* p : {(void*)m->dx_keys, (void*)m->dx_cnt, (void*)m->dx_last})
+      if (p) hipFree(p);
+    m->dx_keys = nullptr, m->dx_cnt = m->dx_last = nullptr, m->dx_slots = 0;
+    RCHK(dalloc(&m->dx_keys, slots));
+    RCHK(dalloc(&m->dx_cnt, slots));
+    RCHK(dalloc(&m->dx_last, slots));
+    m->dx_slots = slots;
+  }
+  if (nev > m->dx_cap) {
+    for (void* p : {(void*)m->dx_slot, (void*)m->dx_flags, (void*)m->dx_out, (void*)m->dx_part})
+      if (p) hipFree(p);
+    m->dx_slot = m->dx_flags = m->dx_part = nullptr, m->dx_out = nullptr, m->dx_cap = 0;
+    const uint64_t want = nev + nev / 4 + 1024;
+    RCHK(dalloc(&m->dx_slot, want));
+    RCHK(dalloc(&m->dx_flags, want + 1));
+    RCHK(dalloc(&m->dx_out, 2 * want));
+    RCHK(dalloc(&m->dx_part, gw::scan_part_words((uint32_t)want + 1)));
+    m->dx_cap = want;
+  }
+  HIPCHK(hipMemsetAsync(m->dx_keys, 0xFF, slots * sizeof(unsigned long long), st));
+  HIPCHK(hipMemsetAsync(m->dx_cnt, 0, slots * sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(m->dx_last, 0, slots * sizeof(uint32_t), st));
+  gw::DeltaExportArgs a;
+  a.ev = m->ev_out;
+  a.nev = (uint32_t)nev;
+  a.mask = (uint32_t)(slots - 1);
+  a.keys = m->dx_keys;
+  a.cnt = m->dx_cnt;
+  a.last = m->dx_last;
+  a.slot_of = m->dx_slot;
+  a.flags = m->dx_flags;
+  a.out = m->dx_out;
+  gw::ScanCtx sc;
+  sc.status = m->dx_part;
+  gw::launch_delta_export(a, sc, st);
+  HIPCHK(hipGetLastError());
+  uint32_t kept = 0;
+  HIPCHK(hipMemcpyAsync(&kept, m->dx_flags + nev, sizeof kept, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  *n = 2ull * kept;
+  if (*n > cap) {
+    set_err("export_relation_delta: cap %llu < %llu changes", (unsigned long long)cap, (unsigned long long)*n);
+    return GWAOI_ERR_INVALID;
+  }
+  if (*n) {
+    HIPCHK(hipMemcpyAsync(out, m->dx_out, *n * sizeof(gwaoi_event), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
   }
   return GWAOI_OK;
 }

@@ -179,6 +179,21 @@ class Engine:
                 continue
             check(rc)
 
+    def relation_delta(self, cap: int = 0) -> np.ndarray:
+        """Net relation changes of the last tick (gwaoi_export_relation_delta): (n, 2) uint32 rows
+        {row, col | GWAOI_EV_ENTER (joined) or col (left)}."""
+        n = ctypes.c_uint64(0)
+        cap = max(cap, 1024)
+        while True:
+            out = np.empty((cap, 2), dtype=np.uint32)
+            rc = self._L.gwaoi_export_relation_delta(self._h, out.ctypes.data, cap, ctypes.byref(n))
+            if rc == _lib.GWAOI_OK:
+                return out[: n.value]
+            if rc == _lib.GWAOI_ERR_INVALID and n.value > cap:
+                cap = int(n.value)
+                continue
+            check(rc)
+
     def relation_device(self):
         """Device-resident CSR view of the relation: (row_ptr device address, cols device address, nnz),
         manager-owned, valid until the next pass (gwaoi_relation_device)."""

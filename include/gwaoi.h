@@ -173,6 +173,18 @@ int gwaoi_count(const gwaoi_mgr* mgr, uint32_t* n_present, uint32_t* n_staged);
 int gwaoi_export_relation(gwaoi_mgr* mgr, uint32_t* row_ptr, uint32_t* cols, uint64_t cols_cap,
                           uint64_t* nnz);
 
+/* The relation's NET changes over the last gwaoi_tick, for a consumer that keeps its own copy of the
+ * sets (Entity.InterestedIn / InterestedBy, Entity.go:53-54, read at Entity.go:1241 and
+ * examples/unity_demo/Monster.go:50,79,89) and patches it instead of re-exporting the whole relation
+ * or replaying every event into maps. One entry per changed pair and direction: {mover = row,
+ * other = col | GWAOI_EV_ENTER} when col joined row's set, {row, col} when it left. Pairs that entered
+ * and left within the tick are omitted. Entries come in pairs (row a col b, then row b col a), in the
+ * order of each pair's last event. Cost O(events): computed on the GPU from the tick's events (still
+ * in HBM), copied into `out` (host, `cap` entries). Call after gwaoi_tick and before the next call
+ * that runs a pass (else GWAOI_ERR_STATE), and not after a tick with SILENT ops. If cap is too small,
+ * *n is set and GWAOI_ERR_INVALID returned. (ABI 2.) */
+int gwaoi_export_relation_delta(gwaoi_mgr* mgr, gwaoi_event* out, uint64_t cap, uint64_t* n);
+
 /* The same relation as a device-resident CSR view (the replay sink's neighbour sets,
  * Entity.InterestedIn / InterestedBy, Entity.go:53-54,236-246, which under the XZ manager are one
  * symmetric set per entity). row_ptr[capacity + 1] and cols[nnz] are HBM buffers owned by the manager

@@ -222,6 +222,37 @@ def test_replay_tool_tracks_the_relation(po):
     rs.close()
 
 
+def test_delta_rows_tool_tracks_the_relation(po):
+    """tools/delta_rows.c (bench.py's relation_delta_apply_ms): per-slot sorted neighbour arrays patched
+    with the net changes of a tick (both directions, as gwaoi_export_relation_delta lists them) equal
+    the relation after the tick; re-applying an entry is reported as inconsistent."""
+    import __graft_entry__ as G
+    G.build_tools()
+    from tools.replay import DeltaRows
+    case = H.case_random_ops(seed=9, n=400, nticks=6, ops_per_tick=300, world=300.0, dist=60.0)
+    orc = po.XZListOracle(60.0, 400)
+    rel = orc.relation()
+    dr = DeltaRows(*rel)
+
+    def keyset(r):
+        rp, cols = r
+        rows = np.repeat(np.arange(len(rp) - 1, dtype=np.uint64), np.diff(rp.astype(np.int64)))
+        return set((rows << np.uint64(32) | cols.astype(np.uint64)).tolist())
+
+    for ops in case["ticks"]:
+        H.oracle_tick(orc, ops)
+        new = orc.relation()
+        a, b = keyset(rel), keyset(new)
+        d = [(k >> 32, (k & 0xFFFFFFFF) | 0x80000000) for k in sorted(b - a)] + \
+            [(k >> 32, k & 0xFFFFFFFF) for k in sorted(a - b)]
+        delta = np.asarray(d, np.uint32).reshape(-1, 2)
+        assert dr.apply(delta) == 0
+        assert dr.diff(*new) == 0
+        rel = new
+    assert dr.apply(delta[:1]) == 1
+    dr.close()
+
+
 def test_config3_cpu_baseline_sample(po):
     """bench.py's config-3 CPU baseline (one oracle (i) manager per Space, a worker
     pool): a bounded sample reports a rate, the threads used and every Space walked the same number of

@@ -39,3 +39,39 @@ class ReplaySets:
         if self._h:
             self._L.rs_destroy(self._h)
             self._h = None
+
+
+_DR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_bin", "libdeltarows.so")
+
+
+class DeltaRows:
+    """ctypes front end of tools/delta_rows.c: per-slot sorted neighbour arrays patched with the
+    entries of gwaoi_export_relation_delta (the Go `Sets` consumer of INTEGRATION.md §2)."""
+
+    def __init__(self, row_ptr: np.ndarray, cols: np.ndarray):
+        L = ctypes.CDLL(_DR)
+        vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
+        L.dr_create.argtypes, L.dr_create.restype = [vp, vp, u32], vp
+        L.dr_destroy.argtypes = [vp]
+        L.dr_apply.argtypes, L.dr_apply.restype = [vp, vp, u64], u64
+        L.dr_diff.argtypes, L.dr_diff.restype = [vp, vp, vp], u64
+        self._L = L
+        rp = np.ascontiguousarray(row_ptr, np.uint32)
+        c = np.ascontiguousarray(cols, np.uint32)
+        self._h = L.dr_create(rp.ctypes.data, c.ctypes.data, len(rp) - 1)
+        if not self._h:
+            raise MemoryError("dr_create")
+
+    def apply(self, delta: np.ndarray) -> int:
+        d = np.ascontiguousarray(delta, np.uint32)
+        return int(self._L.dr_apply(self._h, d.ctypes.data, len(d)))
+
+    def diff(self, row_ptr: np.ndarray, cols: np.ndarray) -> int:
+        rp = np.ascontiguousarray(row_ptr, np.uint32)
+        c = np.ascontiguousarray(cols, np.uint32)
+        return int(self._L.dr_diff(self._h, rp.ctypes.data, c.ctypes.data))
+
+    def close(self):
+        if self._h:
+            self._L.dr_destroy(self._h)
+            self._h = None
