@@ -87,11 +87,17 @@ def cpu_baseline(n, L, dist, seed, target_s):
             "cpu": _cpu_model(), "nproc": os.cpu_count()}
 
 
-def cpu_baseline_spaces(n_per, L, dist, seed0, nspaces, target_s, threads=16):
+def cpu_baseline_spaces(n_per, L, dist, seed0, nspaces, target_s, threads=None):
     """Config 3 on the CPU (one worker per Space, across the cores): oracle (i), one
     XZListAOIManager restatement per Space (C; ctypes drops the GIL), bulk-loaded at tick 0, then `nt`
-    all-moving ticks of Moved() in slot order, Spaces handed to `threads` workers. `nt` is sized from
-    one calibration tick so the pool runs about `target_s`. Rate = updates / wall time of the pool."""
+    all-moving ticks of Moved() in slot order, Spaces handed to `threads` workers (default: every core
+    this process may use, host_cores()). `nt` is sized from one calibration tick so the pool runs about
+    `target_s`. Rate = updates / wall time of the pool; `value_at_nproc` = the rate scaled linearly to the
+    machine's nproc (the Spaces are independent: GOMAXPROCS = nproc, §8(d)), labelled as extrapolated
+    when fewer cores were usable."""
+    usable, nproc = host_cores()
+    if threads is None:  # the process's CPU share (the GPU box sets OMP_NUM_THREADS to it) and usable cores
+        threads = min(usable, int(os.environ.get("OMP_NUM_THREADS", usable) or usable))
     import threading
 
     import numpy as np
@@ -138,12 +144,32 @@ def cpu_baseline_spaces(n_per, L, dist, seed0, nspaces, target_s, threads=16):
         th.join()
     wall = time.perf_counter() - t
     m = nspaces * n_per * nt
+    per_core = m / wall / min(threads, usable)
     return {"value": m / wall, "unit": "entity-updates/s", "cores": threads, "kind": "port",
+            "usable_cores": usable, "nproc": nproc,
+            "value_at_nproc": per_core * nproc,
+            "value_at_nproc_note": "measured" if min(threads, usable) >= nproc else
+            f"linear extrapolation of the {min(threads, usable)}-core rate to nproc={nproc} (independent Spaces, "
+            "one worker per Space); an upper bound for the host",
             "sample": f"oracle (i) go-aoi XZListAOIManager restatement (C), one manager per Space, {threads} worker "
                       f"threads: {nspaces} Spaces x {n_per} (L={L:g}, D={dist:g}, seeds {seed0:#x}+s), each "
                       f"bulk-loaded then {nt} all-moving ticks of Moved(); {m} updates in {wall:.2f}s wall "
                       f"(bulk loads inside the wall time), {state['events']} pair events",
-            "cpu": _cpu_model(), "nproc": os.cpu_count()}
+            "cpu": _cpu_model()}
+
+
+def host_cores():
+    """(usable, nproc): the cores this process may run on (affinity, and the cgroup CPU quota when one is
+    set) and the machine's logical CPU count."""
+    nproc = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            usable = min(usable, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return usable, nproc
 
 
 def _cpu_model():

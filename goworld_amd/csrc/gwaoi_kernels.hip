@@ -328,29 +328,44 @@ void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st) {
 #ifndef GW_BIN_THREADS
 #define GW_BIN_THREADS 1024
 #endif
+// A/B knobs of the build (scripts/variants.py): GW_BIN_XCD = chunks mapped XCD-contiguous (consecutive
+// chunks on one XCD, so the adjacent (tile, chunk) buckets a tile's scatter writes meet in one L2);
+// GW_BIN_RECOUNT = k_bin_tscatter recomputes each record's key and bucket rank (LDS atomics) instead of
+// reading what k_bin_tcount stored (16 B per slot written + read less).
+#ifndef GW_BIN_XCD
+#define GW_BIN_XCD 1
+#endif
+#ifndef GW_BIN_RECOUNT
+#define GW_BIN_RECOUNT 1
+#endif
 constexpr int kBinThreads = GW_BIN_THREADS;  // 16 waves: one block per CU at 1M slots, latency hidden by width
 constexpr int kBinItems = kBinChunk / kBinThreads;
 
-__global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
-  extern __shared__ uint32_t th[];
-  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) th[i] = 0u;
-  __syncthreads();
-  auto body = [&](uint32_t s) {
-    const SlotState t = slot_state(a, s);
-    uint32_t k1 = kNoKey, k0 = kNoKey;
-    if (t.p_end || t.p_start) {
-      const Geom g = a.geom[a.space_of[s]];
-      if (t.p_end) k1 = cell_key_of(g, t.x1, t.z1);
-      if (t.p_start) k0 = cell_key_of(g, t.x0, t.z0);
-      if (k0 == k1) k0 = kNoKey;
-      uint32_t l1 = 0, l0 = 0;
-      if (k1 != kNoKey) l1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
-      if (k0 != kNoKey) l0 = atomicAdd(&th[k0 >> kTileCellShift], 1u);
-      reinterpret_cast<uint2*>(a.local_of)[s] = make_uint2(l1, l0);
-    }
-    reinterpret_cast<uint2*>(a.key_of)[s] = make_uint2(k1, k0);
-  };
-  const uint32_t s0 = blockIdx.x * a.chunk;
+// the chunk a block takes: XCD x (block b runs on XCD b % 8) takes a contiguous run of chunks
+__device__ __forceinline__ uint32_t bin_chunk_of(uint32_t b, uint32_t nblk) {
+#if GW_BIN_XCD
+  const uint32_t x = b % 8u, per = nblk / 8u, rem = nblk % 8u;
+  return x * per + min(x, rem) + b / 8u;
+#else
+  (void)nblk;
+  return b;
+#endif
+}
+
+// keys of slot s's main (k1) and ghost (k0) records, kNoKey for none
+__device__ __forceinline__ void bin_keys(const BinArgs& a, uint32_t s, const SlotState& t, uint32_t& k1, uint32_t& k0) {
+  k1 = kNoKey, k0 = kNoKey;
+  if (t.p_end || t.p_start) {
+    const Geom g = a.geom[a.space_of[s]];
+    if (t.p_end) k1 = cell_key_of(g, t.x1, t.z1);
+    if (t.p_start) k0 = cell_key_of(g, t.x0, t.z0);
+    if (k0 == k1) k0 = kNoKey;
+  }
+}
+
+template <class Body>
+__device__ __forceinline__ void bin_chunk_loop(const BinArgs& a, uint32_t c, Body&& body) {
+  const uint32_t s0 = c * a.chunk;
   if (a.chunk == kBinChunk) {  // the common size: unrolled, every item's loads in flight together
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
@@ -362,41 +377,64 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
     const uint32_t s1 = min(s0 + a.chunk, a.cap);
     for (uint32_t s = s0 + threadIdx.x; s < s1; s += kBinThreads) body(s);
   }
+}
+
+__global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
+  extern __shared__ uint32_t th[];
+  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) th[i] = 0u;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) a.thist[i * a.nblk + blockIdx.x] = th[i];
+  const uint32_t c = bin_chunk_of(blockIdx.x, a.nblk);
+  bin_chunk_loop(a, c, [&](uint32_t s) {
+    const SlotState t = slot_state(a, s);
+    uint32_t k1, k0;
+    bin_keys(a, s, t, k1, k0);
+    uint32_t l1 = 0, l0 = 0;
+    if (k1 != kNoKey) l1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
+    if (k0 != kNoKey) l0 = atomicAdd(&th[k0 >> kTileCellShift], 1u);
+#if !GW_BIN_RECOUNT
+    if (k1 != kNoKey || k0 != kNoKey) reinterpret_cast<uint2*>(a.local_of)[s] = make_uint2(l1, l0);
+    reinterpret_cast<uint2*>(a.key_of)[s] = make_uint2(k1, k0);
+#else
+    (void)l1, (void)l0;
+#endif
+  });
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) a.thist[i * a.nblk + c] = th[i];
   if (blockIdx.x == 0 && threadIdx.x == 0) a.thist[a.ntiles * a.nblk] = 0u;  // the scan's total slot
 }
 
 __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
-  auto body = [&](uint32_t s) {
+  const uint32_t c = bin_chunk_of(blockIdx.x, a.nblk);
+#if GW_BIN_RECOUNT
+  // the bucket offsets of this chunk in LDS, advanced by one LDS atomic per record (ranks inside a
+  // (tile, chunk) bucket are free: k_bin_tsort orders records by cell, not by rank)
+  extern __shared__ uint32_t th[];
+  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) th[i] = a.thist[i * a.nblk + c];
+  __syncthreads();
+#endif
+  bin_chunk_loop(a, c, [&](uint32_t s) {
+    const SlotState t = slot_state(a, s);
+#if GW_BIN_RECOUNT
+    uint32_t k1, k0;
+    bin_keys(a, s, t, k1, k0);
+    if (k1 == kNoKey && k0 == kNoKey) return;
+    uint32_t j1 = 0, j0 = 0;
+    if (k1 != kNoKey) j1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
+    if (k0 != kNoKey) j0 = atomicAdd(&th[k0 >> kTileCellShift], 1u);
+#else
     const uint2 kk = reinterpret_cast<const uint2*>(a.key_of)[s];
     const uint32_t k1 = kk.x, k0 = kk.y;
     if (k1 == kNoKey && k0 == kNoKey) return;
     const uint2 ll = reinterpret_cast<const uint2*>(a.local_of)[s];
-    const SlotState t = slot_state(a, s);
+    const uint32_t j1 = a.thist[(k1 >> kTileCellShift) * a.nblk + c] + ll.x;
+    const uint32_t j0 = a.thist[(k0 >> kTileCellShift) * a.nblk + c] + ll.y;
+#endif
     const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
-    if (k1 != kNoKey) {
-      const uint32_t j = a.thist[(k1 >> kTileCellShift) * a.nblk + blockIdx.x] + ll.x;
-      a.trec[j] = Rec{make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq),
-                      rb};
-    }
-    if (k0 != kNoKey) {
-      const uint32_t j = a.thist[(k0 >> kTileCellShift) * a.nblk + blockIdx.x] + ll.y;
-      a.trec[j] = Rec{make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq), rb};
-    }
-  };
-  const uint32_t s0 = blockIdx.x * a.chunk;
-  if (a.chunk == kBinChunk) {
-#pragma unroll
-    for (int k = 0; k < kBinItems; ++k) {
-      const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
-      if (s >= a.cap) break;
-      body(s);
-    }
-  } else {
-    const uint32_t s1 = min(s0 + a.chunk, a.cap);
-    for (uint32_t s = s0 + threadIdx.x; s < s1; s += kBinThreads) body(s);
-  }
+    if (k1 != kNoKey)
+      a.trec[j1] = Rec{make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq),
+                       rb};
+    if (k0 != kNoKey) a.trec[j0] = Rec{make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq), rb};
+  });
 }
 
 // Tiles of up to 4 * kBlock records (all of config 2's) keep their records in registers between the
@@ -427,6 +465,133 @@ __device__ __forceinline__ uint32_t tile_cell(const TileMap& m, float x, float z
 __device__ __forceinline__ bool bin_walker(const BinArgs& a, const uint4 ra) {
   const uint32_t r = ra.w - a.base;
   return !(ra.z & REC_GHOST) && r < a.n_ops && !(a.op_kind && (a.op_kind[r] & OP_SILENT));
+}
+
+// ---- refined cells (gwaoi_internal.h "Refined cells") ----
+__device__ __forceinline__ uint4 ld_cg4(const uint4* p) {  // bypass the CU cache: written by this block
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+  return make_uint4(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                    __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ __forceinline__ uint32_t refine_k(uint32_t n) {
+  uint32_t k = 2;
+  while (k < 8 && (float)(k * k) * 1.5f < (float)n) ++k;  // k = ceil(sqrt(n / 1.5)) in [2, 8]
+  return k;
+}
+
+// sub-cell coordinate of v inside cell c (fraction of the cell times k, floored): monotone in v; for a
+// record of the cell in [0, k]. The same function bounds the sweep's sub-cell ranges (exactness).
+__device__ __forceinline__ int sub_coord(float v, float o, float inv, int c, uint32_t k) {
+  const float f = ((v - o) * inv - (float)c) * (float)k;
+  if (!(f > -2.0f)) return -2;
+  if (!(f < (float)k + 2.0f)) return (int)k + 2;
+  return (int)floorf(f);
+}
+
+// After k_bin_tsort placed a tile's records by cell: cells of kRefineMin..kRefineMax records (not on the
+// grid's edge) get their records sorted by sub-cell, a sub table in the pool and an entry in the tile's
+// cell table. cso: this thread's 4 cell starts; cnt: the cells' ends (LDS).
+__device__ void refine_tile(const BinArgs& a, uint32_t t, const uint4 cso, const uint32_t* cnt) {
+  __shared__ uint4 rlist[kTileCells];  // refined cells: {start, n, k, sub table offset}
+  __shared__ uint32_t rinfo[3];        // [0] list length, [1] pool offset (~0: none), [2] block sum
+  const Geom* gp = &a.geom[a.tile_space[t]];
+  const float gx0 = gp->x0, gz0 = gp->z0, inv = gp->inv_c;
+  const int ncx = gp->ncx, ncz = gp->ncz, ntx = gp->ntx;
+  const uint32_t tl = t - gp->tile_base;
+  const int tz = (int)(tl / (uint32_t)ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)ntx);
+  __syncthreads();  // every placement atomic done: cnt[] holds the cell ends
+  const uint32_t st[4] = {cso.x, cso.y, cso.z, cso.w};
+  uint32_t need[4], sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = threadIdx.x * 4 + i;
+    const int cx = tx * kTile + (c & (kTile - 1)), cz = tz * kTile + (c >> kTileShift);
+    const uint32_t n = cnt[c] - st[i];
+    const bool ok = n >= kRefineMin && n <= kRefineMax && cx > 0 && cx < ncx - 1 && cz > 0 && cz < ncz - 1;
+    const uint32_t k = ok ? refine_k(n) : 0u;
+    need[i] = ok ? (k + 1) * (k + 1) + 2 : 0u;
+    sum += need[i];
+  }
+  if (!__syncthreads_or(sum != 0u)) {  // no crowded cell (a uniform crowd's tiles): one barrier
+    if (threadIdx.x == 0) a.tref[t] = 0u;
+    return;
+  }
+  uint32_t tot;
+  uint32_t pre = block_excl_scan(sum, &tot);
+  if (threadIdx.x == 0) {
+    uint32_t off = ~0u;
+    if (tot) {
+      off = atomicAdd(&a.ctr[CTR_RPOOL], kTileCells + tot);
+      if ((uint64_t)off + kTileCells + tot > a.rpool_cap) off = ~0u;  // pool full: this tile stays coarse
+    }
+    rinfo[0] = 0;
+    rinfo[1] = off;
+    a.tref[t] = off == ~0u ? 0u : off + 1u;
+  }
+  __syncthreads();
+  const uint32_t off = rinfo[1];
+  if (off == ~0u) return;  // block-uniform
+  uint32_t o = off + kTileCells + pre;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = threadIdx.x * 4 + i;
+    uint32_t w = 0;
+    if (need[i]) {
+      const uint32_t n = cnt[c] - st[i], k = refine_k(n);
+      w = k << 28 | o;
+      rlist[atomicAdd(&rinfo[0], 1u)] = make_uint4(st[i], n, k, o);
+      o += need[i];
+    }
+    a.rpool[off + c] = w;
+  }
+  __threadfence();  // the placed records (global) visible to every wave of the block
+  __syncthreads();
+  const uint32_t nl = rinfo[0];
+  if (threadIdx.x == 0 && nl) atomicAdd(&a.ctr[CTR_REFINED], nl);
+  const int lane = threadIdx.x & 63;
+  for (uint32_t li = threadIdx.x >> 6; li < nl; li += kBlock / 64) {
+    const uint4 L = rlist[li];
+    const uint32_t c0 = L.x, n = L.y, k = L.z, so = L.w;
+    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
+    uint32_t key = 0xFFFFFFFFu;
+    float d = 0.0f;
+    if ((uint32_t)lane < n) {
+      ra = ld_cg4(&a.rec[c0 + lane].a);
+      rb = ld_cg4(&a.rec[c0 + lane].b);
+      const float x = __uint_as_float(ra.x), z = __uint_as_float(ra.y);
+      // the record's cell (the same cellc as its binning; not on the grid edge, so not clamped)
+      const int cx = cellc(x, gx0, inv, ncx), cz = cellc(z, gz0, inv, ncz);
+      const int sx = sub_coord(x, gx0, inv, cx, k), sz = sub_coord(z, gz0, inv, cz, k);
+      key = (uint32_t)sz * (k + 1) + (uint32_t)sx;
+      // judged at its start too: a main record without a ghost that was present at the start
+      if (!(ra.z & (REC_GHOST | REC_HASG)) && rb.z != 0u)
+        d = fmaxf(fabsf(__uint_as_float(rb.x) - x), fabsf(__uint_as_float(rb.y) - z));
+    }
+    uint32_t pos = 0;  // rank by (sub-cell, lane): stable counting over the wave
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t kj = __shfl(key, (int)j, 64);
+      pos += (kj < key || (kj == key && j < (uint32_t)lane)) ? 1u : 0u;
+    }
+    if ((uint32_t)lane < n) {
+      a.rec[c0 + pos].a = ra;
+      a.rec[c0 + pos].b = rb;
+    }
+    for (int sh = 32; sh > 0; sh >>= 1) d = fmaxf(d, __shfl_xor(d, sh, 64));
+    const uint32_t ns = (k + 1) * (k + 1);
+    uint32_t mine = 0;  // lane l keeps the start of sub-cells l and l + 64 (wave-uniform loop, ballots)
+    uint32_t mine2 = 0;
+    for (uint32_t sidx = 0; sidx <= ns; ++sidx) {
+      const uint32_t below = c0 + (uint32_t)__popcll(__ballot(key < sidx));  // keys of empty lanes are ~0
+      if ((uint32_t)lane == sidx) mine = below;
+      if ((uint32_t)lane + 64u == sidx) mine2 = below;
+    }
+    if ((uint32_t)lane <= ns) a.rpool[so + 1 + lane] = mine;
+    if ((uint32_t)lane + 64u <= ns) a.rpool[so + 1 + 64 + lane] = mine2;
+    if (lane == 0) a.rpool[so] = __float_as_uint(d);
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
@@ -510,13 +675,15 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
       o->a = ra, o->b = rb;
     }
   }
+  if (a.refine) refine_tile(a, t, cso, cnt);  // block-uniform
 }
 
 void launch_bin_tiles(const BinArgs& a, ScanCtx& sc, hipStream_t st) {
   if (!a.ntiles) return;
   hipLaunchKernelGGL(k_bin_tcount, dim3(a.nblk), dim3(kBinThreads), a.ntiles * sizeof(uint32_t), st, a);
   launch_scan(sc, a.thist, a.ntiles * a.nblk + 1, st);
-  hipLaunchKernelGGL(k_bin_tscatter, dim3(a.nblk), dim3(kBinThreads), 0, st, a);
+  hipLaunchKernelGGL(k_bin_tscatter, dim3(a.nblk), dim3(kBinThreads), GW_BIN_RECOUNT ? a.ntiles * sizeof(uint32_t) : 0,
+                     st, a);
   hipLaunchKernelGGL(k_bin_tsort, dim3(a.ntiles), dim3(kBlock), 0, st, a);
 }
 
@@ -891,6 +1058,9 @@ __device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const 
   return true;
 }
 
+#ifndef GW_JUDGE_UNROLL
+#define GW_JUDGE_UNROLL 2  // A/B: 4 = four candidates per iteration
+#endif
 // Judge candidates b..b+63 of one stream (idx(k) = LDS record index of candidate k): the hot loop
 // only records which candidates raise an event and of which kind (bit k - b of two per-lane masks).
 // No atomic, branch or LDS write sits in the candidate loop itself. (32-candidate chunks with 32-bit
@@ -902,6 +1072,19 @@ __device__ __forceinline__ void judge_chunk(const SweepSmem& sm, const Judge& J,
   hit = 0;
   ent = 0;
   uint32_t k = 0;
+#if GW_JUDGE_UNROLL >= 4
+  for (; k + 3 < n; k += 4) {  // four candidates per iteration: four LDS record reads in flight
+    const uint32_t j0 = idx(b + k), j1 = idx(b + k + 1), j2 = idx(b + k + 2), j3 = idx(b + k + 3);
+    const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1], p2 = sm.rp[j2], p3 = sm.rp[j3];
+    const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1], q2 = sm.rm[j2], q3 = sm.rm[j3];
+    const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1), e2 = judge_lds(J, p2, q2),
+              e3 = judge_lds(J, p3, q3);
+    hit |= ((unsigned long long)(e0 != 0) << k) | ((unsigned long long)(e1 != 0) << (k + 1)) |
+           ((unsigned long long)(e2 != 0) << (k + 2)) | ((unsigned long long)(e3 != 0) << (k + 3));
+    ent |= ((unsigned long long)(e0 == 2) << k) | ((unsigned long long)(e1 == 2) << (k + 1)) |
+           ((unsigned long long)(e2 == 2) << (k + 2)) | ((unsigned long long)(e3 == 2) << (k + 3));
+  }
+#endif
   for (; k + 1 < n; k += 2) {  // two candidates per iteration: both LDS reads in flight
     const uint32_t j0 = idx(b + k), j1 = idx(b + k + 1);
     const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
@@ -1506,8 +1689,120 @@ constexpr int kDenseGrid = 256 * GW_DENSE_WPE;  // GW_DENSE_WPE waves per SIMD: 
 constexpr uint32_t kEvChunk = GW_EV_CHUNK;  // event slots a wave reserves at a time (one returning atomic
                                       // on the shared counter each: ~11 ns apiece when serialised)
 
-__global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_DENSE_WPE)))
+// The float bounds a dense mover's walk needs inside a refined cell (gwaoi_internal.h "Refined cells"):
+// U = the union of its boxes with qbox's rounding margin (a record binned farther than the cell's
+// maxdisp outside U is outside both boxes from every perspective), I = the ring's inner box of
+// make_walk (a record binned deeper than maxdisp inside I is inside both; empty for row walks).
+struct SubBounds {
+  float ux0, ux1, uz0, uz1;
+  float ix0, ix1, iz0, iz1;
+  bool inner;
+};
+
+__device__ __forceinline__ SubBounds sub_bounds(const Mover& m, const Walk& w) {
+  SubBounds b;
+  const float D = m.D;
+  auto lo = [&](float c) { return (c - D) - (fabsf(c) + D) * kMargin; };
+  auto hi = [&](float c) { return (c + D) + (fabsf(c) + D) * kMargin; };
+  if (m.valid0 && m.valid1) {
+    b.ux0 = fminf(lo(m.mx0), lo(m.mx1)), b.ux1 = fmaxf(hi(m.mx0), hi(m.mx1));
+    b.uz0 = fminf(lo(m.mz0), lo(m.mz1)), b.uz1 = fmaxf(hi(m.mz0), hi(m.mz1));
+  } else {
+    const float cx = m.valid1 ? m.mx1 : m.mx0, cz = m.valid1 ? m.mz1 : m.mz0;
+    b.ux0 = lo(cx), b.ux1 = hi(cx), b.uz0 = lo(cz), b.uz1 = hi(cz);
+  }
+  b.inner = w.ring;
+  if (w.ring) {  // make_walk's inner box (cells strictly inside it are skipped by the coarse walk too)
+    const float ex = (fmaxf(fabsf(m.mx0), fabsf(m.mx1)) + D) * kInner;
+    const float ez = (fmaxf(fabsf(m.mz0), fabsf(m.mz1)) + D) * kInner;
+    b.ix0 = (fmaxf(m.mx0, m.mx1) - D) + ex, b.ix1 = (fminf(m.mx0, m.mx1) + D) - ex;
+    b.iz0 = (fmaxf(m.mz0, m.mz1) - D) + ez, b.iz1 = (fminf(m.mz0, m.mz1) + D) - ez;
+  } else {
+    b.ix0 = b.ix1 = b.iz0 = b.iz1 = 0.0f;
+  }
+  return b;
+}
+
+// The record ranges of one part (row `r`, columns [c0, c1] of one tile, first key pk) of a dense walk,
+// in order, through f(start, end): a coarse tile (tr = 0) is one range; in a refined tile, runs of
+// coarse cells are one range each and a refined cell gives, per sub-row its ring crosses, the sub-cell
+// columns its ring crosses (two pieces where the sub-row is inside the inner box). ONLY_COUNT: no
+// record-start loads.
+template <bool ONLY_COUNT, class F>
+__device__ __forceinline__ void part_ranges(const SweepArgs& a, const Geom& g, const SubBounds& B, int r, int c0,
+                                            int c1, uint32_t pk, uint32_t tr, F&& f) {
+  if (!tr) {
+    if (ONLY_COUNT) f(0u, 0u);
+    else f(a.g.cs[pk], a.g.cs[pk + (uint32_t)(c1 - c0) + 1]);
+    return;
+  }
+  const uint32_t* ct = a.rpool + (tr - 1) + ((uint32_t)(r & (kTile - 1)) << kTileShift);
+  int run = -1;  // first cell of the current run of coarse cells
+  for (int c = c0; c <= c1 + 1; ++c) {
+    const uint32_t w = c <= c1 ? ct[c & (kTile - 1)] : 0xFFFFFFFFu;
+    if (w == 0u) {  // a coarse cell: extend the run
+      if (run < 0) run = c;
+      continue;
+    }
+    if (run >= 0) {  // close the run [run, c)
+      if (ONLY_COUNT) f(0u, 0u);
+      else f(a.g.cs[pk + (uint32_t)(run - c0)], a.g.cs[pk + (uint32_t)(c - c0)]);
+      run = -1;
+    }
+    if (c > c1) break;
+    const uint32_t k = w >> 28, so = w & 0x0FFFFFFFu, kk = k + 1;
+    const float md = __uint_as_float(a.rpool[so]);
+    // maxdisp plus a margin above the float rounding of the bounds below
+    const float mg = md + (fabsf(B.ux0) + fabsf(B.ux1) + fabsf(B.uz0) + fabsf(B.uz1) + md + 1.0f) * 9.5367431640625e-07f;
+    const int ax = max(0, sub_coord(B.ux0 - mg, g.x0, g.inv_c, c, k)), bx = min((int)k, sub_coord(B.ux1 + mg, g.x0, g.inv_c, c, k));
+    const int az = max(0, sub_coord(B.uz0 - mg, g.z0, g.inv_c, r, k)), bz = min((int)k, sub_coord(B.uz1 + mg, g.z0, g.inv_c, r, k));
+    int ix0 = 0, ix1 = 0, iz0 = 0, iz1 = 0;
+    bool cols = false;  // inner sub-columns exist: (ix0, ix1) exclusive
+    if (B.inner) {
+      ix0 = sub_coord(B.ix0 + mg, g.x0, g.inv_c, c, k), ix1 = sub_coord(B.ix1 - mg, g.x0, g.inv_c, c, k);
+      iz0 = sub_coord(B.iz0 + mg, g.z0, g.inv_c, r, k), iz1 = sub_coord(B.iz1 - mg, g.z0, g.inv_c, r, k);
+      cols = ix0 + 1 <= ix1 - 1;
+    }
+    for (int j = az; j <= bz && ax <= bx; ++j) {
+      const uint32_t rowb = so + 1 + (uint32_t)j * kk;
+      if (cols && j > iz0 && j < iz1) {  // inside the inner rows: the pieces left and right of the inner columns
+        const int l1 = min(bx, ix0), r0 = max(ax, ix1);
+        if (ax <= l1) {
+          if (ONLY_COUNT) f(0u, 0u);
+          else f(a.rpool[rowb + ax], a.rpool[rowb + l1 + 1]);
+        }
+        if (r0 <= bx) {
+          if (ONLY_COUNT) f(0u, 0u);
+          else f(a.rpool[rowb + r0], a.rpool[rowb + bx + 1]);
+        }
+      } else {
+        if (ONLY_COUNT) f(0u, 0u);
+        else f(a.rpool[rowb + ax], a.rpool[rowb + bx + 1]);
+      }
+    }
+  }
+}
+
+constexpr uint32_t kDenseQ = 512;  // ranges a wave queues per round (refined batches)
+
+// does the walk's cell box reach a tile with refined cells? (wave-uniform: scalar loads of tref)
+__device__ __forceinline__ bool walk_refined(const SweepArgs& a, const Geom& g, const Walk& w) {
+  if (!a.tref) return false;
+  const int x0 = w.ring ? w.ax0 : min(w.ax0, w.bx0), x1 = w.ring ? w.ax1 : max(w.ax1, w.bx1);
+  for (int tz = w.z0 >> kTileShift; tz <= (w.z1 >> kTileShift); ++tz)
+    for (int tx = x0 >> kTileShift; tx <= (x1 >> kTileShift); ++tx)
+      if (a.tref[g.tile_base + (uint32_t)(tz * g.ntx + tx)]) return true;
+  return false;
+}
+
+// CROWD = false: the dense movers whose walk meets no refined tile (coarse parts: one range each);
+// CROWD = true: the others, every part through the range queue (part_ranges). Two kernels over one
+// list, so each keeps its own register budget.
+template <bool CROWD>
+__global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(CROWD ? 4 : GW_DENSE_WPE)))
 k_sweep_dense(SweepArgs a) {
+  __shared__ uint2 rq_all[CROWD ? kDenseBlock / 64 : 1][CROWD ? kDenseQ : 1];  // {record start, inclusive prefix}
+  uint2* rq = rq_all[CROWD ? threadIdx.x >> 6 : 0];
   const int lane = threadIdx.x & 63;
   const uint32_t wave = (blockIdx.x * kDenseBlock + threadIdx.x) >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
   const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
@@ -1518,6 +1813,8 @@ k_sweep_dense(SweepArgs a) {
     const Geom g = a.g.geom[a.space_of[a.dense[d]]];
     const Mover m = slot_mover(a, a.dense[d], g.D);
     const Judge J = make_judge(m, a.base);
+    const Walk w = make_walk(m, g);
+    if (walk_refined(a, g, w) != CROWD) continue;  // wave-uniform: the other kernel takes it
     uint32_t local = 0;      // wave-uniform
     uint32_t pk = 0, pe = 0;  // this lane's cell-key range [pk, pe) (one tile part of one row segment)
     int np = 0;               // parts collected (wave-uniform)
@@ -1582,9 +1879,72 @@ k_sweep_dense(SweepArgs a) {
       }
       np = 0;
     };
+    // refined tiles in the batch: each lane's part as a list of ranges (part_ranges), queued in the
+    // wave's LDS in rounds of kDenseQ, the candidates of a round judged 64 at a time (a candidate's range
+    // by binary search over the queue's prefixes)
+    int pr = 0, pc0 = 0, pc1 = 0;  // this lane's part: row, first and last column
+    uint32_t ptr = 0;             // its tile's refinement word (tref)
+    auto flush_ref = [&]() {
+      const SubBounds SB = sub_bounds(m, w);  // (here, not live across the walk: registers)
+      uint32_t nr = 0;
+      if (lane < np) part_ranges<true>(a, g, SB, pr, pc0, pc1, pk, ptr, [&](uint32_t, uint32_t) { ++nr; });
+      const uint32_t rincl = wave_incl_scan(nr);
+      const uint32_t roff = rincl - nr;
+      const uint32_t R = __builtin_amdgcn_readlane(rincl, 63);
+      for (uint32_t R0 = 0; R0 < R; R0 += kDenseQ) {
+        if (lane < np && roff < R0 + kDenseQ && roff + nr > R0) {
+          uint32_t gi = roff;
+          part_ranges<false>(a, g, SB, pr, pc0, pc1, pk, ptr, [&](uint32_t st, uint32_t en) {
+            if (gi >= R0 && gi < R0 + kDenseQ) rq[gi - R0] = make_uint2(st, en - st);
+            ++gi;
+          });
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t nq = min(kDenseQ, R - R0);
+        uint32_t carry = 0;  // inclusive prefix of the lengths, in place of them
+        for (uint32_t q0 = 0; q0 < nq; q0 += 64) {
+          const uint32_t q = q0 + (uint32_t)lane;
+          const uint32_t len = q < nq ? rq[q].y : 0u;
+          const uint32_t inc = wave_incl_scan(len) + carry;
+          if (q < nq) rq[q].y = inc;
+          carry = __builtin_amdgcn_readlane(inc, 63);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t total = carry;
+        auto locate = [&](uint32_t k) -> uint32_t {  // record of candidate k: first range whose prefix > k
+          uint32_t lo = 0, hi = nq - 1;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (rq[mid].y > k) hi = mid;
+            else lo = mid + 1;
+          }
+          return rq[lo].x + (k - (lo ? rq[lo - 1].y : 0u));
+        };
+        for (uint32_t b = 0; b < total; b += 128) {
+          const uint32_t kA = b + lane, kB = b + 64 + lane;
+          const bool hasB = b + 64 < total;  // wave-uniform
+          uint4 aA = make_uint4(0, 0, 0, 0), bA = aA, aB = aA, bB = aA;
+          if (kA < total) {
+            const uint32_t jA = locate(kA);
+            aA = a.g.rec[jA].a, bA = a.g.rec[jA].b;
+          }
+          if (hasB && kB < total) {
+            const uint32_t jB = locate(kB);
+            aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
+          }
+          emit_round(kA < total ? judge(J, aA, bA) : 0, aA.z & REC_SLOT);
+          if (hasB) emit_round(kB < total ? judge(J, aB, bB) : 0, aB.z & REC_SLOT);
+        }
+        __builtin_amdgcn_wave_barrier();  // the queue is rewritten by the next round
+      }
+      np = 0;
+    };
     // the walk, lane-parallel: lane = (row, segment) of 32 rows at a time; each segment splits into
     // one part per tile it touches; part p is pulled by lane p % 64 (binary search over the prefix)
-    const Walk w = make_walk(m, g);
     const int h = w.z1 - w.z0 + 1;
     for (int rb = 0; rb < h; rb += 32) {
       const int r = w.z0 + rb + (lane >> 1);
@@ -1612,7 +1972,10 @@ k_sweep_dense(SweepArgs a) {
              (uint32_t)(plo & (kTile - 1));
         pe = pk + (uint32_t)(phi - plo) + 1;
         np = (int)min(64u, T - pb);
-        flush();
+        pr = sr, pc0 = plo, pc1 = phi;
+        ptr = (CROWD && lane < np) ? a.tref[pk >> kTileCellShift] : 0u;
+        if (CROWD) flush_ref();
+        else flush();
       }
     }
     if (lane == 0 && local) a.rank_cnt[m.rank] = local;
@@ -1637,7 +2000,10 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
   // the dense list's length is on the device: a fixed grid that exits at once when it is empty (a
   // small one when the previous pass had none; the kernel is grid-stride, any grid is correct)
   if (a.dense)
-    hipLaunchKernelGGL(k_sweep_dense, dim3(a.dense_hint ? kDenseGrid : 64), dim3(kDenseBlock), 0, st, a);
+    hipLaunchKernelGGL(k_sweep_dense<false>, dim3(a.dense_hint ? kDenseGrid : 64), dim3(kDenseBlock), 0, st, a);
+  if (a.dense && a.tref)  // movers whose walks meet refined (crowded) cells
+    hipLaunchKernelGGL(k_sweep_dense<true>, dim3(a.dense_hint && a.refined_hint ? kDenseGrid : 64), dim3(kDenseBlock),
+                       0, st, a);
 }
 
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each

@@ -93,6 +93,10 @@ struct Grid {  // one pass's cell-sorted records (two buffers, alternating betwe
   uint32_t* cs = nullptr;
   gw::Geom* d_geom = nullptr;
   uint32_t* d_tile_space = nullptr;  // tile -> space
+  uint32_t* tref = nullptr;          // refined cells (crowds): per tile 0 or 1 + pool offset (k_bin_tsort)
+  uint32_t* rpool = nullptr;         // refinement pool (gwaoi_internal.h "Refined cells")
+  uint32_t rpool_cap = 0;
+  bool refined = false;              // built with refinement: tref/rpool describe this grid
   std::vector<gw::Geom> h_geom;  // what d_geom holds
   uint32_t ncells = 0;
   uint32_t ntiles = 0;
@@ -169,6 +173,7 @@ struct gwaoi_mgr {
   uint32_t next_seq = 1;
   uint32_t* rank_cnt = nullptr;  // [cap + 1]
   int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
+  int refine = 1;                // crowded cells refined in the tile-bucketed build (gwaoi_debug_set_refine)
   uint32_t* part = nullptr;     // scan chunk sums
   uint32_t part_words = 0;
   gw::ScanCtx scan;
@@ -183,9 +188,10 @@ struct gwaoi_mgr {
   uint32_t* d_pub = nullptr;     // its device address
   uint32_t pub_seq = 0;
   uint32_t last_dense = ~0u;     // dense movers of the last pass (k_sweep_dense grid size hint)
+  uint32_t last_refined = ~0u;   // refined cells of the last pass (k_sweep_dense<true> grid size hint)
   struct {                       // the last timed pass, collected once its events are complete
     bool pending = false;
-    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0;
+    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0, refined = 0;
   } tpend;
   // events
   uint4* ev_tmp = nullptr;
@@ -461,6 +467,12 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_
   b.trec = m->grid[gi ^ 1].rec;  // the other grid's records are not read by this pass
   b.op_kind = op_kind;
   b.tile_walk = m->tile_walk;
+  b.refine = tiles && m->refine && g.rpool ? 1 : 0;
+  b.tref = g.tref;
+  b.rpool = g.rpool;
+  b.rpool_cap = g.rpool_cap;
+  b.ctr = m->ctr;
+  g.refined = b.refine != 0;
   if (tiles) {
     gw::launch_bin_tiles(b, m->scan, m->stream);
   } else {
@@ -520,6 +532,7 @@ int collect_timing(gwaoi_mgr* m) {
   m->stats.grid_records += m->tpend.records;
   m->stats.grid_cells += m->tpend.ncells;
   m->stats.dense_movers += m->tpend.dense;
+  m->stats.refined_cells += m->tpend.refined;
   return GWAOI_OK;
 }
 
@@ -669,6 +682,9 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.dense_cap = m->cap;
     s.dense_hint = attempt ? ~0u : m->last_dense;
     s.tile_walk = tile_build(G) ? m->tile_walk : nullptr;
+    s.tref = G.refined ? G.tref : nullptr;
+    s.rpool = G.rpool;
+    s.refined_hint = attempt ? ~0u : m->last_refined;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
@@ -721,6 +737,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       m->tpend.records = m->h_ctr[gw::CTR_RECORDS];
       m->tpend.ncells = m->grid[ng].ncells;
       m->tpend.dense = m->h_ctr[gw::CTR_DENSE];
+      m->tpend.refined = m->h_ctr[gw::CTR_REFINED];
     }
     break;
   }
@@ -739,6 +756,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->pass_id++;
   if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
   m->last_dense = m->h_ctr[gw::CTR_DENSE];
+  m->last_refined = m->h_ctr[gw::CTR_REFINED];
   m->n_present_dev = m->n_present;
   m->dv_kind = nullptr;
   m->dv_space = nullptr;
@@ -834,7 +852,7 @@ void free_all(gwaoi_mgr* m) {
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
-    void* gp[] = {g.rec, g.cs, g.d_geom, g.d_tile_space};
+    void* gp[] = {g.rec, g.cs, g.d_geom, g.d_tile_space, g.tref, g.rpool};
     for (void* p : gp)
       if (p) hipFree(p);
   }
@@ -955,6 +973,11 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     chk(dalloc(&g.cs, (size_t)m->max_cells + 1));
     chk(dalloc(&g.d_geom, nspaces));
     chk(dalloc(&g.d_tile_space, (size_t)m->max_cells / gw::kTileCells + 1));
+    chk(dalloc(&g.tref, (size_t)m->max_cells / gw::kTileCells + 1));
+    // a refined cell holds >= kRefineMin records and takes <= 83 words, a refined tile 1024 more: room
+    // for every record of a crowd at ~3 words each (a tile that does not fit stays coarse: slower only)
+    g.rpool_cap = (uint32_t)std::min<uint64_t>(1ull << 28, 3ull * C + (1u << 20));
+    chk(dalloc(&g.rpool, g.rpool_cap));
   }
   static bool sweep_ready = false;
   if (!sweep_ready) {
@@ -1917,6 +1940,12 @@ int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
     return GWAOI_ERR_INVALID;
   }
   m->next_seq = next_seq;
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_refine(gwaoi_mgr* m, int enable) {
+  if (!m) return GWAOI_ERR_INVALID;
+  m->refine = enable != 0;
   return GWAOI_OK;
 }
 

@@ -78,7 +78,7 @@ def test_delta_walk_and_states(gpu, oracle_lib):
         d = eng.relation_delta()
         after = pairs(eng.relation())  # (runs no pass: the tick's events stay exportable)
         check_delta(d, before, after, f"walk tick {t}")
-        assert len(d) == 2 * len(ev)  # one move per slot: no pair changes twice
+        assert 0 < len(d) <= 2 * len(ev)  # both members moving: a leave then an enter can cancel
         assert np.array_equal(eng.relation_delta(), d)  # repeatable until the next pass
         before = after
     eng.moved(0, float(x[0]) + 1.0, float(z[0]))
