@@ -173,7 +173,8 @@ struct gwaoi_mgr {
   uint32_t next_seq = 1;
   uint32_t* rank_cnt = nullptr;  // [cap + 1]
   int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
-  int refine = 1;                // crowded cells refined in the tile-bucketed build (gwaoi_debug_set_refine)
+  int refine = 0;                // crowded cells refined in the tile-bucketed build (gwaoi_debug_set_refine;
+                                 // off by default: the sub-cell walk measured slower)
   uint32_t* part = nullptr;     // scan chunk sums
   uint32_t part_words = 0;
   gw::ScanCtx scan;
