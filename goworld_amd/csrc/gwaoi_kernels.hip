@@ -338,8 +338,34 @@ void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st) {
 #ifndef GW_BIN_RECOUNT
 #define GW_BIN_RECOUNT 1
 #endif
+// GW_BIN_TATOM = bucket offsets without the scan over tiles x chunks: each chunk's count of a tile is
+// added to the tile's total by one returning atomic (its return value = the bucket's offset inside the
+// tile; any order of a tile's buckets will do, k_bin_tsort orders by cell), then one small kernel
+// scans the tile totals into tile starts.
+#ifndef GW_BIN_TATOM
+#define GW_BIN_TATOM 1
+#endif
 constexpr int kBinThreads = GW_BIN_THREADS;  // 16 waves: one block per CU at 1M slots, latency hidden by width
 constexpr int kBinItems = kBinChunk / kBinThreads;
+
+// first record of tile t (t = ntiles: the record total)
+__device__ __forceinline__ uint32_t bin_tile_start(const BinArgs& a, uint32_t t) {
+#if GW_BIN_TATOM
+  return a.tstart[t];
+#else
+  return a.thist[t * a.nblk];
+#endif
+}
+
+// first record of chunk c's bucket of tile t: with GW_BIN_TATOM thist holds the bucket's offset inside
+// its tile, else (scanned) its absolute offset
+__device__ __forceinline__ uint32_t bin_bucket(const BinArgs& a, uint32_t t, uint32_t c) {
+#if GW_BIN_TATOM
+  return a.tstart[t] + a.thist[t * a.nblk + c];
+#else
+  return a.thist[t * a.nblk + c];
+#endif
+}
 
 // the chunk a block takes: XCD x (block b runs on XCD b % 8) takes a contiguous run of chunks
 __device__ __forceinline__ uint32_t bin_chunk_of(uint32_t b, uint32_t nblk) {
@@ -399,8 +425,13 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
 #endif
   });
   __syncthreads();
+#if GW_BIN_TATOM
+  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads)
+    if (th[i]) a.thist[i * a.nblk + c] = atomicAdd(&a.ttot[i], th[i]);
+#else
   for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) a.thist[i * a.nblk + c] = th[i];
   if (blockIdx.x == 0 && threadIdx.x == 0) a.thist[a.ntiles * a.nblk] = 0u;  // the scan's total slot
+#endif
 }
 
 __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
@@ -409,7 +440,8 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
   // the bucket offsets of this chunk in LDS, advanced by one LDS atomic per record (ranks inside a
   // (tile, chunk) bucket are free: k_bin_tsort orders records by cell, not by rank)
   extern __shared__ uint32_t th[];
-  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) th[i] = a.thist[i * a.nblk + c];
+  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads)
+    th[i] = bin_bucket(a, i, c);  // (stale for tiles this chunk has no record of)
   __syncthreads();
 #endif
   bin_chunk_loop(a, c, [&](uint32_t s) {
@@ -426,8 +458,8 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
     const uint32_t k1 = kk.x, k0 = kk.y;
     if (k1 == kNoKey && k0 == kNoKey) return;
     const uint2 ll = reinterpret_cast<const uint2*>(a.local_of)[s];
-    const uint32_t j1 = a.thist[(k1 >> kTileCellShift) * a.nblk + c] + ll.x;
-    const uint32_t j0 = a.thist[(k0 >> kTileCellShift) * a.nblk + c] + ll.y;
+    const uint32_t j1 = k1 != kNoKey ? bin_bucket(a, k1 >> kTileCellShift, c) + ll.x : 0u;
+    const uint32_t j0 = k0 != kNoKey ? bin_bucket(a, k0 >> kTileCellShift, c) + ll.y : 0u;
 #endif
     const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
     if (k1 != kNoKey)
@@ -468,14 +500,6 @@ __device__ __forceinline__ bool bin_walker(const BinArgs& a, const uint4 ra) {
 }
 
 // ---- refined cells (gwaoi_internal.h "Refined cells") ----
-__device__ __forceinline__ uint4 ld_cg4(const uint4* p) {  // bypass the CU cache: written by this block
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
-  return make_uint4(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                    __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                    __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                    __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
 __device__ __forceinline__ uint32_t refine_k(uint32_t n) {
   uint32_t k = 2;
   while (k < 8 && (float)(k * k) * 1.5f < (float)n) ++k;  // k = ceil(sqrt(n / 1.5)) in [2, 8]
@@ -492,11 +516,11 @@ __device__ __forceinline__ int sub_coord(float v, float o, float inv, int c, uin
 }
 
 // After k_bin_tsort placed a tile's records by cell: cells of kRefineMin..kRefineMax records (not on the
-// grid's edge) get their records sorted by sub-cell, a sub table in the pool and an entry in the tile's
-// cell table. cso: this thread's 4 cell starts; cnt: the cells' ends (LDS).
+// grid's edge) get an entry in the tile's cell table, a sub table and room for their z-ordered copies in
+// the pools, and a work item for k_refine (which sorts them). The pools are sized so that no
+// reservation can fail (runtime: refine_pools). cso: this thread's 4 cell starts; cnt: the cell ends.
 __device__ void refine_tile(const BinArgs& a, uint32_t t, const uint4 cso, const uint32_t* cnt) {
-  __shared__ uint4 rlist[kTileCells];  // refined cells: {start, n, k, sub table offset}
-  __shared__ uint32_t rinfo[3];        // [0] list length, [1] pool offset (~0: none), [2] block sum
+  __shared__ uint32_t rinfo[3];  // [0] z copy offset, [1] pool offset, [2] work list offset
   const Geom* gp = &a.geom[a.tile_space[t]];
   const float gx0 = gp->x0, gz0 = gp->z0, inv = gp->inv_c;
   const int ncx = gp->ncx, ncz = gp->ncz, ntx = gp->ntx;
@@ -512,7 +536,7 @@ __device__ void refine_tile(const BinArgs& a, uint32_t t, const uint4 cso, const
     const uint32_t n = cnt[c] - st[i];
     const bool ok = n >= kRefineMin && n <= kRefineMax && cx > 0 && cx < ncx - 1 && cz > 0 && cz < ncz - 1;
     const uint32_t k = ok ? refine_k(n) : 0u;
-    need[i] = ok ? (k + 1) * (k + 1) + 2 : 0u;
+    need[i] = ok ? 2 * (k + 2) + 1 : 0u;
     sum += need[i];
   }
   if (!__syncthreads_or(sum != 0u)) {  // no crowded cell (a uniform crowd's tiles): one barrier
@@ -527,7 +551,6 @@ __device__ void refine_tile(const BinArgs& a, uint32_t t, const uint4 cso, const
       off = atomicAdd(&a.ctr[CTR_RPOOL], kTileCells + tot);
       if ((uint64_t)off + kTileCells + tot > a.rpool_cap) off = ~0u;  // pool full: this tile stays coarse
     }
-    rinfo[0] = 0;
     rinfo[1] = off;
     a.tref[t] = off == ~0u ? 0u : off + 1u;
   }
@@ -535,6 +558,28 @@ __device__ void refine_tile(const BinArgs& a, uint32_t t, const uint4 cso, const
   const uint32_t off = rinfo[1];
   if (off == ~0u) return;  // block-uniform
   uint32_t o = off + kTileCells + pre;
+  // the records' z-ordered copies and the work list (k_refine sorts the cells, one wave each)
+  uint32_t nrec = 0, ncell = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (need[i]) nrec += cnt[threadIdx.x * 4 + i] - st[i], ++ncell;
+  uint32_t totr, totc;
+  uint32_t prer = block_excl_scan(nrec, &totr);
+  uint32_t prec = block_excl_scan(ncell, &totc);
+  if (threadIdx.x == 0) {
+    uint32_t zo = atomicAdd(&a.ctr[CTR_ZREC], totr), lo = atomicAdd(&a.ctr[CTR_REFINED], totc);
+    if ((uint64_t)zo + totr > a.zrec_cap || (uint64_t)lo + totc > a.rlist_cap) zo = lo = ~0u;
+    rinfo[0] = zo;
+    rinfo[2] = lo;
+  }
+  __syncthreads();
+  const uint32_t zo = rinfo[0], lo = rinfo[2];
+  if (zo == ~0u) {  // no room for the copies: this tile stays coarse (block-uniform)
+    if (threadIdx.x == 0) a.tref[t] = 0u;
+    return;
+  }
+  prer += zo;
+  prec += lo;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = threadIdx.x * 4 + i;
@@ -542,63 +587,73 @@ __device__ void refine_tile(const BinArgs& a, uint32_t t, const uint4 cso, const
     if (need[i]) {
       const uint32_t n = cnt[c] - st[i], k = refine_k(n);
       w = k << 28 | o;
-      rlist[atomicAdd(&rinfo[0], 1u)] = make_uint4(st[i], n, k, o);
+      a.rlist[prec++] = make_uint4(st[i], n, o, prer);
+      prer += n;
       o += need[i];
     }
     a.rpool[off + c] = w;
   }
-  __threadfence();  // the placed records (global) visible to every wave of the block
-  __syncthreads();
-  const uint32_t nl = rinfo[0];
-  if (threadIdx.x == 0 && nl) atomicAdd(&a.ctr[CTR_REFINED], nl);
+}
+
+// One wave per refined cell (the list k_bin_tsort wrote): the cell's records sorted by sub-column in
+// place (rec) and by sub-row into the z copy (zrec), with the sub-column / sub-row starts and maxdisp
+// in the cell's sub table {maxdisp, xs[k + 2], zs[k + 2]}. Ranks by one ballot per sub-index value.
+__global__ void __launch_bounds__(kBlock) k_refine(BinArgs a) {
   const int lane = threadIdx.x & 63;
-  for (uint32_t li = threadIdx.x >> 6; li < nl; li += kBlock / 64) {
-    const uint4 L = rlist[li];
-    const uint32_t c0 = L.x, n = L.y, k = L.z, so = L.w;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const uint32_t nl = min(a.ctr[CTR_REFINED], a.rlist_cap);
+  for (uint32_t li = (blockIdx.x * kBlock + threadIdx.x) >> 6; li < nl; li += gridDim.x * (kBlock / 64)) {
+    const uint4 L = a.rlist[li];
+    const uint32_t c0 = L.x, n = L.y, so = L.z, zo = L.w, k = refine_k(n);
+    const bool on = (uint32_t)lane < n;
     uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
-    uint32_t key = 0xFFFFFFFFu;
+    int sx = -1, sz = -1;
     float d = 0.0f;
-    if ((uint32_t)lane < n) {
-      ra = ld_cg4(&a.rec[c0 + lane].a);
-      rb = ld_cg4(&a.rec[c0 + lane].b);
+    if (on) {
+      ra = a.rec[c0 + lane].a;
+      rb = a.rec[c0 + lane].b;
       const float x = __uint_as_float(ra.x), z = __uint_as_float(ra.y);
-      // the record's cell (the same cellc as its binning; not on the grid edge, so not clamped)
-      const int cx = cellc(x, gx0, inv, ncx), cz = cellc(z, gz0, inv, ncz);
-      const int sx = sub_coord(x, gx0, inv, cx, k), sz = sub_coord(z, gz0, inv, cz, k);
-      key = (uint32_t)sz * (k + 1) + (uint32_t)sx;
-      // judged at its start too: a main record without a ghost that was present at the start
-      if (!(ra.z & (REC_GHOST | REC_HASG)) && rb.z != 0u)
+      const Geom* gp = &a.geom[a.space_of[ra.z & REC_SLOT]];
+      const float gx0 = gp->x0, gz0 = gp->z0, inv = gp->inv_c;
+      const int cx = cellc(x, gx0, inv, gp->ncx), cz = cellc(z, gz0, inv, gp->ncz);  // not an edge cell: exact
+      sx = sub_coord(x, gx0, inv, cx, k);
+      sz = sub_coord(z, gz0, inv, cz, k);
+      if (!(ra.z & (REC_GHOST | REC_HASG)) && rb.z != 0u)  // may be judged at its start too
         d = fmaxf(fabsf(__uint_as_float(rb.x) - x), fabsf(__uint_as_float(rb.y) - z));
     }
-    uint32_t pos = 0;  // rank by (sub-cell, lane): stable counting over the wave
-    for (uint32_t j = 0; j < n; ++j) {
-      const uint32_t kj = __shfl(key, (int)j, 64);
-      pos += (kj < key || (kj == key && j < (uint32_t)lane)) ? 1u : 0u;
+    uint32_t px = 0, pz = 0, bx = 0, bz = 0, xs = c0 + n, zs = zo + n;
+    for (int v = 0; v <= (int)k; ++v) {  // wave-uniform
+      const unsigned long long mx = __ballot(sx == v), mz = __ballot(sz == v);
+      if (sx == v) px = bx + (uint32_t)__popcll(mx & below);
+      if (sz == v) pz = bz + (uint32_t)__popcll(mz & below);
+      if (lane == v) xs = c0 + bx, zs = zo + bz;
+      bx += (uint32_t)__popcll(mx);
+      bz += (uint32_t)__popcll(mz);
     }
-    if ((uint32_t)lane < n) {
-      a.rec[c0 + pos].a = ra;
-      a.rec[c0 + pos].b = rb;
+    if (on) {
+      a.rec[c0 + px].a = ra;  // every lane's loads were consumed above: in-place is safe
+      a.rec[c0 + px].b = rb;
+      a.zrec[zo + pz].a = ra;
+      a.zrec[zo + pz].b = rb;
     }
     for (int sh = 32; sh > 0; sh >>= 1) d = fmaxf(d, __shfl_xor(d, sh, 64));
-    const uint32_t ns = (k + 1) * (k + 1);
-    uint32_t mine = 0;  // lane l keeps the start of sub-cells l and l + 64 (wave-uniform loop, ballots)
-    uint32_t mine2 = 0;
-    for (uint32_t sidx = 0; sidx <= ns; ++sidx) {
-      const uint32_t below = c0 + (uint32_t)__popcll(__ballot(key < sidx));  // keys of empty lanes are ~0
-      if ((uint32_t)lane == sidx) mine = below;
-      if ((uint32_t)lane + 64u == sidx) mine2 = below;
-    }
-    if ((uint32_t)lane <= ns) a.rpool[so + 1 + lane] = mine;
-    if ((uint32_t)lane + 64u <= ns) a.rpool[so + 1 + 64 + lane] = mine2;
     if (lane == 0) a.rpool[so] = __float_as_uint(d);
+    if ((uint32_t)lane <= k + 1) {  // lane k + 1 kept the ends
+      a.rpool[so + 1 + lane] = xs;
+      a.rpool[so + 1 + (k + 2) + lane] = zs;
+    }
   }
+}
+
+void launch_refine(const BinArgs& a, hipStream_t st) {
+  if (a.refine) hipLaunchKernelGGL(k_refine, dim3(512), dim3(kBlock), 0, st, a);
 }
 
 __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   __shared__ uint32_t cnt[kTileCells];
   __shared__ uint32_t ws[kBlock / 64];
   const uint32_t t = blockIdx.x;
-  const uint32_t b = a.thist[t * a.nblk], e = a.thist[(t + 1) * a.nblk];
+  const uint32_t b = bin_tile_start(a, t), e = bin_tile_start(a, t + 1);
   for (int c = threadIdx.x; c < kTileCells; c += kBlock) cnt[c] = 0u;
   const TileMap g = tile_map(&a.geom[a.tile_space[t]]);
   const bool small = e - b <= 4u * kBlock;
@@ -678,10 +733,47 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   if (a.refine) refine_tile(a, t, cso, cnt);  // block-uniform
 }
 
+// tile starts = exclusive scan of the tile totals (tstart[n] = total); the totals are zeroed for the
+// next build. One block: n <= kMaxLdsTiles (12,288), 12 per thread.
+__global__ void __launch_bounds__(1024) k_tile_scan(uint32_t* ttot, uint32_t* tstart, uint32_t n) {
+  __shared__ uint32_t ws[16];
+  constexpr uint32_t kPer = (kMaxLdsTiles + 1023) / 1024;
+  const uint32_t b0 = threadIdx.x * kPer;
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    v[k] = b0 + k < n ? ttot[b0 + k] : 0u;
+    sum += v[k];
+  }
+  const uint32_t inc = wave_incl_scan(sum);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t pre = inc - sum, tot = 0;
+  for (int k = 0; k < 16; ++k) {
+    pre += k < w ? ws[k] : 0u;
+    tot += ws[k];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    if (b0 + k < n) {
+      tstart[b0 + k] = pre;
+      ttot[b0 + k] = 0u;
+    }
+    pre += v[k];
+  }
+  if (threadIdx.x == 0) tstart[n] = tot;
+}
+
 void launch_bin_tiles(const BinArgs& a, ScanCtx& sc, hipStream_t st) {
   if (!a.ntiles) return;
   hipLaunchKernelGGL(k_bin_tcount, dim3(a.nblk), dim3(kBinThreads), a.ntiles * sizeof(uint32_t), st, a);
+#if GW_BIN_TATOM
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, st, a.ttot, a.tstart, a.ntiles);
+  (void)sc;
+#else
   launch_scan(sc, a.thist, a.ntiles * a.nblk + 1, st);
+#endif
   hipLaunchKernelGGL(k_bin_tscatter, dim3(a.nblk), dim3(kBinThreads), GW_BIN_RECOUNT ? a.ntiles * sizeof(uint32_t) : 0,
                      st, a);
   hipLaunchKernelGGL(k_bin_tsort, dim3(a.ntiles), dim3(kBlock), 0, st, a);
@@ -1723,86 +1815,63 @@ __device__ __forceinline__ SubBounds sub_bounds(const Mover& m, const Walk& w) {
   return b;
 }
 
-// The record ranges of one part (row `r`, columns [c0, c1] of one tile, first key pk) of a dense walk,
-// in order, through f(start, end): a coarse tile (tr = 0) is one range; in a refined tile, runs of
-// coarse cells are one range each and a refined cell gives, per sub-row its ring crosses, the sub-cell
-// columns its ring crosses (two pieces where the sub-row is inside the inner box). ONLY_COUNT: no
-// record-start loads.
-template <bool ONLY_COUNT, class F>
-__device__ __forceinline__ void part_ranges(const SweepArgs& a, const Geom& g, const SubBounds& B, int r, int c0,
-                                            int c1, uint32_t pk, uint32_t tr, F&& f) {
-  if (!tr) {
-    if (ONLY_COUNT) f(0u, 0u);
-    else f(a.g.cs[pk], a.g.cs[pk + (uint32_t)(c1 - c0) + 1]);
+// The one record range a crowd walk reads of cell (r, c) of a refined tile (cell table word w != 0:
+// k << 28 | sub table offset): for a ring walk, a cell in a top/bottom ring row and inside the inner
+// columns reads the sub-rows of its horizontal band (from the z copy), a cell of an inner row (left or
+// right piece) the sub-columns of its vertical band; corners and row walks read the whole cell. Every
+// record left out is binned deeper than maxdisp inside the inner box or outside the union box (sub
+// indices by the monotone sub_coord on both sides): no event is lost.
+__device__ __forceinline__ void cell_band(const SweepArgs& a, const Geom& g, const Walk& w, const SubBounds& B, int r,
+                                          int c, uint32_t key, uint32_t wd, uint32_t& rs, uint32_t& rl, bool& zsrc) {
+  zsrc = false;
+  const bool ring = w.ring && w.bz0 <= w.bz1 && w.bx0 <= w.bx1;
+  const bool erow = r < w.bz0 || r > w.bz1, ecol = c < w.bx0 || c > w.bx1;
+  if (!ring || (erow && ecol)) {
+    rs = a.g.cs[key];
+    rl = a.g.cs[key + 1] - rs;
     return;
   }
-  const uint32_t* ct = a.rpool + (tr - 1) + ((uint32_t)(r & (kTile - 1)) << kTileShift);
-  int run = -1;  // first cell of the current run of coarse cells
-  for (int c = c0; c <= c1 + 1; ++c) {
-    const uint32_t w = c <= c1 ? ct[c & (kTile - 1)] : 0xFFFFFFFFu;
-    if (w == 0u) {  // a coarse cell: extend the run
-      if (run < 0) run = c;
-      continue;
-    }
-    if (run >= 0) {  // close the run [run, c)
-      if (ONLY_COUNT) f(0u, 0u);
-      else f(a.g.cs[pk + (uint32_t)(run - c0)], a.g.cs[pk + (uint32_t)(c - c0)]);
-      run = -1;
-    }
-    if (c > c1) break;
-    const uint32_t k = w >> 28, so = w & 0x0FFFFFFFu, kk = k + 1;
-    const float md = __uint_as_float(a.rpool[so]);
-    // maxdisp plus a margin above the float rounding of the bounds below
-    const float mg = md + (fabsf(B.ux0) + fabsf(B.ux1) + fabsf(B.uz0) + fabsf(B.uz1) + md + 1.0f) * 9.5367431640625e-07f;
-    const int ax = max(0, sub_coord(B.ux0 - mg, g.x0, g.inv_c, c, k)), bx = min((int)k, sub_coord(B.ux1 + mg, g.x0, g.inv_c, c, k));
-    const int az = max(0, sub_coord(B.uz0 - mg, g.z0, g.inv_c, r, k)), bz = min((int)k, sub_coord(B.uz1 + mg, g.z0, g.inv_c, r, k));
-    int ix0 = 0, ix1 = 0, iz0 = 0, iz1 = 0;
-    bool cols = false;  // inner sub-columns exist: (ix0, ix1) exclusive
-    if (B.inner) {
-      ix0 = sub_coord(B.ix0 + mg, g.x0, g.inv_c, c, k), ix1 = sub_coord(B.ix1 - mg, g.x0, g.inv_c, c, k);
-      iz0 = sub_coord(B.iz0 + mg, g.z0, g.inv_c, r, k), iz1 = sub_coord(B.iz1 - mg, g.z0, g.inv_c, r, k);
-      cols = ix0 + 1 <= ix1 - 1;
-    }
-    for (int j = az; j <= bz && ax <= bx; ++j) {
-      const uint32_t rowb = so + 1 + (uint32_t)j * kk;
-      if (cols && j > iz0 && j < iz1) {  // inside the inner rows: the pieces left and right of the inner columns
-        const int l1 = min(bx, ix0), r0 = max(ax, ix1);
-        if (ax <= l1) {
-          if (ONLY_COUNT) f(0u, 0u);
-          else f(a.rpool[rowb + ax], a.rpool[rowb + l1 + 1]);
-        }
-        if (r0 <= bx) {
-          if (ONLY_COUNT) f(0u, 0u);
-          else f(a.rpool[rowb + r0], a.rpool[rowb + bx + 1]);
-        }
-      } else {
-        if (ONLY_COUNT) f(0u, 0u);
-        else f(a.rpool[rowb + ax], a.rpool[rowb + bx + 1]);
-      }
-    }
+  const uint32_t k = wd >> 28, so = wd & 0x0FFFFFFFu;
+  const float md = __uint_as_float(a.rpool[so]);
+  const float mg = md + (fabsf(B.ux0) + fabsf(B.ux1) + fabsf(B.uz0) + fabsf(B.uz1) + md + 1.0f) * 9.5367431640625e-07f;
+  int lo, hi;
+  if (erow) {  // horizontal band: sub-rows between the union's edge and the inner box's
+    if (r < w.bz0) lo = sub_coord(B.uz0 - mg, g.z0, g.inv_c, r, k), hi = sub_coord(B.iz0 + mg, g.z0, g.inv_c, r, k);
+    else lo = sub_coord(B.iz1 - mg, g.z0, g.inv_c, r, k), hi = sub_coord(B.uz1 + mg, g.z0, g.inv_c, r, k);
+    zsrc = true;
+  } else {     // vertical band: sub-columns
+    if (c < w.bx0) lo = sub_coord(B.ux0 - mg, g.x0, g.inv_c, c, k), hi = sub_coord(B.ix0 + mg, g.x0, g.inv_c, c, k);
+    else lo = sub_coord(B.ix1 - mg, g.x0, g.inv_c, c, k), hi = sub_coord(B.ux1 + mg, g.x0, g.inv_c, c, k);
   }
+  lo = max(lo, 0);
+  hi = min(hi, (int)k);
+  const uint32_t* t = a.rpool + so + 1 + (zsrc ? k + 2 : 0u);
+  if (lo > hi) {
+    rs = 0, rl = 0;
+    return;
+  }
+  rs = t[lo];
+  rl = t[hi + 1] - rs;
+  (void)key;
 }
 
-constexpr uint32_t kDenseQ = 512;  // ranges a wave queues per round (refined batches)
 
-// does the walk's cell box reach a tile with refined cells? (wave-uniform: scalar loads of tref)
-__device__ __forceinline__ bool walk_refined(const SweepArgs& a, const Geom& g, const Walk& w) {
+// Is the mover itself in a refined (crowded) cell? Its ring then mostly crosses crowded cells too, and
+// the crowd walk's bands pay; every other dense mover takes the coarse walk, which reads refined cells
+// whole (their records are still one contiguous range per cell). Wave-uniform (scalar loads).
+__device__ __forceinline__ bool mover_crowded(const SweepArgs& a, const Geom& g, const Mover& m) {
   if (!a.tref) return false;
-  const int x0 = w.ring ? w.ax0 : min(w.ax0, w.bx0), x1 = w.ring ? w.ax1 : max(w.ax1, w.bx1);
-  for (int tz = w.z0 >> kTileShift; tz <= (w.z1 >> kTileShift); ++tz)
-    for (int tx = x0 >> kTileShift; tx <= (x1 >> kTileShift); ++tx)
-      if (a.tref[g.tile_base + (uint32_t)(tz * g.ntx + tx)]) return true;
-  return false;
+  const int cx = cellc(m.mx1, g.x0, g.inv_c, g.ncx), cz = cellc(m.mz1, g.z0, g.inv_c, g.ncz);
+  const uint32_t tr = a.tref[g.tile_base + (uint32_t)((cz >> kTileShift) * g.ntx + (cx >> kTileShift))];
+  return tr && a.rpool[(tr - 1) + ((uint32_t)(cz & (kTile - 1)) << kTileShift) + (uint32_t)(cx & (kTile - 1))] != 0u;
 }
 
-// CROWD = false: the dense movers whose walk meets no refined tile (coarse parts: one range each);
-// CROWD = true: the others, every part through the range queue (part_ranges). Two kernels over one
-// list, so each keeps its own register budget.
+// CROWD = false: the dense movers outside crowded cells (coarse parts: one range each); CROWD = true:
+// the movers in crowded cells, whose parts in refined tiles split into units (a run of coarse cells, or
+// one refined cell's band: cell_band). Two kernels over one list, so each keeps its own register budget.
 template <bool CROWD>
 __global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(CROWD ? 4 : GW_DENSE_WPE)))
 k_sweep_dense(SweepArgs a) {
-  __shared__ uint2 rq_all[CROWD ? kDenseBlock / 64 : 1][CROWD ? kDenseQ : 1];  // {record start, inclusive prefix}
-  uint2* rq = rq_all[CROWD ? threadIdx.x >> 6 : 0];
   const int lane = threadIdx.x & 63;
   const uint32_t wave = (blockIdx.x * kDenseBlock + threadIdx.x) >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
   const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
@@ -1814,7 +1883,7 @@ k_sweep_dense(SweepArgs a) {
     const Mover m = slot_mover(a, a.dense[d], g.D);
     const Judge J = make_judge(m, a.base);
     const Walk w = make_walk(m, g);
-    if (walk_refined(a, g, w) != CROWD) continue;  // wave-uniform: the other kernel takes it
+    if (mover_crowded(a, g, m) != CROWD) continue;  // wave-uniform: the other kernel takes it
     uint32_t local = 0;      // wave-uniform
     uint32_t pk = 0, pe = 0;  // this lane's cell-key range [pk, pe) (one tile part of one row segment)
     int np = 0;               // parts collected (wave-uniform)
@@ -1879,67 +1948,106 @@ k_sweep_dense(SweepArgs a) {
       }
       np = 0;
     };
-    // refined tiles in the batch: each lane's part as a list of ranges (part_ranges), queued in the
-    // wave's LDS in rounds of kDenseQ, the candidates of a round judged 64 at a time (a candidate's range
-    // by binary search over the queue's prefixes)
+    // CROWD: a part in a refined tile expands into one unit per cell (cell_band: one range each, from the
+    // grid or from the z copy), 64 units per flush; a coarse tile's part stays one unit
     int pr = 0, pc0 = 0, pc1 = 0;  // this lane's part: row, first and last column
     uint32_t ptr = 0;             // its tile's refinement word (tref)
-    auto flush_ref = [&]() {
-      const SubBounds SB = sub_bounds(m, w);  // (here, not live across the walk: registers)
-      uint32_t nr = 0;
-      if (lane < np) part_ranges<true>(a, g, SB, pr, pc0, pc1, pk, ptr, [&](uint32_t, uint32_t) { ++nr; });
-      const uint32_t rincl = wave_incl_scan(nr);
-      const uint32_t roff = rincl - nr;
-      const uint32_t R = __builtin_amdgcn_readlane(rincl, 63);
-      for (uint32_t R0 = 0; R0 < R; R0 += kDenseQ) {
-        if (lane < np && roff < R0 + kDenseQ && roff + nr > R0) {
-          uint32_t gi = roff;
-          part_ranges<false>(a, g, SB, pr, pc0, pc1, pk, ptr, [&](uint32_t st, uint32_t en) {
-            if (gi >= R0 && gi < R0 + kDenseQ) rq[gi - R0] = make_uint2(st, en - st);
-            ++gi;
-          });
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t nq = min(kDenseQ, R - R0);
-        uint32_t carry = 0;  // inclusive prefix of the lengths, in place of them
-        for (uint32_t q0 = 0; q0 < nq; q0 += 64) {
-          const uint32_t q = q0 + (uint32_t)lane;
-          const uint32_t len = q < nq ? rq[q].y : 0u;
-          const uint32_t inc = wave_incl_scan(len) + carry;
-          if (q < nq) rq[q].y = inc;
-          carry = __builtin_amdgcn_readlane(inc, 63);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t total = carry;
-        auto locate = [&](uint32_t k) -> uint32_t {  // record of candidate k: first range whose prefix > k
-          uint32_t lo = 0, hi = nq - 1;
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (rq[mid].y > k) hi = mid;
-            else lo = mid + 1;
+    auto flush_units = [&]() {
+      const SubBounds SB = sub_bounds(m, w);
+      // units of this lane's part: a coarse tile's part is one; in a refined tile each refined cell and
+      // each maximal run of coarse cells is one
+      const uint32_t* ctab = ptr ? a.rpool + (ptr - 1) + ((uint32_t)(pr & (kTile - 1)) << kTileShift) : a.rpool;
+      uint32_t nu = 0;
+      if (lane < np) {
+        if (!ptr) {
+          nu = 1;
+        } else {
+          bool run = false;
+          for (int c = pc0; c <= pc1; ++c) {
+            const bool fine = ctab[c & (kTile - 1)] != 0u;
+            nu += (fine || !run) ? 1u : 0u;
+            run = !fine;
           }
-          return rq[lo].x + (k - (lo ? rq[lo - 1].y : 0u));
+        }
+      }
+      const uint32_t uincl = wave_incl_scan(nu);
+      const uint32_t U = __builtin_amdgcn_readlane(uincl, 63);
+      for (uint32_t ub = 0; ub < U; ub += 64) {
+        const uint32_t u = ub + lane;
+        int lo = 0, hi = 63;  // the part of unit u
+#pragma unroll
+        for (int st = 0; st < 6; ++st) {
+          const int mid = (lo + hi) >> 1;
+          if (__shfl(uincl, mid, 64) > u) hi = mid;
+          else lo = mid + 1;
+        }
+        const uint32_t q = u - (__shfl(uincl, lo, 64) - __shfl(nu, lo, 64));
+        const int ur = __shfl(pr, lo, 64), uc0 = __shfl(pc0, lo, 64), uc1 = __shfl(pc1, lo, 64);
+        const uint32_t upk = __shfl(pk, lo, 64), utr = __shfl(ptr, lo, 64);
+        uint32_t rs = 0, rl = 0;
+        bool zs = false;
+        if (u < U) {
+          if (!utr) {  // a coarse tile: the part's one range
+            rs = a.g.cs[upk];
+            rl = a.g.cs[upk + (uint32_t)(uc1 - uc0) + 1] - rs;
+          } else {  // find the q-th unit of the part: a refined cell, or a run [c, e) of coarse cells
+            const uint32_t* ut = a.rpool + (utr - 1) + ((uint32_t)(ur & (kTile - 1)) << kTileShift);
+            uint32_t idx = 0;
+            int c = uc0;
+            uint32_t wd = 0;
+            for (;; ) {  // q < units of the part: terminates inside [uc0, uc1]
+              wd = ut[c & (kTile - 1)];
+              if (idx == q) break;
+              if (wd) {
+                ++c;
+              } else {
+                while (c <= uc1 && !ut[c & (kTile - 1)]) ++c;
+              }
+              ++idx;
+            }
+            const uint32_t key = upk + (uint32_t)(c - uc0);
+            if (wd) {
+              cell_band(a, g, w, SB, ur, c, key, wd, rs, rl, zs);
+            } else {
+              int e = c;
+              while (e <= uc1 && !ut[e & (kTile - 1)]) ++e;
+              rs = a.g.cs[key];
+              rl = a.g.cs[key + (uint32_t)(e - c)] - rs;
+            }
+          }
+        }
+        const uint32_t incl = wave_incl_scan(rl);
+        const uint32_t excl = incl - rl;
+        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        auto locate = [&](uint32_t k, bool& z) -> uint32_t {  // record of candidate k, and its array
+          int l2 = 0, h2 = 63;
+#pragma unroll
+          for (int st = 0; st < 6; ++st) {
+            const int mid = (l2 + h2) >> 1;
+            if (__shfl(incl, mid, 64) > k) h2 = mid;
+            else l2 = mid + 1;
+          }
+          z = __shfl((int)zs, l2, 64) != 0;
+          return __shfl(rs, l2, 64) + (k - __shfl(excl, l2, 64));
         };
         for (uint32_t b = 0; b < total; b += 128) {
           const uint32_t kA = b + lane, kB = b + 64 + lane;
           const bool hasB = b + 64 < total;  // wave-uniform
+          bool zA = false, zB = false;
+          const uint32_t jA = locate(kA, zA);
+          const uint32_t jB = hasB ? locate(kB, zB) : 0u;
           uint4 aA = make_uint4(0, 0, 0, 0), bA = aA, aB = aA, bB = aA;
           if (kA < total) {
-            const uint32_t jA = locate(kA);
-            aA = a.g.rec[jA].a, bA = a.g.rec[jA].b;
+            const Rec* R = zA ? a.zrec : a.g.rec;
+            aA = R[jA].a, bA = R[jA].b;
           }
           if (hasB && kB < total) {
-            const uint32_t jB = locate(kB);
-            aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
+            const Rec* R = zB ? a.zrec : a.g.rec;
+            aB = R[jB].a, bB = R[jB].b;
           }
           emit_round(kA < total ? judge(J, aA, bA) : 0, aA.z & REC_SLOT);
           if (hasB) emit_round(kB < total ? judge(J, aB, bB) : 0, aB.z & REC_SLOT);
         }
-        __builtin_amdgcn_wave_barrier();  // the queue is rewritten by the next round
       }
       np = 0;
     };
@@ -1974,7 +2082,7 @@ k_sweep_dense(SweepArgs a) {
         np = (int)min(64u, T - pb);
         pr = sr, pc0 = plo, pc1 = phi;
         ptr = (CROWD && lane < np) ? a.tref[pk >> kTileCellShift] : 0u;
-        if (CROWD) flush_ref();
+        if (CROWD) flush_units();
         else flush();
       }
     }

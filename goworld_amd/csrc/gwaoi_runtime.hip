@@ -96,6 +96,10 @@ struct Grid {  // one pass's cell-sorted records (two buffers, alternating betwe
   uint32_t* tref = nullptr;          // refined cells (crowds): per tile 0 or 1 + pool offset (k_bin_tsort)
   uint32_t* rpool = nullptr;         // refinement pool (gwaoi_internal.h "Refined cells")
   uint32_t rpool_cap = 0;
+  gw::Rec* zrec = nullptr;           // refined cells' records sorted by sub-row
+  uint32_t zrec_cap = 0;
+  uint4* rlist = nullptr;            // k_refine's work list
+  uint32_t rlist_cap = 0;
   bool refined = false;              // built with refinement: tref/rpool describe this grid
   std::vector<gw::Geom> h_geom;  // what d_geom holds
   uint32_t ncells = 0;
@@ -173,12 +177,13 @@ struct gwaoi_mgr {
   uint32_t next_seq = 1;
   uint32_t* rank_cnt = nullptr;  // [cap + 1]
   int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
-  int refine = 0;                // crowded cells refined in the tile-bucketed build (gwaoi_debug_set_refine;
-                                 // off by default: the sub-cell walk measured slower)
+  int refine = 1;                // crowded cells refined in the tile-bucketed build (gwaoi_debug_set_refine)
   uint32_t* part = nullptr;     // scan chunk sums
   uint32_t part_words = 0;
   gw::ScanCtx scan;
   uint32_t* thist = nullptr;     // tile-bucketed build: [max tiles * nblk + 1]
+  uint32_t* ttot = nullptr;      // tile totals (zeroed by the build itself after use)
+  uint32_t* tstart = nullptr;    // tile starts
   uint32_t* tile_walk = nullptr; // tile-bucketed build: per tile of the pass's grid, holds a reported mover
   uint32_t nblk = 0;
   uint32_t* ctr_buf = nullptr;   // [2][CTR_N]: pass P uses half P&1 and zeroes the other (k_place)
@@ -434,6 +439,27 @@ int upload_geom(gwaoi_mgr* m, Grid& g, const std::vector<gw::Geom>& geo) {
 // cell-atomic counting sort, which needs zeroed cell counts.
 bool tile_build(const Grid& g) { return g.ntiles <= gw::kMaxLdsTiles; }
 
+// The refinement pools of grid g (on first use): sized so that no reservation of k_bin_tsort can fail.
+// A grid holds at most 2 cap records, so at most 2 cap / kRefineMin refined cells (each <= 21 sub table
+// words) and 2 cap z copies; every tile may need its 1024-word cell table.
+int refine_pools(gwaoi_mgr* m, Grid& g) {
+  if (g.rpool) return GWAOI_OK;
+  const uint64_t recs = 2ull * m->cap, cells = recs / gw::kRefineMin + 1;
+  const uint64_t tiles = (uint64_t)m->max_cells / gw::kTileCells + 1;
+  const uint64_t words = tiles * gw::kTileCells + 21 * cells + 1024;
+  if (words > 0xFFFFFFF || recs > 0xFFFFFFFFull) {  // 28-bit pool offsets
+    set_err("refinement pools too large for this capacity");
+    return GWAOI_ERR_NOMEM;
+  }
+  RCHK(dalloc(&g.rpool, words));
+  RCHK(dalloc(&g.zrec, recs));
+  RCHK(dalloc(&g.rlist, cells));
+  g.rpool_cap = (uint32_t)words;
+  g.zrec_cap = (uint32_t)recs;
+  g.rlist_cap = (uint32_t)cells;
+  return GWAOI_OK;
+}
+
 // Build grid `gi` from the per-slot state (pos, seq, space_of).
 // Build grid `gi` for the pass whose ops have seqs [base, base + n_ops) (n_ops = 0: the current
 // state only, no ghosts).
@@ -464,18 +490,26 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_
   b.nblk = m->nblk;
   b.chunk = gw::bin_chunk(m->cap);
   b.thist = m->thist;
+  b.ttot = m->ttot;
+  b.tstart = m->tstart;
   b.tile_space = g.d_tile_space;
   b.trec = m->grid[gi ^ 1].rec;  // the other grid's records are not read by this pass
   b.op_kind = op_kind;
   b.tile_walk = m->tile_walk;
-  b.refine = tiles && m->refine && g.rpool ? 1 : 0;
+  b.refine = tiles && m->refine ? 1 : 0;
+  if (b.refine) RCHK(refine_pools(m, g));
   b.tref = g.tref;
   b.rpool = g.rpool;
   b.rpool_cap = g.rpool_cap;
+  b.zrec = g.zrec;
+  b.zrec_cap = g.zrec_cap;
+  b.rlist = g.rlist;
+  b.rlist_cap = g.rlist_cap;
   b.ctr = m->ctr;
   g.refined = b.refine != 0;
   if (tiles) {
     gw::launch_bin_tiles(b, m->scan, m->stream);
+    gw::launch_refine(b, m->stream);
   } else {
     gw::launch_bin_count(b, m->stream);
     gw::launch_scan(m->scan, g.cs, g.ncells + 1, m->stream);
@@ -685,6 +719,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.tile_walk = tile_build(G) ? m->tile_walk : nullptr;
     s.tref = G.refined ? G.tref : nullptr;
     s.rpool = G.rpool;
+    s.zrec = G.zrec;
     s.refined_hint = attempt ? ~0u : m->last_refined;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
@@ -844,7 +879,7 @@ void free_all(gwaoi_mgr* m) {
   m->sync = nullptr;
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
-                   m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ctr_buf, m->ev_tmp, m->ev_out,
+                   m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
                    m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
@@ -853,7 +888,7 @@ void free_all(gwaoi_mgr* m) {
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
-    void* gp[] = {g.rec, g.cs, g.d_geom, g.d_tile_space, g.tref, g.rpool};
+    void* gp[] = {g.rec, g.cs, g.d_geom, g.d_tile_space, g.tref, g.rpool, g.zrec, g.rlist};
     for (void* p : gp)
       if (p) hipFree(p);
   }
@@ -940,6 +975,8 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   const uint64_t max_tiles = m->max_cells / gw::kTileCells + 1;
   const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
   chk(dalloc(&m->thist, thist_n));
+  chk(dalloc(&m->ttot, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) + 1));
+  chk(dalloc(&m->tstart, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) + 1));
   chk(dalloc(&m->tile_walk, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
   // the scan has at most 1024 chunks up to 16.7M items (scan_ipt), more beyond
   m->part_words = std::max<uint32_t>(1024 + 2, gw::scan_part_words((uint32_t)std::max<uint64_t>(
@@ -975,10 +1012,6 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     chk(dalloc(&g.d_geom, nspaces));
     chk(dalloc(&g.d_tile_space, (size_t)m->max_cells / gw::kTileCells + 1));
     chk(dalloc(&g.tref, (size_t)m->max_cells / gw::kTileCells + 1));
-    // a refined cell holds >= kRefineMin records and takes <= 83 words, a refined tile 1024 more: room
-    // for every record of a crowd at ~3 words each (a tile that does not fit stays coarse: slower only)
-    g.rpool_cap = (uint32_t)std::min<uint64_t>(1ull << 28, 3ull * C + (1u << 20));
-    chk(dalloc(&g.rpool, g.rpool_cap));
   }
   static bool sweep_ready = false;
   if (!sweep_ready) {
@@ -1006,8 +1039,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     z(m->pos_z, C * 4);
     z(m->seq, C * 4);
     z(m->space_of, C * 4);
-    for (int gi = 0; gi < 2; ++gi) {
-    }
+    z(m->ttot, (std::min<uint64_t>(m->max_cells / gw::kTileCells + 1, gw::kMaxLdsTiles) + 1) * 4);
     std::vector<gw::Geom> geo;
     compute_geometry(m, geo);
     m->geom_dirty = false;

@@ -24,6 +24,7 @@ def test_refined_crowd_random_ops_vs_oracle(gpu, oracle_lib, seed, dist, world):
     from goworld_amd.engine import Engine
     case = H.case_random_ops(seed=seed, n=1200, nticks=6, ops_per_tick=300, world=world, dist=dist)
     eng = Engine(case["dist"], capacity=case["cap"])
+    eng.debug_set_refine(True)
     eng.set_timing(True)
     orc = oracle_lib.XZListOracle(case["dist"], case["cap"])
     for t, ops in enumerate(case["ticks"]):
