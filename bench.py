@@ -845,7 +845,7 @@ def _self_launch(cmd):
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
     for line in p.stdout:  # rank 0 prints exactly one JSON line; anything else is relayed to stderr
         if line.lstrip().startswith("{"):
-            print(line.rstrip("\n"), flush=True)
+            print(line.rstrip("\n"), file=_stdout_for_json(), flush=True)
         else:
             log(line.rstrip("\n"))
     rc = p.wait()
@@ -854,7 +854,24 @@ def _self_launch(cmd):
     return rc
 
 
+_JSON_OUT = None
+
+
+def _stdout_for_json():
+    """The bench's stdout carries exactly one JSON line. Native libraries print to file descriptor 1
+    (RCCL's version banner on communicator init, for one), so fd 1 is pointed at stderr and the JSON line
+    goes to a duplicate of the original stdout."""
+    global _JSON_OUT
+    if _JSON_OUT is None:
+        sys.stdout.flush()
+        fd = os.dup(1)
+        os.dup2(2, 1)
+        _JSON_OUT = os.fdopen(fd, "w")
+    return _JSON_OUT
+
+
 def main():
+    _stdout_for_json()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -959,7 +976,7 @@ def main():
     if rank == 0:
         if have_cuda and 0 < ndev < world:  # functional runs only: several ranks time-share one GPU
             result["ranks_share_devices"] = f"{world} ranks on {ndev} device(s)"
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=_stdout_for_json(), flush=True)
 
 
 if __name__ == "__main__":

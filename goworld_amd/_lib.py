@@ -39,7 +39,7 @@ TOOL_SYMBOLS = (
     "gwaoi_device_count", "gwaoi_dev_malloc", "gwaoi_dev_free", "gwaoi_dev_htod", "gwaoi_dev_dtoh",
     "gwaoi_dev_sync", "gwaoi_wl_init", "gwaoi_wl_step", "gwaoi_wl_iota", "gwaoi_wl_init_spaces",
     "gwaoi_wl_step_spaces", "gwaoi_debug_set_next_seq",
-    "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_cell_side", "gwaoi_debug_set_sweep_lds", "gwaoi_debug_set_refine",
+    "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_cell_side", "gwaoi_debug_set_sweep_lds",
     "gwaoi_debug_read_stamps",
     "gwaoi_debug_sweep_occupancy", "gwaoi_wl_pack_ingest", "gwaoi_debug_set_index_limit",
     "gwaoi_debug_set_relation_mode",
@@ -224,7 +224,6 @@ def load(path: str = SO_PATH):
         "gwaoi_debug_set_cells_per_dist": ([vp, f32], ctypes.c_int),
         "gwaoi_debug_set_cell_side": ([vp, f32], ctypes.c_int),
         "gwaoi_debug_set_sweep_lds": ([vp, ctypes.c_int], ctypes.c_int),
-        "gwaoi_debug_set_refine": ([vp, ctypes.c_int], ctypes.c_int),
         "gwaoi_debug_read_stamps": ([vp, ctypes.c_size_t], ctypes.c_int),
         "gwaoi_debug_set_index_limit": ([vp, u64], ctypes.c_int),
         "gwaoi_debug_set_relation_mode": ([vp, ctypes.c_int, ctypes.POINTER(u64), ctypes.POINTER(u64),

@@ -110,43 +110,6 @@ __device__ __forceinline__ int small_div(int n, int d) {
 // [cst[r W + x0], cst[r W + x1 + 1]). load(q) gives the staged form of global record q. Every thread of
 // the block calls it; it ends with a barrier. Returns false (block-uniform, nothing staged) when the
 // region holds more than `cap` records. red: kThreads / 64 words of LDS scratch.
-#if GW_STAGE_V1  // A/B knob: the per-cell staging loop (one dependent load chain per cell and record)
-template <int kThreads, int kMaxCells, int kMaxRecs, class Load>
-__device__ bool stage_region(const Geom& g, const uint32_t* __restrict__ cs, int cx0, int cz0, int W, int ncell,
-                             uint16_t* cst, uint4* out, uint32_t* red, uint32_t* tot_sh, Load&& load) {
-  constexpr int kPer = (kMaxCells + kThreads - 1) / kThreads;
-  const int c0 = threadIdx.x * kPer, c1 = min(c0 + kPer, ncell);
-  uint32_t sum = 0;
-  for (int i = c0; i < c1; ++i) {
-    const uint32_t k = cell_key(g, cx0 + i % W, cz0 + i / W);
-    sum += cs[k + 1] - cs[k];
-  }
-  const int lane = threadIdx.x & 63;
-  uint32_t inc = sum;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t v = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += v;
-  }
-  if (lane == 63) red[threadIdx.x >> 6] = inc;
-  __syncthreads();
-  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) inc += red[w];
-  if (threadIdx.x == kThreads - 1) *tot_sh = inc;
-  __syncthreads();
-  const uint32_t tot = *tot_sh;
-  const bool fits = tot <= (uint32_t)kMaxRecs;
-  if (fits) {
-    uint32_t p = inc - sum;
-    for (int i = c0; i < c1; ++i) {
-      const uint32_t k = cell_key(g, cx0 + i % W, cz0 + i / W);
-      cst[i] = (uint16_t)p;
-      for (uint32_t q = cs[k], e = cs[k + 1]; q < e; ++q, ++p) out[p] = load(q);
-    }
-    if (threadIdx.x == 0) cst[ncell] = (uint16_t)tot;
-  }
-  __syncthreads();
-  return fits;
-}
-#else
 // Each thread takes kPer consecutive cells; every cell-start load is issued up front, and the
 // records are then gathered by a flat pass (thread per staged record, its loads issued together), so
 // the staging costs a few memory round trips instead of one per cell and per record.
@@ -217,7 +180,5 @@ __device__ bool stage_region(const Geom& g, const uint32_t* __restrict__ cs, int
   __syncthreads();
   return true;
 }
-
-#endif
 
 }  // namespace gw

@@ -20,9 +20,6 @@ __host__ __device__ __forceinline__ bool finite_bits(uint32_t b) { return (b & 0
 // Counters block in device memory.
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
        CTR_DENSE = 7, CTR_HOLES = 8, CTR_NOPS = 9,  // ops of the pass (device-counted batches)
-       CTR_RPOOL = 10,  // words of the grid's refinement pool taken by k_bin_tsort (crowded cells)
-       CTR_REFINED = 11,  // cells refined in the pass's grid (k_refine's work list)
-       CTR_ZREC = 12,     // records of the refined cells (their z-ordered copies)
        CTR_N = 32 };
 constexpr int kPubWords = 16;  // counters [0, 16) are what the host reads after a pass
 // CTR_EVENTS counts SLOTS of ev_tmp; k_sweep_dense reserves them in per-wave chunks and marks the
@@ -121,38 +118,16 @@ struct BinArgs {
   // tile-bucketed build (launch_bin_tiles): per-(tile, slot chunk) histogram, bucket buffers
   uint32_t ntiles, nblk;
   uint32_t chunk;             // slots per block: kBinChunk, larger for big capacities (nblk <= ~256)
-  uint32_t* thist;            // [ntiles * nblk + 1]
-  uint32_t* ttot;             // [ntiles] tile totals (GW_BIN_TATOM; zero between builds)
+  uint32_t* thist;            // [ntiles * nblk]: bucket offset of (tile, chunk) inside its tile
+  uint32_t* ttot;             // [kMaxLdsTiles] tile totals (zero on entry; summed by k_bin_tcount)
+  uint32_t* ttot_next;        // [kMaxLdsTiles] the next build's totals (zeroed by k_bin_tscatter)
   uint32_t* tstart;           // [ntiles + 1] tile starts
   const uint32_t* tile_space;  // tile -> space
   Rec* trec;                  // records bucketed by tile (the other grid's buffer: unused this pass)
   const uint8_t* op_kind;     // the pass's op kinds (null: all moves), for tile_walk
   uint32_t* tile_walk;        // [ntiles] out: 1 = the tile holds a reported mover (k_sweep skips the rest)
-  // crowded-cell refinement (k_bin_tsort, see "Refined cells" below); refine = 0: off
-  int refine;
-  uint32_t* tref;             // [ntiles] out: 0, or 1 + pool offset of the tile's 1024-word cell table
-  uint32_t* rpool;            // refinement pool
-  uint32_t rpool_cap;         // its words
-  Rec* zrec;                  // refined cells' records again, sorted by sub-row (k_refine)
-  uint32_t zrec_cap;
-  uint4* rlist;               // k_refine's work: {first record, records, sub table offset, z copy offset}
-  uint32_t rlist_cap;
-  uint32_t* ctr;              // the pass's counter block (CTR_RPOOL, CTR_ZREC, CTR_REFINED)
 };
 
-// Refined cells (crowds). A cell of a grid tile holding kRefineMin..kRefineMax records that is not on
-// the grid's edge is split into (k+1) x (k+1) sub-cells, k = ceil(sqrt(n / 1.5)) clamped to [2, 8]: a
-// record's sub-cell is (floor(fz * k), floor(fx * k)) with fx = (x - x0) * inv_c - cx (its position's
-// offset inside the cell, in [0, 1); floor(fx * k) <= k after rounding), and the cell's records are
-// sorted by sub-COLUMN in the grid itself and by sub-ROW in a copy (zrec). Pool layout: per refined tile
-// a 1024-word cell table (0 = cell not refined, else k << 28 | offset of the cell's sub table), per
-// refined cell a sub table {maxdisp float bits, xs[k + 2], zs[k + 2]}: the record starts of each
-// sub-column in the grid and of each sub-row in zrec. maxdisp = the largest Chebyshev distance between
-// a record's binned position and the other position the sweep may judge it at (its start, for a main
-// record without a ghost), so a band query widened by it is exact. k_sweep_dense reads, of a crowded
-// cell its mover's ring crosses, ONE range: the sub-columns of a vertical ring band, or the sub-rows of
-// a horizontal one (from zrec), or the whole cell at a corner.
-constexpr uint32_t kRefineMin = 8, kRefineMax = 64;
 // Slots per block of the tile-bucketed build (at least; a capacity over 256 chunks gets larger
 // chunks, so the tile x chunk histogram stays ~256 x tiles), and the largest tile count its LDS
 // histogram holds (larger grids use the cell-atomic build).
@@ -200,10 +175,6 @@ struct SweepArgs {
   uint32_t dense_cap;
   uint32_t dense_hint;  // dense movers of the previous pass (0: launch k_sweep_dense small)
   const uint32_t* tile_walk;  // per tile: holds a reported mover (null: k_sweep scans the tile's records)
-  const uint32_t* tref;       // refined cells of the grid (null: none), read by k_sweep_dense
-  const uint32_t* rpool;
-  const Rec* zrec;
-  uint32_t refined_hint;      // refined cells of the previous pass (0: launch the crowd walk small)
 };
 
 struct RelArgs {
@@ -268,8 +239,7 @@ void launch_bin_count(const BinArgs& a, hipStream_t st);
 void launch_bin_scatter(const BinArgs& a, hipStream_t st);
 // Tile-bucketed build: LDS tile histograms per slot chunk -> (scan thist) -> bucket scatter -> per-tile
 // LDS cell sort that writes the records and every cell start. part: scan scratch.
-void launch_bin_tiles(const BinArgs& a, ScanCtx& sc, hipStream_t st);
-void launch_refine(const BinArgs& a, hipStream_t st);  // after launch_bin_tiles, when a.refine
+void launch_bin_tiles(const BinArgs& a, hipStream_t st);
 // In-place exclusive scan of d[0..n); d[n-1] must be 0 on entry if the total is wanted there.
 void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st);
 uint32_t scan_part_words(uint32_t n);

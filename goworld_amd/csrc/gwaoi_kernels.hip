@@ -51,6 +51,13 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* ctr, bool pred) {
   return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
+// An op's event count for the canonical order: only non-zero counts are stored (k_apply zeroed them).
+// (Also adding each count to its scan chunk's sum here, so the order's scan needs no reduce pass:
+// k_sweep 90 -> 107 us at config 2, the device-scope atomics cost more than the pass they save.)
+__device__ __forceinline__ void put_count(uint32_t* rank_cnt, uint32_t rank, uint32_t cnt) {
+  if (cnt) rank_cnt[rank] = cnt;
+}
+
 __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t n_real = a.n_dev ? *a.n_dev : a.n_ops;
@@ -317,65 +324,29 @@ void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st) {
     scan_ipt_launch<64>(c, d, n, nb, st);
 }
 
-// ---- tile-bucketed build: no global atomics ------------------------------------------------------
-// (1) k_bin_tcount: block b takes slots [b * kBinChunk, (b + 1) * kBinChunk); each record's rank
-//     inside (block, tile) comes from an LDS atomic on the block's tile histogram, which is then
-//     stored as thist[tile * nblk + b]. (2) exclusive scan of thist: bucket offsets, tile-major.
-// (3) k_bin_tscatter: records to their (tile, block) bucket. (4) k_bin_tsort: one block per tile
-//     counts its records per cell (LDS), scans the 1024 counts, writes the tile's cell starts and
-//     places every record (LDS atomic rank within its cell). The cell of a record is recomputed from
-//     its binned position with the same cell_key_of as (1).
+// ---- tile-bucketed build -------------------------------------------------------------------------
+// (1) k_bin_tcount: block b takes the slots of chunk c(b) (kBinChunk consecutive slots); an LDS tile
+//     histogram counts the chunk's records per tile, and each non-zero count is added to its tile's
+//     total by ONE returning atomic, whose return value is the (tile, chunk) bucket's offset inside
+//     the tile (any order of a tile's buckets will do: k_bin_tsort orders by cell), kept in
+//     thist[tile * nblk + c]. (2) k_bin_tscatter: every block scans the tile totals in LDS (tile
+//     starts; each block stores its share for k_bin_tsort and zeroes its share of the next build's
+//     totals), then scatters its chunk's records to their buckets, the rank inside a bucket from an LDS
+//     atomic on the bucket cursor. (3) k_bin_tsort: one block per tile counts its records per cell
+//     (LDS), scans the 1024 counts, writes the tile's cell starts and places every record (LDS atomic
+//     rank within its cell). The cell of a record is recomputed from its binned position with the
+//     same cell_key_of as (1).
 #ifndef GW_BIN_THREADS
 #define GW_BIN_THREADS 1024
-#endif
-// A/B knobs of the build (scripts/variants.py): GW_BIN_XCD = chunks mapped XCD-contiguous (consecutive
-// chunks on one XCD, so the adjacent (tile, chunk) buckets a tile's scatter writes meet in one L2);
-// GW_BIN_RECOUNT = k_bin_tscatter recomputes each record's key and bucket rank (LDS atomics) instead of
-// reading what k_bin_tcount stored (16 B per slot written + read less).
-#ifndef GW_BIN_XCD
-#define GW_BIN_XCD 1
-#endif
-#ifndef GW_BIN_RECOUNT
-#define GW_BIN_RECOUNT 1
-#endif
-// GW_BIN_TATOM = bucket offsets without the scan over tiles x chunks: each chunk's count of a tile is
-// added to the tile's total by one returning atomic (its return value = the bucket's offset inside the
-// tile; any order of a tile's buckets will do, k_bin_tsort orders by cell), then one small kernel
-// scans the tile totals into tile starts.
-#ifndef GW_BIN_TATOM
-#define GW_BIN_TATOM 1
 #endif
 constexpr int kBinThreads = GW_BIN_THREADS;  // 16 waves: one block per CU at 1M slots, latency hidden by width
 constexpr int kBinItems = kBinChunk / kBinThreads;
 
-// first record of tile t (t = ntiles: the record total)
-__device__ __forceinline__ uint32_t bin_tile_start(const BinArgs& a, uint32_t t) {
-#if GW_BIN_TATOM
-  return a.tstart[t];
-#else
-  return a.thist[t * a.nblk];
-#endif
-}
-
-// first record of chunk c's bucket of tile t: with GW_BIN_TATOM thist holds the bucket's offset inside
-// its tile, else (scanned) its absolute offset
-__device__ __forceinline__ uint32_t bin_bucket(const BinArgs& a, uint32_t t, uint32_t c) {
-#if GW_BIN_TATOM
-  return a.tstart[t] + a.thist[t * a.nblk + c];
-#else
-  return a.thist[t * a.nblk + c];
-#endif
-}
-
-// the chunk a block takes: XCD x (block b runs on XCD b % 8) takes a contiguous run of chunks
+// the chunk a block takes: XCD x (block b runs on XCD b % 8) takes a contiguous run of chunks, so the
+// adjacent (tile, chunk) buckets a tile's scatter writes meet in one L2
 __device__ __forceinline__ uint32_t bin_chunk_of(uint32_t b, uint32_t nblk) {
-#if GW_BIN_XCD
   const uint32_t x = b % 8u, per = nblk / 8u, rem = nblk % 8u;
   return x * per + min(x, rem) + b / 8u;
-#else
-  (void)nblk;
-  return b;
-#endif
 }
 
 // keys of slot s's main (k1) and ghost (k0) records, kNoKey for none
@@ -414,53 +385,77 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
     const SlotState t = slot_state(a, s);
     uint32_t k1, k0;
     bin_keys(a, s, t, k1, k0);
-    uint32_t l1 = 0, l0 = 0;
-    if (k1 != kNoKey) l1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
-    if (k0 != kNoKey) l0 = atomicAdd(&th[k0 >> kTileCellShift], 1u);
-#if !GW_BIN_RECOUNT
-    if (k1 != kNoKey || k0 != kNoKey) reinterpret_cast<uint2*>(a.local_of)[s] = make_uint2(l1, l0);
-    reinterpret_cast<uint2*>(a.key_of)[s] = make_uint2(k1, k0);
-#else
-    (void)l1, (void)l0;
-#endif
+    if (k1 != kNoKey) atomicAdd(&th[k1 >> kTileCellShift], 1u);
+    if (k0 != kNoKey) atomicAdd(&th[k0 >> kTileCellShift], 1u);
   });
   __syncthreads();
-#if GW_BIN_TATOM
-  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads)
-    if (th[i]) a.thist[i * a.nblk + c] = atomicAdd(&a.ttot[i], th[i]);
-#else
-  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) a.thist[i * a.nblk + c] = th[i];
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.thist[a.ntiles * a.nblk] = 0u;  // the scan's total slot
-#endif
+  // every returning atomic of the thread in flight together (a loop would wait for each in turn)
+  constexpr uint32_t kPer = (kMaxLdsTiles + kBinThreads - 1) / kBinThreads;
+  uint32_t cnt[kPer], off[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = threadIdx.x + k * kBinThreads;
+    cnt[k] = i < a.ntiles ? th[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k)
+    if (cnt[k]) off[k] = atomicAdd(&a.ttot[threadIdx.x + k * kBinThreads], cnt[k]);
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k)
+    if (cnt[k]) a.thist[(threadIdx.x + k * kBinThreads) * a.nblk + c] = off[k];
 }
 
 __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
+  extern __shared__ uint32_t th[];  // [ntiles]: tile starts, then this chunk's bucket cursors
+  __shared__ uint32_t ws[kBinThreads / 64];
+  constexpr uint32_t kPer = (kMaxLdsTiles + kBinThreads - 1) / kBinThreads;
+  const uint32_t n = a.ntiles, i0 = threadIdx.x * kPer;
   const uint32_t c = bin_chunk_of(blockIdx.x, a.nblk);
-#if GW_BIN_RECOUNT
-  // the bucket offsets of this chunk in LDS, advanced by one LDS atomic per record (ranks inside a
-  // (tile, chunk) bucket are free: k_bin_tsort orders records by cell, not by rank)
-  extern __shared__ uint32_t th[];
-  for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads)
-    th[i] = bin_bucket(a, i, c);  // (stale for tiles this chunk has no record of)
+  // this chunk's bucket offsets inside the tiles (strided: tile threadIdx.x + k kBinThreads) and the tile
+  // totals (blocked, for the scan), every load in flight together
+  uint32_t h[kPer], v[kPer], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = threadIdx.x + k * kBinThreads;
+    h[k] = i < n ? a.thist[i * a.nblk + c] : 0u;  // (stale for tiles this chunk has no record of)
+    v[k] = i0 + k < n ? a.ttot[i0 + k] : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) sum += v[k];
+  const uint32_t inc = wave_incl_scan(sum);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = inc;
   __syncthreads();
-#endif
+  uint32_t pre = inc - sum, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kBinThreads / 64; ++k) {
+    pre += k < w ? ws[k] : 0u;
+    tot += ws[k];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    if (i0 + k < n) th[i0 + k] = pre;
+    pre += v[k];
+  }
+  __syncthreads();
+  const uint32_t gt = blockIdx.x * kBinThreads + threadIdx.x, gn = gridDim.x * kBinThreads;
+  for (uint32_t i = gt; i < n; i += gn) a.tstart[i] = th[i];
+  if (gt == 0) a.tstart[n] = tot;
+  for (uint32_t i = gt; i < kMaxLdsTiles; i += gn) a.ttot_next[i] = 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = threadIdx.x + k * kBinThreads;
+    if (i < n) th[i] += h[k];
+  }
+  __syncthreads();
   bin_chunk_loop(a, c, [&](uint32_t s) {
     const SlotState t = slot_state(a, s);
-#if GW_BIN_RECOUNT
     uint32_t k1, k0;
     bin_keys(a, s, t, k1, k0);
     if (k1 == kNoKey && k0 == kNoKey) return;
     uint32_t j1 = 0, j0 = 0;
     if (k1 != kNoKey) j1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
     if (k0 != kNoKey) j0 = atomicAdd(&th[k0 >> kTileCellShift], 1u);
-#else
-    const uint2 kk = reinterpret_cast<const uint2*>(a.key_of)[s];
-    const uint32_t k1 = kk.x, k0 = kk.y;
-    if (k1 == kNoKey && k0 == kNoKey) return;
-    const uint2 ll = reinterpret_cast<const uint2*>(a.local_of)[s];
-    const uint32_t j1 = k1 != kNoKey ? bin_bucket(a, k1 >> kTileCellShift, c) + ll.x : 0u;
-    const uint32_t j0 = k0 != kNoKey ? bin_bucket(a, k0 >> kTileCellShift, c) + ll.y : 0u;
-#endif
     const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
     if (k1 != kNoKey)
       a.trec[j1] = Rec{make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq),
@@ -499,161 +494,11 @@ __device__ __forceinline__ bool bin_walker(const BinArgs& a, const uint4 ra) {
   return !(ra.z & REC_GHOST) && r < a.n_ops && !(a.op_kind && (a.op_kind[r] & OP_SILENT));
 }
 
-// ---- refined cells (gwaoi_internal.h "Refined cells") ----
-__device__ __forceinline__ uint32_t refine_k(uint32_t n) {
-  uint32_t k = 2;
-  while (k < 8 && (float)(k * k) * 1.5f < (float)n) ++k;  // k = ceil(sqrt(n / 1.5)) in [2, 8]
-  return k;
-}
-
-// sub-cell coordinate of v inside cell c (fraction of the cell times k, floored): monotone in v; for a
-// record of the cell in [0, k]. The same function bounds the sweep's sub-cell ranges (exactness).
-__device__ __forceinline__ int sub_coord(float v, float o, float inv, int c, uint32_t k) {
-  const float f = ((v - o) * inv - (float)c) * (float)k;
-  if (!(f > -2.0f)) return -2;
-  if (!(f < (float)k + 2.0f)) return (int)k + 2;
-  return (int)floorf(f);
-}
-
-// After k_bin_tsort placed a tile's records by cell: cells of kRefineMin..kRefineMax records (not on the
-// grid's edge) get an entry in the tile's cell table, a sub table and room for their z-ordered copies in
-// the pools, and a work item for k_refine (which sorts them). The pools are sized so that no
-// reservation can fail (runtime: refine_pools). cso: this thread's 4 cell starts; cnt: the cell ends.
-__device__ void refine_tile(const BinArgs& a, uint32_t t, const uint4 cso, const uint32_t* cnt) {
-  __shared__ uint32_t rinfo[3];  // [0] z copy offset, [1] pool offset, [2] work list offset
-  const Geom* gp = &a.geom[a.tile_space[t]];
-  const float gx0 = gp->x0, gz0 = gp->z0, inv = gp->inv_c;
-  const int ncx = gp->ncx, ncz = gp->ncz, ntx = gp->ntx;
-  const uint32_t tl = t - gp->tile_base;
-  const int tz = (int)(tl / (uint32_t)ntx), tx = (int)(tl - (uint32_t)tz * (uint32_t)ntx);
-  __syncthreads();  // every placement atomic done: cnt[] holds the cell ends
-  const uint32_t st[4] = {cso.x, cso.y, cso.z, cso.w};
-  uint32_t need[4], sum = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = threadIdx.x * 4 + i;
-    const int cx = tx * kTile + (c & (kTile - 1)), cz = tz * kTile + (c >> kTileShift);
-    const uint32_t n = cnt[c] - st[i];
-    const bool ok = n >= kRefineMin && n <= kRefineMax && cx > 0 && cx < ncx - 1 && cz > 0 && cz < ncz - 1;
-    const uint32_t k = ok ? refine_k(n) : 0u;
-    need[i] = ok ? 2 * (k + 2) + 1 : 0u;
-    sum += need[i];
-  }
-  if (!__syncthreads_or(sum != 0u)) {  // no crowded cell (a uniform crowd's tiles): one barrier
-    if (threadIdx.x == 0) a.tref[t] = 0u;
-    return;
-  }
-  uint32_t tot;
-  uint32_t pre = block_excl_scan(sum, &tot);
-  if (threadIdx.x == 0) {
-    uint32_t off = ~0u;
-    if (tot) {
-      off = atomicAdd(&a.ctr[CTR_RPOOL], kTileCells + tot);
-      if ((uint64_t)off + kTileCells + tot > a.rpool_cap) off = ~0u;  // pool full: this tile stays coarse
-    }
-    rinfo[1] = off;
-    a.tref[t] = off == ~0u ? 0u : off + 1u;
-  }
-  __syncthreads();
-  const uint32_t off = rinfo[1];
-  if (off == ~0u) return;  // block-uniform
-  uint32_t o = off + kTileCells + pre;
-  // the records' z-ordered copies and the work list (k_refine sorts the cells, one wave each)
-  uint32_t nrec = 0, ncell = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (need[i]) nrec += cnt[threadIdx.x * 4 + i] - st[i], ++ncell;
-  uint32_t totr, totc;
-  uint32_t prer = block_excl_scan(nrec, &totr);
-  uint32_t prec = block_excl_scan(ncell, &totc);
-  if (threadIdx.x == 0) {
-    uint32_t zo = atomicAdd(&a.ctr[CTR_ZREC], totr), lo = atomicAdd(&a.ctr[CTR_REFINED], totc);
-    if ((uint64_t)zo + totr > a.zrec_cap || (uint64_t)lo + totc > a.rlist_cap) zo = lo = ~0u;
-    rinfo[0] = zo;
-    rinfo[2] = lo;
-  }
-  __syncthreads();
-  const uint32_t zo = rinfo[0], lo = rinfo[2];
-  if (zo == ~0u) {  // no room for the copies: this tile stays coarse (block-uniform)
-    if (threadIdx.x == 0) a.tref[t] = 0u;
-    return;
-  }
-  prer += zo;
-  prec += lo;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = threadIdx.x * 4 + i;
-    uint32_t w = 0;
-    if (need[i]) {
-      const uint32_t n = cnt[c] - st[i], k = refine_k(n);
-      w = k << 28 | o;
-      a.rlist[prec++] = make_uint4(st[i], n, o, prer);
-      prer += n;
-      o += need[i];
-    }
-    a.rpool[off + c] = w;
-  }
-}
-
-// One wave per refined cell (the list k_bin_tsort wrote): the cell's records sorted by sub-column in
-// place (rec) and by sub-row into the z copy (zrec), with the sub-column / sub-row starts and maxdisp
-// in the cell's sub table {maxdisp, xs[k + 2], zs[k + 2]}. Ranks by one ballot per sub-index value.
-__global__ void __launch_bounds__(kBlock) k_refine(BinArgs a) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long below = (1ull << lane) - 1ull;
-  const uint32_t nl = min(a.ctr[CTR_REFINED], a.rlist_cap);
-  for (uint32_t li = (blockIdx.x * kBlock + threadIdx.x) >> 6; li < nl; li += gridDim.x * (kBlock / 64)) {
-    const uint4 L = a.rlist[li];
-    const uint32_t c0 = L.x, n = L.y, so = L.z, zo = L.w, k = refine_k(n);
-    const bool on = (uint32_t)lane < n;
-    uint4 ra = make_uint4(0, 0, 0, 0), rb = ra;
-    int sx = -1, sz = -1;
-    float d = 0.0f;
-    if (on) {
-      ra = a.rec[c0 + lane].a;
-      rb = a.rec[c0 + lane].b;
-      const float x = __uint_as_float(ra.x), z = __uint_as_float(ra.y);
-      const Geom* gp = &a.geom[a.space_of[ra.z & REC_SLOT]];
-      const float gx0 = gp->x0, gz0 = gp->z0, inv = gp->inv_c;
-      const int cx = cellc(x, gx0, inv, gp->ncx), cz = cellc(z, gz0, inv, gp->ncz);  // not an edge cell: exact
-      sx = sub_coord(x, gx0, inv, cx, k);
-      sz = sub_coord(z, gz0, inv, cz, k);
-      if (!(ra.z & (REC_GHOST | REC_HASG)) && rb.z != 0u)  // may be judged at its start too
-        d = fmaxf(fabsf(__uint_as_float(rb.x) - x), fabsf(__uint_as_float(rb.y) - z));
-    }
-    uint32_t px = 0, pz = 0, bx = 0, bz = 0, xs = c0 + n, zs = zo + n;
-    for (int v = 0; v <= (int)k; ++v) {  // wave-uniform
-      const unsigned long long mx = __ballot(sx == v), mz = __ballot(sz == v);
-      if (sx == v) px = bx + (uint32_t)__popcll(mx & below);
-      if (sz == v) pz = bz + (uint32_t)__popcll(mz & below);
-      if (lane == v) xs = c0 + bx, zs = zo + bz;
-      bx += (uint32_t)__popcll(mx);
-      bz += (uint32_t)__popcll(mz);
-    }
-    if (on) {
-      a.rec[c0 + px].a = ra;  // every lane's loads were consumed above: in-place is safe
-      a.rec[c0 + px].b = rb;
-      a.zrec[zo + pz].a = ra;
-      a.zrec[zo + pz].b = rb;
-    }
-    for (int sh = 32; sh > 0; sh >>= 1) d = fmaxf(d, __shfl_xor(d, sh, 64));
-    if (lane == 0) a.rpool[so] = __float_as_uint(d);
-    if ((uint32_t)lane <= k + 1) {  // lane k + 1 kept the ends
-      a.rpool[so + 1 + lane] = xs;
-      a.rpool[so + 1 + (k + 2) + lane] = zs;
-    }
-  }
-}
-
-void launch_refine(const BinArgs& a, hipStream_t st) {
-  if (a.refine) hipLaunchKernelGGL(k_refine, dim3(512), dim3(kBlock), 0, st, a);
-}
-
 __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   __shared__ uint32_t cnt[kTileCells];
   __shared__ uint32_t ws[kBlock / 64];
   const uint32_t t = blockIdx.x;
-  const uint32_t b = bin_tile_start(a, t), e = bin_tile_start(a, t + 1);
+  const uint32_t b = a.tstart[t], e = a.tstart[t + 1];
   for (int c = threadIdx.x; c < kTileCells; c += kBlock) cnt[c] = 0u;
   const TileMap g = tile_map(&a.geom[a.tile_space[t]]);
   const bool small = e - b <= 4u * kBlock;
@@ -730,52 +575,13 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
       o->a = ra, o->b = rb;
     }
   }
-  if (a.refine) refine_tile(a, t, cso, cnt);  // block-uniform
 }
 
-// tile starts = exclusive scan of the tile totals (tstart[n] = total); the totals are zeroed for the
-// next build. One block: n <= kMaxLdsTiles (12,288), 12 per thread.
-__global__ void __launch_bounds__(1024) k_tile_scan(uint32_t* ttot, uint32_t* tstart, uint32_t n) {
-  __shared__ uint32_t ws[16];
-  constexpr uint32_t kPer = (kMaxLdsTiles + 1023) / 1024;
-  const uint32_t b0 = threadIdx.x * kPer;
-  uint32_t v[kPer], sum = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {
-    v[k] = b0 + k < n ? ttot[b0 + k] : 0u;
-    sum += v[k];
-  }
-  const uint32_t inc = wave_incl_scan(sum);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 63) ws[w] = inc;
-  __syncthreads();
-  uint32_t pre = inc - sum, tot = 0;
-  for (int k = 0; k < 16; ++k) {
-    pre += k < w ? ws[k] : 0u;
-    tot += ws[k];
-  }
-#pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {
-    if (b0 + k < n) {
-      tstart[b0 + k] = pre;
-      ttot[b0 + k] = 0u;
-    }
-    pre += v[k];
-  }
-  if (threadIdx.x == 0) tstart[n] = tot;
-}
-
-void launch_bin_tiles(const BinArgs& a, ScanCtx& sc, hipStream_t st) {
+void launch_bin_tiles(const BinArgs& a, hipStream_t st) {
   if (!a.ntiles) return;
-  hipLaunchKernelGGL(k_bin_tcount, dim3(a.nblk), dim3(kBinThreads), a.ntiles * sizeof(uint32_t), st, a);
-#if GW_BIN_TATOM
-  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, st, a.ttot, a.tstart, a.ntiles);
-  (void)sc;
-#else
-  launch_scan(sc, a.thist, a.ntiles * a.nblk + 1, st);
-#endif
-  hipLaunchKernelGGL(k_bin_tscatter, dim3(a.nblk), dim3(kBinThreads), GW_BIN_RECOUNT ? a.ntiles * sizeof(uint32_t) : 0,
-                     st, a);
+  const size_t lds = a.ntiles * sizeof(uint32_t);
+  hipLaunchKernelGGL(k_bin_tcount, dim3(a.nblk), dim3(kBinThreads), lds, st, a);
+  hipLaunchKernelGGL(k_bin_tscatter, dim3(a.nblk), dim3(kBinThreads), lds, st, a);
   hipLaunchKernelGGL(k_bin_tsort, dim3(a.ntiles), dim3(kBlock), 0, st, a);
 }
 
@@ -1068,6 +874,21 @@ __device__ __forceinline__ int judge_lds(const Judge& J, const uint4 rp, const u
   return (valid & (before != after)) ? (after ? 2 : 1) : 0;
 }
 
+// judge_lds without the exact path, for the candidate loop: true for an event (its kind is re-derived
+// at emission, where events are rare), near = a distance within J.eps of D (the caller re-decides those
+// candidates with judge_lds).
+__device__ __forceinline__ bool judge_fast(const Judge& J, const uint4 rp, const uint2 rm, bool& near) {
+  const uint32_t r = rm.x & ~kTopBit;
+  const bool ae = r < J.rank;
+  const bool valid = (r != J.rank) & (!(rm.x & kTopBit) | !ae) & (!(rm.y & kTopBit) | ae);
+  const float px = __uint_as_float(ae ? rp.z : rp.x);
+  const float pz = __uint_as_float(ae ? rp.w : rp.y);
+  const float b = fmaxf(fabsf(px - J.mx0), fabsf(pz - J.mz0));
+  const float f = fmaxf(fabsf(px - J.mx1), fabsf(pz - J.mz1));
+  near = fminf(fabsf(b - J.D), fabsf(f - J.D)) <= J.eps;
+  return valid & ((J.v0 & (b <= J.D)) != (J.v1 & (f <= J.D)));
+}
+
 template <class Q>
 __device__ __forceinline__ uint32_t sweep_global(const SweepArgs& a, Q& q, const Mover& m, const Geom& g,
                                                  uint32_t& nent) {
@@ -1150,62 +971,78 @@ __device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const 
   return true;
 }
 
-#ifndef GW_JUDGE_UNROLL
-#define GW_JUDGE_UNROLL 2  // A/B: 4 = four candidates per iteration
-#endif
 // Judge candidates b..b+63 of one stream (idx(k) = LDS record index of candidate k): the hot loop
-// only records which candidates raise an event and of which kind (bit k - b of two per-lane masks).
-// No atomic, branch or LDS write sits in the candidate loop itself. (32-candidate chunks with 32-bit
-// masks: the register allocator spills 5x more in this kernel, measured slower.)
+// only records which candidates raise an event (bit k - b of a per-lane mask; the kind is re-derived
+// when the event is queued). Two candidates per iteration, both LDS reads in flight, their two bits
+// merged before the 64-bit shift, and one (rarely taken) branch per pair for the exact tests. No
+// atomic or LDS write sits in the candidate loop itself. (32-candidate chunks with 32-bit masks: the
+// register allocator spills 5x more in this kernel, measured slower.)
 template <class IdxF>
-__device__ __forceinline__ void judge_chunk(const SweepSmem& sm, const Judge& J, uint32_t b, uint32_t total,
-                                            IdxF&& idx, unsigned long long& hit, unsigned long long& ent) {
+__device__ __forceinline__ unsigned long long judge_chunk(const SweepSmem& sm, const Judge& J, uint32_t b,
+                                                          uint32_t total, IdxF&& idx) {
   const uint32_t n = b < total ? min(total - b, 64u) : 0u;
-  hit = 0;
-  ent = 0;
-  uint32_t k = 0;
-#if GW_JUDGE_UNROLL >= 4
-  for (; k + 3 < n; k += 4) {  // four candidates per iteration: four LDS record reads in flight
-    const uint32_t j0 = idx(b + k), j1 = idx(b + k + 1), j2 = idx(b + k + 2), j3 = idx(b + k + 3);
-    const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1], p2 = sm.rp[j2], p3 = sm.rp[j3];
-    const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1], q2 = sm.rm[j2], q3 = sm.rm[j3];
-    const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1), e2 = judge_lds(J, p2, q2),
-              e3 = judge_lds(J, p3, q3);
-    hit |= ((unsigned long long)(e0 != 0) << k) | ((unsigned long long)(e1 != 0) << (k + 1)) |
-           ((unsigned long long)(e2 != 0) << (k + 2)) | ((unsigned long long)(e3 != 0) << (k + 3));
-    ent |= ((unsigned long long)(e0 == 2) << k) | ((unsigned long long)(e1 == 2) << (k + 1)) |
-           ((unsigned long long)(e2 == 2) << (k + 2)) | ((unsigned long long)(e3 == 2) << (k + 3));
-  }
+  unsigned long long hit = 0;
+#ifndef GW_JUDGE_PIPE
+#define GW_JUDGE_PIPE 1
 #endif
-  for (; k + 1 < n; k += 2) {  // two candidates per iteration: both LDS reads in flight
+#if GW_JUDGE_PIPE
+  // software-pipelined: the next pair's LDS reads are issued before the current pair is judged, so a
+  // wave's LDS latency overlaps its own VALU work (a phantom candidate past n re-reads the last one and
+  // its bit is dropped)
+  if (n == 0) return 0;
+  auto at = [&](uint32_t k) { return idx(b + min(k, n - 1)); };
+  uint32_t j0 = at(0), j1 = at(1);
+  uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
+  uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
+  for (uint32_t k = 0; k < n; k += 2) {
+    j0 = at(k + 2), j1 = at(k + 3);
+    const uint4 np0 = sm.rp[j0], np1 = sm.rp[j1];
+    const uint2 nq0 = sm.rm[j0], nq1 = sm.rm[j1];
+    bool n0, n1;
+    bool h0 = judge_fast(J, p0, q0, n0), h1 = judge_fast(J, p1, q1, n1);
+    if (GW_JUDGE_EXACT || __builtin_expect(n0 | n1, 0)) {
+      h0 = judge_lds(J, p0, q0) != 0;
+      h1 = judge_lds(J, p1, q1) != 0;
+    }
+    h1 = h1 && k + 1 < n;
+    hit |= (unsigned long long)((uint32_t)h0 | ((uint32_t)h1 << 1)) << k;
+    p0 = np0, p1 = np1, q0 = nq0, q1 = nq1;
+  }
+#else
+  uint32_t k = 0;
+  for (; k + 1 < n; k += 2) {
     const uint32_t j0 = idx(b + k), j1 = idx(b + k + 1);
     const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
     const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
-    const int e0 = judge_lds(J, p0, q0), e1 = judge_lds(J, p1, q1);
-    hit |= ((unsigned long long)(e0 != 0) << k) | ((unsigned long long)(e1 != 0) << (k + 1));
-    ent |= ((unsigned long long)(e0 == 2) << k) | ((unsigned long long)(e1 == 2) << (k + 1));
+    bool n0, n1;
+    bool h0 = judge_fast(J, p0, q0, n0), h1 = judge_fast(J, p1, q1, n1);
+    if (GW_JUDGE_EXACT || __builtin_expect(n0 | n1, 0)) {
+      h0 = judge_lds(J, p0, q0) != 0;
+      h1 = judge_lds(J, p1, q1) != 0;
+    }
+    hit |= (unsigned long long)((uint32_t)h0 | ((uint32_t)h1 << 1)) << k;
   }
   if (k < n) {
     const uint32_t j0 = idx(b + k);
-    const int e0 = judge_lds(J, sm.rp[j0], sm.rm[j0]);
-    hit |= (unsigned long long)(e0 != 0) << k;
-    ent |= (unsigned long long)(e0 == 2) << k;
+    hit |= (unsigned long long)(judge_lds(J, sm.rp[j0], sm.rm[j0]) != 0) << k;
   }
+#endif
+  return hit;
 }
 
-// Queue the events marked in two mask pairs (hA/eA: candidates ia(bit), hB/eB: ib(bit)) for every
+// Queue the events marked in two hit masks (hA: candidates ia(bit), hB: ib(bit); each event's kind
+// re-derived by judge_lds from the candidate's LDS record) for every
 // lane of the wave at once: each lane's event count c, the wave's exclusive prefix and total by one
 // ballot per bit of c (no LDS round trip), ONE LDS atomic per wave for the queue range, one global
 // atomic per wave when the range runs past the queue; then each lane writes its own events in mask
 // order (its `local` numbering). Every lane that reached the call takes part (the masks of a lane
 // without events are zero).
 template <class IdxA, class IdxB>
-__device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, const Mover& m, unsigned long long hA,
-                                           unsigned long long eA, IdxA&& ia, unsigned long long hB,
-                                           unsigned long long eB, IdxB&& ib, uint32_t& local, uint32_t& nent) {
+__device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Judge& J,
+                                           unsigned long long hA, IdxA&& ia, unsigned long long hB, IdxB&& ib,
+                                           uint32_t& local, uint32_t& nent) {
   const uint32_t c = (uint32_t)(__popcll(hA) + __popcll(hB));
-#if GW_ABL_NOEMIT  // ablation (timing only): events counted, not queued
-  nent += (uint32_t)(__popcll(eA) + __popcll(eB));
+#if GW_ABL_NOEMIT  // ablation (timing only): events queued nowhere (enter count not kept)
   local += c;
   return;
 #endif
@@ -1229,11 +1066,12 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, co
     g0 = __builtin_amdgcn_readfirstlane(g0);
   }
   uint32_t p = q0 + pre;
-  auto put = [&](unsigned long long& h, unsigned long long e, auto&& idx) {
+  auto put = [&](unsigned long long& h, auto&& idx) {
     while (h) {
       const int bit = __ffsll((long long)h) - 1;
-      const bool enter = (e >> bit) & 1ull;
-      const uint32_t j = idx((uint32_t)bit), eb = enter ? 0x80000000u : 0u;
+      const uint32_t j = idx((uint32_t)bit);
+      const bool enter = judge_lds(J, sm.rp[j], sm.rm[j]) == 2;
+      const uint32_t eb = enter ? 0x80000000u : 0u;
       nent += enter ? 1u : 0u;
       if (p < (uint32_t)kEvLds) {
         sm.ev[p] = make_uint4(m.rank, local, m.slot, sm.rslot[j] | eb);
@@ -1246,8 +1084,8 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, co
       h &= h - 1ull;
     }
   };
-  put(hA, eA, ia);
-  put(hB, eB, ib);
+  put(hA, ia);
+  put(hB, ib);
 }
 
 // Judge candidates 0..total-1 of one stream, 64 at a time, queueing each chunk's events.
@@ -1255,10 +1093,9 @@ template <class IdxF>
 __device__ __forceinline__ void judge_stream(const SweepArgs& a, SweepSmem& sm, const Judge& J, const Mover& m,
                                              uint32_t total, IdxF&& idx, uint32_t& local, uint32_t& nent) {
   for (uint32_t b = 0; __any(b < total); b += 64) {
-    unsigned long long hit, ent;
-    judge_chunk(sm, J, b, total, idx, hit, ent);
-    emit_masks(a, sm, m, hit, ent, [&](uint32_t k) { return idx(b + k); }, 0ull, 0ull,
-               [&](uint32_t k) { return k; }, local, nent);
+    const unsigned long long hit = judge_chunk(sm, J, b, total, idx);
+    emit_masks(a, sm, m, J, hit, [&](uint32_t k) { return idx(b + k); }, 0ull, [&](uint32_t k) { return k; }, local,
+               nent);
   }
 }
 
@@ -1272,10 +1109,9 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     auto ri = [&](uint32_t k) { return stream_at(Rs, k); };
     auto ci = [&](uint32_t k) { return (uint32_t)sm.cidx[stream_at(Cs, k)]; };
     if (__all(Rs.total <= 64u && Cs.total <= 64u)) {  // the usual ring: both streams in one chunk, one emission
-      unsigned long long hR, eR, hC, eC;
-      judge_chunk(sm, J, 0, Rs.total, ri, hR, eR);
-      judge_chunk(sm, J, 0, Cs.total, ci, hC, eC);
-      emit_masks(a, sm, m, hR, eR, ri, hC, eC, ci, local, nent);
+      const unsigned long long hR = judge_chunk(sm, J, 0, Rs.total, ri);
+      const unsigned long long hC = judge_chunk(sm, J, 0, Cs.total, ci);
+      emit_masks(a, sm, m, J, hR, ri, hC, ci, local, nent);
       return local;
     }
     judge_stream(a, sm, J, m, Rs.total, ri, local, nent);
@@ -1601,7 +1437,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
       }
       const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
       const uint32_t cnt = sweep_global(a, sm, m, g, nent);
-      if (cnt) a.rank_cnt[m.rank] = cnt;
+      put_count(a.rank_cnt, m.rank, cnt);
     }
   } else {
     const uint32_t nm = sm.nmv;
@@ -1622,7 +1458,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
           continue;
         }
         const uint32_t cnt = sweep_lds(a, sm, m, make_walk(m, g, A0, A1), R, g, nent);
-        if (cnt) a.rank_cnt[m.rank] = cnt;  // zeroed by k_apply (one coalesced pass instead of a scatter)
+        put_count(a.rank_cnt, m.rank, cnt);  // zeroed by k_apply
       }
     }
   }
@@ -1709,14 +1545,14 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
       const uint32_t slot = ra.z & REC_SLOT;
       const Geom g = a.g.geom[a.space_of[slot]];
       const Mover m = mover_of(ra, a.g.rec[t].b, a.base, g.D);
-      a.rank_cnt[m.rank] = sweep_global(a, q, m, g, nent);
+      put_count(a.rank_cnt, m.rank, sweep_global(a, q, m, g, nent));
     }
   } else if (t >= a.n_rec && t < a.n_rec + (a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves) &&
              !(a.op_kind && (a.op_kind[a.leave_ops[t - a.n_rec]] & OP_SILENT))) {
     const uint32_t i = a.leave_ops[t - a.n_rec];
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
-    a.rank_cnt[i] = sweep_global(a, q, m, g, nent);
+    put_count(a.rank_cnt, i, sweep_global(a, q, m, g, nent));
   }
   if (nent) atomicAdd(&q.enter, nent);
   __syncthreads();
@@ -1748,7 +1584,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
     if (a.op_kind && (a.op_kind[i] & OP_SILENT)) continue;
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
-    a.rank_cnt[i] = sweep_global(a, q, m, g, nent);
+    put_count(a.rank_cnt, i, sweep_global(a, q, m, g, nent));
   }
   if (nent) atomicAdd(&q.enter, nent);
   __syncthreads();
@@ -1764,12 +1600,17 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
   }
 }
 
-// Dense movers: one WAVE per mover (grid-stride over the list k_sweep built). The walk is the same
-// row walk as sweep_global, but its cell ranges are collected one per lane, and the concatenated
-// candidate stream is judged 64 at a time (each lane finds its range by a binary search over the
-// lanes' inclusive prefix), so every 64 candidates cost one coalesced memory round trip whatever the
-// number of cells they come from. A mover's events are numbered by a ballot prefix on top of the
-// wave-uniform running count and written with one atomic per 64 candidates.
+// Dense movers: one WAVE per mover (k_sweep lists them: boxes beyond the tile's LDS region, tiles whose
+// region does not fit, Spaces whose region cannot). The walk is the same row walk as sweep_global, but
+// lane-parallel: each lane takes one part (a row segment inside one tile: ONE contiguous record range),
+// the parts' ranges come in with one round trip for up to 64 parts, and the concatenated candidate
+// stream is judged 128 at a time (each lane finds its range by a binary search over the lanes'
+// inclusive prefix), so every 128 candidates cost one coalesced memory round trip whatever the number
+// of cells they come from. A mover's events are numbered by a ballot prefix on top of the
+// wave-uniform running count and written into event slots the wave reserves kEvChunk at a time.
+// (Measured against this, on skew50 / skew: the candidates listed in LDS by the wave instead of the
+// binary search, 6.53 -> 6.95 / 3.06 -> 3.30 ms; four candidates per lane per round at 5 waves/SIMD,
+// slower again. The walk is bound by its candidate records, not by locating them.)
 constexpr int kDenseBlock = 256;
 #ifndef GW_DENSE_WPE
 #define GW_DENSE_WPE 6
@@ -1781,312 +1622,150 @@ constexpr int kDenseGrid = 256 * GW_DENSE_WPE;  // GW_DENSE_WPE waves per SIMD: 
 constexpr uint32_t kEvChunk = GW_EV_CHUNK;  // event slots a wave reserves at a time (one returning atomic
                                       // on the shared counter each: ~11 ns apiece when serialised)
 
-// The float bounds a dense mover's walk needs inside a refined cell (gwaoi_internal.h "Refined cells"):
-// U = the union of its boxes with qbox's rounding margin (a record binned farther than the cell's
-// maxdisp outside U is outside both boxes from every perspective), I = the ring's inner box of
-// make_walk (a record binned deeper than maxdisp inside I is inside both; empty for row walks).
-struct SubBounds {
-  float ux0, ux1, uz0, uz1;
-  float ix0, ix1, iz0, iz1;
-  bool inner;
-};
-
-__device__ __forceinline__ SubBounds sub_bounds(const Mover& m, const Walk& w) {
-  SubBounds b;
-  const float D = m.D;
-  auto lo = [&](float c) { return (c - D) - (fabsf(c) + D) * kMargin; };
-  auto hi = [&](float c) { return (c + D) + (fabsf(c) + D) * kMargin; };
-  if (m.valid0 && m.valid1) {
-    b.ux0 = fminf(lo(m.mx0), lo(m.mx1)), b.ux1 = fmaxf(hi(m.mx0), hi(m.mx1));
-    b.uz0 = fminf(lo(m.mz0), lo(m.mz1)), b.uz1 = fmaxf(hi(m.mz0), hi(m.mz1));
-  } else {
-    const float cx = m.valid1 ? m.mx1 : m.mx0, cz = m.valid1 ? m.mz1 : m.mz0;
-    b.ux0 = lo(cx), b.ux1 = hi(cx), b.uz0 = lo(cz), b.uz1 = hi(cz);
-  }
-  b.inner = w.ring;
-  if (w.ring) {  // make_walk's inner box (cells strictly inside it are skipped by the coarse walk too)
-    const float ex = (fmaxf(fabsf(m.mx0), fabsf(m.mx1)) + D) * kInner;
-    const float ez = (fmaxf(fabsf(m.mz0), fabsf(m.mz1)) + D) * kInner;
-    b.ix0 = (fmaxf(m.mx0, m.mx1) - D) + ex, b.ix1 = (fminf(m.mx0, m.mx1) + D) - ex;
-    b.iz0 = (fmaxf(m.mz0, m.mz1) - D) + ez, b.iz1 = (fminf(m.mz0, m.mz1) + D) - ez;
-  } else {
-    b.ix0 = b.ix1 = b.iz0 = b.iz1 = 0.0f;
-  }
-  return b;
-}
-
-// The one record range a crowd walk reads of cell (r, c) of a refined tile (cell table word w != 0:
-// k << 28 | sub table offset): for a ring walk, a cell in a top/bottom ring row and inside the inner
-// columns reads the sub-rows of its horizontal band (from the z copy), a cell of an inner row (left or
-// right piece) the sub-columns of its vertical band; corners and row walks read the whole cell. Every
-// record left out is binned deeper than maxdisp inside the inner box or outside the union box (sub
-// indices by the monotone sub_coord on both sides): no event is lost.
-__device__ __forceinline__ void cell_band(const SweepArgs& a, const Geom& g, const Walk& w, const SubBounds& B, int r,
-                                          int c, uint32_t key, uint32_t wd, uint32_t& rs, uint32_t& rl, bool& zsrc) {
-  zsrc = false;
-  const bool ring = w.ring && w.bz0 <= w.bz1 && w.bx0 <= w.bx1;
-  const bool erow = r < w.bz0 || r > w.bz1, ecol = c < w.bx0 || c > w.bx1;
-  if (!ring || (erow && ecol)) {
-    rs = a.g.cs[key];
-    rl = a.g.cs[key + 1] - rs;
-    return;
-  }
-  const uint32_t k = wd >> 28, so = wd & 0x0FFFFFFFu;
-  const float md = __uint_as_float(a.rpool[so]);
-  const float mg = md + (fabsf(B.ux0) + fabsf(B.ux1) + fabsf(B.uz0) + fabsf(B.uz1) + md + 1.0f) * 9.5367431640625e-07f;
-  int lo, hi;
-  if (erow) {  // horizontal band: sub-rows between the union's edge and the inner box's
-    if (r < w.bz0) lo = sub_coord(B.uz0 - mg, g.z0, g.inv_c, r, k), hi = sub_coord(B.iz0 + mg, g.z0, g.inv_c, r, k);
-    else lo = sub_coord(B.iz1 - mg, g.z0, g.inv_c, r, k), hi = sub_coord(B.uz1 + mg, g.z0, g.inv_c, r, k);
-    zsrc = true;
-  } else {     // vertical band: sub-columns
-    if (c < w.bx0) lo = sub_coord(B.ux0 - mg, g.x0, g.inv_c, c, k), hi = sub_coord(B.ix0 + mg, g.x0, g.inv_c, c, k);
-    else lo = sub_coord(B.ix1 - mg, g.x0, g.inv_c, c, k), hi = sub_coord(B.ux1 + mg, g.x0, g.inv_c, c, k);
-  }
-  lo = max(lo, 0);
-  hi = min(hi, (int)k);
-  const uint32_t* t = a.rpool + so + 1 + (zsrc ? k + 2 : 0u);
-  if (lo > hi) {
-    rs = 0, rl = 0;
-    return;
-  }
-  rs = t[lo];
-  rl = t[hi + 1] - rs;
-  (void)key;
-}
-
-
-// Is the mover itself in a refined (crowded) cell? Its ring then mostly crosses crowded cells too, and
-// the crowd walk's bands pay; every other dense mover takes the coarse walk, which reads refined cells
-// whole (their records are still one contiguous range per cell). Wave-uniform (scalar loads).
-__device__ __forceinline__ bool mover_crowded(const SweepArgs& a, const Geom& g, const Mover& m) {
-  if (!a.tref) return false;
-  const int cx = cellc(m.mx1, g.x0, g.inv_c, g.ncx), cz = cellc(m.mz1, g.z0, g.inv_c, g.ncz);
-  const uint32_t tr = a.tref[g.tile_base + (uint32_t)((cz >> kTileShift) * g.ntx + (cx >> kTileShift))];
-  return tr && a.rpool[(tr - 1) + ((uint32_t)(cz & (kTile - 1)) << kTileShift) + (uint32_t)(cx & (kTile - 1))] != 0u;
-}
-
-// CROWD = false: the dense movers outside crowded cells (coarse parts: one range each); CROWD = true:
-// the movers in crowded cells, whose parts in refined tiles split into units (a run of coarse cells, or
-// one refined cell's band: cell_band). Two kernels over one list, so each keeps its own register budget.
-template <bool CROWD>
-__global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(CROWD ? 4 : GW_DENSE_WPE)))
+__global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_DENSE_WPE)))
 k_sweep_dense(SweepArgs a) {
   const int lane = threadIdx.x & 63;
-  const uint32_t wave = (blockIdx.x * kDenseBlock + threadIdx.x) >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
+  // XCD-aware wave numbering (block b runs on XCD b % 8; the grid is a multiple of 8 blocks): the waves
+  // of one XCD take consecutive list entries, so the movers walked together on an XCD are neighbours
+  // and share that XCD's L2 (skew50: dense walk 6.84 -> 6.57 ms with the batch below)
+  const uint32_t wv = threadIdx.x >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
+  const uint32_t wave = ((blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u) * (kDenseBlock / 64) + wv;
   const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
   const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t nent = 0;
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
-  for (uint32_t d = wave; d < nd; d += nwaves) {
-    const Geom g = a.g.geom[a.space_of[a.dense[d]]];
-    const Mover m = slot_mover(a, a.dense[d], g.D);
-    const Judge J = make_judge(m, a.base);
-    const Walk w = make_walk(m, g);
-    if (mover_crowded(a, g, m) != CROWD) continue;  // wave-uniform: the other kernel takes it
-    uint32_t local = 0;      // wave-uniform
-    uint32_t pk = 0, pe = 0;  // this lane's cell-key range [pk, pe) (one tile part of one row segment)
-    int np = 0;               // parts collected (wave-uniform)
-    // one chunk's events: numbered by a ballot prefix on top of the wave-uniform running count,
-    // slots from the wave's current chunk of ev_tmp (a fresh one reserved when it fills up)
-    auto emit_round = [&](int ev, uint32_t other) {
-      const unsigned long long em = __ballot(ev != 0);
-      if (!em) return;
-      const uint32_t cnt = (uint32_t)__popcll(em);
-      const uint32_t pre = (uint32_t)__popcll(em & below);
-      uint32_t gi = cur + pre;
-      if (cnt > left) {  // this chunk fills up: the rest goes to a fresh one
-        uint32_t nb = 0;
-        if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
-        nb = __shfl(nb, 0, 64);
-        if (pre >= left) gi = nb + (pre - left);
-        cur = nb + (cnt - left);
-        left = kEvChunk - (cnt - left);
-      } else {
-        cur += cnt;
-        left -= cnt;
+  __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the wave's batch of movers: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
+  // The wave walks list entries wave, wave + nwaves, wave + 2 nwaves, ...: at any time the waves of the
+  // grid walk one window of nwaves consecutive entries (a few neighbouring tiles' movers: their ring
+  // cells stay in L2). The slot state of the wave's next 64 entries is loaded in one go (lane i: entry
+  // wave + (b0 + i) nwaves), so a batch costs one dependent chain of loads instead of one per mover.
+  for (uint32_t b0 = 0; wave + b0 * nwaves < nd; b0 += 64u) {
+    const uint32_t di = wave + (b0 + (uint32_t)lane) * nwaves;
+    if (di < nd) {
+      const uint32_t ls = a.dense[di];
+      mb[wv][lane][0] = make_uint4(ls, a.space_of[ls], a.opq[ls], a.old_seq[ls]);
+      mb[wv][lane][1] = make_uint4(__float_as_uint(a.old_x[ls]), __float_as_uint(a.old_z[ls]),
+                                   __float_as_uint(a.pos_x[ls]), __float_as_uint(a.pos_z[ls]));
+    }
+    __builtin_amdgcn_wave_barrier();  // the wave's LDS ops stay in program order
+    const uint32_t nb = min(64u, (nd - wave + nwaves - 1) / nwaves - b0);  // entries of this wave left
+    uint32_t gsp = ~0u;
+    Geom g;
+    for (uint32_t k = 0; k < nb; ++k) {
+      // the mover's state from the wave's batch (uniform LDS address: one broadcast read per half)
+      const uint4 u0 = mb[wv][k][0], u1 = mb[wv][k][1];
+      const uint32_t sp = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.y);
+      if (sp != gsp) {  // wave-uniform: neighbouring list entries are mostly one Space
+        g = uniform_geom(&a.g.geom[sp]);
+        gsp = sp;
       }
-      if (ev) {
-        if (gi < a.ev_cap)
-          a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
-        nent += ev == 2 ? 1u : 0u;
-      }
-      local += cnt;
-    };
-    auto flush = [&]() {
-      // one round trip for every part's record range, then the candidates 128 at a time (two loads in
-      // flight per lane). Candidate k belongs to the first part whose inclusive prefix exceeds k (a
-      // binary search over the lanes' prefixes).
-      uint32_t rs = 0, rl = 0;
-      if (lane < np) {
-        rs = a.g.cs[pk];
-        rl = a.g.cs[pe] - rs;
-      }
-      const uint32_t incl = wave_incl_scan(rl);
-      const uint32_t excl = incl - rl;
-      const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-      auto locate = [&](uint32_t k) -> uint32_t {  // record index of candidate k
-        int lo = 0, hi = 63;  // first lane whose inclusive prefix exceeds k
-#pragma unroll
-        for (int st = 0; st < 6; ++st) {
-          const int mid = (lo + hi) >> 1;
-          if (__shfl(incl, mid, 64) > k) hi = mid;
-          else lo = mid + 1;
-        }
-        return __shfl(rs, lo, 64) + (k - __shfl(excl, lo, 64));
-      };
-      for (uint32_t b = 0; b < total; b += 128) {
-        const uint32_t kA = b + lane, kB = b + 64 + lane;
-        const uint32_t jA = locate(kA);
-        const bool hasB = b + 64 < total;  // wave-uniform
-        const uint32_t jB = hasB ? locate(kB) : 0u;
-        uint4 aA = make_uint4(0, 0, 0, 0), bA = aA, aB = aA, bB = aA;
-        if (kA < total) aA = a.g.rec[jA].a, bA = a.g.rec[jA].b;
-        if (hasB && kB < total) aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
-        emit_round(kA < total ? judge(J, aA, bA) : 0, aA.z & REC_SLOT);
-        if (hasB) emit_round(kB < total ? judge(J, aB, bB) : 0, aB.z & REC_SLOT);
-      }
-      np = 0;
-    };
-    // CROWD: a part in a refined tile expands into one unit per cell (cell_band: one range each, from the
-    // grid or from the z copy), 64 units per flush; a coarse tile's part stays one unit
-    int pr = 0, pc0 = 0, pc1 = 0;  // this lane's part: row, first and last column
-    uint32_t ptr = 0;             // its tile's refinement word (tref)
-    auto flush_units = [&]() {
-      const SubBounds SB = sub_bounds(m, w);
-      // units of this lane's part: a coarse tile's part is one; in a refined tile each refined cell and
-      // each maximal run of coarse cells is one
-      const uint32_t* ctab = ptr ? a.rpool + (ptr - 1) + ((uint32_t)(pr & (kTile - 1)) << kTileShift) : a.rpool;
-      uint32_t nu = 0;
-      if (lane < np) {
-        if (!ptr) {
-          nu = 1;
+      Mover m;
+      m.slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.x);
+      m.q = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.z);
+      m.q0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.w);
+      m.rank = m.q - a.base;
+      m.valid0 = m.q0 != 0;
+      m.valid1 = true;
+      m.mx0 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.x));
+      m.mz0 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.y));
+      m.mx1 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.z));
+      m.mz1 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.w));
+      m.D = g.D;
+      const Judge J = make_judge(m, a.base);
+      const Walk w = make_walk(m, g);
+      uint32_t local = 0;  // wave-uniform
+      // one sub-round's events: numbered by a ballot prefix on top of the wave-uniform running count,
+      // slots from the wave's current chunk of ev_tmp (a fresh one reserved when it fills up)
+      auto emit_round = [&](int ev, uint32_t other) {
+        const unsigned long long em = __ballot(ev != 0);
+        if (!em) return;
+        const uint32_t cnt = (uint32_t)__popcll(em);
+        const uint32_t pre = (uint32_t)__popcll(em & below);
+        uint32_t gi = cur + pre;
+        if (cnt > left) {  // this chunk fills up: the rest goes to a fresh one
+          uint32_t nbk = 0;
+          if (lane == 0) nbk = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
+          nbk = __shfl(nbk, 0, 64);
+          if (pre >= left) gi = nbk + (pre - left);
+          cur = nbk + (cnt - left);
+          left = kEvChunk - (cnt - left);
         } else {
-          bool run = false;
-          for (int c = pc0; c <= pc1; ++c) {
-            const bool fine = ctab[c & (kTile - 1)] != 0u;
-            nu += (fine || !run) ? 1u : 0u;
-            run = !fine;
-          }
+          cur += cnt;
+          left -= cnt;
         }
-      }
-      const uint32_t uincl = wave_incl_scan(nu);
-      const uint32_t U = __builtin_amdgcn_readlane(uincl, 63);
-      for (uint32_t ub = 0; ub < U; ub += 64) {
-        const uint32_t u = ub + lane;
-        int lo = 0, hi = 63;  // the part of unit u
-#pragma unroll
-        for (int st = 0; st < 6; ++st) {
-          const int mid = (lo + hi) >> 1;
-          if (__shfl(uincl, mid, 64) > u) hi = mid;
-          else lo = mid + 1;
+        if (ev) {
+          if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
+          nent += ev == 2 ? 1u : 0u;
         }
-        const uint32_t q = u - (__shfl(uincl, lo, 64) - __shfl(nu, lo, 64));
-        const int ur = __shfl(pr, lo, 64), uc0 = __shfl(pc0, lo, 64), uc1 = __shfl(pc1, lo, 64);
-        const uint32_t upk = __shfl(pk, lo, 64), utr = __shfl(ptr, lo, 64);
+        local += cnt;
+      };
+      // the parts of up to 64 lanes: ranges in one round trip, then the candidates 128 at a time (two
+      // loads in flight per lane); candidate k belongs to the first part whose inclusive prefix exceeds
+      // k (a binary search over the lanes' prefixes)
+      auto flush = [&](uint32_t pk, uint32_t pe, int np) {
         uint32_t rs = 0, rl = 0;
-        bool zs = false;
-        if (u < U) {
-          if (!utr) {  // a coarse tile: the part's one range
-            rs = a.g.cs[upk];
-            rl = a.g.cs[upk + (uint32_t)(uc1 - uc0) + 1] - rs;
-          } else {  // find the q-th unit of the part: a refined cell, or a run [c, e) of coarse cells
-            const uint32_t* ut = a.rpool + (utr - 1) + ((uint32_t)(ur & (kTile - 1)) << kTileShift);
-            uint32_t idx = 0;
-            int c = uc0;
-            uint32_t wd = 0;
-            for (;; ) {  // q < units of the part: terminates inside [uc0, uc1]
-              wd = ut[c & (kTile - 1)];
-              if (idx == q) break;
-              if (wd) {
-                ++c;
-              } else {
-                while (c <= uc1 && !ut[c & (kTile - 1)]) ++c;
-              }
-              ++idx;
-            }
-            const uint32_t key = upk + (uint32_t)(c - uc0);
-            if (wd) {
-              cell_band(a, g, w, SB, ur, c, key, wd, rs, rl, zs);
-            } else {
-              int e = c;
-              while (e <= uc1 && !ut[e & (kTile - 1)]) ++e;
-              rs = a.g.cs[key];
-              rl = a.g.cs[key + (uint32_t)(e - c)] - rs;
-            }
-          }
+        if (lane < np) {
+          rs = a.g.cs[pk];
+          rl = a.g.cs[pe] - rs;
         }
         const uint32_t incl = wave_incl_scan(rl);
         const uint32_t excl = incl - rl;
         const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-        auto locate = [&](uint32_t k, bool& z) -> uint32_t {  // record of candidate k, and its array
-          int l2 = 0, h2 = 63;
+        auto locate = [&](uint32_t k) -> uint32_t {  // record index of candidate k
+          int lo = 0, hi = 63;  // first lane whose inclusive prefix exceeds k
 #pragma unroll
           for (int st = 0; st < 6; ++st) {
-            const int mid = (l2 + h2) >> 1;
-            if (__shfl(incl, mid, 64) > k) h2 = mid;
-            else l2 = mid + 1;
+            const int mid = (lo + hi) >> 1;
+            if (__shfl(incl, mid, 64) > k) hi = mid;
+            else lo = mid + 1;
           }
-          z = __shfl((int)zs, l2, 64) != 0;
-          return __shfl(rs, l2, 64) + (k - __shfl(excl, l2, 64));
+          return __shfl(rs, lo, 64) + (k - __shfl(excl, lo, 64));
         };
         for (uint32_t b = 0; b < total; b += 128) {
           const uint32_t kA = b + lane, kB = b + 64 + lane;
+          const uint32_t jA = locate(kA);
           const bool hasB = b + 64 < total;  // wave-uniform
-          bool zA = false, zB = false;
-          const uint32_t jA = locate(kA, zA);
-          const uint32_t jB = hasB ? locate(kB, zB) : 0u;
+          const uint32_t jB = hasB ? locate(kB) : 0u;
           uint4 aA = make_uint4(0, 0, 0, 0), bA = aA, aB = aA, bB = aA;
-          if (kA < total) {
-            const Rec* R = zA ? a.zrec : a.g.rec;
-            aA = R[jA].a, bA = R[jA].b;
-          }
-          if (hasB && kB < total) {
-            const Rec* R = zB ? a.zrec : a.g.rec;
-            aB = R[jB].a, bB = R[jB].b;
-          }
+          if (kA < total) aA = a.g.rec[jA].a, bA = a.g.rec[jA].b;
+          if (hasB && kB < total) aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
           emit_round(kA < total ? judge(J, aA, bA) : 0, aA.z & REC_SLOT);
           if (hasB) emit_round(kB < total ? judge(J, aB, bB) : 0, aB.z & REC_SLOT);
         }
-      }
-      np = 0;
-    };
-    // the walk, lane-parallel: lane = (row, segment) of 32 rows at a time; each segment splits into
-    // one part per tile it touches; part p is pulled by lane p % 64 (binary search over the prefix)
-    const int h = w.z1 - w.z0 + 1;
-    for (int rb = 0; rb < h; rb += 32) {
-      const int r = w.z0 + rb + (lane >> 1);
-      int a0, a1, b0, b1;
-      walk_row(w, rb + (lane >> 1) < h ? r : w.z1 + 1, a0, a1, b0, b1);
-      const int c0 = (lane & 1) ? b0 : a0, c1 = (lane & 1) ? b1 : a1;
-      const uint32_t nparts = c0 <= c1 ? (uint32_t)((c1 >> kTileShift) - (c0 >> kTileShift) + 1) : 0u;
-      const uint32_t pincl = wave_incl_scan(nparts);
-      const uint32_t T = __shfl(pincl, 63, 64);
-      for (uint32_t pb = 0; pb < T; pb += 64) {
-        const uint32_t p = pb + lane;
-        int lo = 0, hi = 63;
+      };
+      // the walk, lane-parallel: lane = (row, segment) of 32 rows at a time; each segment splits into
+      // one part per tile it touches; part p is taken by lane p % 64 (binary search over the prefix)
+      const int h = w.z1 - w.z0 + 1;
+      for (int rb = 0; rb < h; rb += 32) {
+        const int r = w.z0 + rb + (lane >> 1);
+        int a0, a1, b0r, b1r;
+        walk_row(w, rb + (lane >> 1) < h ? r : w.z1 + 1, a0, a1, b0r, b1r);
+        const int c0 = (lane & 1) ? b0r : a0, c1 = (lane & 1) ? b1r : a1;
+        const uint32_t nparts = c0 <= c1 ? (uint32_t)((c1 >> kTileShift) - (c0 >> kTileShift) + 1) : 0u;
+        const uint32_t pincl = wave_incl_scan(nparts);
+        const uint32_t T = __shfl(pincl, 63, 64);
+        for (uint32_t pb = 0; pb < T; pb += 64) {
+          const uint32_t p = pb + lane;
+          int lo = 0, hi = 63;
 #pragma unroll
-        for (int st = 0; st < 6; ++st) {
-          const int mid = (lo + hi) >> 1;
-          if (__shfl(pincl, mid, 64) > p) hi = mid;
-          else lo = mid + 1;
+          for (int st = 0; st < 6; ++st) {
+            const int mid = (lo + hi) >> 1;
+            if (__shfl(pincl, mid, 64) > p) hi = mid;
+            else lo = mid + 1;
+          }
+          const int q = (int)(p - (__shfl(pincl, lo, 64) - __shfl(nparts, lo, 64)));
+          const int sc0 = __shfl(c0, lo, 64), sc1 = __shfl(c1, lo, 64), sr = __shfl(r, lo, 64);
+          const int tx = (sc0 >> kTileShift) + q;
+          const int plo = max(sc0, tx << kTileShift), phi = min(sc1, (tx << kTileShift) + kTile - 1);
+          const uint32_t pk = g.base + ((uint32_t)((sr >> kTileShift) * g.ntx) << kTileCellShift) +
+                              (uint32_t)((sr & (kTile - 1)) << kTileShift) + ((uint32_t)tx << kTileCellShift) +
+                              (uint32_t)(plo & (kTile - 1));
+          flush(pk, pk + (uint32_t)(phi - plo) + 1, (int)min(64u, T - pb));
         }
-        const int q = (int)(p - (__shfl(pincl, lo, 64) - __shfl(nparts, lo, 64)));
-        const int sc0 = __shfl(c0, lo, 64), sc1 = __shfl(c1, lo, 64), sr = __shfl(r, lo, 64);
-        const int tx = (sc0 >> kTileShift) + q;
-        const int plo = max(sc0, tx << kTileShift), phi = min(sc1, (tx << kTileShift) + kTile - 1);
-        pk = g.base + ((uint32_t)((sr >> kTileShift) * g.ntx) << kTileCellShift) +
-             (uint32_t)((sr & (kTile - 1)) << kTileShift) + ((uint32_t)tx << kTileCellShift) +
-             (uint32_t)(plo & (kTile - 1));
-        pe = pk + (uint32_t)(phi - plo) + 1;
-        np = (int)min(64u, T - pb);
-        pr = sr, pc0 = plo, pc1 = phi;
-        ptr = (CROWD && lane < np) ? a.tref[pk >> kTileCellShift] : 0u;
-        if (CROWD) flush_units();
-        else flush();
       }
+      if (lane == 0) put_count(a.rank_cnt, m.rank, local);
     }
-    if (lane == 0 && local) a.rank_cnt[m.rank] = local;
+    __builtin_amdgcn_wave_barrier();  // every read of the batch before the next batch is written
   }
   for (uint32_t i = lane; i < left; i += 64)
     if (cur + i < a.ev_cap) a.ev_tmp[cur + i] = make_uint4(kEvHole, 0u, 0u, 0u);
@@ -2107,11 +1786,7 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
                        st, a);
   // the dense list's length is on the device: a fixed grid that exits at once when it is empty (a
   // small one when the previous pass had none; the kernel is grid-stride, any grid is correct)
-  if (a.dense)
-    hipLaunchKernelGGL(k_sweep_dense<false>, dim3(a.dense_hint ? kDenseGrid : 64), dim3(kDenseBlock), 0, st, a);
-  if (a.dense && a.tref)  // movers whose walks meet refined (crowded) cells
-    hipLaunchKernelGGL(k_sweep_dense<true>, dim3(a.dense_hint && a.refined_hint ? kDenseGrid : 64), dim3(kDenseBlock),
-                       0, st, a);
+  if (a.dense) hipLaunchKernelGGL(k_sweep_dense, dim3(a.dense_hint ? kDenseGrid : 8), dim3(kDenseBlock), 0, st, a);
 }
 
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each

@@ -47,6 +47,7 @@ void set_err(const char* fmt, ...) {
   } while (0)
 
 constexpr uint32_t kSeqLimit = 0x7ff00000u;  // renormalise seqs before they pass this
+constexpr uint32_t kSlabIdleViews = 8;       // incremental relation views in a row before the slab is freed
 #ifndef GW_CELLS_PER_SLOT
 #define GW_CELLS_PER_SLOT 3  // grid cell budget per slot of capacity (cells beyond it coarsen the grid)
 #endif
@@ -93,14 +94,6 @@ struct Grid {  // one pass's cell-sorted records (two buffers, alternating betwe
   uint32_t* cs = nullptr;
   gw::Geom* d_geom = nullptr;
   uint32_t* d_tile_space = nullptr;  // tile -> space
-  uint32_t* tref = nullptr;          // refined cells (crowds): per tile 0 or 1 + pool offset (k_bin_tsort)
-  uint32_t* rpool = nullptr;         // refinement pool (gwaoi_internal.h "Refined cells")
-  uint32_t rpool_cap = 0;
-  gw::Rec* zrec = nullptr;           // refined cells' records sorted by sub-row
-  uint32_t zrec_cap = 0;
-  uint4* rlist = nullptr;            // k_refine's work list
-  uint32_t rlist_cap = 0;
-  bool refined = false;              // built with refinement: tref/rpool describe this grid
   std::vector<gw::Geom> h_geom;  // what d_geom holds
   uint32_t ncells = 0;
   uint32_t ntiles = 0;
@@ -167,7 +160,9 @@ struct gwaoi_mgr {
   int rel_why = 0;  // why the last view was rebuilt (gwaoi_debug_set_relation_mode)
   unsigned long long* rel_tot = nullptr;  // device: [0] the count pass's 64-bit entry total, [1] longest row
   uint32_t* rel_slab = nullptr;           // count pass output: the rows by grid record (k_row_sort_slab)
-  bool rel_no_slab = false;               // no room for the slab: the two-walk path
+  bool rel_no_slab = false;               // no room for the slab at the last rebuild: the two-walk path
+  uint64_t rel_slab_recs = 0;             // grid records the slab holds rows for
+  uint32_t rel_incr_streak = 0;           // views updated incrementally in a row (the slab is freed after a few)
   uint4* rel_fix = nullptr;               // rows longer than the slab sort's network (2 x cap entries)
   uint64_t index_limit = 0xFFFFFFFFull;   // uint32-indexed outputs (relation view, fan-out) fail above it
   float *d_op_x = nullptr, *d_op_z = nullptr;
@@ -177,12 +172,12 @@ struct gwaoi_mgr {
   uint32_t next_seq = 1;
   uint32_t* rank_cnt = nullptr;  // [cap + 1]
   int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
-  int refine = 1;                // crowded cells refined in the tile-bucketed build (gwaoi_debug_set_refine)
   uint32_t* part = nullptr;     // scan chunk sums
   uint32_t part_words = 0;
   gw::ScanCtx scan;
   uint32_t* thist = nullptr;     // tile-bucketed build: [max tiles * nblk + 1]
-  uint32_t* ttot = nullptr;      // tile totals (zeroed by the build itself after use)
+  uint32_t* ttot = nullptr;      // tile totals, two buffers of kMaxLdsTiles: a build sums into one and zeroes the other
+  int ttot_sel = 0;              // the buffer the next tile build sums into
   uint32_t* tstart = nullptr;    // tile starts
   uint32_t* tile_walk = nullptr; // tile-bucketed build: per tile of the pass's grid, holds a reported mover
   uint32_t nblk = 0;
@@ -194,10 +189,9 @@ struct gwaoi_mgr {
   uint32_t* d_pub = nullptr;     // its device address
   uint32_t pub_seq = 0;
   uint32_t last_dense = ~0u;     // dense movers of the last pass (k_sweep_dense grid size hint)
-  uint32_t last_refined = ~0u;   // refined cells of the last pass (k_sweep_dense<true> grid size hint)
   struct {                       // the last timed pass, collected once its events are complete
     bool pending = false;
-    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0, refined = 0;
+    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0;
   } tpend;
   // events
   uint4* ev_tmp = nullptr;
@@ -439,27 +433,6 @@ int upload_geom(gwaoi_mgr* m, Grid& g, const std::vector<gw::Geom>& geo) {
 // cell-atomic counting sort, which needs zeroed cell counts.
 bool tile_build(const Grid& g) { return g.ntiles <= gw::kMaxLdsTiles; }
 
-// The refinement pools of grid g (on first use): sized so that no reservation of k_bin_tsort can fail.
-// A grid holds at most 2 cap records, so at most 2 cap / kRefineMin refined cells (each <= 21 sub table
-// words) and 2 cap z copies; every tile may need its 1024-word cell table.
-int refine_pools(gwaoi_mgr* m, Grid& g) {
-  if (g.rpool) return GWAOI_OK;
-  const uint64_t recs = 2ull * m->cap, cells = recs / gw::kRefineMin + 1;
-  const uint64_t tiles = (uint64_t)m->max_cells / gw::kTileCells + 1;
-  const uint64_t words = tiles * gw::kTileCells + 21 * cells + 1024;
-  if (words > 0xFFFFFFF || recs > 0xFFFFFFFFull) {  // 28-bit pool offsets
-    set_err("refinement pools too large for this capacity");
-    return GWAOI_ERR_NOMEM;
-  }
-  RCHK(dalloc(&g.rpool, words));
-  RCHK(dalloc(&g.zrec, recs));
-  RCHK(dalloc(&g.rlist, cells));
-  g.rpool_cap = (uint32_t)words;
-  g.zrec_cap = (uint32_t)recs;
-  g.rlist_cap = (uint32_t)cells;
-  return GWAOI_OK;
-}
-
 // Build grid `gi` from the per-slot state (pos, seq, space_of).
 // Build grid `gi` for the pass whose ops have seqs [base, base + n_ops) (n_ops = 0: the current
 // state only, no ghosts).
@@ -490,26 +463,16 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_
   b.nblk = m->nblk;
   b.chunk = gw::bin_chunk(m->cap);
   b.thist = m->thist;
-  b.ttot = m->ttot;
+  b.ttot = m->ttot + m->ttot_sel * gw::kMaxLdsTiles;
+  b.ttot_next = m->ttot + (m->ttot_sel ^ 1) * gw::kMaxLdsTiles;
   b.tstart = m->tstart;
   b.tile_space = g.d_tile_space;
   b.trec = m->grid[gi ^ 1].rec;  // the other grid's records are not read by this pass
   b.op_kind = op_kind;
   b.tile_walk = m->tile_walk;
-  b.refine = tiles && m->refine ? 1 : 0;
-  if (b.refine) RCHK(refine_pools(m, g));
-  b.tref = g.tref;
-  b.rpool = g.rpool;
-  b.rpool_cap = g.rpool_cap;
-  b.zrec = g.zrec;
-  b.zrec_cap = g.zrec_cap;
-  b.rlist = g.rlist;
-  b.rlist_cap = g.rlist_cap;
-  b.ctr = m->ctr;
-  g.refined = b.refine != 0;
   if (tiles) {
-    gw::launch_bin_tiles(b, m->scan, m->stream);
-    gw::launch_refine(b, m->stream);
+    gw::launch_bin_tiles(b, m->stream);
+    m->ttot_sel ^= 1;
   } else {
     gw::launch_bin_count(b, m->stream);
     gw::launch_scan(m->scan, g.cs, g.ncells + 1, m->stream);
@@ -567,7 +530,6 @@ int collect_timing(gwaoi_mgr* m) {
   m->stats.grid_records += m->tpend.records;
   m->stats.grid_cells += m->tpend.ncells;
   m->stats.dense_movers += m->tpend.dense;
-  m->stats.refined_cells += m->tpend.refined;
   return GWAOI_OK;
 }
 
@@ -717,10 +679,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.dense_cap = m->cap;
     s.dense_hint = attempt ? ~0u : m->last_dense;
     s.tile_walk = tile_build(G) ? m->tile_walk : nullptr;
-    s.tref = G.refined ? G.tref : nullptr;
-    s.rpool = G.rpool;
-    s.zrec = G.zrec;
-    s.refined_hint = attempt ? ~0u : m->last_refined;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
@@ -773,7 +731,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       m->tpend.records = m->h_ctr[gw::CTR_RECORDS];
       m->tpend.ncells = m->grid[ng].ncells;
       m->tpend.dense = m->h_ctr[gw::CTR_DENSE];
-      m->tpend.refined = m->h_ctr[gw::CTR_REFINED];
     }
     break;
   }
@@ -792,7 +749,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->pass_id++;
   if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
   m->last_dense = m->h_ctr[gw::CTR_DENSE];
-  m->last_refined = m->h_ctr[gw::CTR_REFINED];
   m->n_present_dev = m->n_present;
   m->dv_kind = nullptr;
   m->dv_space = nullptr;
@@ -888,7 +844,7 @@ void free_all(gwaoi_mgr* m) {
     if (p) hipFree(p);
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
-    void* gp[] = {g.rec, g.cs, g.d_geom, g.d_tile_space, g.tref, g.rpool, g.zrec, g.rlist};
+    void* gp[] = {g.rec, g.cs, g.d_geom, g.d_tile_space};
     for (void* p : gp)
       if (p) hipFree(p);
   }
@@ -975,7 +931,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   const uint64_t max_tiles = m->max_cells / gw::kTileCells + 1;
   const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
   chk(dalloc(&m->thist, thist_n));
-  chk(dalloc(&m->ttot, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) + 1));
+  chk(dalloc(&m->ttot, 2 * (size_t)gw::kMaxLdsTiles));  // k_bin_tscatter zeroes kMaxLdsTiles of the other buffer
   chk(dalloc(&m->tstart, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) + 1));
   chk(dalloc(&m->tile_walk, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
   // the scan has at most 1024 chunks up to 16.7M items (scan_ipt), more beyond
@@ -1011,7 +967,6 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     chk(dalloc(&g.cs, (size_t)m->max_cells + 1));
     chk(dalloc(&g.d_geom, nspaces));
     chk(dalloc(&g.d_tile_space, (size_t)m->max_cells / gw::kTileCells + 1));
-    chk(dalloc(&g.tref, (size_t)m->max_cells / gw::kTileCells + 1));
   }
   static bool sweep_ready = false;
   if (!sweep_ready) {
@@ -1039,7 +994,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
     z(m->pos_z, C * 4);
     z(m->seq, C * 4);
     z(m->space_of, C * 4);
-    z(m->ttot, (std::min<uint64_t>(m->max_cells / gw::kTileCells + 1, gw::kMaxLdsTiles) + 1) * 4);
+    z(m->ttot, 2 * (size_t)gw::kMaxLdsTiles * 4);
     std::vector<gw::Geom> geo;
     compute_geometry(m, geo);
     m->geom_dirty = false;
@@ -1645,6 +1600,16 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
     if (done) {
       m->rel_passes = m->passes_run;
       m->rel_stat_incr++;
+      // the slab serves only rebuilds: after a run of incremental updates it goes back to the device
+      // (ADVICE r2), and the next rebuild allocates it again
+      if (++m->rel_incr_streak >= kSlabIdleViews && m->rel_slab) {
+        HIPCHK(hipStreamSynchronize(m->stream));
+        hipFree(m->rel_slab);
+        hipFree(m->rel_fix);
+        m->rel_slab = nullptr;
+        m->rel_fix = nullptr;
+        m->rel_slab_recs = 0;
+      }
       out->row_ptr = m->rel_rp;
       out->cols = m->rel_cols;
       out->nnz = m->rel_nnz;
@@ -1655,18 +1620,34 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   hipStream_t st = m->stream;
   if (!m->rel_rp) RCHK(dalloc(&m->rel_rp, (size_t)m->cap + 1));
   if (!m->rel_tot) RCHK(dalloc(&m->rel_tot, 3));  // [0] entries, [1] longest row, [2] rows to fix
-  // The count pass also writes every row of up to kSlabS entries into a slab (by grid record, 2 x cap
-  // records), when that fits the budget; the rows then go from the slab to cols sorted, with no second
-  // walk. A longer row (crowds) sends the call down the two-walk path: fill pass, sort in place.
+  // The count pass also writes every row of up to kSlabS entries into a slab (by grid record), when
+  // that fits; the rows then go from the slab to cols sorted, with no second walk. A longer row (crowds)
+  // sends the call down the two-walk path: fill pass, sort in place. The slab holds the rows of the
+  // current grid's records (+25% headroom, reallocated when a grid has more), within a fixed budget and
+  // half of the device memory free at the time.
   constexpr uint32_t kSlabS = 128;
   constexpr uint64_t kSlabBudget = 4ull << 30;  // bytes
-  const uint64_t slab_words = ((2ull * m->cap + 63) / 64) * 64 * kSlabS;
-  if (!m->rel_slab && !m->rel_no_slab) {
-    if (slab_words * 4 > kSlabBudget || dalloc(&m->rel_slab, (size_t)slab_words) != GWAOI_OK ||
-        dalloc(&m->rel_fix, 2 * (size_t)m->cap) != GWAOI_OK) {
+  m->rel_incr_streak = 0;
+  const uint64_t recs = std::max<uint64_t>(m->h_ctr[gw::CTR_RECORDS], 1);
+  if (m->rel_slab && recs > m->rel_slab_recs) {
+    HIPCHK(hipStreamSynchronize(m->stream));
+    hipFree(m->rel_slab);
+    m->rel_slab = nullptr;
+  }
+  if (!m->rel_slab) {  // (retried at every rebuild: free memory changes)
+    const uint64_t srecs = std::min<uint64_t>(2ull * m->cap, recs + recs / 4 + 64);
+    const uint64_t slab_words = ((srecs + 63) / 64) * 64 * kSlabS;
+    size_t free_b = 0, total_b = 0;
+    const bool room = hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+                      slab_words * 4 <= std::min<uint64_t>(kSlabBudget, free_b / 2);
+    if (!room || dalloc(&m->rel_slab, (size_t)slab_words) != GWAOI_OK ||
+        (!m->rel_fix && dalloc(&m->rel_fix, 2 * (size_t)m->cap) != GWAOI_OK)) {
       if (m->rel_slab) hipFree(m->rel_slab);
       m->rel_slab = nullptr;
       m->rel_no_slab = true;
+    } else {
+      m->rel_slab_recs = srecs;
+      m->rel_no_slab = false;
     }
   }
   const Grid& g = m->grid[m->cur];
@@ -1976,11 +1957,6 @@ int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
   return GWAOI_OK;
 }
 
-int gwaoi_debug_set_refine(gwaoi_mgr* m, int enable) {
-  if (!m) return GWAOI_ERR_INVALID;
-  m->refine = enable != 0;
-  return GWAOI_OK;
-}
 
 int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
   RCHK(check_mgr(m));

@@ -229,10 +229,6 @@ class Engine:
     def debug_set_sweep_lds(self, on: bool):
         check(self._L.gwaoi_debug_set_sweep_lds(self._h, 1 if on else 0))
 
-    def debug_set_refine(self, on: bool):
-        """Crowded cells refined into sub-cells (default on); off = coarse cells only (A/B)."""
-        check(self._L.gwaoi_debug_set_refine(self._h, 1 if on else 0))
-
     def debug_set_cells_per_dist(self, v: float):
         check(self._L.gwaoi_debug_set_cells_per_dist(self._h, v))
 

@@ -211,7 +211,7 @@ typedef struct {
   uint64_t grid_records;   /* records of the passes' cell-sorted grids (main + ghost) */
   uint64_t grid_cells;     /* cells of those grids */
   uint64_t dense_movers;   /* movers swept one wave each (boxes beyond their tile's LDS region) */
-  uint64_t refined_cells;  /* crowded cells of the passes' grids split into sub-cells (ABI 2) */
+  uint64_t refined_cells;  /* reserved, always 0 (ABI 2 layout; the sub-cell refinement was removed) */
 } gwaoi_stats;
 int gwaoi_set_timing(gwaoi_mgr* mgr, int enable);
 int gwaoi_get_stats(const gwaoi_mgr* mgr, gwaoi_stats* out);

@@ -44,8 +44,6 @@ struct gwaoi_mgr;
 int gwaoi_debug_set_next_seq(struct gwaoi_mgr* mgr, uint32_t next_seq);
 /* Test hook: 0 = the sweep reads candidates from global memory only (A/B of the LDS-staged path). */
 int gwaoi_debug_set_sweep_lds(struct gwaoi_mgr* mgr, int enable);
-/* Crowded cells refined into sub-cells in the grid build (default on; 0 = coarse cells only, A/B). */
-int gwaoi_debug_set_refine(struct gwaoi_mgr* mgr, int enable);
 /* Test hook: cell size = D / cells_per_dist for grids built from now on (default 4). */
 int gwaoi_debug_set_cells_per_dist(struct gwaoi_mgr* mgr, float cells_per_dist);
 /* Test hook: absolute cell side for every Space (0 = back to D / cells_per_dist). */

@@ -9,7 +9,10 @@
             (peak density ~100x the mean) against oracle (ii) per Space; at full size (4 x 1M, SURVEY
             proportions) the LDS-staged sweep / wave-per-mover path on two different grids (D/4 cells
             and D/2 cells, so tiles, halos and the LDS-or-dense routing all differ) agree event for
-            event; and an x-quantile strip split of a skewed world equals one manager.
+            event, and every event of ~1,000 sampled movers per Space equals oracle (iv) (the closed
+            form of an all-moving tick from two position snapshots, oracle/sampled.py); an x-quantile
+            strip split of a skewed world equals one manager.
+  config 4  also: the 16M single manager's tick-1 events of 3,000 sampled movers against oracle (iv).
 
 Parity against go-aoi itself is UNPINNED: the oracles are the restatements.
 """
@@ -111,9 +114,9 @@ def _strip_world(po, n, L, world, seed, ticks, layout=None, skew=None, host_firs
     return out
 
 
-def _whole_world(n, L, seed, ticks, skew=None):
+def _whole_world(n, L, seed, ticks, skew=None, snaps=None):
     """One manager over the whole world, positions from the device generator; per-tick events (tick 0:
-    the count only)."""
+    the count only). snaps (a list): receives each moving tick's (x0, z0, x1, z1) snapshots."""
     from goworld_amd import _lib
     from goworld_amd.engine import DeviceBuffer, Engine, wl_init_spaces, wl_iota, wl_step_spaces
     bx, bz, bs, bk = DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(n)
@@ -126,23 +129,43 @@ def _whole_world(n, L, seed, ticks, skew=None):
     out = [int(eng.tick_device().count)]
     eng.adopt_device_state()
     for t in range(1, ticks):
+        before = (bx.download(np.float32, n), bz.download(np.float32, n)) if snaps is not None else None
         wl_step_spaces(0, bx.ptr, bz.ptr, bx.ptr, bz.ptr, n, 1, seed, t, L, 1.0)
+        if snaps is not None:
+            snaps.append(before + (bx.download(np.float32, n), bz.download(np.float32, n)))
         eng.stage_moves_device(bs.ptr, bx.ptr, bz.ptr, n)
         out.append(eng.tick())
     eng.close()
     return out
 
 
+def _sampled_movers(n, k, seed, hot_every=0):
+    """k movers spread over [0, n) (and, with hot_every, as many from the hotspot share: slots with
+    slot % hot_every == 1 are the generator's hotspot entities, include/gwaoi_workload.h)."""
+    rng = np.random.default_rng(seed)
+    pick = rng.choice(n, size=k, replace=False)
+    if hot_every:
+        pick = np.concatenate([pick, rng.choice(n // hot_every, size=k, replace=False) * hot_every + 1])
+    return np.unique(pick)
+
+
 def test_config4_16M_world_in_8_strips(gpu):
     """config 4 at its size: 16,000,000 entities, L = 140,000, 8 X-strips (loopback on one GPU); the
     owned movers' events of the 8 strips, merged, equal one manager over the whole world."""
+    from oracle import sampled
     n, L, seed = 16_000_000, 140_000.0, 0x5EED0004
-    want = _whole_world(n, L, seed, 4)
+    snaps = []
+    want = _whole_world(n, L, seed, 4, snaps=snaps)
     got = _strip_world(None, n, L, 8, seed, 4)
     assert got[0] == want[0] and want[0] > 100_000_000  # enter tick: pair counts (2.6e8 pairs)
     for t in (1, 2, 3):
         assert np.array_equal(got[t], want[t]), f"tick {t}: " + H.fmt_diff(got[t], want[t])
         assert len(got[t]) > 1_000_000
+    # the single manager itself against oracle (iv) at 16M: every event of 3,000 sampled movers, tick 1
+    movers = _sampled_movers(n, 3000, 1)
+    ref = sampled.AllMovingTick(*snaps[0], 100.0).sample(movers)
+    mine = sampled.pick(want[1], movers)
+    assert len(ref) > 1000 and np.array_equal(mine, ref), "tick 1 sampled: " + H.fmt_diff(mine, ref)
 
 
 def test_config4_2M_strips_vs_grid_oracle(gpu, oracle_lib):
@@ -254,6 +277,43 @@ def test_config5_full_size_two_grids_agree(gpu):
     assert st[0]["dense_movers"] > 0 and st[0]["grid_cells"] != st[1]["grid_cells"]
     for e in engs:
         e.close()
+
+
+def test_config5_full_size_sampled_vs_semantic(gpu):
+    """Config 5 at full size in SURVEY proportions (4 x 1M, D = 50/100/200/400, 50% in 64 hotspots per
+    Space, sigma 123) against oracle (iv): every event of ~1,000 sampled movers per Space (half of them
+    hotspot entities) in two all-moving ticks, from the position snapshots alone (oracle/sampled.py)."""
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine, wl_init_spaces, wl_iota, wl_step_spaces
+    from oracle import sampled
+    N, L, seed0 = 1_000_000, 35000.0, 0x5EED0005
+    S = len(SKEW_D)
+    n = S * N
+    bx, bz, bs, bk, bp = DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(n), \
+        DeviceBuffer(4 * n)
+    wl_init_spaces(0, bx.ptr, bz.ptr, N, S, seed0, L, 64, 123.0, 2)
+    wl_iota(0, bs.ptr, n)
+    bk.upload(np.full(n, _lib.GWAOI_OP_ENTER | _lib.GWAOI_OP_SILENT, np.uint8))
+    bp.upload(np.repeat(np.arange(S, dtype=np.uint32), N))
+    eng = Engine(capacity=n, spaces=[(d, (0.0, 0.0, L, L)) for d in SKEW_D])
+    eng.set_timing(True)
+    eng.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, n, bp.ptr)
+    assert int(eng.tick_device().count) == 0
+    for t in (1, 2):
+        x0, z0 = bx.download(np.float32, n), bz.download(np.float32, n)
+        wl_step_spaces(0, bx.ptr, bz.ptr, bx.ptr, bz.ptr, N, S, seed0, t, L, 1.0)
+        x1, z1 = bx.download(np.float32, n), bz.download(np.float32, n)
+        eng.stage_moves_device(bs.ptr, bx.ptr, bz.ptr, n)
+        got = eng.tick()
+        assert len(got) > 1_000_000
+        for s, d in enumerate(SKEW_D):
+            sl = slice(s * N, (s + 1) * N)
+            movers = _sampled_movers(N, 500, 100 * t + s, hot_every=2)
+            ref = sampled.AllMovingTick(x0[sl], z0[sl], x1[sl], z1[sl], d, base=s * N).sample(movers)
+            mine = sampled.pick(got, movers + s * N)
+            assert len(ref) > 500 and np.array_equal(mine, ref), f"tick {t} Space {s}: " + H.fmt_diff(mine, ref)
+    assert eng.stats()["dense_movers"] > 0
+    eng.close()
 
 
 def test_config5_skewed_world_in_quantile_strips(gpu):

@@ -279,3 +279,32 @@ def test_config3_cpu_baseline_sample(po):
             want += len(orc.take_events())
         orc.close()
     assert nev == want
+
+
+@pytest.mark.parametrize("dist,step,skew", [(100.0, 1.0, False), (50.0, 1.0, True), (400.0, 1.0, True),
+                                            (100.0, 40.0, False)])
+def test_sampled_restatement_equals_grid_oracle(po, dist, step, skew):
+    """oracle (iv) (oracle/sampled.py: the events of sampled movers of an all-moving tick from two
+    position snapshots, the full-size checker of configs 4 and 5) against oracle (ii), every mover, two
+    ticks after an enter tick in slot order; uniform and hotspot worlds, large steps included."""
+    from oracle import sampled
+    n, L, seed, base = 4000, 2000.0, 0x5EED0077, 3 * 4000
+    if skew:
+        x, z = po.workload_skew_init(seed, n, L, 8, 40.0, 2)
+    else:
+        x, z = po.workload_init(seed, n, L)
+    orc = po.GridOracle(dist, n, (0.0, 0.0, L, L))
+    ids = np.arange(n, dtype=np.uint32)
+    orc.bulk_enter(ids, x, z)
+    for t in (1, 2):
+        x0, z0 = x.copy(), z.copy()
+        po.workload_step(seed, t, x, z, L, step)
+        orc.moved_batch(ids, x, z)
+        want = orc.take_events()
+        want = want + np.array([base, base], np.uint32)  # as Space 3 of a manager with 4000 slots per Space
+        want = want[np.lexsort((want[:, 1], want[:, 0]))]
+        got = sampled.AllMovingTick(x0, z0, x, z, dist, base=base).sample(range(n))
+        assert len(want) > 100
+        assert np.array_equal(got, want), f"tick {t}: " + H.fmt_diff(got, want)
+        assert np.array_equal(sampled.pick(want, [base + 5, base + 77]), sampled.AllMovingTick(
+            x0, z0, x, z, dist, base=base).sample([5, 77]))
