@@ -976,39 +976,13 @@ __device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const 
 // when the event is queued). Two candidates per iteration, both LDS reads in flight, their two bits
 // merged before the 64-bit shift, and one (rarely taken) branch per pair for the exact tests. No
 // atomic or LDS write sits in the candidate loop itself. (32-candidate chunks with 32-bit masks: the
-// register allocator spills 5x more in this kernel, measured slower.)
+// register allocator spills 5x more in this kernel, measured slower; the next pair's LDS reads issued
+// before the current pair is judged: 94.9 -> 96.3 us at config 2.)
 template <class IdxF>
 __device__ __forceinline__ unsigned long long judge_chunk(const SweepSmem& sm, const Judge& J, uint32_t b,
                                                           uint32_t total, IdxF&& idx) {
   const uint32_t n = b < total ? min(total - b, 64u) : 0u;
   unsigned long long hit = 0;
-#ifndef GW_JUDGE_PIPE
-#define GW_JUDGE_PIPE 1
-#endif
-#if GW_JUDGE_PIPE
-  // software-pipelined: the next pair's LDS reads are issued before the current pair is judged, so a
-  // wave's LDS latency overlaps its own VALU work (a phantom candidate past n re-reads the last one and
-  // its bit is dropped)
-  if (n == 0) return 0;
-  auto at = [&](uint32_t k) { return idx(b + min(k, n - 1)); };
-  uint32_t j0 = at(0), j1 = at(1);
-  uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
-  uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
-  for (uint32_t k = 0; k < n; k += 2) {
-    j0 = at(k + 2), j1 = at(k + 3);
-    const uint4 np0 = sm.rp[j0], np1 = sm.rp[j1];
-    const uint2 nq0 = sm.rm[j0], nq1 = sm.rm[j1];
-    bool n0, n1;
-    bool h0 = judge_fast(J, p0, q0, n0), h1 = judge_fast(J, p1, q1, n1);
-    if (GW_JUDGE_EXACT || __builtin_expect(n0 | n1, 0)) {
-      h0 = judge_lds(J, p0, q0) != 0;
-      h1 = judge_lds(J, p1, q1) != 0;
-    }
-    h1 = h1 && k + 1 < n;
-    hit |= (unsigned long long)((uint32_t)h0 | ((uint32_t)h1 << 1)) << k;
-    p0 = np0, p1 = np1, q0 = nq0, q1 = nq1;
-  }
-#else
   uint32_t k = 0;
   for (; k + 1 < n; k += 2) {
     const uint32_t j0 = idx(b + k), j1 = idx(b + k + 1);
@@ -1026,7 +1000,6 @@ __device__ __forceinline__ unsigned long long judge_chunk(const SweepSmem& sm, c
     const uint32_t j0 = idx(b + k);
     hit |= (unsigned long long)(judge_lds(J, sm.rp[j0], sm.rm[j0]) != 0) << k;
   }
-#endif
   return hit;
 }
 
@@ -1622,6 +1595,26 @@ constexpr int kDenseGrid = 256 * GW_DENSE_WPE;  // GW_DENSE_WPE waves per SIMD: 
 constexpr uint32_t kEvChunk = GW_EV_CHUNK;  // event slots a wave reserves at a time (one returning atomic
                                       // on the shared counter each: ~11 ns apiece when serialised)
 
+// Diagnostic build only (GW_STAMPS=1): per-wave cycle accounting of the dense walk's phases, summed over
+// the waves into the last 16 words of gw_stamps (bench.py --stamps): [0] batch loads, [1] mover setup,
+// [2] part enumeration, [3] range loads, [4] candidate rounds, [8] movers, [9] flushes, [10] rounds.
+#if GW_STAMPS
+#define GW_DPH(k)                                           \
+  do {                                                      \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    dph[k] += t_ - dt0;                                     \
+    dt0 = t_;                                               \
+  } while (0)
+#define GW_DCNT(k) (++dph[k])
+#else
+#define GW_DPH(k) \
+  do {            \
+  } while (0)
+#define GW_DCNT(k) \
+  do {             \
+  } while (0)
+#endif
+
 __global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_DENSE_WPE)))
 k_sweep_dense(SweepArgs a) {
   const int lane = threadIdx.x & 63;
@@ -1635,6 +1628,9 @@ k_sweep_dense(SweepArgs a) {
   uint32_t nent = 0;
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
   __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the wave's batch of movers: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
+#if GW_STAMPS
+  unsigned long long dph[16] = {}, dt0 = __builtin_amdgcn_s_memtime();
+#endif
   // The wave walks list entries wave, wave + nwaves, wave + 2 nwaves, ...: at any time the waves of the
   // grid walk one window of nwaves consecutive entries (a few neighbouring tiles' movers: their ring
   // cells stay in L2). The slot state of the wave's next 64 entries is loaded in one go (lane i: entry
@@ -1648,6 +1644,7 @@ k_sweep_dense(SweepArgs a) {
                                    __float_as_uint(a.pos_x[ls]), __float_as_uint(a.pos_z[ls]));
     }
     __builtin_amdgcn_wave_barrier();  // the wave's LDS ops stay in program order
+    GW_DPH(0);
     const uint32_t nb = min(64u, (nd - wave + nwaves - 1) / nwaves - b0);  // entries of this wave left
     uint32_t gsp = ~0u;
     Geom g;
@@ -1674,6 +1671,8 @@ k_sweep_dense(SweepArgs a) {
       const Judge J = make_judge(m, a.base);
       const Walk w = make_walk(m, g);
       uint32_t local = 0;  // wave-uniform
+      GW_DCNT(8);
+      GW_DPH(1);
       // one sub-round's events: numbered by a ballot prefix on top of the wave-uniform running count,
       // slots from the wave's current chunk of ev_tmp (a fresh one reserved when it fills up)
       auto emit_round = [&](int ev, uint32_t other) {
@@ -1711,6 +1710,8 @@ k_sweep_dense(SweepArgs a) {
         const uint32_t incl = wave_incl_scan(rl);
         const uint32_t excl = incl - rl;
         const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        GW_DCNT(9);
+        GW_DPH(3);
         auto locate = [&](uint32_t k) -> uint32_t {  // record index of candidate k
           int lo = 0, hi = 63;  // first lane whose inclusive prefix exceeds k
 #pragma unroll
@@ -1731,7 +1732,9 @@ k_sweep_dense(SweepArgs a) {
           if (hasB && kB < total) aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
           emit_round(kA < total ? judge(J, aA, bA) : 0, aA.z & REC_SLOT);
           if (hasB) emit_round(kB < total ? judge(J, aB, bB) : 0, aB.z & REC_SLOT);
+          GW_DCNT(10);
         }
+        GW_DPH(4);
       };
       // the walk, lane-parallel: lane = (row, segment) of 32 rows at a time; each segment splits into
       // one part per tile it touches; part p is taken by lane p % 64 (binary search over the prefix)
@@ -1760,6 +1763,7 @@ k_sweep_dense(SweepArgs a) {
           const uint32_t pk = g.base + ((uint32_t)((sr >> kTileShift) * g.ntx) << kTileCellShift) +
                               (uint32_t)((sr & (kTile - 1)) << kTileShift) + ((uint32_t)tx << kTileCellShift) +
                               (uint32_t)(plo & (kTile - 1));
+          GW_DPH(2);
           flush(pk, pk + (uint32_t)(phi - plo) + 1, (int)min(64u, T - pb));
         }
       }
@@ -1772,6 +1776,10 @@ k_sweep_dense(SweepArgs a) {
   if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
   const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);  // one add per wave, not per lane
   if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
+#if GW_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 16; ++k) atomicAdd(&gw_stamps[kStampWords * 16383 + k], dph[k]);
+#endif
 }
 
 void launch_sweep(const SweepArgs& a, hipStream_t st) {

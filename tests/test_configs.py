@@ -12,7 +12,7 @@
             event, and every event of ~1,000 sampled movers per Space equals oracle (iv) (the closed
             form of an all-moving tick from two position snapshots, oracle/sampled.py); an x-quantile
             strip split of a skewed world equals one manager.
-  config 4  also: the 16M single manager's tick-1 events of 3,000 sampled movers against oracle (iv).
+  config 4  also: the 16M single manager's tick-1 events of 8,000 sampled movers against oracle (iv).
 
 Parity against go-aoi itself is UNPINNED: the oracles are the restatements.
 """
@@ -161,8 +161,8 @@ def test_config4_16M_world_in_8_strips(gpu):
     for t in (1, 2, 3):
         assert np.array_equal(got[t], want[t]), f"tick {t}: " + H.fmt_diff(got[t], want[t])
         assert len(got[t]) > 1_000_000
-    # the single manager itself against oracle (iv) at 16M: every event of 3,000 sampled movers, tick 1
-    movers = _sampled_movers(n, 3000, 1)
+    # the single manager itself against oracle (iv) at 16M: every event of 8,000 sampled movers, tick 1
+    movers = _sampled_movers(n, 8000, 1)
     ref = sampled.AllMovingTick(*snaps[0], 100.0).sample(movers)
     mine = sampled.pick(want[1], movers)
     assert len(ref) > 1000 and np.array_equal(mine, ref), "tick 1 sampled: " + H.fmt_diff(mine, ref)
