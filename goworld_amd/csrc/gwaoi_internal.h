@@ -110,6 +110,7 @@ struct BinArgs {
   const uint32_t* opq;
   uint32_t base, n_ops;
   const Geom* geom;
+  uint32_t nspaces;
   uint32_t cap;
   uint32_t* key_of;    // [2 cap]: main / ghost key per slot (kNoKey = none)
   uint32_t* local_of;  // [2 cap]

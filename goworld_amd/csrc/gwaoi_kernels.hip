@@ -135,23 +135,21 @@ struct SlotState {
   uint32_t q0, q1, oq;
 };
 
+// (the start-of-pass fields are loaded whatever opq says, so all seven loads of a slot are in flight
+// together instead of waiting for opq first)
 __device__ __forceinline__ SlotState slot_state(const BinArgs& a, uint32_t s) {
   SlotState t;
   t.oq = a.opq[s];
-  t.acted = (t.oq - a.base) < a.n_ops;
   t.q1 = a.seq[s];
-  t.p_end = t.q1 != 0;
   t.x1 = a.pos_x[s];
   t.z1 = a.pos_z[s];
-  if (t.acted) {
-    t.q0 = a.old_seq[s];
-    t.x0 = a.old_x[s];
-    t.z0 = a.old_z[s];
-  } else {
-    t.q0 = t.q1;
-    t.x0 = t.x1;
-    t.z0 = t.z1;
-  }
+  const uint32_t q0 = a.old_seq[s];
+  const float x0 = a.old_x[s], z0 = a.old_z[s];
+  t.acted = (t.oq - a.base) < a.n_ops;
+  t.p_end = t.q1 != 0;
+  t.q0 = t.acted ? q0 : t.q1;
+  t.x0 = t.acted ? x0 : t.x1;
+  t.z0 = t.acted ? z0 : t.z1;
   t.p_start = t.q0 != 0;
   return t;
 }
@@ -198,15 +196,27 @@ void launch_bin_scatter(const BinArgs& a, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Exclusive scan (u32) building blocks: wave64 prefix sums by __shfl_up, block scan over 256 threads.
+// Exclusive scan (u32) building blocks: wave64 prefix sums, block scan over 256 threads.
 
+// Inclusive wave64 scan through DPP lane moves (row_shr 1/2/4/8 inside rows of 16 lanes, then
+// row_bcast 15/31 across rows: gfx9 wave64 DPP), i.e. VALU ops instead of the six LDS-crossbar round
+// trips of __shfl_up (dense walk: skew 3.07 -> 2.90 ms; k_sweep's staging scans: 95.1 -> 93.8 us).
+// Every lane of the wave must be active.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
+  const int lane = threadIdx.x & 63, rl = lane & 15;
+  int t;
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  if (rl >= 1) v += (uint32_t)t;
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  if (rl >= 2) v += (uint32_t)t;
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  if (rl >= 4) v += (uint32_t)t;
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  if (rl >= 8) v += (uint32_t)t;
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+  if ((lane & 31) >= 16) v += (uint32_t)t;
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+  if (lane >= 32) v += (uint32_t)t;
   return v;
 }
 
@@ -349,11 +359,21 @@ __device__ __forceinline__ uint32_t bin_chunk_of(uint32_t b, uint32_t nblk) {
   return x * per + min(x, rem) + b / 8u;
 }
 
+// The Spaces' geometry in LDS for the build kernels when there are few Spaces (one load chain less per
+// slot: space_of -> geometry becomes space_of -> LDS); more Spaces read it from global memory.
+constexpr uint32_t kLdsGeoms = 64;
+__device__ __forceinline__ const Geom* bin_geoms(const BinArgs& a, Geom* gs) {
+  if (a.nspaces > kLdsGeoms) return a.geom;
+  for (uint32_t i = threadIdx.x; i < a.nspaces; i += blockDim.x) gs[i] = a.geom[i];
+  return gs;  // (the caller's barrier makes them visible)
+}
+
 // keys of slot s's main (k1) and ghost (k0) records, kNoKey for none
-__device__ __forceinline__ void bin_keys(const BinArgs& a, uint32_t s, const SlotState& t, uint32_t& k1, uint32_t& k0) {
+__device__ __forceinline__ void bin_keys(const BinArgs& a, const Geom* geoms, uint32_t s, const SlotState& t,
+                                         uint32_t& k1, uint32_t& k0) {
   k1 = kNoKey, k0 = kNoKey;
   if (t.p_end || t.p_start) {
-    const Geom g = a.geom[a.space_of[s]];
+    const Geom g = geoms[a.space_of[s]];
     if (t.p_end) k1 = cell_key_of(g, t.x1, t.z1);
     if (t.p_start) k0 = cell_key_of(g, t.x0, t.z0);
     if (k0 == k1) k0 = kNoKey;
@@ -378,13 +398,15 @@ __device__ __forceinline__ void bin_chunk_loop(const BinArgs& a, uint32_t c, Bod
 
 __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
   extern __shared__ uint32_t th[];
+  __shared__ Geom gs[kLdsGeoms];
+  const Geom* const geoms = bin_geoms(a, gs);
   for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) th[i] = 0u;
   __syncthreads();
   const uint32_t c = bin_chunk_of(blockIdx.x, a.nblk);
   bin_chunk_loop(a, c, [&](uint32_t s) {
     const SlotState t = slot_state(a, s);
     uint32_t k1, k0;
-    bin_keys(a, s, t, k1, k0);
+    bin_keys(a, geoms, s, t, k1, k0);
     if (k1 != kNoKey) atomicAdd(&th[k1 >> kTileCellShift], 1u);
     if (k0 != kNoKey) atomicAdd(&th[k0 >> kTileCellShift], 1u);
   });
@@ -408,6 +430,8 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
 __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
   extern __shared__ uint32_t th[];  // [ntiles]: tile starts, then this chunk's bucket cursors
   __shared__ uint32_t ws[kBinThreads / 64];
+  __shared__ Geom gs[kLdsGeoms];
+  const Geom* const geoms = bin_geoms(a, gs);  // (visible after the scan's barriers below)
   constexpr uint32_t kPer = (kMaxLdsTiles + kBinThreads - 1) / kBinThreads;
   const uint32_t n = a.ntiles, i0 = threadIdx.x * kPer;
   const uint32_t c = bin_chunk_of(blockIdx.x, a.nblk);
@@ -451,7 +475,7 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
   bin_chunk_loop(a, c, [&](uint32_t s) {
     const SlotState t = slot_state(a, s);
     uint32_t k1, k0;
-    bin_keys(a, s, t, k1, k0);
+    bin_keys(a, geoms, s, t, k1, k0);
     if (k1 == kNoKey && k0 == kNoKey) return;
     uint32_t j1 = 0, j0 = 0;
     if (k1 != kNoKey) j1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
@@ -1202,6 +1226,8 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
   }
   __syncthreads();
   GW_STAMP(9, __builtin_amdgcn_s_memrealtime());  // row-major table and source map written
+  uint32_t src[kStageIters];
+  Rec r[kStageIters];
   // column-major cell starts (cell counts from the row-major table; cell (rr, cc) is column-major
   // cell cc * nrows + rr), then the column-major index array by one scatter per record: record i of
   // region cell (rr, cc) goes to ccs[cc * nrows + rr] + (i - lcs[rr * ncols + cc])
@@ -1239,8 +1265,7 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
     __syncthreads();  // mv is reused for the mover list below
   }
   GW_STAMP(10, __builtin_amdgcn_s_memrealtime());  // column-major tables
-  uint32_t src[kStageIters];
-  Rec r[kStageIters];
+  // (issuing these gathers before the column-major pass instead, to overlap the two: 93.8 -> 94.2 us)
 #pragma unroll
   for (int k = 0; k < kStageIters; ++k) {
     const uint32_t i = threadIdx.x + k * kSweepBlock;
@@ -1746,7 +1771,7 @@ k_sweep_dense(SweepArgs a) {
         const int c0 = (lane & 1) ? b0r : a0, c1 = (lane & 1) ? b1r : a1;
         const uint32_t nparts = c0 <= c1 ? (uint32_t)((c1 >> kTileShift) - (c0 >> kTileShift) + 1) : 0u;
         const uint32_t pincl = wave_incl_scan(nparts);
-        const uint32_t T = __shfl(pincl, 63, 64);
+        const uint32_t T = __builtin_amdgcn_readlane(pincl, 63);
         for (uint32_t pb = 0; pb < T; pb += 64) {
           const uint32_t p = pb + lane;
           int lo = 0, hi = 63;

@@ -454,6 +454,7 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_
   b.base = base;
   b.n_ops = n_ops;
   b.geom = g.d_geom;
+  b.nspaces = m->nspaces;
   b.cap = m->cap;
   b.key_of = m->key_of;
   b.local_of = m->local_of;
