@@ -145,7 +145,10 @@ inline uint32_t bin_chunk(uint32_t cap) {
   const uint64_t c = (per + kBinChunk - 1) / kBinChunk * kBinChunk;
   return (uint32_t)(c > kBinChunk ? c : kBinChunk);
 }
-constexpr uint32_t kMaxLdsTiles = 12288;
+#ifndef GW_MAX_LDS_TILES
+#define GW_MAX_LDS_TILES 12288
+#endif
+constexpr uint32_t kMaxLdsTiles = GW_MAX_LDS_TILES;
 
 struct SweepArgs {
   GridView g;

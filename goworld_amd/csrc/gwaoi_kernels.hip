@@ -360,20 +360,18 @@ __device__ __forceinline__ uint32_t bin_chunk_of(uint32_t b, uint32_t nblk) {
 }
 
 // The Spaces' geometry in LDS for the build kernels when there are few Spaces (one load chain less per
-// slot: space_of -> geometry becomes space_of -> LDS); more Spaces read it from global memory.
+// slot: space_of -> geometry becomes space_of -> LDS); more Spaces read it from global memory. The two
+// cases are two instantiations of the slot loop (bin_slots), so every access has a known address
+// space (a pointer that may be either is a FLAT access, slower for both).
 constexpr uint32_t kLdsGeoms = 64;
-__device__ __forceinline__ const Geom* bin_geoms(const BinArgs& a, Geom* gs) {
-  if (a.nspaces > kLdsGeoms) return a.geom;
-  for (uint32_t i = threadIdx.x; i < a.nspaces; i += blockDim.x) gs[i] = a.geom[i];
-  return gs;  // (the caller's barrier makes them visible)
-}
 
-// keys of slot s's main (k1) and ghost (k0) records, kNoKey for none
-__device__ __forceinline__ void bin_keys(const BinArgs& a, const Geom* geoms, uint32_t s, const SlotState& t,
+// keys of slot s's main (k1) and ghost (k0) records, kNoKey for none; geom_of(space) gives a Geom
+template <class GeomOf>
+__device__ __forceinline__ void bin_keys(const BinArgs& a, GeomOf&& geom_of, uint32_t s, const SlotState& t,
                                          uint32_t& k1, uint32_t& k0) {
   k1 = kNoKey, k0 = kNoKey;
   if (t.p_end || t.p_start) {
-    const Geom g = geoms[a.space_of[s]];
+    const Geom g = geom_of(a.space_of[s]);
     if (t.p_end) k1 = cell_key_of(g, t.x1, t.z1);
     if (t.p_start) k0 = cell_key_of(g, t.x0, t.z0);
     if (k0 == k1) k0 = kNoKey;
@@ -396,17 +394,37 @@ __device__ __forceinline__ void bin_chunk_loop(const BinArgs& a, uint32_t c, Bod
   }
 }
 
+// body(s, t, k1, k0) for every slot of chunk c, with the Spaces' geometry from gs (LDS, filled here
+// when there are few Spaces; the caller's barrier follows before the first use) or global memory
+template <class Body>
+__device__ __forceinline__ void bin_slots(const BinArgs& a, uint32_t c, Geom* gs, Body&& body) {
+  auto run = [&](auto&& geom_of) {
+    bin_chunk_loop(a, c, [&](uint32_t s) {
+      const SlotState t = slot_state(a, s);
+      uint32_t k1, k0;
+      bin_keys(a, geom_of, s, t, k1, k0);
+      body(s, t, k1, k0);
+    });
+  };
+  if (a.nspaces <= kLdsGeoms)  // block-uniform
+    run([&](uint32_t sp) { return gs[sp]; });
+  else
+    run([&](uint32_t sp) { return a.geom[sp]; });
+}
+
+__device__ __forceinline__ void bin_load_geoms(const BinArgs& a, Geom* gs) {
+  if (a.nspaces <= kLdsGeoms)
+    for (uint32_t i = threadIdx.x; i < a.nspaces; i += blockDim.x) gs[i] = a.geom[i];
+}
+
 __global__ void __launch_bounds__(kBinThreads) k_bin_tcount(BinArgs a) {
   extern __shared__ uint32_t th[];
   __shared__ Geom gs[kLdsGeoms];
-  const Geom* const geoms = bin_geoms(a, gs);
+  bin_load_geoms(a, gs);
   for (uint32_t i = threadIdx.x; i < a.ntiles; i += kBinThreads) th[i] = 0u;
   __syncthreads();
   const uint32_t c = bin_chunk_of(blockIdx.x, a.nblk);
-  bin_chunk_loop(a, c, [&](uint32_t s) {
-    const SlotState t = slot_state(a, s);
-    uint32_t k1, k0;
-    bin_keys(a, geoms, s, t, k1, k0);
+  bin_slots(a, c, gs, [&](uint32_t, const SlotState&, uint32_t k1, uint32_t k0) {
     if (k1 != kNoKey) atomicAdd(&th[k1 >> kTileCellShift], 1u);
     if (k0 != kNoKey) atomicAdd(&th[k0 >> kTileCellShift], 1u);
   });
@@ -431,7 +449,7 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
   extern __shared__ uint32_t th[];  // [ntiles]: tile starts, then this chunk's bucket cursors
   __shared__ uint32_t ws[kBinThreads / 64];
   __shared__ Geom gs[kLdsGeoms];
-  const Geom* const geoms = bin_geoms(a, gs);  // (visible after the scan's barriers below)
+  bin_load_geoms(a, gs);  // (visible after the scan's barriers below)
   constexpr uint32_t kPer = (kMaxLdsTiles + kBinThreads - 1) / kBinThreads;
   const uint32_t n = a.ntiles, i0 = threadIdx.x * kPer;
   const uint32_t c = bin_chunk_of(blockIdx.x, a.nblk);
@@ -472,10 +490,7 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
     if (i < n) th[i] += h[k];
   }
   __syncthreads();
-  bin_chunk_loop(a, c, [&](uint32_t s) {
-    const SlotState t = slot_state(a, s);
-    uint32_t k1, k0;
-    bin_keys(a, geoms, s, t, k1, k0);
+  bin_slots(a, c, gs, [&](uint32_t s, const SlotState& t, uint32_t k1, uint32_t k0) {
     if (k1 == kNoKey && k0 == kNoKey) return;
     uint32_t j1 = 0, j0 = 0;
     if (k1 != kNoKey) j1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
@@ -695,6 +710,7 @@ __device__ __forceinline__ void emit(const SweepArgs& a, Q& sm, uint32_t rank, u
     // not one per event on the single counter every block shares
     const uint32_t gi = wave_append(&a.ctr[CTR_EVENTS], true);
     if (gi < a.ev_cap) a.ev_tmp[gi] = rec;
+    asm volatile("" ::: "memory");  // two stores, not one FLAT store (emit_masks)
   }
   nent += enter ? 1u : 0u;
 }
@@ -1075,6 +1091,10 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, co
       } else {
         const uint32_t gi = g0 + (p - qs);
         if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local, m.slot, sm.rslot[j] | eb);
+        // (keeps the two stores apart: merged into one store through a pointer that may be LDS or
+        // global, they become a FLAT store, which also counts on lgkmcnt and so holds up every later
+        // LDS wait of the wave; the ring walks spent 71% of their time in this emission that way)
+        asm volatile("" ::: "memory");
       }
       ++local;
       ++p;
@@ -1096,8 +1116,44 @@ __device__ __forceinline__ void judge_stream(const SweepArgs& a, SweepSmem& sm, 
   }
 }
 
+// Diagnostic build only (GW_STAMPS=1, scripts/variants.py): per-block timestamps of the sweep's
+// phases, read back with gwaoi_debug_read_stamps. The product build compiles none of this.
+#ifndef GW_STAMPS
+#define GW_STAMPS 0
+#endif
+#if GW_STAMPS
+constexpr int kStampWords = 16;
+__device__ unsigned long long gw_stamps[kStampWords * 16384];
+#define GW_STAMP(k, v)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0 && sm.item < 16384) gw_stamps[sm.item * kStampWords + (k)] = (v); \
+  } while (0)
+#else
+#define GW_STAMP(k, v) \
+  do {                 \
+  } while (0)
+#endif
+
+// Diagnostic build only (GW_STAMPS=1): the ring walk's phases per wave, summed into words 16 * 16382 + k
+// of gw_stamps: [0] judge setup + ring plan, [1] row stream, [2] column stream, [3] emission, [4] waves
+#if GW_STAMPS
+#define GW_SPH(k)                                                                            \
+  do {                                                                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                              \
+    if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63)))       \
+      atomicAdd(&gw_stamps[kStampWords * 16382 + (k)], t_ - st0);                           \
+    st0 = t_;                                                                                \
+  } while (0)
+#else
+#define GW_SPH(k) \
+  do {            \
+  } while (0)
+#endif
 __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Walk& w,
                                               const Region& R, const Geom& g, uint32_t& nent) {
+#if GW_STAMPS
+  unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#endif
   const Judge J = make_judge(m, a.base);
   uint32_t local = 0;
   RingStream Rs, Cs;
@@ -1106,9 +1162,17 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     auto ri = [&](uint32_t k) { return stream_at(Rs, k); };
     auto ci = [&](uint32_t k) { return (uint32_t)sm.cidx[stream_at(Cs, k)]; };
     if (__all(Rs.total <= 64u && Cs.total <= 64u)) {  // the usual ring: both streams in one chunk, one emission
+      GW_SPH(0);
       const unsigned long long hR = judge_chunk(sm, J, 0, Rs.total, ri);
+      GW_SPH(1);
       const unsigned long long hC = judge_chunk(sm, J, 0, Cs.total, ci);
+      GW_SPH(2);
       emit_masks(a, sm, m, J, hR, ri, hC, ci, local, nent);
+      GW_SPH(3);
+#if GW_STAMPS
+      if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63)))
+        atomicAdd(&gw_stamps[kStampWords * 16382 + 4], 1ull);
+#endif
       return local;
     }
     judge_stream(a, sm, J, m, Rs.total, ri, local, nent);
@@ -1143,23 +1207,6 @@ __device__ __forceinline__ uint32_t block_excl_scan_big(uint32_t v, uint32_t* ws
   return pre + inc - v;
 }
 
-// Diagnostic build only (GW_STAMPS=1, scripts/variants.py): per-block timestamps of the sweep's
-// phases, read back with gwaoi_debug_read_stamps. The product build compiles none of this.
-#ifndef GW_STAMPS
-#define GW_STAMPS 0
-#endif
-#if GW_STAMPS
-constexpr int kStampWords = 16;
-__device__ unsigned long long gw_stamps[kStampWords * 16384];
-#define GW_STAMP(k, v)                                                              \
-  do {                                                                              \
-    if (threadIdx.x == 0 && sm.item < 16384) gw_stamps[sm.item * kStampWords + (k)] = (v); \
-  } while (0)
-#else
-#define GW_STAMP(k, v) \
-  do {                 \
-  } while (0)
-#endif
 
 constexpr int kCellsPerThread = (kRegCells + kSweepBlock - 1) / kSweepBlock;
 constexpr int kStageIters = (kCap + kSweepBlock - 1) / kSweepBlock;  // staged records per thread
