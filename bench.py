@@ -260,6 +260,8 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         eng.debug_set_cell_side(args.cell_side)
     if args.sweep_lds != 1:
         eng._L.gwaoi_debug_set_sweep_lds(eng.handle, args.sweep_lds)
+    if args.counting_build:
+        eng.debug_build_mode(1)
     # bulk restore (untimed): one device-staged pass of SILENT Enters into their Spaces; the relation
     # is rebuilt without reporting its pairs (billions for config 5 in SURVEY proportions)
     kinds = DeviceBuffer(n, dev)
@@ -897,6 +899,8 @@ def main():
     ap.add_argument("--dists", default=None, help="skew workloads: comma list of per-Space D (A/B)")
     ap.add_argument("--cell-side", type=float, default=None, help="absolute cell side for every Space (A/B)")
     ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
+    ap.add_argument("--counting-build", action="store_true",
+                    help="grid built by the counting tile build every pass, not the one-pass build (A/B)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch + rendezvous + barrier only, no GPU work (CPU test of the multi-rank plumbing)")
     ap.add_argument("--stamps", default=None, help="diagnostic GW_STAMPS build: dump the last sweep's per-block "

@@ -20,6 +20,8 @@ __host__ __device__ __forceinline__ bool finite_bits(uint32_t b) { return (b & 0
 // Counters block in device memory.
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
        CTR_DENSE = 7, CTR_HOLES = 8, CTR_NOPS = 9,  // ops of the pass (device-counted batches)
+       CTR_BOVF = 10,   // the one-pass build overflowed a tile's bucket: the pass is re-run (counting build)
+       CTR_BDONE = 16,  // blocks of the one-pass build done (not published)
        CTR_N = 32 };
 constexpr int kPubWords = 16;  // counters [0, 16) are what the host reads after a pass
 // CTR_EVENTS counts SLOTS of ev_tmp; k_sweep_dense reserves them in per-wave chunks and marks the
@@ -122,7 +124,11 @@ struct BinArgs {
   uint32_t* thist;            // [ntiles * nblk]: bucket offset of (tile, chunk) inside its tile
   uint32_t* ttot;             // [kMaxLdsTiles] tile totals (zero on entry; summed by k_bin_tcount)
   uint32_t* ttot_next;        // [kMaxLdsTiles] the next build's totals (zeroed by k_bin_tscatter)
-  uint32_t* tstart;           // [ntiles + 1] tile starts
+  uint32_t* tstart;           // [ntiles + 1] tile starts (this build's)
+  const uint32_t* tprev;      // [ntiles + 1] the previous tile build's starts: the one-pass build's plan
+  uint32_t fused;             // 1: one-pass build (k_bin_tfused), records bucketed at plan_start(tprev, tile)
+  uint32_t trec_cap;          // records trec holds
+  uint32_t* ctr;              // pass counters (CTR_BOVF, CTR_BDONE)
   const uint32_t* tile_space;  // tile -> space
   Rec* trec;                  // records bucketed by tile (the other grid's buffer: unused this pass)
   const uint8_t* op_kind;     // the pass's op kinds (null: all moves), for tile_walk
@@ -244,6 +250,8 @@ void launch_bin_scatter(const BinArgs& a, hipStream_t st);
 // Tile-bucketed build: LDS tile histograms per slot chunk -> (scan thist) -> bucket scatter -> per-tile
 // LDS cell sort that writes the records and every cell start. part: scan scratch.
 void launch_bin_tiles(const BinArgs& a, hipStream_t st);
+// (the one-pass build when a.fused: the previous build's tile starts as the bucket plan, a bucket past
+// its tile's room raises ctr[CTR_BOVF]; else the counting build)
 // In-place exclusive scan of d[0..n); d[n-1] must be 0 on entry if the total is wanted there.
 void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st);
 uint32_t scan_part_words(uint32_t n);

@@ -503,6 +503,148 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tscatter(BinArgs a) {
   });
 }
 
+// ---- one-pass tile build (the steady state) -------------------------------------------------------
+// Bucket layout planned from the PREVIOUS tile build's starts: tile i's records go to
+// [plan_start(i), plan_start(i + 1)), which leaves every tile 25% + 15 records of room over its previous
+// count. A block can then place its chunk's records as soon as its tile histogram has been added to
+// the tile totals (the returning atomic gives the bucket's offset inside the tile): no count pass
+// over the slots before the scatter, and no scan between them. A bucket that passes its tile's room
+// (a tile that grew by more than that since the previous build: mass Enter, teleports) raises
+// CTR_BOVF, and the host re-runs the pass with the counting build (k_bin_tcount / k_bin_tscatter);
+// every write stays inside trec whatever the plan. The last block to finish scans the exact tile
+// totals into this build's (compact) tile starts, which k_bin_tsort writes the cells at.
+__device__ __forceinline__ uint32_t plan_start(const uint32_t* __restrict__ prev, uint32_t i) {
+  return (uint32_t)min<uint64_t>((uint64_t)prev[i] * 5u / 4u + 16ull * i, 0xffffffffull);
+}
+
+// Chunks of kBinChunk slots (capacities up to 256 kBinChunk) keep each slot's state in registers between
+// the histogram and the scatter; larger chunks load it again for the scatter.
+constexpr int kFusedItems = kBinItems;
+
+template <bool HOLD>
+__global__ void __launch_bounds__(kBinThreads) k_bin_tfused(BinArgs a) {
+  extern __shared__ uint32_t th[];  // [ntiles]: this chunk's tile counts, then its bucket cursors
+  __shared__ Geom gs[kLdsGeoms];
+  __shared__ uint32_t ws[kBinThreads / 64];
+  __shared__ uint32_t is_last;
+  bin_load_geoms(a, gs);
+  const uint32_t n = a.ntiles;
+  for (uint32_t i = threadIdx.x; i < n; i += kBinThreads) th[i] = 0u;
+  {
+    const uint32_t gt = blockIdx.x * kBinThreads + threadIdx.x, gn = gridDim.x * kBinThreads;
+    for (uint32_t i = gt; i < kMaxLdsTiles; i += gn) a.ttot_next[i] = 0u;
+  }
+  __syncthreads();
+  const uint32_t c = bin_chunk_of(blockIdx.x, a.nblk);
+  // scatter of one slot's records through the chunk's bucket cursors
+  auto place = [&](uint32_t s, const SlotState& t, uint32_t k1, uint32_t k0) {
+    if (k1 == kNoKey && k0 == kNoKey) return;
+    uint32_t j1 = 0, j0 = 0;
+    if (k1 != kNoKey) j1 = atomicAdd(&th[k1 >> kTileCellShift], 1u);
+    if (k0 != kNoKey) j0 = atomicAdd(&th[k0 >> kTileCellShift], 1u);
+    const uint4 rb = make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), t.q0, t.q1);
+    if (k1 != kNoKey && j1 < a.trec_cap)
+      a.trec[j1] = Rec{make_uint4(__float_as_uint(t.x1), __float_as_uint(t.z1), s | (k0 != kNoKey ? REC_HASG : 0u), t.oq),
+                       rb};
+    if (k0 != kNoKey && j0 < a.trec_cap)
+      a.trec[j0] = Rec{make_uint4(__float_as_uint(t.x0), __float_as_uint(t.z0), s | REC_GHOST, t.oq), rb};
+  };
+  SlotState t[HOLD ? kFusedItems : 1];
+  uint32_t k1[HOLD ? kFusedItems : 1], k0[HOLD ? kFusedItems : 1];
+  if constexpr (HOLD) {  // a.chunk == kBinChunk
+    const uint32_t s0 = c * kBinChunk;
+    auto load = [&](auto&& geom_of) {
+#pragma unroll
+      for (int k = 0; k < kFusedItems; ++k) {
+        const uint32_t s = s0 + k * kBinThreads + threadIdx.x;
+        k1[k] = k0[k] = kNoKey;
+        if (s < a.cap) {
+          t[k] = slot_state(a, s);
+          bin_keys(a, geom_of, s, t[k], k1[k], k0[k]);
+        }
+      }
+    };
+    if (a.nspaces <= kLdsGeoms)  // block-uniform; two code paths, so no access goes through a FLAT pointer
+      load([&](uint32_t sp) { return gs[sp]; });
+    else
+      load([&](uint32_t sp) { return a.geom[sp]; });
+#pragma unroll
+    for (int k = 0; k < kFusedItems; ++k) {
+      if (k1[k] != kNoKey) atomicAdd(&th[k1[k] >> kTileCellShift], 1u);
+      if (k0[k] != kNoKey) atomicAdd(&th[k0[k] >> kTileCellShift], 1u);
+    }
+  } else {
+    bin_slots(a, c, gs, [&](uint32_t, const SlotState&, uint32_t q1, uint32_t q0) {
+      if (q1 != kNoKey) atomicAdd(&th[q1 >> kTileCellShift], 1u);
+      if (q0 != kNoKey) atomicAdd(&th[q0 >> kTileCellShift], 1u);
+    });
+  }
+  __syncthreads();
+  constexpr uint32_t kPer = (kMaxLdsTiles + kBinThreads - 1) / kBinThreads;
+  {
+    uint32_t cnt[kPer], off[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t i = threadIdx.x + k * kBinThreads;
+      cnt[k] = i < n ? th[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k)
+      if (cnt[k]) off[k] = atomicAdd(&a.ttot[threadIdx.x + k * kBinThreads], cnt[k]);
+    bool ovf = false;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t i = threadIdx.x + k * kBinThreads;
+      if (cnt[k]) {
+        const uint64_t pe = (uint64_t)plan_start(a.tprev, i) + off[k] + cnt[k];
+        const bool fits = pe <= a.trec_cap;
+        ovf |= !fits || pe > plan_start(a.tprev, i + 1);
+        th[i] = fits ? (uint32_t)(pe - cnt[k]) : a.trec_cap;  // (past trec: nothing written)
+      }
+    }
+    if (ovf) a.ctr[CTR_BOVF] = 1u;
+  }
+  __syncthreads();
+  if constexpr (HOLD) {
+#pragma unroll
+    for (int k = 0; k < kFusedItems; ++k) place(c * kBinChunk + k * kBinThreads + threadIdx.x, t[k], k1[k], k0[k]);
+  } else {
+    bin_slots(a, c, gs, place);
+  }
+  // the last block to finish scans the tile totals (every block's returning atomics are done by then)
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    is_last = __hip_atomic_fetch_add(&a.ctr[CTR_BDONE], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+              gridDim.x - 1;
+  __syncthreads();
+  if (!is_last) return;
+  __threadfence();
+  const uint32_t i0 = threadIdx.x * kPer;
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    v[k] = i0 + k < n ? __hip_atomic_load(&a.ttot[i0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    sum += v[k];
+  }
+  const uint32_t inc = wave_incl_scan(sum);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t pre = inc - sum, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kBinThreads / 64; ++k) {
+    pre += k < w ? ws[k] : 0u;
+    tot += ws[k];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    if (i0 + k < n) a.tstart[i0 + k] = pre;
+    pre += v[k];
+  }
+  if (threadIdx.x == 0) a.tstart[n] = tot;
+}
+
 // Tiles of up to 4 * kBlock records (all of config 2's) keep their records in registers between the
 // count and the placement (one read); larger tiles stream them twice.
 // cell index inside its tile, with the Space's geometry fields read as scalars (a local Geom copy
@@ -537,7 +679,14 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   __shared__ uint32_t cnt[kTileCells];
   __shared__ uint32_t ws[kBlock / 64];
   const uint32_t t = blockIdx.x;
-  const uint32_t b = a.tstart[t], e = a.tstart[t + 1];
+  if (a.fused && a.ctr[CTR_BOVF]) {  // the plan did not hold: an empty grid (nothing walks), the pass re-runs
+    for (int c = threadIdx.x; c < kTileCells; c += kBlock) a.cs[(t << kTileCellShift) + c] = 0u;
+    if (threadIdx.x == 0) a.tile_walk[t] = 0u;
+    if (t + 1 == a.ntiles && threadIdx.x == 0) a.cs[a.ntiles << kTileCellShift] = 0u;
+    return;
+  }
+  const uint32_t ob = a.tstart[t], oe = a.tstart[t + 1];  // the tile's cells, in rec
+  const uint32_t b = a.fused ? plan_start(a.tprev, t) : ob, e = b + (oe - ob);  // its bucket, in trec
   for (int c = threadIdx.x; c < kTileCells; c += kBlock) cnt[c] = 0u;
   const TileMap g = tile_map(&a.geom[a.tile_space[t]]);
   const bool small = e - b <= 4u * kBlock;
@@ -583,12 +732,12 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 63) ws[w] = inc;
   __syncthreads();
-  uint32_t pre = b + inc - sum;
+  uint32_t pre = ob + inc - sum;
   for (int k = 0; k < w; ++k) pre += ws[k];
   const uint4 cso = make_uint4(pre, pre + cv.x, pre + cv.x + cv.y, pre + cv.x + cv.y + cv.z);
   *reinterpret_cast<uint4*>(&cnt[threadIdx.x * kPer]) = cso;
   *reinterpret_cast<uint4*>(&a.cs[(t << kTileCellShift) + threadIdx.x * kPer]) = cso;
-  if (t + 1 == a.ntiles && threadIdx.x == 0) a.cs[a.ntiles << kTileCellShift] = e;
+  if (t + 1 == a.ntiles && threadIdx.x == 0) a.cs[a.ntiles << kTileCellShift] = oe;
   __syncthreads();
   if (small) {
     if (on0) {
@@ -619,8 +768,14 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
 void launch_bin_tiles(const BinArgs& a, hipStream_t st) {
   if (!a.ntiles) return;
   const size_t lds = a.ntiles * sizeof(uint32_t);
-  hipLaunchKernelGGL(k_bin_tcount, dim3(a.nblk), dim3(kBinThreads), lds, st, a);
-  hipLaunchKernelGGL(k_bin_tscatter, dim3(a.nblk), dim3(kBinThreads), lds, st, a);
+  if (a.fused && a.chunk == kBinChunk) {
+    hipLaunchKernelGGL(k_bin_tfused<true>, dim3(a.nblk), dim3(kBinThreads), lds, st, a);
+  } else if (a.fused) {
+    hipLaunchKernelGGL(k_bin_tfused<false>, dim3(a.nblk), dim3(kBinThreads), lds, st, a);
+  } else {
+    hipLaunchKernelGGL(k_bin_tcount, dim3(a.nblk), dim3(kBinThreads), lds, st, a);
+    hipLaunchKernelGGL(k_bin_tscatter, dim3(a.nblk), dim3(kBinThreads), lds, st, a);
+  }
   hipLaunchKernelGGL(k_bin_tsort, dim3(a.ntiles), dim3(kBlock), 0, st, a);
 }
 

@@ -178,7 +178,12 @@ struct gwaoi_mgr {
   uint32_t* thist = nullptr;     // tile-bucketed build: [max tiles * nblk + 1]
   uint32_t* ttot = nullptr;      // tile totals, two buffers of kMaxLdsTiles: a build sums into one and zeroes the other
   int ttot_sel = 0;              // the buffer the next tile build sums into
-  uint32_t* tstart = nullptr;    // tile starts
+  uint32_t* tstart = nullptr;    // tile starts, two buffers of kMaxLdsTiles + 1 (with ttot_sel): this build's, and
+                                 // the previous tile build's (the one-pass build's bucket plan)
+  int build_mode = 0;            // gwaoi_debug_set_build_mode: 1 = always the counting build
+  bool plan_ok = false;          // the previous tile build's starts describe a grid of the geometry in plan_geom
+  std::vector<gw::Geom> plan_geom;
+  uint64_t builds_fused = 0, builds_counting = 0, build_reruns = 0;
   uint32_t* tile_walk = nullptr; // tile-bucketed build: per tile of the pass's grid, holds a reported mover
   uint32_t nblk = 0;
   uint32_t* ctr_buf = nullptr;   // [2][CTR_N]: pass P uses half P&1 and zeroes the other (k_place)
@@ -436,7 +441,12 @@ bool tile_build(const Grid& g) { return g.ntiles <= gw::kMaxLdsTiles; }
 // Build grid `gi` from the per-slot state (pos, seq, space_of).
 // Build grid `gi` for the pass whose ops have seqs [base, base + n_ops) (n_ops = 0: the current
 // state only, no ghosts).
-int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_t* op_kind) {
+// kBuildAuto: the one-pass build when the previous tile build's starts fit this grid, else counting;
+// kBuildCounting: the counting build (outside a pass: nothing would see an overflow); kBuildRerun: the
+// re-run of a pass whose one-pass build overflowed (the same buffers, counting build).
+enum BuildMode { kBuildAuto, kBuildCounting, kBuildRerun };
+int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_t* op_kind, BuildMode mode = kBuildAuto) {
+  const bool counting = mode == kBuildRerun;
   Grid& g = m->grid[gi];
   const bool tiles = tile_build(g);
   if (!tiles && g.cs_zeroed < g.ncells + 1)
@@ -464,17 +474,28 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_
   b.nblk = m->nblk;
   b.chunk = gw::bin_chunk(m->cap);
   b.thist = m->thist;
-  b.ttot = m->ttot + m->ttot_sel * gw::kMaxLdsTiles;
-  b.ttot_next = m->ttot + (m->ttot_sel ^ 1) * gw::kMaxLdsTiles;
-  b.tstart = m->tstart;
+  const int sel = counting ? m->ttot_sel ^ 1 : m->ttot_sel;  // a re-run uses the failed build's buffers
+  b.ttot = m->ttot + sel * gw::kMaxLdsTiles;
+  b.ttot_next = m->ttot + (sel ^ 1) * gw::kMaxLdsTiles;
+  b.tstart = m->tstart + sel * (gw::kMaxLdsTiles + 1);
+  b.tprev = m->tstart + (sel ^ 1) * (gw::kMaxLdsTiles + 1);
   b.tile_space = g.d_tile_space;
   b.trec = m->grid[gi ^ 1].rec;  // the other grid's records are not read by this pass
+  b.trec_cap = 2 * m->cap;
   b.op_kind = op_kind;
   b.tile_walk = m->tile_walk;
+  b.ctr = m->ctr;
+  b.fused = 0;
   if (tiles) {
+    b.fused = mode == kBuildAuto && m->build_mode == 0 && m->plan_ok && same_geom(m->plan_geom, g.h_geom);
+    if (counting) HIPCHK(hipMemsetAsync(b.ttot, 0, (size_t)gw::kMaxLdsTiles * sizeof(uint32_t), m->stream));
     gw::launch_bin_tiles(b, m->stream);
-    m->ttot_sel ^= 1;
+    if (!counting) m->ttot_sel ^= 1;
+    (b.fused ? m->builds_fused : m->builds_counting)++;
+    if (!m->plan_ok || !same_geom(m->plan_geom, g.h_geom)) m->plan_geom = g.h_geom;
+    m->plan_ok = true;
   } else {
+    m->plan_ok = false;
     gw::launch_bin_count(b, m->stream);
     gw::launch_scan(m->scan, g.cs, g.ncells + 1, m->stream);
     gw::launch_bin_scatter(b, m->stream);
@@ -496,7 +517,7 @@ int renormalise(gwaoi_mgr* m) {
   for (size_t i = 0; i < v.size(); ++i) q[v[i].second] = (uint32_t)i + 1;
   HIPCHK(hipMemcpy(m->seq, q.data(), m->cap * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemsetAsync(m->opq, 0, (size_t)m->cap * sizeof(uint32_t), m->stream));  // stale op seqs
-  RCHK(build_grid(m, m->cur, 0, 0, nullptr));
+  RCHK(build_grid(m, m->cur, 0, 0, nullptr, kBuildCounting));
   m->next_seq = (uint32_t)v.size() + 1;
   HIPCHK(hipStreamSynchronize(m->stream));
   return GWAOI_OK;
@@ -641,7 +662,14 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   const uint32_t n_start = m->n_present_dev;  // present at the start of the pass
   const uint64_t keep = m->tick_events;
   // events: expected count is small; grow and re-run the (pure) sweep on overflow
+  bool rebuild = false;
   for (int attempt = 0;; ++attempt) {
+    if (rebuild) {  // the one-pass build's plan did not hold: the same pass with the counting build
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_BOVF, 0, sizeof(uint32_t), st));
+      RCHK(build_grid(m, ng, base, n_ops, a.op_kind, kBuildRerun));
+      m->build_reruns++;
+      rebuild = false;
+    }
     if (attempt) {  // re-run after growing the event buffers: reset what the sweep accumulates
       // the scan turned the counts into offsets, and the sweep stores non-zero counts only
       HIPCHK(hipMemsetAsync(m->rank_cnt, 0, ((size_t)n_ops + 1) * sizeof(uint32_t), st));
@@ -715,6 +743,14 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
               "64=non-finite coordinate); the manager is unusable",
               m->h_ctr[gw::CTR_ERR]);
       return GWAOI_ERR_DEVICE_CHECK;
+    }
+    if (m->h_ctr[gw::CTR_BOVF]) {  // (the sweep saw an empty grid)
+      if (attempt < 3) {
+        rebuild = true;
+        continue;
+      }
+      set_err("tile build overflow persisted");
+      return GWAOI_ERR_NOMEM;
     }
     const uint32_t slots = m->h_ctr[gw::CTR_EVENTS], nev = slots - m->h_ctr[gw::CTR_HOLES];
     if (slots > m->tmp_cap || keep + nev > m->ev_cap) {
@@ -933,7 +969,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
   chk(dalloc(&m->thist, thist_n));
   chk(dalloc(&m->ttot, 2 * (size_t)gw::kMaxLdsTiles));  // k_bin_tscatter zeroes kMaxLdsTiles of the other buffer
-  chk(dalloc(&m->tstart, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) + 1));
+  chk(dalloc(&m->tstart, 2 * ((size_t)gw::kMaxLdsTiles + 1)));
   chk(dalloc(&m->tile_walk, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
   // the scan has at most 1024 chunks up to 16.7M items (scan_ipt), more beyond
   m->part_words = std::max<uint32_t>(1024 + 2, gw::scan_part_words((uint32_t)std::max<uint64_t>(
@@ -1962,6 +1998,19 @@ int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
 int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
   RCHK(check_mgr(m));
   m->sweep_lds = enable < 0 ? 0 : (enable > 2 ? 1 : enable);
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_build_mode(gwaoi_mgr* m, int mode, uint64_t* n_fused, uint64_t* n_counting, uint64_t* n_reruns) {
+  RCHK(check_mgr(m));
+  if (mode > 1) {
+    set_err("build mode %d (0 one-pass when possible, 1 counting)", mode);
+    return GWAOI_ERR_INVALID;
+  }
+  if (mode >= 0) m->build_mode = mode;
+  if (n_fused) *n_fused = m->builds_fused;
+  if (n_counting) *n_counting = m->builds_counting;
+  if (n_reruns) *n_reruns = m->build_reruns;
   return GWAOI_OK;
 }
 

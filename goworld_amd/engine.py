@@ -226,6 +226,14 @@ class Engine:
                                                     ctypes.byref(why)))
         return ni.value, nf.value, why.value
 
+    def debug_build_mode(self, mode: int = -1):
+        """Grid build: 0 = one-pass tile build when the previous build's tile starts fit (re-run with the
+        counting build on overflow), 1 = always counting, -1 = unchanged. Returns (one-pass builds,
+        counting builds, re-runs)."""
+        nf, nc, nr = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check(self._L.gwaoi_debug_set_build_mode(self._h, mode, ctypes.byref(nf), ctypes.byref(nc), ctypes.byref(nr)))
+        return nf.value, nc.value, nr.value
+
     def debug_set_sweep_lds(self, on: bool):
         check(self._L.gwaoi_debug_set_sweep_lds(self._h, 1 if on else 0))
 

@@ -62,6 +62,11 @@ int gwaoi_debug_set_index_limit(struct gwaoi_mgr* mgr, uint64_t limit);
  * bound, 7 a row with too many changes, 8 inconsistent size). */
 int gwaoi_debug_set_relation_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* n_incremental, uint64_t* n_full,
                                   int* last_rebuild_reason);
+/* Grid build mode: 0 = the one-pass tile build whenever the previous tile build's starts fit the grid
+ * (default; a pass whose plan overflows is re-run with the counting build), 1 = always the counting
+ * build; -1 leaves the mode. Reports the builds of each kind and the re-runs since the manager was made. */
+int gwaoi_debug_set_build_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* n_fused, uint64_t* n_counting,
+                               uint64_t* n_reruns);
 /* Diagnostics: resident sweep workgroups per CU (HIP occupancy API) and the sweep's LDS bytes. */
 int gwaoi_debug_sweep_occupancy(int device, int* blocks_per_cu, int* lds_bytes);
 
