@@ -721,6 +721,8 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
     else:
         lay = StripLayout(world, L, args.dist, 1.0)
     nd = StripNode(lay, rank, n, device=dev, seed=seed, skew=skew)
+    if args.counting_build:
+        nd.eng.debug_build_mode(1)
     comm = None
     if not via_cpu:
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")

@@ -611,22 +611,20 @@ __global__ void __launch_bounds__(kBinThreads) k_bin_tfused(BinArgs a) {
   } else {
     bin_slots(a, c, gs, place);
   }
-  // the last block to finish scans the tile totals (every block's returning atomics are done by then)
-  __threadfence();
+  // The last block to finish scans the tile totals. No fence: a fence here (L2 write-back by every wave,
+  // with the scatter's records dirty in it) made the build 3.6x slower. Every block's total atomics
+  // have returned before its barrier and its ticket, and the last block reads the totals by atomics
+  // too, all at the point device-scope atomics meet from every XCD.
   __syncthreads();
-  if (threadIdx.x == 0)
-    is_last = __hip_atomic_fetch_add(&a.ctr[CTR_BDONE], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-              gridDim.x - 1;
+  if (threadIdx.x == 0) is_last = atomicAdd(&a.ctr[CTR_BDONE], 1u) == gridDim.x - 1;
   __syncthreads();
   if (!is_last) return;
-  __threadfence();
   const uint32_t i0 = threadIdx.x * kPer;
   uint32_t v[kPer], sum = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < kPer; ++k) {
-    v[k] = i0 + k < n ? __hip_atomic_load(&a.ttot[i0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    sum += v[k];
-  }
+  for (uint32_t k = 0; k < kPer; ++k) v[k] = i0 + k < n ? atomicAdd(&a.ttot[i0 + k], 0u) : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) sum += v[k];
   const uint32_t inc = wave_incl_scan(sum);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 63) ws[w] = inc;
