@@ -751,8 +751,6 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
 
     for t in range(1, W + 1):
         tick(t)
-    nd.eng.set_timing(True)
-    nd.eng.reset_stats()
     sync_all()
     lat, sent, ops, evs = [], 0, 0, 0
     t0 = time.perf_counter()
@@ -765,7 +763,14 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
         evs += int(ev.count)
     sync_all()
     elapsed = allmax(time.perf_counter() - t0)
+    # per-stage hipEvents over the next ticks of the walk (every rank runs them: the exchange is collective)
+    S = min(K, args.stage_ticks)
+    nd.eng.set_timing(True)
+    nd.eng.reset_stats()
+    for t in range(W + K + 1, W + K + S + 1):
+        tick(t)
     st = nd.eng.stats()
+    nd.eng.set_timing(False)
     if comm is not None:  # the last tick's halo sizes (the RCCL path keeps them on the device)
         sent = int(nd.counts[:2].sum().item()) * K
     nd.close()
