@@ -554,7 +554,8 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
     n, L, D = args.n, args.L, args.dist
     seed = args.seed + rank
     W, K = args.warmup, args.steps
-    T = W + K + 1
+    S = min(K, args.stage_ticks)  # instrumented steps (per-stage hipEvents) after the timed region
+    T = W + K + S + 1
     L_ = _lib.load()
     t_setup = time.perf_counter()
     snap = DeviceBuffer(2 * 4 * n * T, dev)
@@ -608,9 +609,6 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
 
     for t in range(1, W + 1):
         step(t, None)
-    eng.set_timing(True)
-    eng.reset_stats()
-    sy.reset_stats()
     sync_all()
     lat = []
     t0 = time.perf_counter()
@@ -618,8 +616,15 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
         step(t, lat)
     sync_all()
     elapsed = allmax(time.perf_counter() - t0)
+    # per-stage device times: the next S steps with hipEvents on (they cost host time between kernels)
+    eng.set_timing(True)
+    eng.reset_stats()
+    sy.reset_stats()
+    for t in range(W + K + 1, W + K + S + 1):
+        step(t, None)
     st = eng.stats()
     ss = sy.stats()
+    eng.set_timing(False)
     eng.close()
     if rank != 0:
         return None

@@ -677,14 +677,17 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   __shared__ uint32_t cnt[kTileCells];
   __shared__ uint32_t ws[kBlock / 64];
   const uint32_t t = blockIdx.x;
-  if (a.fused && a.ctr[CTR_BOVF]) {  // the plan did not hold: an empty grid (nothing walks), the pass re-runs
+  // (every load of the block's start issued together: the overflow flag, the tile's starts, its plan)
+  const uint32_t ovf = a.fused ? a.ctr[CTR_BOVF] : 0u;
+  const uint32_t ob = a.tstart[t], oe = a.tstart[t + 1];  // the tile's cells, in rec
+  const uint32_t pb = a.fused ? plan_start(a.tprev, t) : ob;
+  if (ovf) {  // the plan did not hold: an empty grid (nothing walks), the pass re-runs
     for (int c = threadIdx.x; c < kTileCells; c += kBlock) a.cs[(t << kTileCellShift) + c] = 0u;
     if (threadIdx.x == 0) a.tile_walk[t] = 0u;
     if (t + 1 == a.ntiles && threadIdx.x == 0) a.cs[a.ntiles << kTileCellShift] = 0u;
     return;
   }
-  const uint32_t ob = a.tstart[t], oe = a.tstart[t + 1];  // the tile's cells, in rec
-  const uint32_t b = a.fused ? plan_start(a.tprev, t) : ob, e = b + (oe - ob);  // its bucket, in trec
+  const uint32_t b = pb, e = b + (oe - ob);  // the tile's bucket, in trec
   for (int c = threadIdx.x; c < kTileCells; c += kBlock) cnt[c] = 0u;
   const TileMap g = tile_map(&a.geom[a.tile_space[t]]);
   const bool small = e - b <= 4u * kBlock;
