@@ -128,8 +128,8 @@ struct FanArgs {
   uint32_t* cnt;        // count pass: pairs per grid record ([rec_bound + 1], scanned afterwards)
   const uint32_t* off;  // write pass: the scanned counts
   uint2* pairs;         // {entity, receiver} (receiver == entity: own client)
-  uint32_t* n_ent;      // entities collected (count pass)
-  unsigned long long* npairs64;  // count pass: pair total in 64 bits (uint32 overflow guard)
+  uint4* tstat;         // count pass: per tile {pairs (64 bits: lo, hi), entities collected, 0}, summed by
+                        // k_fan_total (one atomic per wave on one word serialised the count pass: 172 us)
   // client sub-grid: the main records of entities WITH a client, in grid order (the only candidates
   // a fan-out can name), with their own cell starts over the same cell keys
   const uint32_t* ccs;  // [ncells + 1]
@@ -226,7 +226,10 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
   const int tx = lt % g.ntx, tz = lt / g.ntx;
   const uint32_t k0 = g.base + ((uint32_t)lt << kTileCellShift);
   const uint32_t j0 = a.g.cs[k0], j1 = a.g.cs[k0 + kTileCells];
-  if (j0 == j1) return;
+  if (j0 == j1) {
+    if (!kWrite && threadIdx.x == 0) a.tstat[t] = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
   const int R = g.reach;
   const int cx0 = max(tx * kTile - R, 0), cx1 = min(tx * kTile + kTile - 1 + R, g.ncx - 1);
   const int cz0 = max(tz * kTile - R, 0), cz1 = min(tz * kTile + kTile - 1 + R, g.ncz - 1);
@@ -324,17 +327,41 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
       visit(j, [&](uint32_t w, uint2 v) { pairs[w] = v; });
     }
   }
-  if (!kWrite) {
+  if (!kWrite) {  // the tile's totals, stored (no atomics)
+    __shared__ unsigned long long rp[kSy / 64];
     for (int o = 32; o > 0; o >>= 1) psum += __shfl_xor(psum, o, 64);
-    if ((threadIdx.x & 63) == 0 && psum) atomicAdd(a.npairs64, psum);
     for (int o = 32; o > 0; o >>= 1) ents += __shfl_xor(ents, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ents;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ents, rp[threadIdx.x >> 6] = psum;
     __syncthreads();
     if (threadIdx.x == 0) {
       uint32_t tot = 0;
-      for (int k = 0; k < kSy / 64; ++k) tot += red[k];
-      if (tot) atomicAdd(a.n_ent, tot);
+      unsigned long long pt = 0;
+      for (int k = 0; k < kSy / 64; ++k) tot += red[k], pt += rp[k];
+      a.tstat[t] = make_uint4((uint32_t)pt, (uint32_t)(pt >> 32), tot, 0u);
     }
+  }
+}
+
+// The count pass's totals: entities collected (n_ent) and pairs in 64 bits (npairs64, the guard against
+// uint32 pair offsets), summed over the tiles by one block.
+__global__ void __launch_bounds__(1024) k_fan_total(const uint4* __restrict__ tstat, uint32_t ntiles, uint32_t* n_ent,
+                                                    unsigned long long* npairs64) {
+  __shared__ unsigned long long sp[1024 / 64];
+  __shared__ uint32_t se[1024 / 64];
+  unsigned long long p = 0;
+  uint32_t e = 0;
+  for (uint32_t i = threadIdx.x; i < ntiles; i += 1024) {
+    const uint4 v = tstat[i];
+    p += (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+    e += v.z;
+  }
+  for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64), e += __shfl_xor(e, o, 64);
+  if ((threadIdx.x & 63) == 0) sp[threadIdx.x >> 6] = p, se[threadIdx.x >> 6] = e;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 1024 / 64; ++k) p += sp[k], e += se[k];
+    *npairs64 = p;
+    *n_ent = e;
   }
 }
 
@@ -631,6 +658,8 @@ struct SyncState {
   uint32_t ccid_n = 0;
   uint4* info = nullptr;
   uint64_t info_cap = 0;
+  uint4* tstat = nullptr;  // per tile count-pass totals
+  uint32_t tstat_n = 0;
   uint2* pairs = nullptr;
   uint64_t pairs_cap = 0;
   uint32_t* ghist = nullptr;
@@ -664,7 +693,7 @@ struct SyncState {
 void sync_free(SyncState* s) {
   if (!s) return;
   void* p[] = {s->flags, s->gate, s->cid, s->eid, s->y, s->yaw, s->d_hkey, s->d_hval, s->cnt, s->cpos, s->ccs,
-               s->crec, s->cgate, s->ccid, s->info, s->pairs,
+               s->crec, s->cgate, s->ccid, s->info, s->tstat, s->pairs,
                s->ghist, s->out, s->d_goff, s->scan.status, s->d_payload, s->res, s->first, s->ictr, s->bcnt,
                s->op_slot, s->op_x, s->op_z};
   for (void* q : p)
@@ -1222,14 +1251,15 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   f.gate = s->gate;
   f.clear = !(opts & GWAOI_COLLECT_KEEP_FLAGS);
   f.cnt = s->cnt;
-  f.n_ent = s->ictr + 8;
-  f.npairs64 = (unsigned long long*)(s->ictr + 10);
-  SCHK(hipMemsetAsync(s->ictr + 8, 0, 16, st));
   SCHK(hipMemsetAsync(s->cnt, 0, ((size_t)bound + 1) * 4, st));
   const uint32_t ntiles = v.ntiles;
   if (!ntiles) return GWAOI_OK;
+  SRCHK(gw::dgrow32(&s->tstat, &s->tstat_n, ntiles));
+  f.tstat = s->tstat;
   if (v.timing) SCHK(hipEventRecord(s->tev[1], st));
   hipLaunchKernelGGL(gw::k_fan_tile<false>, dim3(ntiles), dim3(gw::kSy), 0, st, f);
+  hipLaunchKernelGGL(gw::k_fan_total, dim3(1), dim3(1024), 0, st, (const uint4*)s->tstat, ntiles, s->ictr + 8,
+                     (unsigned long long*)(s->ictr + 10));
   gw::launch_scan(s->scan, s->cnt, bound + 1, st);
   if (v.timing) SCHK(hipEventRecord(s->tev[2], st));
   SCHK(hipMemcpyAsync(s->h_small, s->cnt + bound, 4, hipMemcpyDeviceToHost, st));
