@@ -21,11 +21,13 @@ __host__ __device__ __forceinline__ bool finite_bits(uint32_t b) { return (b & 0
 enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 4, CTR_PRESENT = 5, CTR_LEAVES = 6,
        CTR_DENSE = 7, CTR_HOLES = 8, CTR_NOPS = 9,  // ops of the pass (device-counted batches)
        CTR_BOVF = 10,   // the one-pass build overflowed a tile's bucket: the pass is re-run (counting build)
+       CTR_NEV = 11,    // events of the pass (scan total of the per-op counts; k_place)
        CTR_BDONE = 16,  // blocks of the one-pass build done (not published)
        CTR_N = 32 };
 constexpr int kPubWords = 16;  // counters [0, 16) are what the host reads after a pass
-// CTR_EVENTS counts SLOTS of ev_tmp; k_sweep_dense reserves them in per-wave chunks and marks the
-// unused tail of its last chunk as holes (x == kEvHole), counted in CTR_HOLES. Events = slots - holes.
+// CTR_EVENTS counts SLOTS of ev_tmp's shared region (after the per-tile regions, SweepArgs.ev_fix);
+// k_sweep_dense reserves them in per-wave chunks and marks the unused tail of its last chunk as holes
+// (x == kEvHole), counted in CTR_HOLES. The pass's event count is CTR_NEV.
 constexpr uint32_t kEvHole = 0xFFFFFFFFu;
 
 // Cells are grouped in square tiles of kTile x kTile cells; cell keys are tile-major,
@@ -177,8 +179,13 @@ struct SweepArgs {
   uint32_t n_leaves;          // host-staged: the count; device-staged mixed batch: see leaves_dev
   const uint32_t* n_leaves_dev;  // non-null: the count is on the device (ctr[CTR_LEAVES])
   uint32_t leave_blocks;      // blocks after the tiles that walk the Leave ops
-  uint4* ev_tmp;    // {rank, local index within rank, mover, other|kind}
+  uint4* ev_tmp;    // shared region, slots from ctr[CTR_EVENTS]: {rank, local index within rank, mover, other|kind}
   uint32_t ev_cap;
+  // k_sweep's tile blocks (tile builds): tile t's queued events at ev_fix[t * kEvLds ...], their count in
+  // tile_ev[t] and its enter events in tile_ent[t] (stores, no atomics); null: the shared region only
+  uint4* ev_fix;
+  uint32_t* tile_ev;
+  uint32_t* tile_ent;
   uint32_t* rank_cnt;
   uint32_t* ctr;
   uint32_t* dense;      // slots of movers for k_sweep_dense (boxes beyond the tile's LDS region)
@@ -256,6 +263,7 @@ void launch_bin_tiles(const BinArgs& a, hipStream_t st);
 void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st);
 uint32_t scan_part_words(uint32_t n);
 void launch_sweep(const SweepArgs& a, hipStream_t st);
+uint32_t sweep_ev_lds();  // events queued per tile block (the per-tile region size)
 size_t sweep_lds_bytes();
 uint32_t sweep_block();  // threads per sweep block
 void sweep_init();  // once per process (dynamic LDS limit of the sweep)
@@ -270,8 +278,13 @@ struct EvGuard {
   uint64_t out_cap;
 };
 struct OrderArgs {
-  EvGuard g;
-  const uint4* ev_tmp;
+  EvGuard g;                 // g.tmp_cap: slots of the shared region
+  const uint4* ev_tmp;       // the shared region
+  const uint4* ev_fix;       // per-tile regions (null: none), ntiles_fix x kEvLds
+  const uint32_t* tile_ev;
+  const uint32_t* tile_ent;
+  uint32_t ntiles_fix;
+  uint2* scratch;            // k_slice_sort's scratch (the whole ev_tmp: 2 x its slots >= events)
   const uint32_t* rank_off;  // exclusive scan of per-op event counts, [n_ops + 1]
   uint2* ev_out;             // this pass's slice of the output (offset by g.keep)
   uint2* host_out;           // mapped pinned host slice, or null (events stay in HBM)

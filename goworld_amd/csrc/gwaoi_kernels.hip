@@ -1584,13 +1584,16 @@ __device__ __forceinline__ Mover lds_mover(const SweepSmem& sm, uint32_t i, uint
 __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, const uint32_t item) {
   uint32_t nent = 0;  // enter events of this thread's movers
   const uint32_t t = item;
+  auto no_events = [&]() {
+    if (a.ev_fix && threadIdx.x == 0) a.tile_ev[t] = 0u, a.tile_ent[t] = 0u;
+  };
   if (a.tile_walk) {
-    if (!a.tile_walk[t]) return;  // block-uniform: no reported mover in the tile (flag from k_bin_tsort)
+    if (!a.tile_walk[t]) return no_events();  // block-uniform: no reported mover in the tile (k_bin_tsort)
   } else {
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
     bool mine = false;
     for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_walker(a, a.g.rec[j].a);
-    if (!__syncthreads_or(mine)) return;  // nothing queued: the caller's barrier follows
+    if (!__syncthreads_or(mine)) return no_events();  // nothing queued: the caller's barrier follows
   }
   // block-uniform: a scalar index, so the Space's geometry comes in with scalar loads
   const uint32_t sp = __builtin_amdgcn_readfirstlane(a.g.tile_space[t]);
@@ -1669,14 +1672,20 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
   __syncthreads();
   GW_STAMP(3, __builtin_amdgcn_s_memrealtime());
   const uint32_t nq = min(sm.n, (uint32_t)kEvLds);
-  if (threadIdx.x == 0) {
-    sm.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
-    if (sm.enter) atomicAdd(&a.ctr[CTR_ENTER], sm.enter);
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nq; i += kSweepBlock) {
-    const uint32_t gi = sm.base + i;
-    if (gi < a.ev_cap) a.ev_tmp[gi] = sm.ev[i];
+  if (a.ev_fix) {  // the tile's own region: counts stored, no atomics (two per block cost 10 us at config 2)
+    if (threadIdx.x == 0) a.tile_ev[t] = nq, a.tile_ent[t] = sm.enter;
+    uint4* dst = a.ev_fix + (size_t)t * kEvLds;
+    for (uint32_t i = threadIdx.x; i < nq; i += kSweepBlock) dst[i] = sm.ev[i];
+  } else {
+    if (threadIdx.x == 0) {
+      sm.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
+      if (sm.enter) atomicAdd(&a.ctr[CTR_ENTER], sm.enter);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nq; i += kSweepBlock) {
+      const uint32_t gi = sm.base + i;
+      if (gi < a.ev_cap) a.ev_tmp[gi] = sm.ev[i];
+    }
   }
   GW_STAMP(4, __builtin_amdgcn_s_memrealtime());
 }
@@ -2010,8 +2019,10 @@ k_sweep_dense(SweepArgs a) {
 #endif
 }
 
+uint32_t sweep_ev_lds() { return kEvLds; }
+
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
-  if (a.use_lds == 0) {
+  if (a.use_lds == 0) {  // (the host passes no per-tile regions for this variant)
     const uint32_t n = a.n_rec + (a.n_leaves_dev ? a.n_ops : a.n_leaves);
     if (n) hipLaunchKernelGGL(k_sweep_flat, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
     return;
@@ -2031,21 +2042,58 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
 // re-runs), so the host synchronises once per pass. Two side jobs ride along: k_place zeroes the
 // cell counts of the grid the NEXT pass builds and the next pass's counter block; k_slice_sort
 // validates device-staged batches (every op's slot must carry that op's seq).
-__device__ __forceinline__ bool ev_fits(const EvGuard& g, uint32_t* slots, uint32_t* n) {
-  *slots = g.ctr[CTR_EVENTS];
-  *n = *slots - g.ctr[CTR_HOLES];
-  return *slots <= g.tmp_cap && g.keep + *n <= g.out_cap;
+// slots of the shared region, and the pass's events (the scan total of the per-op counts)
+__device__ __forceinline__ bool ev_fits(const OrderArgs& o, uint32_t* slots, uint32_t* n) {
+  *slots = o.g.ctr[CTR_EVENTS];
+  *n = o.rank_off[o.n_ops];
+  return *slots <= o.g.tmp_cap && o.g.keep + *n <= o.g.out_cap;
 }
 
 __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
   const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
   uint32_t slots, n;
+  const bool fits = ev_fits(o, &slots, &n);
+  if (tid == 0) const_cast<uint32_t*>(o.g.ctr)[CTR_NEV] = n;  // (also on overflow: the host sizes ev_out by it)
   // An overflowing pass is re-run from the sweep, which still reads the old grid: side jobs only
   // once the pass is final.
-  if (!ev_fits(o.g, &slots, &n)) return;
+  if (!fits) return;
   for (uint32_t i = tid; i < o.zero_n; i += nth) o.zero_cs[i] = 0u;
   if (tid < CTR_N) o.ctr_next[tid] = 0u;
   if (tid == 0) const_cast<uint32_t*>(o.g.ctr)[CTR_RECORDS] = *o.grid_total;
+  if (o.ev_fix) {
+    // the tiles' regions: entry r of tile t holds an event when r < tile_ev[t]. Four entries per thread
+    // and round, every entry and count loaded before any test (one memory round trip, then the gathers)
+    const uint32_t nf = o.ntiles_fix * (uint32_t)kEvLds;
+    constexpr int kU = 4;
+    for (uint32_t i0 = tid; i0 < nf; i0 += kU * nth) {
+      uint4 e[kU];
+      uint32_t c[kU];
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const uint32_t i = i0 + k * nth;
+        c[k] = i < nf ? o.tile_ev[i / (uint32_t)kEvLds] : 0u;
+        e[k] = i < nf ? o.ev_fix[i] : make_uint4(0u, 0u, 0u, 0u);
+      }
+      uint32_t pos[kU];
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const uint32_t i = i0 + k * nth;
+        const bool on = i < nf && i % (uint32_t)kEvLds < c[k];
+        c[k] = on;
+        pos[k] = on ? o.rank_off[e[k].x] + e[k].y : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < kU; ++k)
+        if (c[k]) o.ev_out[pos[k]] = make_uint2(e[k].z, e[k].w);
+    }
+    if (blockIdx.x == 0) {  // the tiles' enter events into the pass counter (one atomic)
+      uint32_t ne = 0;
+      for (uint32_t t = threadIdx.x; t < o.ntiles_fix; t += kBlock) ne += o.tile_ent[t];
+      uint32_t tot;
+      block_excl_scan(ne, &tot);
+      if (threadIdx.x == 0 && tot) atomicAdd(const_cast<uint32_t*>(&o.g.ctr[CTR_ENTER]), tot);
+    }
+  }
   for (uint32_t i = tid; i < slots; i += nth) {
     const uint4 e = o.ev_tmp[i];
     if (e.x != kEvHole) o.ev_out[o.rank_off[e.x] + e.y] = make_uint2(e.z, e.w);
@@ -2197,17 +2245,17 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
     if (s < o.cap && o.opq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
   }
   uint32_t slots, n;
-  if (!ev_fits(o.g, &slots, &n)) return;  // grid-uniform
+  if (!ev_fits(o, &slots, &n)) return;  // grid-uniform
   const uint32_t b = op ? o.rank_off[r] : 0u, len = op ? o.rank_off[r + 1] - b : 0u;
-  // ev_tmp is free once k_place has run; its uint2 view has 2 x slots >= n entries
-  seg_sort(o.ev_out, reinterpret_cast<uint2*>(const_cast<uint4*>(o.ev_tmp)), b, len, sk, ss.bigq, &ss.nbig);
+  // ev_tmp is free once k_place has run; its uint2 view has 2 x (tile regions + slots) >= n entries
+  seg_sort(o.ev_out, o.scratch, b, len, sk, ss.bigq, &ss.nbig);
 }
 
 // Deliver the ordered events to mapped pinned host memory (GPU-initiated PCIe writes), so the host
 // needs no second round trip to learn the count before a copy.
 __global__ void __launch_bounds__(kBlock) k_copy_out(OrderArgs o) {
   uint32_t slots, n;
-  if (!ev_fits(o.g, &slots, &n)) return;
+  if (!ev_fits(o, &slots, &n)) return;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) o.host_out[i] = o.ev_out[i];
 }
 

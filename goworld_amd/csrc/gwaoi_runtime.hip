@@ -185,6 +185,8 @@ struct gwaoi_mgr {
   std::vector<gw::Geom> plan_geom;
   uint64_t builds_fused = 0, builds_counting = 0, build_reruns = 0;
   uint32_t* tile_walk = nullptr; // tile-bucketed build: per tile of the pass's grid, holds a reported mover
+  uint32_t* tile_ev = nullptr;   // per tile: events k_sweep queued in the tile's region of ev_tmp
+  uint32_t* tile_ent = nullptr;  // per tile: their enter events
   uint32_t nblk = 0;
   uint32_t* ctr_buf = nullptr;   // [2][CTR_N]: pass P uses half P&1 and zeroes the other (k_place)
   uint32_t* ctr = nullptr;       // current half
@@ -661,6 +663,10 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   const uint32_t n_new = dev ? m->n_present_dev : m->n_present;
   const uint32_t n_start = m->n_present_dev;  // present at the start of the pass
   const uint64_t keep = m->tick_events;
+  // ev_tmp: k_sweep's per-tile regions (F slots, tile builds with the LDS sweep), then the shared region
+  const bool fixed = tile_build(m->grid[ng]) && m->sweep_lds != 0 && m->grid[ng].ntiles;
+  const uint32_t F = fixed ? m->grid[ng].ntiles * gw::sweep_ev_lds() : 0u;
+  if (m->tmp_cap < F + 4096u) RCHK(ensure_events(m, m->ev_cap, F + 4096u, keep, false));
   // events: expected count is small; grow and re-run the (pure) sweep on overflow
   bool rebuild = false;
   for (int attempt = 0;; ++attempt) {
@@ -700,8 +706,11 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.n_leaves_dev = dev_mixed ? m->ctr + gw::CTR_LEAVES : nullptr;
     s.leave_blocks = dev_mixed ? std::min<uint32_t>(256u, (n_ops + gw::sweep_block() - 1) / gw::sweep_block())
                                : (s.n_leaves + gw::sweep_block() - 1) / gw::sweep_block();
-    s.ev_tmp = m->ev_tmp;
-    s.ev_cap = m->tmp_cap;
+    s.ev_tmp = m->ev_tmp + F;
+    s.ev_cap = m->tmp_cap - F;
+    s.ev_fix = fixed ? m->ev_tmp : nullptr;
+    s.tile_ev = m->tile_ev;
+    s.tile_ent = m->tile_ent;
     s.rank_cnt = m->rank_cnt;
     s.ctr = m->ctr;
     s.dense = m->d_dense;
@@ -716,8 +725,13 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     // synchronises once, at the end of the pass
     gw::launch_scan(m->scan, m->rank_cnt, n_ops + 1, st);
     gw::OrderArgs o;
-    o.g = {m->ctr, m->tmp_cap, keep, m->ev_cap};
-    o.ev_tmp = m->ev_tmp;
+    o.g = {m->ctr, m->tmp_cap - F, keep, m->ev_cap};
+    o.ev_tmp = m->ev_tmp + F;
+    o.ev_fix = fixed ? m->ev_tmp : nullptr;
+    o.tile_ev = m->tile_ev;
+    o.tile_ent = m->tile_ent;
+    o.ntiles_fix = fixed ? m->grid[ng].ntiles : 0u;
+    o.scratch = reinterpret_cast<uint2*>(m->ev_tmp);
     o.rank_off = m->rank_cnt;
     o.ev_out = m->ev_out + keep;
     o.host_out = copy_events ? m->d_hev + keep : nullptr;
@@ -752,9 +766,9 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       set_err("tile build overflow persisted");
       return GWAOI_ERR_NOMEM;
     }
-    const uint32_t slots = m->h_ctr[gw::CTR_EVENTS], nev = slots - m->h_ctr[gw::CTR_HOLES];
-    if (slots > m->tmp_cap || keep + nev > m->ev_cap) {
-      RCHK(ensure_events(m, keep + nev, slots, keep, copy_events));
+    const uint32_t slots = m->h_ctr[gw::CTR_EVENTS], nev = m->h_ctr[gw::CTR_NEV];
+    if (slots > m->tmp_cap - F || keep + nev > m->ev_cap) {
+      RCHK(ensure_events(m, keep + nev, F + slots, keep, copy_events));
       if (attempt < 3) continue;
       set_err("event buffer overflow persisted");
       return GWAOI_ERR_NOMEM;
@@ -873,7 +887,7 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->rel_tot, m->rel_slab, m->rel_fix,
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
                    m->dx_part, m->dx_out};
@@ -971,6 +985,8 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->ttot, 2 * (size_t)gw::kMaxLdsTiles));  // k_bin_tscatter zeroes kMaxLdsTiles of the other buffer
   chk(dalloc(&m->tstart, 2 * ((size_t)gw::kMaxLdsTiles + 1)));
   chk(dalloc(&m->tile_walk, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
+  chk(dalloc(&m->tile_ev, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
+  chk(dalloc(&m->tile_ent, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
   // the scan has at most 1024 chunks up to 16.7M items (scan_ipt), more beyond
   m->part_words = std::max<uint32_t>(1024 + 2, gw::scan_part_words((uint32_t)std::max<uint64_t>(
                                                    {(uint64_t)m->max_cells, (uint64_t)capacity, thist_n}) + 1));
