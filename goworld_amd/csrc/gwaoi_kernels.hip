@@ -802,10 +802,11 @@ void launch_bin_tiles(const BinArgs& a, hipStream_t st) {
 // per-row loop whose trip count is the max over lanes row by row. Enter and Leave ops, and moves
 // whose ring is wider, walk the box row by row.
 //
-// Events are rare (~0.3 per mover per tick), but one global counter hit by every event serialises
-// at the memory side, so each block stages its events in LDS and reserves its output range with ONE
-// global atomic; a mover's events are numbered in a register (one thread per mover) and its count is
-// stored once, without atomics.
+// Events are rare (~0.3 per mover per tick), but atomics on one global counter serialise at the
+// memory side (even one per block: 2 x 2,304 per launch cost 10 us), so each block stages its events in
+// LDS and copies them into its tile's own region of ev_tmp, storing the count; only a queue overflow
+// takes slots of the shared region by atomics. A mover's events are numbered in a register (one thread
+// per mover) and its count is stored once, without atomics.
 #ifndef GW_SWEEP_BLOCK
 #define GW_SWEEP_BLOCK 512
 #endif
