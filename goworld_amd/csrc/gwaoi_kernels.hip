@@ -1631,15 +1631,24 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
   }
   if (!lds) {
     // region over the LDS budget (crowds, large D): every mover of the tile to k_sweep_dense
+    // (the tile's entries reserved by ONE atomic per block: an append per wave on the one counter
+    // serialised at the memory side, ~48k of them per skew50 launch)
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
+    uint32_t mine = 0;
+    for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) mine += is_walker(a, a.g.rec[j].a) ? 1u : 0u;
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan_big(mine, sm.ws, &tot);
+    if (threadIdx.x == 0) sm.base = tot ? atomicAdd(&a.ctr[CTR_DENSE], tot) : 0u;
+    __syncthreads();
+    uint32_t di = sm.base + pre;
     for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) {
       const uint4 ra = a.g.rec[j].a;
       if (!is_walker(a, ra)) continue;
-      const uint32_t di = wave_append(&a.ctr[CTR_DENSE], true);
       if (di < a.dense_cap) {
-        a.dense[di] = ra.z & REC_SLOT;
+        a.dense[di++] = ra.z & REC_SLOT;
         continue;
       }
+      ++di;
       const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
       const uint32_t cnt = sweep_global(a, sm, m, g, nent);
       put_count(a.rank_cnt, m.rank, cnt);
