@@ -206,6 +206,7 @@ struct RelArgs {
   uint32_t* cols;
   uint32_t ntiles;          // tiles of the grid (one block each)
   unsigned long long* total64;  // count pass: sum of the row lengths in 64 bits (uint32 overflow guard)
+  uint4* tstat;             // count pass: per tile {row lengths' sum lo, hi, longest row, 0} (summed after)
   uint32_t* maxlen;         // count pass: longest row
   uint32_t* slab;           // count pass, optional: the rows by grid record, interleaved (k_row_sort_slab)
   uint32_t slab_s;          // entries per row kept in the slab (rows longer than this: not kept)

@@ -2314,7 +2314,10 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
   const int tx = lt % g.ntx, tz = lt / g.ntx;
   const uint32_t k0 = g.base + ((uint32_t)lt << kTileCellShift);
   const uint32_t j0 = a.g.cs[k0], j1 = a.g.cs[k0 + kTileCells];
-  if (j0 == j1) return;
+  if (j0 == j1) {
+    if (!a.row_ptr && threadIdx.x == 0) a.tstat[t] = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
   const int R = g.reach;
   const int cx0 = max(tx * kTile - R, 0), cx1 = min(tx * kTile + kTile - 1 + R, g.ncx - 1);
   const int cz0 = max(tz * kTile - R, 0), cz1 = min(tz * kTile + kTile - 1 + R, g.ncz - 1);
@@ -2372,16 +2375,50 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
     }
     if (!a.row_ptr) a.row_cnt[s] = n, rsum += n, rmax = max(rmax, n);
   }
-  if (!a.row_ptr) {  // one 64-bit atomic per wave: the host checks the total before it sizes cols
+  if (!a.row_ptr) {  // the tile's totals, stored (k_rel_total sums them; the host checks the total
+                     // before it sizes cols). One atomic per wave on one word instead: serialised.
+    __shared__ unsigned long long rs[kBlock / 64];
+    __shared__ uint32_t rm[kBlock / 64];
     for (int o = 32; o > 0; o >>= 1) rsum += __shfl_xor(rsum, o, 64);
     for (int o = 32; o > 0; o >>= 1) rmax = max(rmax, (uint32_t)__shfl_xor((int)rmax, o, 64));
-    if ((threadIdx.x & 63) == 0 && rsum) atomicAdd(a.total64, rsum);
-    if ((threadIdx.x & 63) == 0 && rmax) atomicMax(a.maxlen, rmax);
+    if ((threadIdx.x & 63) == 0) rs[threadIdx.x >> 6] = rsum, rm[threadIdx.x >> 6] = rmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long ts = 0;
+      uint32_t tm = 0;
+      for (int k = 0; k < kBlock / 64; ++k) ts += rs[k], tm = max(tm, rm[k]);
+      a.tstat[t] = make_uint4((uint32_t)ts, (uint32_t)(ts >> 32), tm, 0u);
+    }
+  }
+}
+
+// the count pass's totals over the tiles: sum of the row lengths (64 bits) and the longest row
+__global__ void __launch_bounds__(1024) k_rel_total(const uint4* __restrict__ tstat, uint32_t ntiles,
+                                                    unsigned long long* total64, uint32_t* maxlen) {
+  __shared__ unsigned long long ss[1024 / 64];
+  __shared__ uint32_t sm_[1024 / 64];
+  unsigned long long p = 0;
+  uint32_t mx = 0;
+  for (uint32_t i = threadIdx.x; i < ntiles; i += 1024) {
+    const uint4 v = tstat[i];
+    p += (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+    mx = max(mx, v.z);
+  }
+  for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64), mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+  if ((threadIdx.x & 63) == 0) ss[threadIdx.x >> 6] = p, sm_[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 1024 / 64; ++k) p += ss[k], mx = max(mx, sm_[k]);
+    *total64 = p;
+    *maxlen = mx;
   }
 }
 
 void launch_relation(const RelArgs& a, hipStream_t st) {
-  if (a.ntiles) hipLaunchKernelGGL(k_relation, dim3(a.ntiles), dim3(kBlock), 0, st, a);
+  if (!a.ntiles) return;
+  hipLaunchKernelGGL(k_relation, dim3(a.ntiles), dim3(kBlock), 0, st, a);
+  if (!a.row_ptr)
+    hipLaunchKernelGGL(k_rel_total, dim3(1), dim3(1024), 0, st, (const uint4*)a.tstat, a.ntiles, a.total64, a.maxlen);
 }
 
 // Neighbours of each row in ascending slot order. A wave takes 64 consecutive rows (a contiguous

@@ -159,6 +159,7 @@ struct gwaoi_mgr {
   uint64_t rel_stat_incr = 0, rel_stat_full = 0;
   int rel_why = 0;  // why the last view was rebuilt (gwaoi_debug_set_relation_mode)
   unsigned long long* rel_tot = nullptr;  // device: [0] the count pass's 64-bit entry total, [1] longest row
+  uint4* rel_tstat = nullptr;              // device: the count pass's per-tile totals
   uint32_t* rel_slab = nullptr;           // count pass output: the rows by grid record (k_row_sort_slab)
   bool rel_no_slab = false;               // no room for the slab at the last rebuild: the two-walk path
   uint64_t rel_slab_recs = 0;             // grid records the slab holds rows for
@@ -887,7 +888,7 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_slab, m->rel_fix,
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
                    m->dx_part, m->dx_out};
@@ -1673,6 +1674,7 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   hipStream_t st = m->stream;
   if (!m->rel_rp) RCHK(dalloc(&m->rel_rp, (size_t)m->cap + 1));
   if (!m->rel_tot) RCHK(dalloc(&m->rel_tot, 3));  // [0] entries, [1] longest row, [2] rows to fix
+  if (!m->rel_tstat) RCHK(dalloc(&m->rel_tstat, (size_t)m->max_cells / gw::kTileCells + 1));
   // The count pass also writes every row of up to kSlabS entries into a slab (by grid record), when
   // that fits; the rows then go from the slab to cols sorted, with no second walk. A longer row (crowds)
   // sends the call down the two-walk path: fill pass, sort in place. The slab holds the rows of the
@@ -1717,6 +1719,7 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   a.ntiles = g.ncells ? g.ntiles : 0u;
   a.total64 = m->rel_tot;
   a.maxlen = reinterpret_cast<uint32_t*>(m->rel_tot + 1);
+  a.tstat = m->rel_tstat;
   a.slab = m->rel_slab;
   a.slab_s = a.slab ? kSlabS : 0u;
   // count pass, scan, then the row lengths' total is the one value the host must know (allocation)
