@@ -329,9 +329,22 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
     };
     int64_t tx, tz;
     dims(c, &tx, &tz);
+    const double c_want = c;
+    bool grown = false;
     while ((uint64_t)(tx * tz) * gw::kTileCells > share || tx * gw::kTile > (1 << 22) || tz * gw::kTile > (1 << 22)) {
       c *= 1.25;
       dims(c, &tx, &tz);
+      grown = true;
+    }
+    if (grown) {
+      // back down to the finest cells that keep this tile count (config 3: a 1,600-wide Space at D / 4
+      // = 25 needs 65 cells, one over two tiles; the 1.25x steps gave cells of 31.25, with 1.5x the
+      // ring candidates, where 25.0000x fits two tiles exactly)
+      const double cf = std::max({c_want, ((double)x1 - x0) / (double)(tx * gw::kTile),
+                                  ((double)z1 - z0) / (double)(tz * gw::kTile)}) * (1.0 + 1e-6);
+      int64_t fx, fz;
+      dims(cf, &fx, &fz);
+      if (cf < c && fx <= tx && fz <= tz) c = cf, tx = fx, tz = fz;
     }
     gw::Geom g;
     g.x0 = x0;
