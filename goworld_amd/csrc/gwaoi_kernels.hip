@@ -119,8 +119,88 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   }
 }
 
+// Moved-only batches (no kinds, no Leave list) with 16-B aligned op arrays: four ops per thread. A
+// group whose slots are four consecutive slots from a multiple of 4 (a batch in slot order) moves every
+// per-slot array with 16-B accesses; any other group, or one failing a check, takes the per-op path
+// (which raises the error flags).
+__device__ __forceinline__ void apply_move(const ApplyArgs& a, uint32_t i) {
+  const uint32_t s = a.op_slot[i];
+  if (a.check && s >= a.cap) {
+    atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SLOT);
+    return;
+  }
+  const uint32_t q0 = a.seq[s];
+  const float x = a.op_x[i], z = a.op_z[i];
+  if (a.check && q0 == 0) {
+    atomicOr(&a.ctr[CTR_ERR], ERR_ABSENT_SLOT);
+    return;
+  }
+  if (a.check && !(finite_bits(__float_as_uint(x)) && finite_bits(__float_as_uint(z)))) {
+    atomicOr(&a.ctr[CTR_ERR], ERR_BAD_COORD);
+    return;
+  }
+  const uint32_t q = a.base + i;
+  a.old_x[s] = a.pos_x[s];
+  a.old_z[s] = a.pos_z[s];
+  a.old_seq[s] = q0;
+  a.opq[s] = q;
+  a.pos_x[s] = x;
+  a.pos_z[s] = z;
+  a.seq[s] = q;
+}
+
+__global__ void __launch_bounds__(kBlock) k_apply_moves4(ApplyArgs a) {
+  const uint32_t i0 = 4u * (blockIdx.x * kBlock + threadIdx.x);
+  const uint32_t n_real = a.n_dev ? *a.n_dev : a.n_ops;
+  const uint32_t n = min(n_real, a.n_ops);
+  if (i0 == 0) {
+    a.ctr[CTR_NOPS] = n;
+    if (n_real > a.n_ops) atomicOr(&a.ctr[CTR_ERR], ERR_BAD_COUNT);
+    a.rank_cnt[a.n_ops] = 0u;
+  }
+  if (i0 >= a.n_ops) return;
+  if (i0 + 4 <= a.n_ops) {  // the sweep stores only non-zero event counts
+    *reinterpret_cast<uint4*>(&a.rank_cnt[i0]) = make_uint4(0u, 0u, 0u, 0u);
+  } else {
+    for (uint32_t i = i0; i < a.n_ops; ++i) a.rank_cnt[i] = 0u;
+  }
+  if (i0 + 4 <= n) {
+    const uint4 sl = *reinterpret_cast<const uint4*>(&a.op_slot[i0]);
+    if ((sl.x & 3u) == 0 && sl.y == sl.x + 1 && sl.z == sl.x + 2 && sl.w == sl.x + 3 && sl.w < a.cap) {
+      const uint32_t s = sl.x;
+      const uint4 q0 = *reinterpret_cast<const uint4*>(&a.seq[s]);
+      const float4 px = *reinterpret_cast<const float4*>(&a.pos_x[s]);
+      const float4 pz = *reinterpret_cast<const float4*>(&a.pos_z[s]);
+      const float4 ox = *reinterpret_cast<const float4*>(&a.op_x[i0]);
+      const float4 oz = *reinterpret_cast<const float4*>(&a.op_z[i0]);
+      auto fin = [](float v) { return finite_bits(__float_as_uint(v)); };
+      const bool ok = !a.check || (q0.x && q0.y && q0.z && q0.w && fin(ox.x) && fin(ox.y) && fin(ox.z) && fin(ox.w) &&
+                                   fin(oz.x) && fin(oz.y) && fin(oz.z) && fin(oz.w));
+      if (ok) {
+        const uint32_t q = a.base + i0;
+        const uint4 qn = make_uint4(q, q + 1, q + 2, q + 3);
+        *reinterpret_cast<float4*>(&a.old_x[s]) = px;
+        *reinterpret_cast<float4*>(&a.old_z[s]) = pz;
+        *reinterpret_cast<uint4*>(&a.old_seq[s]) = q0;
+        *reinterpret_cast<uint4*>(&a.opq[s]) = qn;
+        *reinterpret_cast<float4*>(&a.pos_x[s]) = ox;
+        *reinterpret_cast<float4*>(&a.pos_z[s]) = oz;
+        *reinterpret_cast<uint4*>(&a.seq[s]) = qn;
+        return;
+      }
+    }
+  }
+  for (uint32_t i = i0; i < i0 + 4 && i < n; ++i) apply_move(a, i);
+}
+
 void launch_apply(const ApplyArgs& a, hipStream_t st) {
   if (!a.n_ops) return;
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
+  if (!a.op_kind && !a.leaves && al16(a.op_slot) && al16(a.op_x) && al16(a.op_z)) {
+    const uint32_t groups = (a.n_ops + 3) / 4;
+    hipLaunchKernelGGL(k_apply_moves4, dim3((groups + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
+    return;
+  }
   hipLaunchKernelGGL(k_apply, dim3((a.n_ops + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
 }
 
