@@ -182,15 +182,39 @@ def _cpu_model():
     return None
 
 
-def load_pmc_traffic():
+def lib_stamp(L_):
+    """The source stamp compiled into the loaded library (gwaoi_version() ends with "src <hash>")."""
+    v = L_.gwaoi_version().decode()
+    return v, (v.rsplit(" src ", 1)[1] if " src " in v else None)
+
+
+def pmc_traffic(workload, n, stamp, kernels=None):
+    """HBM bytes per launch of the workload's roofline kernel(s), from the PMC passes summarised in
+    profiles/pmc_latest.json (scripts/make_pmc_latest.py), used only when those passes ran the SAME
+    library build as this run (the source stamp) at the same size. Returns (bytes or None, note)."""
     p = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if not os.path.exists(p):
-        return None
     try:
         with open(p) as f:
-            return json.load(f)
-    except Exception:
-        return None
+            pmc = json.load(f)
+    except Exception as e:
+        return None, f"no PMC summary ({e.__class__.__name__})"
+    w = pmc.get("workloads", {}).get(workload)
+    if w is None:
+        return None, f"no PMC pass for workload {workload} in profiles/pmc_latest.json"
+    if stamp is None or w.get("lib_src") != stamp:
+        return None, (f"stale: the PMC pass ran library src {w.get('lib_src')}, this run loaded src {stamp}; "
+                      "traffic withheld")
+    if w.get("n") != n:
+        return None, f"PMC pass at n={w.get('n')}, this run n={n}; traffic withheld"
+    if kernels is None:
+        kernels, b = w.get("kernels_summed", []), w.get("bytes_per_launch")
+    else:
+        kt = w.get("kernels", {})
+        b = sum(kt[k]["bytes"] for k in kernels) if all("bytes" in kt.get(k, {}) for k in kernels) else None
+    if b is None:
+        return None, f"no FETCH_SIZE/WRITE_SIZE for {kernels} in the PMC pass"
+    return b, (f"{w.get('source')}: {' + '.join(kernels)}, FETCH_SIZE x 2 (gfx950 wide-read correction) + "
+               "WRITE_SIZE, median per launch")
 
 
 def spaces_workload(args, rank):
@@ -377,6 +401,27 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     if rs is not None:
         rs.close()
 
+    # ---- a fixed loop of P device-resident ticks (events left in HBM), independent of
+    # --steps; the walk continues from the last staged tick, each tick's positions generated (and
+    # synchronised) before its clock starts ----
+    walk = DeviceBuffer(2 * 2 * 4 * n, dev)  # two [x|z][n] tick slots, ping-pong
+    wstate = {"prev": (px(T - 1), pz(T - 1)), "t": T, "k": 0}
+
+    def walk_next():
+        k = wstate["k"]
+        bx, bz = walk.ptr + (2 * k) * 4 * n, walk.ptr + (2 * k + 1) * 4 * n
+        wl_step_spaces(dev, *wstate["prev"], bx, bz, n_per, nsp, seed0, wstate["t"], L, 1.0)
+        wstate.update(prev=(bx, bz), t=wstate["t"] + 1, k=k ^ 1)
+        return bx, bz
+
+    lat_p = []
+    for _ in range(args.p99_ticks):
+        bx, bz = walk_next()
+        ts = time.perf_counter()
+        eng.stage_moves_device(slots.ptr, bx, bz, n)
+        eng.tick_device()
+        lat_p.append(time.perf_counter() - ts)
+
     # relation size for the SURVEY §8(d) formula (directed entries |S|)
     nnz = None
     rel_ms = rel_upd_ms = rel_upd_n = rel_delta_ms = rel_delta_n = rel_export_ms = rel_apply_ms = None
@@ -404,10 +449,10 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         except Exception as e:  # a bench aid: report, never fail the GPU line
             log(f"[rank {rank}] delta rows unavailable: {e!r}")
         dr_bad = 0
-        for j in range(10):  # more ticks of the walk, into snapshot slots 0/1 (their ticks are over)
-            a, b = (T - 1) if j == 0 else (j - 1) % 2, j % 2
-            wl_step_spaces(dev, px(a), pz(a), px(b), pz(b), n_per, nsp, seed0, T + j, L, 1.0)
-            tick_dev(b)
+        for j in range(10):  # more ticks of the walk
+            bx, bz = walk_next()
+            eng.stage_moves_device(slots.ptr, bx, bz, n)
+            eng.tick_device()
             L_.gwaoi_dev_sync(dev)
             # the consumer by delta: the tick's net relation changes, computed from its events in HBM
             # and copied to the host (gwaoi_export_relation_delta)
@@ -439,6 +484,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             reps.append(time.perf_counter() - t0)
         rel_export_ms = sorted(reps)[1] * 1e3
     eng.close()
+    walk.free()
     if rank != 0:
         return None
 
@@ -453,10 +499,9 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     cells = st["grid_cells"] / ticks
     b_sweep = 32.0 * rec_per_tick + 4.0 * cells + 4.0 * n + 16.0 * ev_per_tick
     achieved = b_sweep / (sweep_ms * 1e-3) / 1e9
-    pmc = load_pmc_traffic() if args.workload == "config2" else None
-    traffic = None
-    if pmc and pmc.get("n") == n and "sweep_bytes_per_launch" in pmc:
-        traffic = pmc["sweep_bytes_per_launch"] / (sweep_ms * 1e-3) / 1e9  # GB/s, same unit as achieved
+    lib_v, stamp = lib_stamp(L_)
+    t_bytes, t_note = pmc_traffic(args.workload if not args.dists else None, n, stamp)
+    traffic = t_bytes / (sweep_ms * 1e-3) / 1e9 if t_bytes else None  # GB/s, same unit as achieved
     # SURVEY.md §8(d) whole-tick formula (assumes a CSR-state design; ours keeps no lists)
     b_survey = 24.0 * n + 4.0 * (2 * nnz) + 8.0 * ev_per_tick if nnz is not None else None
     return {
@@ -478,8 +523,14 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "seed": hex(seed0 - rank * (nsp if nsp > 1 else 1)),
             "parallelism": "independent Spaces, one manager per GPU, no data-path collective" if world > 1 else "1 GPU",
         },
-        "p50_tick_ms": percentile(lat, 50) * 1e3,
-        "p99_tick_ms": percentile(lat, 99) * 1e3,
+        "p50_tick_ms": percentile(lat_p or lat, 50) * 1e3,
+        "p99_tick_ms": percentile(lat_p or lat, 99) * 1e3,
+        "p99_samples": len(lat_p or lat),
+        "p99_note": (f"host wall time of {len(lat_p)} device-resident ticks (stage_moves_device -> events ordered in "
+                     "HBM, count on the host) run after the timed region, each tick's positions generated before "
+                     "its clock starts" if lat_p else "over the timed ticks"),
+        "p50_tick_ms_timed": percentile(lat, 50) * 1e3,
+        "p99_tick_ms_timed": percentile(lat, 99) * 1e3,
         "p50_tick_ms_host_events": percentile(lat_host, 50) * 1e3 if lat_host else None,
         "p99_tick_ms_host_events": percentile(lat_host, 99) * 1e3 if lat_host else None,
         "p50_tick_ms_host_staged": percentile(lat_hs, 50) * 1e3 if lat_hs else None,
@@ -522,13 +573,15 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_bytes_per_launch": (pmc or {}).get("sweep_bytes_per_launch") if traffic else None,
+            "traffic_bytes_per_launch": t_bytes if traffic else None,
+            "traffic_note": t_note,
             "algorithmic_bytes_per_launch": b_sweep,
             "grid_records_per_tick": rec_per_tick,
             "grid_cells": cells,
             "dense_movers_per_tick": st["dense_movers"] / ticks,
-            "traffic_source": (pmc or {}).get("source") if traffic else None,
             "avg_launch_ms": sweep_ms,
+            "kernels_timed": "k_sweep" + (" + k_sweep_dense" if st["dense_movers"] else "") +
+                             " (the pass's sweep stage, hipEvents on the manager's stream)",
             "survey_formula": None if b_survey is None else {
                 "bytes_per_tick": b_survey,
                 "achieved_GBps_over_tick": b_survey / (ms_step * 1e-3) / 1e9,
@@ -537,6 +590,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
                         "design does not have (relation is recomputed from positions + op order)",
             },
         },
+        "lib": lib_v,
         "cpu_baseline": None,
     }
 
@@ -659,6 +713,9 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
     dom = max(stages, key=lambda k: stages[k][0])
     dd, db, dk = stages[dom]
     ach = gbs(db, dd)
+    lib_v, stamp = lib_stamp(L_)
+    t_bytes, t_note = pmc_traffic("gametick", n, stamp,
+                                  ["k_fan_tile<true>"] if dom == "write_walk" else ["k_gate_hist", "k_gate_scatter"])
     return {
         "metric": "GoWorld game tick (client position ingest + AOI tick + sync fan-out) entity-updates/s at 1M "
                   "entities per Space",
@@ -693,13 +750,15 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
                             "gate_partition": d_gate},
         "roofline": {
             "bound": "hbm", "kernel": dk, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": db,
+            "frac": ach / HBM_PEAK_GBS, "traffic": gbs(t_bytes, dd) if t_bytes else None,
+            "traffic_bytes_per_launch": t_bytes, "traffic_note": t_note, "algorithmic_bytes_per_launch": db,
             "avg_launch_ms": dd, "timing": "hipEvents on the manager's stream (gwaoi_sync_get_stats)",
             "stages": {k: {"kernel": v[2], "ms": v[0], "algorithmic_bytes": v[1], "achieved": gbs(v[1], v[0]),
                            "frac": gbs(v[1], v[0]) / HBM_PEAK_GBS} for k, v in stages.items()}
                       | {"ingest": {"ms": d_ing, "algorithmic_bytes": b_ing, "achieved": gbs(b_ing, d_ing),
                                     "frac": gbs(b_ing, d_ing) / HBM_PEAK_GBS}},
         },
+        "lib": lib_v,
         "cpu_baseline": None,
     }
 
@@ -795,6 +854,9 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
     rec_t = st["grid_records"] / ticks
     b_sweep = 32.0 * rec_t + 4.0 * st["grid_cells"] / ticks + 4.0 * ops_t + 16.0 * ev0_t
     ach = b_sweep / (sweep_ms * 1e-3) / 1e9 if sweep_ms > 0 else 0.0
+    from goworld_amd import _lib
+    lib_v, stamp = lib_stamp(_lib.load())
+    t_bytes, t_note = pmc_traffic(args.workload, n, stamp) if world == 1 else (None, "PMC passes run at one rank")
     return {
         "metric": METRIC,
         "value": n * K / elapsed,
@@ -830,11 +892,14 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
         "stage_ms_rank0": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
         "roofline": {
             "bound": "hbm", "kernel": "k_sweep (rank 0's strip)", "achieved": ach, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes_per_launch": b_sweep,
+            "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": t_bytes / (sweep_ms * 1e-3) / 1e9 if t_bytes and sweep_ms > 0 else None,
+            "traffic_bytes_per_launch": t_bytes, "traffic_note": t_note, "algorithmic_bytes_per_launch": b_sweep,
             "avg_launch_ms": sweep_ms, "grid_records_per_tick": rec_t, "movers_per_tick": ops_t,
             "timing": "hipEvents around the sweep launch (gwaoi_get_stats)",
             "halo_bytes_per_tick": 16.0 * sent / K,
         },
+        "lib": lib_v,
         "cpu_baseline": None,
     }
 
@@ -908,6 +973,8 @@ def main():
     ap.add_argument("--gates", type=int, default=8, help="gametick: gates (dense indices)")
     ap.add_argument("--client-frac", type=float, default=0.25, help="gametick: fraction of entities with a client")
     ap.add_argument("--latency-ticks", type=int, default=200, help="extra ticks with events delivered to host")
+    ap.add_argument("--p99-ticks", type=int, default=1000,
+                    help="device-resident ticks after the timed region for p50/p99 (SURVEY 8(d): >= 1,000)")
     ap.add_argument("--host-staged-ticks", type=int, default=50,
                     help="extra ticks staged from host arrays (gwaoi_stage_moves), events to host, replayed")
     ap.add_argument("--no-replay", dest="replay", action="store_false",

@@ -36,16 +36,35 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def source_hash(defines=()) -> str:
+    """sha256 (16 hex digits) over the library's sources, headers, compile flags and A/B defines. It is
+    compiled into the library (gwaoi_version() ends with "src <hash>") so that measurements taken with
+    one build (the PMC traffic in profiles/pmc_latest.json) can be matched to the library bench.py loads."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(SOURCES + HEADERS + ["gwaoi_device.h"]):
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    for f in sorted(PUBLIC):
+        with open(os.path.join(ROOT, "include", f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    h.update(" ".join(_FLAGS + [f"-D{d}" for d in defines] + [ARCH]).encode())
+    return h.hexdigest()[:16]
+
+
+_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+          "-fno-gpu-flush-denormals-to-zero", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
+
+
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
     """Compile the library to `out`; `defines` (e.g. ["GW_SWEEP_BLOCK=512"]) builds an A/B variant."""
     if not force and out == OUT and not _stale():
         return OUT
+    # _FLAGS: IEEE binary32 (no contraction, denormals kept); LDS event-queue atomics are one
+    # ds_add_rtn each (the wave-reduction rewrite the atomic optimizer wraps around every call costs
+    # more than it saves at ~1 event per 100 candidates)
     cmd = [
-        hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-ffp-contract=off", "-fno-fast-math", "-fno-gpu-flush-denormals-to-zero",
-        # LDS event-queue atomics are one ds_add_rtn each; the wave-reduction rewrite the atomic
-        # optimizer wraps around every call costs more than it saves at ~1 event per 100 candidates
-        "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
+        hipcc(), f"--offload-arch={ARCH}", *_FLAGS, f'-DGWAOI_SRC_HASH="{source_hash(defines)}"',
         "-Wall", "-Wno-unused-result", "-Wno-unused-value",
         f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}",
         *[f"-D{d}" for d in defines],

@@ -1141,7 +1141,11 @@ int mgr_stage_moves_device_n(gwaoi_mgr* m, const uint32_t* d_slots, const float*
 
 extern "C" {
 
-const char* gwaoi_version(void) { return "gwaoi 0.3.0 (gfx950, abi 2)"; }
+#ifndef GWAOI_SRC_HASH
+#define GWAOI_SRC_HASH "unstamped"
+#endif
+// the source stamp (goworld_amd/build.py source_hash) ties measurements to the build they came from
+const char* gwaoi_version(void) { return "gwaoi 0.4.0 (gfx950, abi 2) src " GWAOI_SRC_HASH; }
 int gwaoi_abi_version(void) { return GWAOI_ABI_VERSION; }
 const char* gwaoi_last_error(void) { return g_err.c_str(); }
 
