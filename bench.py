@@ -158,6 +158,13 @@ def cpu_baseline_spaces(n_per, L, dist, seed0, nspaces, target_s, threads=None):
             "cpu": _cpu_model()}
 
 
+def sink_workers():
+    """Worker threads of the sharded host sinks: the process's CPU share (OMP_NUM_THREADS on the GPU box),
+    at most the usable cores."""
+    usable, _ = host_cores()
+    return max(1, min(usable, int(os.environ.get("OMP_NUM_THREADS", usable) or usable), 16))
+
+
 def host_cores():
     """(usable, nproc): the cores this process may run on (affinity, and the cgroup CPU quota when one is
     set) and the machine's logical CPU count."""
@@ -348,19 +355,23 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     # tick) to the events in the pinned host buffer; then the events replayed into per-entity hash sets
     # (tools/replay_sets.c: Entity.interest/uninterest, 4 set ops per pair event, Entity.go:227-246) ----
     lat_hs, stage_hs, replay_s, replay_bad = [], [], [], 0
-    rs = None
+    replay_sh_s, replay_sh_bad = [], 0
+    rs = rss = None
+    sink_threads = sink_workers()
     if HS and args.replay and nsp == 1:
         try:
-            from tools.replay import ReplaySets
+            from tools.replay import ReplaySets, ShardedReplaySets
             rp_h, cols_h = eng.relation()
             rs = ReplaySets(2 * len(cols_h))
             t_ld = time.perf_counter()
             rs.load_relation(rp_h, cols_h)
             log(f"[rank {rank}] replay sets: {rs.size()} entries loaded in {time.perf_counter() - t_ld:.1f}s")
+            rss = ShardedReplaySets(2 * len(cols_h), sink_threads)
+            rss.load_relation(rp_h, cols_h)
             del rp_h, cols_h
         except Exception as e:  # the tool is a bench aid: report, never fail the GPU line
             log(f"[rank {rank}] replay sets unavailable: {e!r}")
-            rs = None
+            rs = rss = None
     if HS:
         eng.adopt_device_state()  # the restore was a device batch: host staging from here on
     # the cgo wrapper's path: Moved calls written into the manager's pinned staging arrays as the client
@@ -398,8 +409,14 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             tr = time.perf_counter()
             replay_bad += rs.replay(ctypes.cast(ev.events, ctypes.c_void_p).value, int(ev.count))
             replay_s.append(time.perf_counter() - tr)
+        if rss is not None and ev.count:
+            tr = time.perf_counter()
+            replay_sh_bad += rss.replay(ctypes.cast(ev.events, ctypes.c_void_p).value, int(ev.count))
+            replay_sh_s.append(time.perf_counter() - tr)
     if rs is not None:
         rs.close()
+    if rss is not None:
+        rss.close()
 
     # ---- a fixed loop of P device-resident ticks (events left in HBM), independent of
     # --steps; the walk continues from the last staged tick, each tick's positions generated (and
@@ -425,6 +442,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     # relation size for the SURVEY §8(d) formula (directed entries |S|)
     nnz = None
     rel_ms = rel_upd_ms = rel_upd_n = rel_delta_ms = rel_delta_n = rel_export_ms = rel_apply_ms = None
+    rel_apply_mt_ms = None
     dr_bad = None
     if args.workload in ("config2", "config3"):  # config 5's relation runs to billions of entries
         # the relation as a device-resident CSR (SURVEY 8(f)3 view), timed host-side incl. its syncs:
@@ -441,7 +459,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         rel_ms = sorted(reps)[len(reps) // 2] * 1e3
         eng.debug_relation_mode(0)
         n_inc0 = eng.debug_relation_mode()[0]
-        reps, dreps, dlen, areps = [], [], [], []
+        reps, dreps, dlen, areps, areps_mt = [], [], [], [], []
         dr = None
         try:  # the consumer by delta on the host: per-slot sorted neighbour arrays (tools/delta_rows.c)
             from tools.replay import DeltaRows
@@ -460,10 +478,10 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             dl = eng.relation_delta(cap=4 * n)
             dreps.append(time.perf_counter() - t0)
             dlen.append(len(dl))
-            if dr is not None:
+            if dr is not None:  # (alternate ticks: one thread, then the rows over sink_threads workers)
                 t0 = time.perf_counter()
-                dr_bad += dr.apply(dl)
-                areps.append(time.perf_counter() - t0)
+                dr_bad += dr.apply(dl, threads=1 if j % 2 == 0 else sink_threads)
+                (areps if j % 2 == 0 else areps_mt).append(time.perf_counter() - t0)
             t0 = time.perf_counter()
             eng.relation_device()
             L_.gwaoi_dev_sync(dev)
@@ -472,6 +490,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         rel_delta_ms = sorted(dreps)[len(dreps) // 2] * 1e3
         rel_delta_n = float(np.mean(dlen))
         rel_apply_ms = sorted(areps)[len(areps) // 2] * 1e3 if areps else None
+        rel_apply_mt_ms = sorted(areps_mt)[len(areps_mt) // 2] * 1e3 if areps_mt else None
         if dr is not None:
             dr_bad += dr.diff(*eng.relation())  # the patched arrays must equal the relation now
             dr.close()
@@ -538,6 +557,10 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         "host_stage_ms": percentile(stage_hs, 50) * 1e3 if stage_hs else None,
         "host_stage_copyin_ms": percentile(stage_ci, 50) * 1e3 if stage_ci else None,
         "replay_ms": percentile(replay_s, 50) * 1e3 if replay_s else None,
+        "replay_ms_sharded": percentile(replay_sh_s, 50) * 1e3 if replay_sh_s else None,
+        "replay_sharded_note": (f"the same set operations split by owning entity over {sink_threads} worker threads "
+                                f"(tools/replay_sets.c rs_sharded_*); {replay_sh_bad} inconsistent set ops")
+        if replay_sh_s else None,
         "replay_note": ("events replayed into per-entity InterestedIn/InterestedBy hash sets in C, 4 set ops per "
                         "pair event (tools/replay_sets.c); host_staged = gwaoi_stage_moves_pinned (the positions "
                         "written into the manager's pinned staging arrays; one DMA copy, validated on the GPU) -> "
@@ -552,6 +575,8 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         "relation_delta_entries": rel_delta_n,
         "relation_export_ms": rel_export_ms,
         "relation_delta_apply_ms": rel_apply_ms,
+        "relation_delta_apply_ms_threads": rel_apply_mt_ms,
+        "sink_threads": sink_threads,
         "relation_delta_inconsistent": dr_bad,
         "relation_consumer_note": None if rel_delta_ms is None else
         "relation_delta_ms = gwaoi_export_relation_delta (net changes of the tick from its events in HBM, "
@@ -579,8 +604,10 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "grid_records_per_tick": rec_per_tick,
             "grid_cells": cells,
             "dense_movers_per_tick": st["dense_movers"] / ticks,
+            "chunked_movers_per_tick": st["chunked_movers"] / ticks,
             "avg_launch_ms": sweep_ms,
-            "kernels_timed": "k_sweep" + (" + k_sweep_dense" if st["dense_movers"] else "") +
+            "kernels_timed": "k_sweep" + (" + k_sweep_chunked" if st["chunked_movers"] else "") +
+                             (" + k_sweep_dense" if st["dense_movers"] else "") +
                              " (the pass's sweep stage, hipEvents on the manager's stream)",
             "survey_formula": None if b_survey is None else {
                 "bytes_per_tick": b_survey,
@@ -802,9 +829,9 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
     log(f"[rank {rank}] strips setup {time.perf_counter() - t_setup:.1f}s: world {n} entities, L={L:.0f}, "
         f"{nd.last_ops} in this region, {int(ev0.count)} owned enter pairs")
 
-    def tick(t):
+    def tick(t, time_exchange=False):
         if comm is not None:
-            ev = nd.tick_rccl(t, comm)
+            ev = nd.tick_rccl(t, comm, time_exchange=time_exchange)
             return ev, 0  # halo counts are read from the device after the run
         lo, ro = nd.prepare(t)
         if world > 1:
@@ -832,9 +859,10 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
     nd.eng.set_timing(True)
     nd.eng.reset_stats()
     for t in range(W + K + 1, W + K + S + 1):
-        tick(t)
+        tick(t, time_exchange=True)
     st = nd.eng.stats()
     nd.eng.set_timing(False)
+    xms = nd.exchange_ms() if comm is not None else None
     if comm is not None:  # the last tick's halo sizes (the RCCL path keeps them on the device)
         sent = int(nd.counts[:2].sum().item()) * K
     nd.close()
@@ -845,6 +873,7 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
         tot = torch.tensor([evs, sent], dtype=torch.float64, device="cpu" if via_cpu else torch.device("cuda", dev))
         dist.all_reduce(tot)
         evs, sent = float(tot[0]), float(tot[1])
+    xms_max = allmax(xms) if xms is not None else None
     if rank != 0:
         return None
     ticks = max(1, st["ticks"])
@@ -888,6 +917,10 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
         "p99_tick_ms": percentile(lat, 99) * 1e3,
         "events_per_tick": evs / K,
         "halo_records_per_tick": sent / K,
+        "exchange_ms": xms_max,
+        "exchange_note": None if xms_max is None else
+        f"gwaoi_strip_exchange device time per tick (hipEvents on the strip's stream around the RCCL group, the "
+        f"wait for the neighbours included), mean over {S} instrumented ticks, max over ranks",
         "rank0_ops_per_tick": ops / K,
         "stage_ms_rank0": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
         "roofline": {
@@ -902,6 +935,61 @@ def run_strips(args, rank, world, dev, sync_all, allmax, via_cpu):
         "lib": lib_v,
         "cpu_baseline": None,
     }
+
+
+def strips_submeasurement(args, rank, world, dev, sync_all, allmax, backend):
+    """The config-4 strips line of this world size, condensed (run by every rank: the exchange is
+    collective). Under --dry-run (CPU rehearsal of the plumbing) only the rendezvous and its shape."""
+    import copy
+    sa = copy.copy(args)
+    sa.workload, sa.steps, sa.warmup = "strips", args.strips_steps, min(args.warmup, 5)
+    sa.stage_ticks = min(args.stage_ticks, 20)
+    if args.dry_run:
+        sync_all()
+        return {"dry_run": True, "workload": "strips", "n_gpus": world, "steps": sa.steps,
+                "elapsed": allmax(0.001 * (rank + 1))} if rank == 0 else (allmax(0.001 * (rank + 1)) and None)
+    r = run_strips(sa, rank, world, dev, sync_all, allmax, via_cpu=(backend == "gloo"))
+    if rank != 0:
+        return None
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "scaling", "p50_tick_ms",
+            "p99_tick_ms", "events_per_tick", "halo_records_per_tick", "exchange_ms", "exchange_note",
+            "stage_ms_rank0", "config", "roofline")
+    return {k: r.get(k) for k in keep}
+
+
+def arm_deadline(seconds, rank, result):
+    """Timer for a sub-measurement: when it fires, rank 0 prints `result` (the measured line) with the
+    sub-measurement marked as timed out, and every rank exits with status 0."""
+    import threading
+
+    def fire():
+        log(f"[rank {rank}] strips sub-measurement still running after {seconds:.0f}s: abandoned")
+        if rank == 0:
+            result["strips"] = {"error": f"did not finish within {seconds:.0f}s (abandoned; the headline line "
+                                         "above it was measured before it started)"}
+            print(json.dumps(result), file=_stdout_for_json(), flush=True)
+        os._exit(0)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
+def arm_watchdog(seconds, rank):
+    """A daemon timer that ends this rank with status 3 after `seconds` (a hung collective or kernel then
+    fails the launcher instead of holding the GPUs). os._exit from the timer thread: no exec, no
+    cleanup that could itself block on the device."""
+    import threading
+
+    def fire():
+        log(f"[rank {rank}] watchdog: still running after {seconds:.0f}s, exiting with status 3")
+        os._exit(3)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def self_launch_command(argv, env, gpus, port):
@@ -993,6 +1081,12 @@ def main():
                     help="launch + rendezvous + barrier only, no GPU work (CPU test of the multi-rank plumbing)")
     ap.add_argument("--stamps", default=None, help="diagnostic GW_STAMPS build: dump the last sweep's per-block "
                                                    "phase timestamps to this .npy file")
+    ap.add_argument("--strips-steps", type=int, default=100,
+                    help="N > 1 (config 2): ticks of the config-4 X-strip sub-measurement (RCCL halo exchange over "
+                         "xGMI) appended to the line as \"strips\" (0: none)")
+    ap.add_argument("--watchdog", type=float, default=None,
+                    help="seconds after which a rank still running exits with status 3 (a hung collective ends the "
+                         "job instead of holding the GPUs; default 900 + 2 ms per step)")
     args = ap.parse_args()
 
     # N > 1 without an external launcher: start the ranks as a child before any GPU call
@@ -1003,6 +1097,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    arm_watchdog(args.watchdog if args.watchdog is not None else 900.0 + 0.002 * (args.steps + args.strips_steps),
+                 rank)
     if world != args.gpus:
         log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
 
@@ -1042,13 +1138,23 @@ def main():
     if args.dry_run:
         sync_all()
         result = {"dry_run": True, "n_gpus": world, "devices": ndev, "backend": backend,
-                  "elapsed": allmax(0.001 * (rank + 1))}
+                  "elapsed": allmax(0.001 * (rank + 1)), "workload": args.workload}
     elif args.workload in ("strips", "strips_skew"):
         result = run_strips(args, rank, world, dev, sync_all, allmax, via_cpu=(backend == "gloo"))
     elif args.workload == "gametick":
         result = run_gametick(args, rank, world, dev, sync_all, allmax)
     else:
         result = run_spaces(args, rank, world, dev, sync_all, allmax)
+    # N > 1: the config-4 X-strip world (2M per GPU, halo exchange by RCCL p2p over xGMI inside libgwaoi)
+    # measured after the headline line and appended to it; `value` stays the headline workload's
+    if world > 1 and args.workload == "config2" and args.strips_steps > 0:
+        # its own deadline: the headline line is already measured, so a strips run that does not finish
+        # (a hung RCCL peer) is reported in it, and every rank ends cleanly, instead of losing the line
+        guard = arm_deadline(120.0 + 0.05 * args.strips_steps, rank, result)
+        sub = strips_submeasurement(args, rank, world, dev, sync_all, allmax, backend)
+        guard.cancel()
+        if rank == 0:
+            result["strips"] = sub
 
     # ---- CPU baseline (rank 0, N=1: config 2, and config 3 per Space) ----
     if rank == 0 and world == 1 and args.workload == "config2" and not args.no_cpu_baseline:

@@ -74,6 +74,20 @@ __device__ __forceinline__ void row_entries_global(const Geom& g, const uint32_t
   }
 }
 
+// The same rows as [begin, end) record ranges: f(b, e) once per tile crossed.
+template <class F>
+__device__ __forceinline__ void row_entries_ranges(const Geom& g, const uint32_t* __restrict__ cs, int r, int c0,
+                                                   int c1, F&& f) {
+  if (c0 > c1) return;
+  const uint32_t rowbase = g.base + ((uint32_t)((r >> kTileShift) * g.ntx) << kTileCellShift) +
+                           (uint32_t)((r & (kTile - 1)) << kTileShift);
+  for (int tx = c0 >> kTileShift; tx <= (c1 >> kTileShift); ++tx) {
+    const int lo = max(c0, tx << kTileShift), hi = min(c1, (tx << kTileShift) + kTile - 1);
+    const uint32_t k = rowbase + ((uint32_t)tx << kTileCellShift) + (uint32_t)(lo & (kTile - 1));
+    f(cs[k], cs[k + (uint32_t)(hi - lo) + 1]);
+  }
+}
+
 // A Space's geometry as block-uniform values: every field read through readfirstlane, so the
 // compiler keeps them (and what is derived from them) in scalar registers. The loads themselves are
 // vector loads (the kernels also store to global memory, so the compiler does not use the scalar
@@ -92,7 +106,7 @@ __device__ __forceinline__ Geom uniform_geom(const Geom* p) {
   g.base = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.base);
   g.tile_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.tile_base);
   g.reach = __builtin_amdgcn_readfirstlane(v.reach);
-  g.pad = 0;
+  g.pad = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.pad);
   return g;
 }
 

@@ -22,7 +22,12 @@ enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 
        CTR_DENSE = 7, CTR_HOLES = 8, CTR_NOPS = 9,  // ops of the pass (device-counted batches)
        CTR_BOVF = 10,   // the one-pass build overflowed a tile's bucket: the pass is re-run (counting build)
        CTR_NEV = 11,    // events of the pass (scan total of the per-op counts; k_place)
+       CTR_UNSORTED = 12,  // set when some op's events were numbered out of canonical order (k_slice_sort sorts)
+       CTR_BAND_ITEMS = 13,  // items of k_sweep_chunked listed by k_sweep (crowded tiles)
+       CTR_BAND_MV = 14,     // movers in those items
        CTR_BDONE = 16,  // blocks of the one-pass build done (not published)
+       CTR_SDONE = 17,  // blocks of k_slice_sort done (the last one publishes the counters)
+       CTR_BAND_NEXT = 18,  // k_sweep_chunked's work counter
        CTR_N = 32 };
 constexpr int kPubWords = 16;  // counters [0, 16) are what the host reads after a pass
 // CTR_EVENTS counts SLOTS of ev_tmp's shared region (after the per-tile regions, SweepArgs.ev_fix);
@@ -54,8 +59,8 @@ struct Geom {
   int32_t ntx, ntz;   // tiles per axis
   uint32_t base;      // first cell key of this Space
   uint32_t tile_base; // first tile index of this Space (base / kTileCells)
-  int32_t reach;      // halo (cells) staged around a tile in the sweep
-  uint32_t pad;
+  int32_t reach;      // halo (cells) staged around a tile in the sweep (0: the region does not fit k_sweep)
+  uint32_t pad;       // halo of the chunked sweep (k_sweep_chunked; 0: none, the dense walk instead)
 };
 
 // The pass's grid: every record sorted by cell key (counting sort). Per slot: a MAIN record at its
@@ -101,7 +106,43 @@ struct ApplyArgs {
   uint32_t* opq;             // op seq of this pass (stale for slots without an op)
   uint32_t* ctr;
   uint32_t* rank_cnt;        // [n_ops + 1]: zeroed here (the sweep stores non-zero counts; [n_ops] = scan total)
+  // small pass (ov_rec non-null): every op's slot joins the overlay (the slots with an op since the grid
+  // was built): ov_tag[slot] = gen marks it, ov_idx[slot] its entry, ov_rec[entry] its record as a grid
+  // build would write it (main record, or a ghost for a Leave)
+  uint32_t gen;
+  uint32_t* ov_tag;
+  uint32_t* ov_idx;
+  Rec* ov_rec;
+  uint32_t* ov_count;        // device: overlay entries
+  uint32_t ov_cap;
 };
+
+// Small pass: the movers of a pass with few ops judged against the last full build's grid (records of
+// slots without an op since then; their state is the record's end state) plus the overlay (every slot
+// with an op since then, one record each), without rebuilding the grid (k_sweep_small).
+struct SmallArgs {
+  GridView g;                // the grid of the last full build
+  uint32_t base, n_ops;
+  const uint32_t* n_dev;     // device-counted batch (null: n_ops)
+  const uint32_t* op_slot;
+  const uint8_t* op_kind;    // null: all moves
+  const uint32_t* space_of;
+  const float* pos_x;
+  const float* pos_z;
+  const float* old_x;
+  const float* old_z;
+  const uint32_t* old_seq;
+  const uint32_t* opq;
+  uint32_t gen;
+  const uint32_t* ov_tag;
+  const Rec* ov_rec;
+  const uint32_t* ov_count;
+  uint4* ev_tmp;             // shared region (slots from ctr[CTR_EVENTS], reserved per wave)
+  uint32_t ev_cap;
+  uint32_t* rank_cnt;
+  uint32_t* ctr;
+};
+void launch_sweep_small(const SmallArgs& a, hipStream_t st);
 
 struct BinArgs {
   const float* pos_x;
@@ -135,6 +176,7 @@ struct BinArgs {
   Rec* trec;                  // records bucketed by tile (the other grid's buffer: unused this pass)
   const uint8_t* op_kind;     // the pass's op kinds (null: all moves), for tile_walk
   uint32_t* tile_walk;        // [ntiles] out: 1 = the tile holds a reported mover (k_sweep skips the rest)
+  uint32_t* tile_acted;       // [ntiles] out: slots with an op in this pass, counted once per slot (k_bin_tsort)
 };
 
 // Slots per block of the tile-bucketed build (at least; a capacity over 256 chunks gets larger
@@ -190,7 +232,14 @@ struct SweepArgs {
   uint32_t* ctr;
   uint32_t* dense;      // slots of movers for k_sweep_dense (boxes beyond the tile's LDS region)
   uint32_t dense_cap;
-  uint32_t dense_hint;  // dense movers of the previous pass (0: launch k_sweep_dense small)
+  uint32_t dense_hint;  // dense movers of the previous pass (0: k_sweep_dense not launched)
+  uint32_t* band_mv;    // k_sweep_chunked: movers (grid indices) of crowded tiles, null: no chunked sweep
+  uint32_t band_mv_cap;
+  uint4* band_items;    // {tile, first mover, movers, 0}
+  uint32_t band_items_cap;
+  uint32_t band_hint;   // items of the previous pass (0: k_sweep_chunked not launched)
+  uint32_t chunk_max_recs;  // tiles holding more records take the dense walk instead (hotspot crowds)
+  uint32_t chunk_grid;  // its blocks (one per CU)
   const uint32_t* tile_walk;  // per tile: holds a reported mover (null: k_sweep scans the tile's records)
 };
 
@@ -210,6 +259,8 @@ struct RelArgs {
   uint32_t* maxlen;         // count pass: longest row
   uint32_t* slab;           // count pass, optional: the rows by grid record, interleaved (k_row_sort_slab)
   uint32_t slab_s;          // entries per row kept in the slab (rows longer than this: not kept)
+  uint32_t slab_recs;       // grid records the slab has rows for: a record past them writes no slab row and
+                            // reports a row longer than slab_s (the host then takes the two-walk path)
 };
 
 // Incremental relation view (gwaoi_relation_device after a tick whose events are all in ev_out).
@@ -268,6 +319,8 @@ uint32_t sweep_ev_lds();  // events queued per tile block (the per-tile region s
 size_t sweep_lds_bytes();
 uint32_t sweep_block();  // threads per sweep block
 void sweep_init();  // once per process (dynamic LDS limit of the sweep)
+void chunk_init();  // once per process (dynamic LDS limit of the chunked sweep)
+size_t chunk_lds_bytes();
 int read_stamps(void* host, size_t bytes);
 int sweep_occupancy(int* blocks);  // resident sweep blocks per CU (HIP occupancy API)  // GW_STAMPS diagnostic builds only (else -1)
 // Event ordering runs without a host round trip: each step checks on the device that the sweep's
@@ -297,10 +350,20 @@ struct OrderArgs {
   const uint32_t* op_slot;   // device-staged batch check: every op's slot carries that op's seq
   const uint32_t* opq;
   uint32_t base, cap;
-  int check_ops;
+  int check_ops;             // k_slice_sort checks every op's slot carries its seq (non-tile builds)
   const uint32_t* n_dev;  // device-counted batch: ranks >= *n_dev are not ops
+  // tile builds of device batches: k_place compares the slots that acted (k_bin_tsort's per-tile counts)
+  // with the op count instead (a duplicate slot leaves one slot for two ops)
+  const uint32_t* tile_acted;
+  uint32_t ntiles_acted;     // 0: no such check
+  uint32_t* pub;             // mapped host publication buffer (null: the host copies the counters itself)
+  uint32_t pub_seq;          // sequence word published with the counters
+  int sorted_hint;           // the previous pass needed no slice sort: k_slice_sort runs as a few blocks,
+                             // the last of which publishes (else one thread per op, then k_publish)
+  uint32_t place_blocks;     // k_place's grid (0: 1024)
 };
-// k_place (+ zeroing side jobs) -> k_slice_sort (+ batch check) -> k_copy_out (if host_out)
+// k_place (+ zeroing side jobs, duplicate-slot check) -> k_slice_sort (+ batch check, publication of
+// the counters by its last block when o.pub) -> k_copy_out (if host_out)
 void launch_order(const OrderArgs& o, hipStream_t st);
 void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_t st);
 void launch_relation(const RelArgs& a, hipStream_t st);

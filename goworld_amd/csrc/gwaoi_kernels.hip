@@ -58,6 +58,27 @@ __device__ __forceinline__ void put_count(uint32_t* rank_cnt, uint32_t rank, uin
   if (cnt) rank_cnt[rank] = cnt;
 }
 
+// Small pass: slot s's overlay record after its op (seq q; q0 = its seq before, 0 = absent): the main
+// record a grid build would write at its end position (start state in .b), or for a Leave its ghost at
+// the start position. The slot joins the overlay the first time it has an op since the grid was built.
+__device__ __forceinline__ void overlay_put(const ApplyArgs& a, uint32_t s, uint8_t kind, uint32_t q, uint32_t q0,
+                                            float x0, float z0, float x1, float z1) {
+  uint32_t e;
+  if (a.ov_tag[s] == a.gen) {
+    e = a.ov_idx[s];
+  } else {
+    e = atomicAdd(a.ov_count, 1u);  // (small passes only: a few ops)
+    a.ov_tag[s] = a.gen;
+    a.ov_idx[s] = e;
+  }
+  if (e >= a.ov_cap) return;  // (the host bounds the overlay below ov_cap)
+  const bool leave = kind == OP_LEAVE;
+  const uint4 ra = make_uint4(__float_as_uint(leave ? x0 : x1), __float_as_uint(leave ? z0 : z1),
+                              s | (leave ? REC_GHOST : 0u), q);
+  const uint4 rb = make_uint4(__float_as_uint(q0 ? x0 : x1), __float_as_uint(q0 ? z0 : z1), q0, leave ? 0u : q);
+  a.ov_rec[e] = Rec{ra, rb};
+}
+
 __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t n_real = a.n_dev ? *a.n_dev : a.n_ops;
@@ -105,8 +126,9 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   }
   if (!ok) return;
   const uint32_t q = a.base + i;
-  a.old_x[s] = a.pos_x[s];
-  a.old_z[s] = a.pos_z[s];
+  const float x0 = a.pos_x[s], z0 = a.pos_z[s];
+  a.old_x[s] = x0;
+  a.old_z[s] = z0;
   a.old_seq[s] = q0;
   a.opq[s] = q;
   if (kind == OP_LEAVE) {
@@ -117,6 +139,7 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
     a.seq[s] = q;
     if (kind == OP_ENTER) a.space_of[s] = a.op_space ? a.op_space[i] : 0u;
   }
+  if (a.ov_rec) overlay_put(a, s, kind, q, q0, x0, z0, kind == OP_LEAVE ? x0 : a.op_x[i], kind == OP_LEAVE ? z0 : a.op_z[i]);
 }
 
 // Moved-only batches (no kinds, no Leave list) with 16-B aligned op arrays: four ops per thread. A
@@ -196,7 +219,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_moves4(ApplyArgs a) {
 void launch_apply(const ApplyArgs& a, hipStream_t st) {
   if (!a.n_ops) return;
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15u) == 0; };
-  if (!a.op_kind && !a.leaves && al16(a.op_slot) && al16(a.op_x) && al16(a.op_z)) {
+  if (!a.op_kind && !a.leaves && !a.ov_rec && al16(a.op_slot) && al16(a.op_x) && al16(a.op_z)) {
     const uint32_t groups = (a.n_ops + 3) / 4;
     hipLaunchKernelGGL(k_apply_moves4, dim3((groups + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
     return;
@@ -753,6 +776,13 @@ __device__ __forceinline__ bool bin_walker(const BinArgs& a, const uint4 ra) {
   return !(ra.z & REC_GHOST) && r < a.n_ops && !(a.op_kind && (a.op_kind[r] & OP_SILENT));
 }
 
+// a record that stands for a slot with an op in this pass, once per slot: its main record, or, for a
+// slot that left (absent at the end: seq_end 0), its ghost. k_place compares the sum with the op count:
+// two ops on one slot (a device batch's duplicate) leave one acted slot for two ops.
+__device__ __forceinline__ uint32_t bin_acted(const BinArgs& a, const uint4 ra, const uint4 rb) {
+  return ((ra.w - a.base) < a.n_ops && (!(ra.z & REC_GHOST) || rb.w == 0u)) ? 1u : 0u;
+}
+
 __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   __shared__ uint32_t cnt[kTileCells];
   __shared__ uint32_t ws[kBlock / 64];
@@ -763,7 +793,7 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   const uint32_t pb = a.fused ? plan_start(a.tprev, t) : ob;
   if (ovf) {  // the plan did not hold: an empty grid (nothing walks), the pass re-runs
     for (int c = threadIdx.x; c < kTileCells; c += kBlock) a.cs[(t << kTileCellShift) + c] = 0u;
-    if (threadIdx.x == 0) a.tile_walk[t] = 0u;
+    if (threadIdx.x == 0) a.tile_walk[t] = 0u, a.tile_acted[t] = 0u;
     if (t + 1 == a.ntiles && threadIdx.x == 0) a.cs[a.ntiles << kTileCellShift] = 0u;
     return;
   }
@@ -790,20 +820,33 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
   }
   __syncthreads();
   bool walk = false;  // the tile holds a mover whose events are reported (k_sweep skips the others)
+  uint32_t acted = 0;  // slots of this pass's ops, each counted once (bin_acted)
   if (small) {
-    if (on0) atomicAdd(&cnt[c0], 1u), walk |= bin_walker(a, a0);
-    if (on1) atomicAdd(&cnt[c1], 1u), walk |= bin_walker(a, a1);
-    if (on2) atomicAdd(&cnt[c2], 1u), walk |= bin_walker(a, a2);
-    if (on3) atomicAdd(&cnt[c3], 1u), walk |= bin_walker(a, a3);
+    if (on0) atomicAdd(&cnt[c0], 1u), walk |= bin_walker(a, a0), acted += bin_acted(a, a0, b0);
+    if (on1) atomicAdd(&cnt[c1], 1u), walk |= bin_walker(a, a1), acted += bin_acted(a, a1, b1);
+    if (on2) atomicAdd(&cnt[c2], 1u), walk |= bin_walker(a, a2), acted += bin_acted(a, a2, b2);
+    if (on3) atomicAdd(&cnt[c3], 1u), walk |= bin_walker(a, a3), acted += bin_acted(a, a3, b3);
   } else {
     for (uint32_t j = b + threadIdx.x; j < e; j += kBlock) {
       const uint4 ra = a.trec[j].a;
       atomicAdd(&cnt[tile_cell(g, __uint_as_float(ra.x), __uint_as_float(ra.y))], 1u);
       walk |= bin_walker(a, ra);
+      acted += bin_acted(a, ra, a.trec[j].b);
     }
   }
   const int any_walker = __syncthreads_or(walk);
   if (threadIdx.x == 0) a.tile_walk[t] = any_walker ? 1u : 0u;
+  {
+    const uint32_t wa = __builtin_amdgcn_readlane(wave_incl_scan(acted), 63);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = wa;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (int k = 0; k < kBlock / 64; ++k) tot += ws[k];
+      a.tile_acted[t] = tot;
+    }
+    __syncthreads();  // ws is reused by the scan below
+  }
   // exclusive scan of the 1024 counts (4 per thread, consecutive)
   constexpr int kPer = kTileCells / kBlock;
   static_assert(kPer == 4, "one uint4 of counts per thread");
@@ -893,6 +936,7 @@ void launch_bin_tiles(const BinArgs& a, hipStream_t st) {
 #ifndef GW_SWEEP_WAVES_PER_EU
 #define GW_SWEEP_WAVES_PER_EU 6
 #endif
+constexpr int kChunkBlock = 1024;  // k_sweep_chunked: threads per block = movers per item
 constexpr int kSweepBlock = GW_SWEEP_BLOCK;  // 8 waves: a config-2 tile holds ~520 movers (one round, a few twice)
 #ifndef GW_EV_LDS
 #define GW_EV_LDS 256
@@ -907,8 +951,9 @@ constexpr int kMaxRows = 48;
 constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
 struct SweepSmem {  // dynamic LDS (16-B aligned carve)
+  static constexpr uint32_t kEv = kEvLds;  // event queue entries
   uint32_t n, enter, base, item;
-  uint32_t nmv, pad0, pad1, pad2;  // nmv: movers in mv
+  uint32_t nmv, unsorted, pad1, pad2;  // nmv: movers in mv; unsorted: a mover's events left unsorted
   uint32_t ws[16];                 // block-scan scratch
   uint4 ev[kEvLds];             // event queue
   uint16_t lcs[kRegCells + 8];  // row-major: LDS start of each region cell (+ total)
@@ -1255,9 +1300,9 @@ __device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const 
 // atomic or LDS write sits in the candidate loop itself. (32-candidate chunks with 32-bit masks: the
 // register allocator spills 5x more in this kernel, measured slower; the next pair's LDS reads issued
 // before the current pair is judged: 94.9 -> 96.3 us at config 2.)
-template <class IdxF>
-__device__ __forceinline__ unsigned long long judge_chunk(const SweepSmem& sm, const Judge& J, uint32_t b,
-                                                          uint32_t total, IdxF&& idx) {
+template <class S, class IdxF>
+__device__ __forceinline__ unsigned long long judge_chunk(const S& sm, const Judge& J, uint32_t b, uint32_t total,
+                                                          IdxF&& idx) {
   const uint32_t n = b < total ? min(total - b, 64u) : 0u;
   unsigned long long hit = 0;
   uint32_t k = 0;
@@ -1287,8 +1332,15 @@ __device__ __forceinline__ unsigned long long judge_chunk(const SweepSmem& sm, c
 // atomic per wave when the range runs past the queue; then each lane writes its own events in mask
 // order (its `local` numbering). Every lane that reached the call takes part (the masks of a lane
 // without events are zero).
-template <class IdxA, class IdxB>
-__device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Judge& J,
+// kSortLocal (a mover's whole walk in this one call): each event's `local` index is its rank in the
+// canonical order of the mover's events (LEAVE first, then other slot ascending: the key other | ENTER),
+// so k_place writes the op's slice already sorted and k_slice_sort has nothing to do: the lane renumbers
+// its own queue entries after writing them (no keys held in registers: the walk sits at the kernel's
+// VGPR limit). A lane with more than kSortMax events, or with events past the queue, flags the block
+// (sm.unsorted) instead.
+constexpr uint32_t kSortMax = 8;
+template <bool kSortLocal, class S, class IdxA, class IdxB>
+__device__ __forceinline__ void emit_masks(const SweepArgs& a, S& sm, const Mover& m, const Judge& J,
                                            unsigned long long hA, IdxA&& ia, unsigned long long hB, IdxB&& ib,
                                            uint32_t& local, uint32_t& nent) {
   const uint32_t c = (uint32_t)(__popcll(hA) + __popcll(hB));
@@ -1309,13 +1361,14 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, co
   uint32_t q0 = 0;
   if (lane == leader) q0 = atomicAdd(&sm.n, tot);
   q0 = __builtin_amdgcn_readfirstlane(q0);  // the first active lane is the leader
-  const uint32_t qs = max(q0, (uint32_t)kEvLds);  // first queue position that spills
+  const uint32_t qs = max(q0, S::kEv);  // first queue position that spills
   uint32_t g0 = 0;
   if (q0 + tot > qs) {  // wave-uniform
     if (lane == leader) g0 = atomicAdd(&a.ctr[CTR_EVENTS], q0 + tot - qs);
     g0 = __builtin_amdgcn_readfirstlane(g0);
   }
   uint32_t p = q0 + pre;
+  const uint32_t l0 = local;
   auto put = [&](unsigned long long& h, auto&& idx) {
     while (h) {
       const int bit = __ffsll((long long)h) - 1;
@@ -1323,7 +1376,7 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, co
       const bool enter = judge_lds(J, sm.rp[j], sm.rm[j]) == 2;
       const uint32_t eb = enter ? 0x80000000u : 0u;
       nent += enter ? 1u : 0u;
-      if (p < (uint32_t)kEvLds) {
+      if (p < S::kEv) {
         sm.ev[p] = make_uint4(m.rank, local, m.slot, sm.rslot[j] | eb);
       } else {
         const uint32_t gi = g0 + (p - qs);
@@ -1340,16 +1393,31 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, SweepSmem& sm, co
   };
   put(hA, ia);
   put(hB, ib);
+  if (kSortLocal && c >= 2u) {
+    // renumber the lane's own queue entries by canonical rank (keys other | ENTER are distinct: one
+    // event per other entity); entries that spilled past the queue, or too many, are left to k_slice_sort
+    const uint32_t p0 = q0 + pre;
+    if (c <= kSortMax && p0 + c <= S::kEv) {
+      for (uint32_t i = 0; i < c; ++i) {
+        const uint32_t ki = sm.ev[p0 + i].w;
+        uint32_t rk = 0;
+        for (uint32_t j = 0; j < c; ++j) rk += sm.ev[p0 + j].w < ki ? 1u : 0u;
+        sm.ev[p0 + i].y = l0 + rk;
+      }
+    } else {
+      sm.unsorted = 1u;
+    }
+  }
 }
 
 // Judge candidates 0..total-1 of one stream, 64 at a time, queueing each chunk's events.
-template <class IdxF>
-__device__ __forceinline__ void judge_stream(const SweepArgs& a, SweepSmem& sm, const Judge& J, const Mover& m,
+template <class S, class IdxF>
+__device__ __forceinline__ void judge_stream(const SweepArgs& a, S& sm, const Judge& J, const Mover& m,
                                              uint32_t total, IdxF&& idx, uint32_t& local, uint32_t& nent) {
   for (uint32_t b = 0; __any(b < total); b += 64) {
     const unsigned long long hit = judge_chunk(sm, J, b, total, idx);
-    emit_masks(a, sm, m, J, hit, [&](uint32_t k) { return idx(b + k); }, 0ull, [&](uint32_t k) { return k; }, local,
-               nent);
+    emit_masks<false>(a, sm, m, J, hit, [&](uint32_t k) { return idx(b + k); }, 0ull, [&](uint32_t k) { return k; },
+                      local, nent);
   }
 }
 
@@ -1404,7 +1472,7 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
       GW_SPH(1);
       const unsigned long long hC = judge_chunk(sm, J, 0, Cs.total, ci);
       GW_SPH(2);
-      emit_masks(a, sm, m, J, hR, ri, hC, ci, local, nent);
+      emit_masks<true>(a, sm, m, J, hR, ri, hC, ci, local, nent);
       GW_SPH(3);
 #if GW_STAMPS
       if ((threadIdx.x & 63) == __builtin_amdgcn_readfirstlane((int)(threadIdx.x & 63)))
@@ -1414,6 +1482,7 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     }
     judge_stream(a, sm, J, m, Rs.total, ri, local, nent);
     judge_stream(a, sm, J, m, Cs.total, ci, local, nent);
+    if (local > 1u) sm.unsorted = 1u;  // numbered in walk order
     return local;
   }
   walk_cells(w, [&](int r, int c0, int c1) {
@@ -1422,6 +1491,7 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
     const uint32_t e = (c0 <= c1) ? (uint32_t)sm.lcs[b + c1 + 1] : j;
     judge_stream(a, sm, J, m, e - j, [&](uint32_t k) { return j + k; }, local, nent);
   });
+  if (local > 1u) sm.unsorted = 1u;
   return local;
 }
 
@@ -1709,10 +1779,36 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     GW_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
                     ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32));
   }
-  if (!lds) {
-    // region over the LDS budget (crowds, large D): every mover of the tile to k_sweep_dense
-    // (the tile's entries reserved by ONE atomic per block: an append per wave on the one counter
-    // serialised at the memory side, ~48k of them per skew50 launch)
+  if (!lds && a.band_mv && g.pad > 0 &&
+      a.g.cs[(t + 1) << kTileCellShift] - a.g.cs[t << kTileCellShift] <= a.chunk_max_recs) {
+    // region over the LDS budget (crowds, large D): the tile's movers (grid indices, in grid order) to
+    // k_sweep_chunked, in items of up to kChunkBlock; one atomic per block on each list's counter (the
+    // lists are sized so that every pass's movers fit)
+    const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
+    uint32_t mine = 0;
+    for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) mine += is_walker(a, a.g.rec[j].a) ? 1u : 0u;
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan_big(mine, sm.ws, &tot);
+    const uint32_t nit = (tot + kChunkBlock - 1) / kChunkBlock;
+    if (threadIdx.x == 0) {
+      sm.base = tot ? atomicAdd(&a.ctr[CTR_BAND_MV], tot) : 0u;
+      sm.item = nit ? atomicAdd(&a.ctr[CTR_BAND_ITEMS], nit) : 0u;
+    }
+    __syncthreads();
+    const uint32_t mb = sm.base, ib = sm.item;
+    uint32_t di = mb + pre;
+    for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock)
+      if (is_walker(a, a.g.rec[j].a)) {
+        if (di < a.band_mv_cap) a.band_mv[di] = j;
+        ++di;
+      }
+    for (uint32_t i = threadIdx.x; i < nit; i += kSweepBlock)
+      if (ib + i < a.band_items_cap)
+        a.band_items[ib + i] = make_uint4(t, mb + i * kChunkBlock, min((uint32_t)kChunkBlock, tot - i * kChunkBlock), 0u);
+  } else if (!lds) {
+    // region over the LDS budget, no chunked sweep (its halo is wider than a tile): every mover of the
+    // tile to k_sweep_dense (the tile's entries reserved by ONE atomic per block: an append per wave on
+    // the one counter serialised at the memory side, ~48k of them per skew50 launch)
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
     uint32_t mine = 0;
     for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) mine += is_walker(a, a.g.rec[j].a) ? 1u : 0u;
@@ -1731,6 +1827,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
       ++di;
       const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
       const uint32_t cnt = sweep_global(a, sm, m, g, nent);
+      if (cnt > 1u) sm.unsorted = 1u;  // numbered in walk order
       put_count(a.rank_cnt, m.rank, cnt);
     }
   } else {
@@ -1761,6 +1858,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
   GW_STAMP(7, __builtin_amdgcn_s_memrealtime());  // thread 0's walk done
   __syncthreads();
   GW_STAMP(3, __builtin_amdgcn_s_memrealtime());
+  if (threadIdx.x == 0 && sm.unsorted) a.ctr[CTR_UNSORTED] = 1u;
   const uint32_t nq = min(sm.n, (uint32_t)kEvLds);
   if (a.ev_fix) {  // the tile's own region: counts stored, no atomics (two per block cost 10 us at config 2)
     if (threadIdx.x == 0) a.tile_ev[t] = nq, a.tile_ent[t] = sm.enter;
@@ -1795,6 +1893,7 @@ k_sweep(SweepArgs a) {
     sm.item = xcd * per + min(xcd, rem) + b / kXcds;
     sm.n = 0;
     sm.enter = 0;
+    sm.unsorted = 0;
   }
   __syncthreads();
   GW_STAMP(0, __builtin_amdgcn_s_memrealtime());
@@ -1835,31 +1934,35 @@ __global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
   if (threadIdx.x == 0) {
     q.n = 0;
     q.enter = 0;
+    q.flags = 0;
   }
   __syncthreads();
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t n_rec = a.g.cs[a.ncells];
+  uint32_t cnt = 0;
   if (t < n_rec) {
     const uint4 ra = a.g.rec[t].a;
     if (is_walker(a, ra)) {
       const uint32_t slot = ra.z & REC_SLOT;
       const Geom g = a.g.geom[a.space_of[slot]];
       const Mover m = mover_of(ra, a.g.rec[t].b, a.base, g.D);
-      put_count(a.rank_cnt, m.rank, sweep_global(a, q, m, g, nent));
+      put_count(a.rank_cnt, m.rank, cnt = sweep_global(a, q, m, g, nent));
     }
   } else if (t >= a.n_rec && t < a.n_rec + (a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves) &&
              !(a.op_kind && (a.op_kind[a.leave_ops[t - a.n_rec]] & OP_SILENT))) {
     const uint32_t i = a.leave_ops[t - a.n_rec];
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
-    put_count(a.rank_cnt, i, sweep_global(a, q, m, g, nent));
+    put_count(a.rank_cnt, i, cnt = sweep_global(a, q, m, g, nent));
   }
+  if (cnt > 1u) q.flags = 1u;  // numbered in walk order: k_slice_sort sorts
   if (nent) atomicAdd(&q.enter, nent);
   __syncthreads();
   const uint32_t nq = min(q.n, (uint32_t)kEvLds);
   if (threadIdx.x == 0) {
     q.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
     if (q.enter) atomicAdd(&a.ctr[CTR_ENTER], q.enter);
+    if (q.flags) a.ctr[CTR_UNSORTED] = 1u;
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
@@ -1876,6 +1979,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
   if (threadIdx.x == 0) {
     q.n = 0;
     q.enter = 0;
+    q.flags = 0;
   }
   __syncthreads();
   const uint32_t nl = a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves;
@@ -1884,7 +1988,9 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
     if (a.op_kind && (a.op_kind[i] & OP_SILENT)) continue;
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
-    put_count(a.rank_cnt, i, sweep_global(a, q, m, g, nent));
+    const uint32_t cnt = sweep_global(a, q, m, g, nent);
+    if (cnt > 1u) q.flags = 1u;  // numbered in walk order: k_slice_sort sorts
+    put_count(a.rank_cnt, i, cnt);
   }
   if (nent) atomicAdd(&q.enter, nent);
   __syncthreads();
@@ -1892,6 +1998,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
   if (threadIdx.x == 0) {
     q.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
     if (q.enter) atomicAdd(&a.ctr[CTR_ENTER], q.enter);
+    if (q.flags) a.ctr[CTR_UNSORTED] = 1u;
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
@@ -1953,6 +2060,7 @@ k_sweep_dense(SweepArgs a) {
   const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
   const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t nent = 0;
+  bool uns = false;  // a mover of this wave has events numbered in walk order (wave-uniform)
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
   __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the wave's batch of movers: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
 #if GW_STAMPS
@@ -2095,6 +2203,7 @@ k_sweep_dense(SweepArgs a) {
         }
       }
       if (lane == 0) put_count(a.rank_cnt, m.rank, local);
+      uns |= local > 1u;
     }
     __builtin_amdgcn_wave_barrier();  // every read of the batch before the next batch is written
   }
@@ -2103,10 +2212,422 @@ k_sweep_dense(SweepArgs a) {
   if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
   const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);  // one add per wave, not per lane
   if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
+  if (lane == 0 && uns) a.ctr[CTR_UNSORTED] = 1u;
 #if GW_STAMPS
   if (lane == 0)
     for (int k = 0; k < 16; ++k) atomicAdd(&gw_stamps[kStampWords * 16383 + k], dph[k]);
 #endif
+}
+
+// ---- Chunked sweep: tiles whose LDS region does not fit k_sweep's budget ----------------------------
+// (crowds: a hotspot tile's region holds thousands of records; large D: a Space whose region is wider
+// than k_sweep's cell tables). k_sweep lists such a tile's movers (grid indices, in grid order, i.e. by
+// cell) and cuts them into items of up to kChunkBlock movers. One 1024-thread block per CU takes items
+// from a work counter; per item, one thread per mover (its state, walk and judge kept in registers):
+//   - the union of the item's walks (rows zu0..zu1, columns xu0..xu1 of the tile's region: movers that
+//     are neighbours in the grid walk neighbouring rings, so the union is small even in a crowd);
+//   - that window cut into chunks of whole rows, each at most kChunkCap records and kChunkCells cells;
+//   - per chunk: its records staged into LDS (row-major cell order: a box row's cells are one contiguous
+//     LDS range), then every mover walks the rows of its walk inside the chunk (judge_stream: the
+//     candidates 64 at a time, hit masks, events queued in LDS).
+// Each region record is read from L2 once per item and chunk, instead of once per candidate mover as
+// k_sweep_dense does (config 5: ~10^9 candidates per tick at 32 B each). Events go out per block through
+// ev_tmp slots reserved kChunkEvRes at a time (holes marked, skipped by k_place): no per-wave atomics on
+// the shared counter. A mover's events are numbered in walk order over several chunks (k_slice_sort
+// sorts). A mover whose boxes leave the region (teleports), and every mover of an item whose window has
+// a row over kChunkCap records, goes to the dense list (k_sweep_dense).
+constexpr int kChunkCap = 3584;
+constexpr int kChunkCells = 4096;
+constexpr int kChunkRows = 96;          // region rows at most (tile + 2 reach, reach <= 32)
+constexpr uint32_t kChunkEvRes = 2048;  // ev_tmp slots a block reserves at a time
+constexpr int kChunkCellsPT = kChunkCells / kChunkBlock;
+
+struct ChunkSmem {
+  static constexpr uint32_t kEv = 2048;  // event queue entries
+  uint32_t n, enter, unsorted, item;
+  uint32_t cur, left, fcur, hole_cur;
+  uint32_t hole_n, nchunk, crowded, pad;
+  int bx[4];                    // window: zu0, zu1, xu0, xu1 (block reduction)
+  uint32_t ws[16];
+  uint32_t rc[kChunkRows];      // records per window row
+  uint16_t cb[kChunkRows + 1];  // chunk k: window rows [cb[k], cb[k + 1])
+  uint4 ev[kEv];
+  uint16_t lcs[kChunkCells + 8];  // chunk cells, row-major: LDS start (+ total)
+  uint4 rp[kChunkCap];
+  uint2 rm[kChunkCap];
+  uint32_t rslot[kChunkCap];  // slot; while staging: global record index
+};
+static_assert(sizeof(ChunkSmem) <= 163840, "chunked sweep LDS");
+
+size_t chunk_lds_bytes() { return sizeof(ChunkSmem); }
+
+// exclusive scan of v over a kChunkBlock-thread block; *total = block sum (LDS scratch ws[16])
+__device__ __forceinline__ uint32_t chunk_block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
+  constexpr int NW = kChunkBlock / 64;
+  const uint32_t inc = wave_incl_scan(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const uint32_t x = ws[k];
+    pre += k < w ? x : 0u;
+    tot += x;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc - v;
+}
+
+// flush the block's LDS event queue into ev_tmp through the block's reserved slots (every thread)
+__device__ __forceinline__ void chunk_flush(const SweepArgs& a, ChunkSmem& sm) {
+  __syncthreads();
+  const uint32_t n = min(sm.n, ChunkSmem::kEv);
+  if (n == 0u) return;  // block-uniform
+  if (threadIdx.x == 0) {
+    sm.hole_n = 0;
+    if (sm.left < n) {  // the rest of the current reservation becomes holes; a fresh one
+      sm.hole_cur = sm.cur;
+      sm.hole_n = sm.left;
+      const uint32_t need = max(kChunkEvRes, n);
+      sm.cur = atomicAdd(&a.ctr[CTR_EVENTS], need);
+      sm.left = need;
+      if (sm.hole_n) atomicAdd(&a.ctr[CTR_HOLES], sm.hole_n);
+    }
+    sm.fcur = sm.cur;
+    sm.cur += n;
+    sm.left -= n;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < sm.hole_n; i += kChunkBlock)
+    if (sm.hole_cur + i < a.ev_cap) a.ev_tmp[sm.hole_cur + i] = make_uint4(kEvHole, 0u, 0u, 0u);
+  for (uint32_t i = threadIdx.x; i < n; i += kChunkBlock)
+    if (sm.fcur + i < a.ev_cap) a.ev_tmp[sm.fcur + i] = sm.ev[i];
+  __syncthreads();
+  if (threadIdx.x == 0) sm.n = 0;
+  __syncthreads();
+}
+
+// block min (k = 0, 2) / max (k = 1, 3) of four ints into sm.bx (every thread)
+__device__ __forceinline__ void chunk_window(ChunkSmem& sm, int z0, int z1, int x0, int x1) {
+  if (threadIdx.x < 4) sm.bx[threadIdx.x] = (threadIdx.x & 1) ? INT_MIN : INT_MAX;
+  __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    z0 = min(z0, __shfl_xor(z0, o, 64));
+    z1 = max(z1, __shfl_xor(z1, o, 64));
+    x0 = min(x0, __shfl_xor(x0, o, 64));
+    x1 = max(x1, __shfl_xor(x1, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&sm.bx[0], z0);
+    atomicMax(&sm.bx[1], z1);
+    atomicMin(&sm.bx[2], x0);
+    atomicMax(&sm.bx[3], x1);
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kChunkBlock) k_sweep_chunked(SweepArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  ChunkSmem& sm = *reinterpret_cast<ChunkSmem*>(smem_raw);
+  const uint32_t nitems = min(a.ctr[CTR_BAND_ITEMS], a.band_items_cap);
+  if (threadIdx.x == 0) {
+    sm.n = 0;
+    sm.enter = 0;
+    sm.unsorted = 0;
+    sm.cur = 0;
+    sm.left = 0;
+  }
+  uint32_t nent = 0;
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) sm.item = atomicAdd(&a.ctr[CTR_BAND_NEXT], 1u);
+    __syncthreads();
+    const uint32_t item = sm.item;
+    if (item >= nitems) break;  // block-uniform
+    const uint4 it = a.band_items[item];
+    const uint32_t t = __builtin_amdgcn_readfirstlane(it.x), first = it.y, count = it.z;
+    const uint32_t sp = __builtin_amdgcn_readfirstlane(a.g.tile_space[t]);
+    const Geom g = uniform_geom(&a.g.geom[sp]);
+    const int reach = (int)g.pad;
+    const uint32_t tl = t - g.tile_base;
+    const int tz = __builtin_amdgcn_readfirstlane((int)(tl / (uint32_t)g.ntx));
+    const int tx = __builtin_amdgcn_readfirstlane((int)(tl - (uint32_t)tz * (uint32_t)g.ntx));
+    Region R;
+    R.zr0 = max(0, tz * kTile - reach);
+    R.zr1 = min(g.ncz - 1, tz * kTile + kTile - 1 + reach);
+    R.xr0 = max(0, tx * kTile - reach);
+    R.xr1 = min(g.ncx - 1, tx * kTile + kTile - 1 + reach);
+    // this thread's mover: state, walk and judge in registers for the whole item
+    bool act = false;
+    Mover m;
+    Walk w;
+    int wx0 = INT_MAX, wx1 = INT_MIN, wz0 = INT_MAX, wz1 = INT_MIN;
+    if (threadIdx.x < count) {
+      const uint32_t j = a.band_mv[first + threadIdx.x];
+      m = mover_of(a.g.rec[j].a, a.g.rec[j].b, a.base, g.D);
+      const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
+      act = R.holds(A1) && (!m.valid0 || R.holds(A0));
+      if (act) {
+        w = make_walk(m, g, A0, A1);
+        wz0 = w.z0, wz1 = w.z1;
+        wx0 = w.ring ? w.ax0 : min(w.ax0, w.bx0);  // (ring: a = the union's columns, b = the inner ones)
+        wx1 = w.ring ? w.ax1 : max(w.ax1, w.bx1);
+      }
+    }
+    // (a mover outside the region: the dense list, as k_sweep does)
+    {
+      const bool out = threadIdx.x < count && !act;
+      const uint32_t di = wave_append(&a.ctr[CTR_DENSE], out);
+      if (out && di < a.dense_cap) a.dense[di] = m.slot;  // (sized to the capacity: every mover fits)
+    }
+    chunk_window(sm, wz0, wz1, wx0, wx1);
+    const int zu0 = sm.bx[0], zu1 = sm.bx[1], xu0 = sm.bx[2], xu1 = sm.bx[3];
+    if (zu0 > zu1) continue;  // no mover to walk (block-uniform)
+    const int W = xu1 - xu0 + 1, nrows = zu1 - zu0 + 1;
+    // records per window row: the row's cells [xu0, xu1] are one contiguous range per tile crossed
+    for (int r = threadIdx.x; r < nrows; r += kChunkBlock) {
+      uint32_t c = 0;
+      row_entries_ranges(g, a.g.cs, zu0 + r, xu0, xu1, [&](uint32_t b, uint32_t e) { c += e - b; });
+      sm.rc[r] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // chunks of whole rows (sequential: at most kChunkRows rows)
+      uint32_t k = 0, sum = 0, rows = 0;
+      sm.crowded = 0;
+      sm.cb[0] = 0;
+      for (int r = 0; r < nrows; ++r) {
+        const uint32_t c = sm.rc[r];
+        if (c > (uint32_t)kChunkCap) sm.crowded = 1;
+        if (rows && (sum + c > (uint32_t)kChunkCap || (int)(rows + 1) * W > kChunkCells)) {
+          sm.cb[++k] = (uint16_t)r;
+          sum = 0, rows = 0;
+        }
+        sum += c, ++rows;
+      }
+      sm.cb[++k] = (uint16_t)nrows;
+      sm.nchunk = k;
+    }
+    __syncthreads();
+    if (sm.crowded) {  // a row of the window holds more than a chunk: every mover to the dense list
+      const uint32_t di = wave_append(&a.ctr[CTR_DENSE], act);
+      if (act && di < a.dense_cap) a.dense[di] = m.slot;
+      continue;
+    }
+    uint32_t local = 0;
+    const uint32_t nchunk = sm.nchunk;
+    for (uint32_t ck = 0; ck < nchunk; ++ck) {
+      const int c0 = zu0 + sm.cb[ck], c1 = zu0 + sm.cb[ck + 1] - 1;
+      const int ncell = (c1 - c0 + 1) * W;
+      // ---- stage: cell starts (kChunkCellsPT consecutive cells per thread), block scan, source map,
+      // then one 32-B gather per record into the LDS form ----
+      {
+        uint32_t n[kChunkCellsPT], s0[kChunkCellsPT], sum = 0;
+        const int cc0 = threadIdx.x * kChunkCellsPT;
+        const int rr0 = small_div(cc0, W);
+        int rr = rr0, col = cc0 - rr0 * W;
+#pragma unroll
+        for (int k = 0; k < kChunkCellsPT; ++k) {
+          n[k] = 0, s0[k] = 0;
+          if (cc0 + k < ncell) {
+            const uint32_t key = cell_key(g, xu0 + col, c0 + rr);
+            s0[k] = a.g.cs[key];
+            n[k] = a.g.cs[key + 1] - s0[k];
+          }
+          sum += n[k];
+          if (++col == W) col = 0, ++rr;
+        }
+        uint32_t total;
+        uint32_t pre = chunk_block_scan(sum, sm.ws, &total);
+#pragma unroll
+        for (int k = 0; k < kChunkCellsPT; ++k) {
+          if (cc0 + k < ncell) {
+            sm.lcs[cc0 + k] = (uint16_t)pre;
+            for (uint32_t q = 0; q < n[k]; ++q) sm.rslot[pre + q] = s0[k] + q;
+          }
+          pre += n[k];
+        }
+        if (threadIdx.x == 0) sm.lcs[ncell] = (uint16_t)total;
+        __syncthreads();
+        // entry i of the source map is read and then overwritten by the same thread only: no barrier in
+        // between; two gathers in flight per thread (the mover state held across the item leaves room
+        // for no more)
+        for (uint32_t i = threadIdx.x; i < total; i += 2 * kChunkBlock) {
+          const uint32_t i2 = i + kChunkBlock;
+          const uint32_t s1 = sm.rslot[i], s2 = i2 < total ? sm.rslot[i2] : s1;
+          const Rec r1 = a.g.rec[s1], r2 = a.g.rec[s2];
+          lds_record(r1.a, r1.b, a.base, a.n_ops, sm.rp[i], sm.rm[i], sm.rslot[i]);
+          if (i2 < total) lds_record(r2.a, r2.b, a.base, a.n_ops, sm.rp[i2], sm.rm[i2], sm.rslot[i2]);
+        }
+        __syncthreads();
+      }
+      // ---- walk: this mover's rows inside the chunk ----
+      const Judge J = make_judge(m, a.base);  // (recomputed per chunk: not held across the staging)
+      const int r0 = act ? max(w.z0, c0) : 1, r1 = act ? min(w.z1, c1) : 0;
+      const int h = r1 - r0;
+      for (int rel = 0; __any(rel <= h); ++rel) {  // wave-uniform trip count
+        const int r = r0 + rel;
+        int a0 = 1, a1 = 0, b0 = 1, b1 = 0;
+        if (rel <= h) walk_row(w, r, a0, a1, b0, b1);
+        const int rb = (r - c0) * W - xu0;
+        auto seg = [&](int x0, int x1) {
+          const uint32_t jb = x0 <= x1 ? (uint32_t)sm.lcs[rb + x0] : 0u;
+          const uint32_t je = x0 <= x1 ? (uint32_t)sm.lcs[rb + x1 + 1] : 0u;
+          judge_stream(a, sm, J, m, je - jb, [&](uint32_t k) { return jb + k; }, local, nent);
+        };
+        seg(a0, a1);
+        seg(b0, b1);
+      }
+      __syncthreads();  // the chunk's LDS records are read by every walk before the next staging
+      if (sm.n >= ChunkSmem::kEv / 2) chunk_flush(a, sm);  // block-uniform
+    }
+    if (act) {
+      put_count(a.rank_cnt, m.rank, local);
+      if (local > 1u) sm.unsorted = 1u;  // numbered in walk order over the chunks
+    }
+  }
+  chunk_flush(a, sm);
+  if (threadIdx.x == 0 && sm.left) {  // the unused rest of the last reservation: holes
+    sm.hole_cur = sm.cur;
+    sm.hole_n = sm.left;
+    atomicAdd(&a.ctr[CTR_HOLES], sm.left);
+  } else if (threadIdx.x == 0) {
+    sm.hole_n = 0;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < sm.hole_n; i += kChunkBlock)
+    if (sm.hole_cur + i < a.ev_cap) a.ev_tmp[sm.hole_cur + i] = make_uint4(kEvHole, 0u, 0u, 0u);
+  if (nent) atomicAdd(&sm.enter, nent);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (sm.enter) atomicAdd(&a.ctr[CTR_ENTER], sm.enter);
+    if (sm.unsorted) a.ctr[CTR_UNSORTED] = 1u;
+  }
+}
+
+void chunk_init() {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep_chunked),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ChunkSmem));
+}
+
+// ---- Small pass (k_sweep_small) ---------------------------------------------------------------------
+// A pass with few ops does not rebuild the grid: each op's mover (one wave) walks its boxes' cells in the
+// grid of the last full build, then scans the overlay, and judges as the full sweep does:
+//   - a grid record stands for its slot's CURRENT state when the slot has had no op since that build
+//     (ov_tag != gen): its end position and seq (a slot without an op in a pass has start = end); ghosts
+//     of that build are stale and skipped, as is every record of a slot in the overlay;
+//   - an overlay record (one per slot with an op since the build, written by k_apply) is the record the
+//     grid build would have written for the slot's last op; if that op was not in this pass, it is
+//     likewise read as the slot's current state (a ghost: the slot is absent).
+// Events are numbered in walk order (k_slice_sort sorts) and written into event slots the wave reserves
+// kEvChunk at a time.
+__device__ __forceinline__ int judge_small(const Judge& J, uint32_t base, uint32_t n_ops, uint4 ra, uint4 rb) {
+  if (ra.w - base >= n_ops) {  // no op in this pass: the record's end state is the slot's state now
+    if (ra.z & REC_GHOST) return 0;
+    ra.z &= REC_SLOT;
+    rb = make_uint4(ra.x, ra.y, rb.w, rb.w);
+  }
+  return judge(J, ra, rb);
+}
+
+__global__ void __launch_bounds__(kBlock) k_sweep_small(SmallArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // the wave's op
+  const uint32_t n = a.n_dev ? min(*a.n_dev, a.n_ops) : a.n_ops;
+  if (i >= n) return;  // wave-uniform
+  const uint8_t kind = a.op_kind ? a.op_kind[i] : (uint8_t)OP_MOVE;
+  if (kind & OP_SILENT) return;
+  const uint32_t s = a.op_slot[i];
+  if (a.opq[s] != a.base + i) return;  // (a failed op: the batch is refused anyway)
+  const uint32_t sp = __builtin_amdgcn_readfirstlane(a.space_of[s]);
+  const Geom g = uniform_geom(&a.g.geom[sp]);
+  Mover m;
+  m.slot = s;
+  m.q = a.base + i;
+  m.q0 = a.old_seq[s];
+  m.rank = i;
+  m.valid0 = m.q0 != 0;
+  m.valid1 = (kind & OP_KIND) != OP_LEAVE;
+  m.mx0 = a.old_x[s];
+  m.mz0 = a.old_z[s];
+  m.mx1 = m.valid1 ? a.pos_x[s] : m.mx0;
+  m.mz1 = m.valid1 ? a.pos_z[s] : m.mz0;
+  m.D = g.D;
+  const Judge J = make_judge(m, a.base);
+  const Walk w = make_walk(m, g);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t local = 0, nent = 0, cur = 0, left = 0;  // (wave-uniform but local/cur/left)
+  auto emit_round = [&](int ev, uint32_t other) {
+    const unsigned long long em = __ballot(ev != 0);
+    if (!em) return;
+    const uint32_t cnt = (uint32_t)__popcll(em), pre = (uint32_t)__popcll(em & below);
+    uint32_t gi = cur + pre;
+    if (cnt > left) {  // this reservation fills up: the rest goes to a fresh one
+      uint32_t nb = 0;
+      if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
+      nb = __shfl(nb, 0, 64);
+      if (pre >= left) gi = nb + (pre - left);
+      cur = nb + (cnt - left);
+      left = kEvChunk - (cnt - left);
+    } else {
+      cur += cnt;
+      left -= cnt;
+    }
+    if (ev) {
+      if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
+      nent += ev == 2 ? 1u : 0u;
+    }
+    local += cnt;
+  };
+  auto cand = [&](uint32_t j, bool on) {  // grid record j (on: a candidate of this lane)
+    int ev = 0;
+    uint32_t o = 0;
+    if (on) {
+      const uint4 ra = a.g.rec[j].a;
+      o = ra.z & REC_SLOT;
+      if (a.ov_tag[o] != a.gen) ev = judge_small(J, a.base, a.n_ops, ra, a.g.rec[j].b);
+    }
+    emit_round(ev, o);
+  };
+  // the grid: the walk's rows, each row segment's records 64 at a time across the lanes
+  for (int r = w.z0; r <= w.z1; ++r) {
+    int a0, a1, b0, b1;
+    walk_row(w, r, a0, a1, b0, b1);
+    auto seg = [&](int c0, int c1) {
+      row_entries_ranges(g, a.g.cs, r, c0, c1, [&](uint32_t jb, uint32_t je) {
+        for (uint32_t j = jb; j < je; j += 64) cand(j + lane, j + lane < je);
+      });
+    };
+    seg(a0, a1);
+    seg(b0, b1);
+  }
+  // the overlay
+  const uint32_t nov = *a.ov_count;
+  for (uint32_t e = 0; e < nov; e += 64) {
+    int ev = 0;
+    uint32_t o = 0;
+    if (e + lane < nov) {
+      const Rec r = a.ov_rec[e + lane];
+      o = r.a.z & REC_SLOT;
+      ev = judge_small(J, a.base, a.n_ops, r.a, r.b);
+    }
+    emit_round(ev, o);
+  }
+  if (lane == 0) {
+    put_count(a.rank_cnt, m.rank, local);
+    if (local > 1u) a.ctr[CTR_UNSORTED] = 1u;
+  }
+  for (uint32_t k = lane; k < left; k += 64)
+    if (cur + k < a.ev_cap) a.ev_tmp[cur + k] = make_uint4(kEvHole, 0u, 0u, 0u);
+  if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
+  const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);
+  if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
+}
+
+void launch_sweep_small(const SmallArgs& a, hipStream_t st) {
+  if (a.n_ops)
+    hipLaunchKernelGGL(k_sweep_small, dim3((a.n_ops + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, a);
 }
 
 uint32_t sweep_ev_lds() { return kEvLds; }
@@ -2121,9 +2642,14 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
   if (a.leave_blocks)
     hipLaunchKernelGGL(k_sweep_leaves, dim3(a.leave_blocks * ((kSweepBlock + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        st, a);
-  // the dense list's length is on the device: a fixed grid that exits at once when it is empty (a
-  // small one when the previous pass had none; the kernel is grid-stride, any grid is correct)
-  if (a.dense) hipLaunchKernelGGL(k_sweep_dense, dim3(a.dense_hint ? kDenseGrid : 8), dim3(kDenseBlock), 0, st, a);
+  // crowded tiles' items: one block per CU pulling items; launched when the previous pass had some (the
+  // host re-runs the sweep when this one lists items after all, as for the dense list)
+  if (a.band_items && a.band_hint)
+    hipLaunchKernelGGL(k_sweep_chunked, dim3(a.chunk_grid), dim3(kChunkBlock), sizeof(ChunkSmem), st, a);
+  // the dense list's length is on the device: a fixed grid that exits at once when it is empty. Not
+  // launched at all when the previous pass had no dense mover (an empty launch cost 4.8 us per config-2
+  // tick): if this pass lists some after all, the host re-runs the sweep with it (run_pass)
+  if (a.dense && a.dense_hint) hipLaunchKernelGGL(k_sweep_dense, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
 }
 
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each
@@ -2183,6 +2709,15 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
       block_excl_scan(ne, &tot);
       if (threadIdx.x == 0 && tot) atomicAdd(const_cast<uint32_t*>(&o.g.ctr[CTR_ENTER]), tot);
     }
+  }
+  if (o.ntiles_acted && blockIdx.x == 1 % gridDim.x) {  // device batch: every op on a slot of its own
+    uint32_t na = 0;
+    for (uint32_t t = threadIdx.x; t < o.ntiles_acted; t += kBlock) na += o.tile_acted[t];
+    uint32_t tot;
+    block_excl_scan(na, &tot);
+    // (an overflowed one-pass build published an empty grid: the pass re-runs, nothing to check)
+    if (threadIdx.x == 0 && tot != o.g.ctr[CTR_NOPS] && !o.g.ctr[CTR_BOVF])
+      atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
   }
   for (uint32_t i = tid; i < slots; i += nth) {
     const uint4 e = o.ev_tmp[i];
@@ -2325,20 +2860,51 @@ struct SegSmem {
   uint32_t nbig;
 };
 
+// Grid-stride over the ops (kBlock per block and round). Nothing to sort when every op's events were
+// numbered in canonical order by the sweep (CTR_UNSORTED clear) and no batch check is asked. When the
+// previous pass needed no sort either (o.sorted_hint), the kernel runs as kSortFewBlocks blocks and the
+// last one to finish (a ticket) publishes the pass's counters to mapped host memory (o.pub): no separate
+// one-thread kernel (3.8 us per pass at config 2). (A ticket per block of the one-thread-per-op grid,
+// 3,907 blocks at config 2, serialises on the one counter: 9 -> 15 us measured with 1,024 blocks.)
+// Otherwise one thread per op, and k_publish after it.
+constexpr uint32_t kSortFewBlocks = 32;
 __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
   __shared__ uint2 sk[kBigChunk];
   __shared__ SegSmem ss;
-  const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-  const bool op = r < o.n_ops && !(o.n_dev && r >= *o.n_dev);
-  if (op && o.check_ops) {
-    const uint32_t s = o.op_slot[r];
-    if (s < o.cap && o.opq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
-  }
+  __shared__ uint32_t last;
   uint32_t slots, n;
-  if (!ev_fits(o, &slots, &n)) return;  // grid-uniform
-  const uint32_t b = op ? o.rank_off[r] : 0u, len = op ? o.rank_off[r + 1] - b : 0u;
-  // ev_tmp is free once k_place has run; its uint2 view has 2 x (tile regions + slots) >= n entries
-  seg_sort(o.ev_out, o.scratch, b, len, sk, ss.bigq, &ss.nbig);
+  const bool fits = ev_fits(o, &slots, &n);
+  const bool sort = fits && o.g.ctr[CTR_UNSORTED] != 0u;  // grid-uniform
+  if (sort || o.check_ops) {
+    const uint32_t nr = o.n_dev ? min(*o.n_dev, o.n_ops) : o.n_ops;
+    for (uint32_t r0 = blockIdx.x * kBlock; r0 < o.n_ops; r0 += gridDim.x * kBlock) {  // block-uniform
+      const uint32_t r = r0 + threadIdx.x;
+      const bool op = r < nr;
+      if (op && o.check_ops) {
+        const uint32_t s = o.op_slot[r];
+        if (s < o.cap && o.opq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
+      }
+      if (!sort) continue;
+      const uint32_t b = op ? o.rank_off[r] : 0u, len = op ? o.rank_off[r + 1] - b : 0u;
+      // ev_tmp is free once k_place has run; its uint2 view has 2 x (tile regions + slots) >= n entries
+      seg_sort(o.ev_out, o.scratch, b, len, sk, ss.bigq, &ss.nbig);
+    }
+  }
+  if (!o.pub || !o.sorted_hint) return;
+  // publication: the last block's ticket. Every earlier block's device-scope atomics (CTR_ERR) were
+  // performed before its ticket; the counters are read with atomics too, where those meet.
+  __syncthreads();
+  if (threadIdx.x == 0) last = (atomicAdd(const_cast<uint32_t*>(&o.g.ctr[CTR_SDONE]), 1u) + 1u) % gridDim.x == 0u;
+  __syncthreads();
+  if (!last) return;
+  uint32_t* ctr = const_cast<uint32_t*>(o.g.ctr);
+  if (threadIdx.x < (uint32_t)kPubWords) {  // one counter per lane
+    __hip_atomic_store(&o.pub[threadIdx.x], atomicAdd(&ctr[threadIdx.x], 0u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();  // complete before the flag below
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&o.pub[kPubWords], o.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Deliver the ordered events to mapped pinned host memory (GPU-initiated PCIe writes), so the host
@@ -2350,16 +2916,17 @@ __global__ void __launch_bounds__(kBlock) k_copy_out(OrderArgs o) {
 }
 
 void launch_order(const OrderArgs& o, hipStream_t st) {
-  hipLaunchKernelGGL(k_place, dim3(1024), dim3(kBlock), 0, st, o);
-  if (o.n_ops) {
-    hipLaunchKernelGGL(k_slice_sort, dim3((o.n_ops + kBlock - 1) / kBlock), dim3(kBlock), 0, st, o);
-  }
+  hipLaunchKernelGGL(k_place, dim3(o.place_blocks ? o.place_blocks : 1024u), dim3(kBlock), 0, st, o);
+  const uint32_t per_op = std::max(1u, (o.n_ops + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_slice_sort, dim3(o.sorted_hint ? std::min(per_op, kSortFewBlocks) : per_op), dim3(kBlock), 0,
+                     st, o);
   if (o.host_out) hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, o);
+  if (o.pub && !o.sorted_hint) launch_publish(o.g.ctr, o.pub, o.pub_seq, st);
 }
 
-// End-of-pass publication: the counters the host reads, then a sequence word, written by one thread
-// into mapped (coherent) host memory with system-scope stores; the host spins on the sequence word
-// instead of a DMA copy plus a stream synchronisation.
+// End-of-pass publication (when k_slice_sort does not publish): the counters the host reads, then a
+// sequence word, written by one thread into mapped (coherent) host memory with system-scope stores;
+// the host spins on the sequence word instead of a DMA copy plus a stream synchronisation.
 __global__ void k_publish(const uint32_t* __restrict__ ctr, uint32_t* pub, uint32_t seq) {
   const int i = threadIdx.x;
   if (i < kPubWords) {  // one counter per lane
@@ -2423,7 +2990,7 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
     // slab output, interleaved by record: entry k of grid record j at
     // slab[(j / 64) * slab_s * 64 + k * 64 + j % 64], so the lanes of a wave (consecutive j) that find
     // their k-th neighbour together store into one 256-B run
-    uint32_t* const srow = a.slab ? a.slab + (size_t)(j >> 6) * a.slab_s * 64 + (j & 63u) : nullptr;
+    uint32_t* const srow = a.slab && j < a.slab_recs ? a.slab + (size_t)(j >> 6) * a.slab_s * 64 + (j & 63u) : nullptr;
     auto judge = [&](uint32_t rz, uint32_t qo, float ox, float oz) {
       const uint32_t o = rz & REC_SLOT;
       if ((rz & REC_GHOST) || o == s) return;
@@ -2453,7 +3020,7 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
         });
       }
     }
-    if (!a.row_ptr) a.row_cnt[s] = n, rsum += n, rmax = max(rmax, n);
+    if (!a.row_ptr) a.row_cnt[s] = n, rsum += n, rmax = max(rmax, (a.slab && !srow) ? a.slab_s + 1u : n);
   }
   if (!a.row_ptr) {  // the tile's totals, stored (k_rel_total sums them; the host checks the total
                      // before it sizes cols). One atomic per wave on one word instead: serialised.

@@ -184,8 +184,11 @@ struct gwaoi_mgr {
   int build_mode = 0;            // gwaoi_debug_set_build_mode: 1 = always the counting build
   bool plan_ok = false;          // the previous tile build's starts describe a grid of the geometry in plan_geom
   std::vector<gw::Geom> plan_geom;
-  uint64_t builds_fused = 0, builds_counting = 0, build_reruns = 0;
+  uint64_t builds_fused = 0, builds_counting = 0, build_reruns = 0, dense_reruns = 0;
   uint32_t* tile_walk = nullptr; // tile-bucketed build: per tile of the pass's grid, holds a reported mover
+  uint32_t* tile_acted = nullptr;  // per tile: slots of the pass's ops (k_bin_tsort; duplicate-slot check)
+  bool rerun_counting = false;   // the previous pass re-ran its build: this one uses the counting build
+  bool chunked = true;           // crowded tiles take k_sweep_chunked (gwaoi_debug_set_sweep_lds(3): off)
   uint32_t* tile_ev = nullptr;   // per tile: events k_sweep queued in the tile's region of ev_tmp
   uint32_t* tile_ent = nullptr;  // per tile: their enter events
   uint32_t nblk = 0;
@@ -196,10 +199,26 @@ struct gwaoi_mgr {
   uint32_t* h_pub = nullptr;     // mapped coherent host memory: [kPubWords] counters + sequence word
   uint32_t* d_pub = nullptr;     // its device address
   uint32_t pub_seq = 0;
-  uint32_t last_dense = ~0u;     // dense movers of the last pass (k_sweep_dense grid size hint)
+  uint32_t last_dense = ~0u;     // dense movers of the last pass (k_sweep_dense launched when non-zero)
+  uint32_t last_band = ~0u;      // chunked-sweep items of the last pass (k_sweep_chunked launched when non-zero)
+  uint32_t* band_mv = nullptr;   // k_sweep_chunked's movers (grid indices) and items
+  uint4* band_items = nullptr;
+  uint32_t band_mv_cap = 0, band_items_cap = 0, chunk_grid = 256;
+  uint64_t band_reruns = 0;
+  bool last_unsorted = true;     // the last pass needed k_slice_sort (its grid: one thread per op)
+  // small passes (run_small_pass): the overlay of slots with an op since the grid was last built
+  uint32_t* ov_tag = nullptr;    // [cap] grid generation in which the slot joined the overlay
+  uint32_t* ov_idx = nullptr;    // [cap] its overlay entry
+  gw::Rec* ov_rec = nullptr;     // [ov_cap] entries
+  uint32_t* ov_count = nullptr;  // device: entries
+  uint32_t ov_cap = 0;
+  uint32_t grid_gen = 1;         // generation of the current grid (ov_tag values of earlier ones are stale)
+  uint64_t ov_bound = 0;         // ops of the small passes since the grid was built (>= entries)
+  int small_mode = 1;            // 0: off, 1: auto, 2: whenever the overlay has room (tests)
+  uint64_t small_passes = 0;
   struct {                       // the last timed pass, collected once its events are complete
     bool pending = false;
-    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0;
+    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0, chunked = 0;
   } tpend;
   // events
   uint4* ev_tmp = nullptr;
@@ -364,9 +383,11 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
                                   std::fabs((double)z1)});
     const double span = ((double)sh.desc.dist * (1.0 + 1e-5) + (maxc + sh.desc.dist) * 1e-6) / c;
     int reach = (int)std::ceil(span) + 1;
+    // the chunked sweep (crowded tiles, and every tile of a Space whose region is over k_sweep's budget)
+    // takes halos up to one tile wide; wider ones walk from L2 (k_sweep_dense)
+    g.pad = reach <= gw::kTile ? (uint32_t)reach : 0u;
     if ((gw::kTile + 2 * reach) * (gw::kTile + 2 * reach) > gw::kSweepRegCells) reach = 0;  // LDS path off for this Space
     g.reach = reach;
-    g.pad = 0;
     base += (uint32_t)(tx * tz) * gw::kTileCells;
     sh.gx0 = x0;
     sh.gz0 = z0;
@@ -468,7 +489,7 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_
   if (!tiles && g.cs_zeroed < g.ncells + 1)
     HIPCHK(hipMemsetAsync(g.cs, 0, (size_t)(g.ncells + 1) * sizeof(uint32_t), m->stream));
   g.cs_zeroed = 0;
-  gw::BinArgs b;
+  gw::BinArgs b{};
   b.pos_x = m->pos_x;
   b.pos_z = m->pos_z;
   b.seq = m->seq;
@@ -500,10 +521,18 @@ int build_grid(gwaoi_mgr* m, int gi, uint32_t base, uint32_t n_ops, const uint8_
   b.trec_cap = 2 * m->cap;
   b.op_kind = op_kind;
   b.tile_walk = m->tile_walk;
+  b.tile_acted = m->tile_acted;
   b.ctr = m->ctr;
   b.fused = 0;
   if (tiles) {
-    b.fused = mode == kBuildAuto && m->build_mode == 0 && m->plan_ok && same_geom(m->plan_geom, g.h_geom);
+    // the one-pass build only when its plan fits the bucket buffer: the last tile's planned start is
+    // the previous build's records x 5/4 + 16 per tile (plan_start); a full world whose entities mostly
+    // change cell (2 records each) would otherwise overflow every pass. After a re-run (the plan did not
+    // hold), one counting build first.
+    const uint64_t plan_end = (uint64_t)m->h_ctr[gw::CTR_RECORDS] * 5u / 4u + 16ull * g.ntiles;
+    b.fused = mode == kBuildAuto && m->build_mode == 0 && m->plan_ok && same_geom(m->plan_geom, g.h_geom) &&
+              !m->rerun_counting && plan_end <= b.trec_cap;
+    m->rerun_counting = false;
     if (counting) HIPCHK(hipMemsetAsync(b.ttot, 0, (size_t)gw::kMaxLdsTiles * sizeof(uint32_t), m->stream));
     gw::launch_bin_tiles(b, m->stream);
     if (!counting) m->ttot_sel ^= 1;
@@ -568,6 +597,7 @@ int collect_timing(gwaoi_mgr* m) {
   m->stats.grid_records += m->tpend.records;
   m->stats.grid_cells += m->tpend.ncells;
   m->stats.dense_movers += m->tpend.dense;
+  m->stats.chunked_movers += m->tpend.chunked;
   return GWAOI_OK;
 }
 
@@ -575,16 +605,21 @@ int collect_timing(gwaoi_mgr* m) {
 // publication buffer, a one-thread kernel writes them there and the host spins on the sequence word
 // (polling the stream for errors now and then); host event delivery (GPU writes into mapped memory
 // by k_copy_out) keeps the stream synchronisation.
-int finish_pass(gwaoi_mgr* m, bool copy_events) {
+// The order stage's last kernel publishes (k_slice_sort's last block, OrderArgs.pub) when
+// publish_seq() gave it a sequence word; otherwise (host event delivery, no mapped buffer) the counters
+// are copied and the stream synchronised.
+uint32_t publish_seq(gwaoi_mgr* m, bool copy_events) {
+  if (!m->h_pub || copy_events) return 0u;
+  return ++m->pub_seq ? m->pub_seq : ++m->pub_seq;  // never 0 (the initial value)
+}
+
+int finish_pass(gwaoi_mgr* m, uint32_t seq) {
   hipStream_t st = m->stream;
-  if (!m->h_pub || copy_events) {
+  if (!seq) {
     HIPCHK(hipMemcpyAsync(m->h_ctr, m->ctr, gw::CTR_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return GWAOI_OK;
   }
-  const uint32_t seq = ++m->pub_seq ? m->pub_seq : ++m->pub_seq;  // never 0 (the initial value)
-  gw::launch_publish(m->ctr, m->d_pub, seq, st);
-  HIPCHK(hipGetLastError());
   volatile uint32_t* flag = m->h_pub + gw::kPubWords;
   for (uint64_t spin = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++spin) {
     if ((spin & 0xFFFF) == 0) {
@@ -601,6 +636,203 @@ int finish_pass(gwaoi_mgr* m, bool copy_events) {
     __builtin_ia32_pause();
   }
   std::memcpy(m->h_ctr, m->h_pub, gw::kPubWords * sizeof(uint32_t));
+  return GWAOI_OK;
+}
+
+// ---- small passes -------------------------------------------------------------------------------
+// A pass with few ops (an Enter or Leave flushed on its own, EntityManager.go:229-273 / Space.go:188-251,
+// a handful of Moved calls) does not rebuild the grid: k_apply adds its ops' slots to the overlay, and
+// each op's mover is judged against the current grid plus the overlay (k_sweep_small, one wave per op).
+// The overlay grows until a pass with many ops rebuilds the grid (or a consumer of the grid refreshes it,
+// ensure_grid_current). Cost: O(ops x (box + overlay)) instead of the full build and sweep over every slot.
+constexpr uint32_t kSmallMaxOps = 1024;                   // ops of a small pass at most
+constexpr uint64_t kSmallWork = 1ull << 22;               // ops x overlay entries at most (the overlay scan)
+constexpr size_t kOverlayCap = 16384;
+
+bool small_pass_ok(gwaoi_mgr* m, uint32_t n_ops) {
+  if (!m->small_mode || m->geom_dirty || m->sweep_lds != 1 || !m->passes_run || !m->grid[m->cur].ntiles) return false;
+  const uint64_t ov = m->ov_bound + n_ops;
+  if (ov > m->ov_cap) return false;
+  if (m->small_mode == 2) return true;
+  // a full pass over the present slots costs about as much as ~16k overlay-walk ops: stay below a small
+  // fraction of it
+  return n_ops <= kSmallMaxOps && (uint64_t)n_ops * ov <= kSmallWork && (uint64_t)n_ops * 64 <= m->n_present_dev;
+}
+
+int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops) {
+  const bool dev = m->dv_n != 0;
+  const bool dev_mixed = dev && m->dv_kind;
+  hipStream_t st = m->stream;
+  RCHK(collect_timing(m));
+  if (m->timing) HIPCHK(hipEventRecord(m->tev[0], st));
+  if (!dev) {
+    HIPCHK(hipMemcpyAsync(m->d_op_slot, m->h_op_slot, n_ops * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->d_op_x, m->h_op_x, n_ops * sizeof(float), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->d_op_z, m->h_op_z, n_ops * sizeof(float), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->d_op_kind, m->h_op_kind, n_ops, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->d_op_space, m->h_op_space, n_ops * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  }
+  gw::ApplyArgs a{};
+  a.n_dev = dev ? m->dv_count : nullptr;
+  a.op_slot = dev ? m->dv_slot : m->d_op_slot;
+  a.op_x = dev ? m->dv_x : m->d_op_x;
+  a.op_z = dev ? m->dv_z : m->d_op_z;
+  a.op_kind = dev ? m->dv_kind : m->d_op_kind;
+  a.op_space = dev ? m->dv_space : m->d_op_space;
+  a.nspaces = m->nspaces;
+  a.leaves = dev_mixed ? m->d_leaves : nullptr;  // (the presence delta of a mixed batch is counted with it)
+  a.n_ops = n_ops;
+  a.base = base;
+  a.cap = m->cap;
+  a.check = dev ? 1 : 0;
+  a.pos_x = m->pos_x;
+  a.pos_z = m->pos_z;
+  a.seq = m->seq;
+  a.space_of = m->space_of;
+  a.old_x = m->old_x;
+  a.old_z = m->old_z;
+  a.old_seq = m->old_seq;
+  a.opq = m->opq;
+  a.ctr = m->ctr;
+  a.rank_cnt = m->rank_cnt;
+  a.gen = m->grid_gen;
+  a.ov_tag = m->ov_tag;
+  a.ov_idx = m->ov_idx;
+  a.ov_rec = m->ov_rec;
+  a.ov_count = m->ov_count;
+  a.ov_cap = m->ov_cap;
+  gw::launch_apply(a, st);
+  HIPCHK(hipGetLastError());
+  if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
+  if (m->timing) HIPCHK(hipEventRecord(m->tev[2], st));
+  const uint64_t keep = m->tick_events;
+  const Grid& G = m->grid[m->cur];
+  if (m->tmp_cap < 4096u) RCHK(ensure_events(m, m->ev_cap, 4096u, keep, false));
+  for (int attempt = 0;; ++attempt) {
+    if (attempt) {
+      HIPCHK(hipMemsetAsync(m->rank_cnt, 0, ((size_t)n_ops + 1) * sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_DENSE, 0, 2 * sizeof(uint32_t), st));  // + CTR_HOLES
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 3 * sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, 2 * sizeof(uint32_t), st));
+    }
+    gw::SmallArgs sa{};
+    sa.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
+    sa.base = base;
+    sa.n_ops = n_ops;
+    sa.n_dev = a.n_dev;
+    sa.op_slot = a.op_slot;
+    sa.op_kind = a.op_kind;
+    sa.space_of = m->space_of;
+    sa.pos_x = m->pos_x;
+    sa.pos_z = m->pos_z;
+    sa.old_x = m->old_x;
+    sa.old_z = m->old_z;
+    sa.old_seq = m->old_seq;
+    sa.opq = m->opq;
+    sa.gen = m->grid_gen;
+    sa.ov_tag = m->ov_tag;
+    sa.ov_rec = m->ov_rec;
+    sa.ov_count = m->ov_count;
+    sa.ev_tmp = m->ev_tmp;
+    sa.ev_cap = m->tmp_cap;
+    sa.rank_cnt = m->rank_cnt;
+    sa.ctr = m->ctr;
+    gw::launch_sweep_small(sa, st);
+    HIPCHK(hipGetLastError());
+    if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
+    if (copy_events) RCHK(ensure_host_events(m, m->ev_cap, keep));
+    gw::launch_scan(m->scan, m->rank_cnt, n_ops + 1, st);
+    gw::OrderArgs o{};
+    o.g = {m->ctr, m->tmp_cap, keep, m->ev_cap};
+    o.ev_tmp = m->ev_tmp;
+    o.ev_fix = nullptr;
+    o.tile_ev = m->tile_ev;
+    o.tile_ent = m->tile_ent;
+    o.ntiles_fix = 0;
+    o.scratch = reinterpret_cast<uint2*>(m->ev_tmp);
+    o.rank_off = m->rank_cnt;
+    o.ev_out = m->ev_out + keep;
+    o.host_out = copy_events ? m->d_hev + keep : nullptr;
+    o.n_ops = n_ops;
+    o.zero_cs = nullptr;  // (the next full build's target was zeroed by the last full pass)
+    o.zero_n = 0;
+    o.ctr_next = m->ctr_buf + (m->ctr_sel ^ 1) * gw::CTR_N;
+    o.grid_total = G.cs + G.ncells;
+    o.op_slot = a.op_slot;
+    o.opq = m->opq;
+    o.base = base;
+    o.cap = m->cap;
+    o.check_ops = dev ? 1 : 0;  // (no per-tile acted counts: k_slice_sort checks every op's slot)
+    o.tile_acted = nullptr;
+    o.ntiles_acted = 0;
+    o.n_dev = a.n_dev;
+    o.pub_seq = publish_seq(m, copy_events);
+    o.pub = o.pub_seq ? m->d_pub : nullptr;
+    o.sorted_hint = !o.check_ops ? 1 : 0;  // few blocks: a small pass sorts few slices
+    o.place_blocks = 16;
+    gw::launch_order(o, st);
+    HIPCHK(hipGetLastError());
+    if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
+    RCHK(finish_pass(m, o.pub_seq));
+    if (m->h_ctr[gw::CTR_ERR]) {
+      m->broken = true;
+      set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
+              "capacity, 8=Enter of a present slot, 16=Space id out of range, 32=op count above its bound, "
+              "64=non-finite coordinate); the manager is unusable",
+              m->h_ctr[gw::CTR_ERR]);
+      return GWAOI_ERR_DEVICE_CHECK;
+    }
+    const uint32_t slots = m->h_ctr[gw::CTR_EVENTS], nev = m->h_ctr[gw::CTR_NEV];
+    if (slots > m->tmp_cap || keep + nev > m->ev_cap) {
+      RCHK(ensure_events(m, keep + nev, slots, keep, copy_events));
+      if (attempt < 3) continue;
+      set_err("event buffer overflow persisted");
+      return GWAOI_ERR_NOMEM;
+    }
+    m->tick_events += nev;
+    m->tick_enter += m->h_ctr[gw::CTR_ENTER];
+    if (m->timing) {
+      m->tpend.pending = true;
+      m->tpend.n_ops = m->h_ctr[gw::CTR_NOPS];
+      m->tpend.nev = nev;
+      m->tpend.records = 0;
+      m->tpend.ncells = 0;
+      m->tpend.dense = 0;
+      m->tpend.chunked = 0;
+    }
+    break;
+  }
+  m->ov_bound += n_ops;
+  m->small_passes++;
+  m->passes_run++;
+  m->ctr_sel ^= 1;
+  m->ctr = m->ctr_buf + m->ctr_sel * gw::CTR_N;
+  m->tick_passes++;
+  m->tick_ops += m->h_ctr[gw::CTR_NOPS];
+  m->n_ops = 0;
+  m->n_leaves = 0;
+  m->dv_n = 0;
+  m->dv_slot = nullptr;
+  m->dv_x = m->dv_z = nullptr;
+  m->pass_id++;
+  if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
+  m->n_present_dev = m->n_present;
+  m->dv_kind = nullptr;
+  m->dv_space = nullptr;
+  m->dv_count = nullptr;
+  return GWAOI_OK;  // (last_unsorted and the dense / chunked hints stay the last full pass's)
+}
+
+// The grid of the last full build plus an overlay is current for the sweep, not for readers of the grid
+// itself (relation view, sync fan-out, strips): rebuild it from the slots' state first.
+int ensure_grid_current(gwaoi_mgr* m) {
+  if (!m->ov_bound) return GWAOI_OK;
+  RCHK(build_grid(m, m->cur, m->next_seq, 0, nullptr, kBuildCounting));
+  m->grid_gen++;
+  m->ov_bound = 0;
+  HIPCHK(hipMemsetAsync(m->ov_count, 0, sizeof(uint32_t), m->stream));
   return GWAOI_OK;
 }
 
@@ -621,8 +853,14 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   if ((uint64_t)m->next_seq + n_ops >= kSeqLimit) RCHK(renormalise(m));
   const uint32_t base = m->next_seq;
   m->next_seq += n_ops;
+  if (small_pass_ok(m, n_ops)) return run_small_pass(m, copy_events, base, n_ops);
   const int og = m->cur, ng = m->cur ^ 1;
   hipStream_t st = m->stream;
+  if (m->ov_bound) {  // the grid is rebuilt from the slots' state: the overlay starts over
+    m->grid_gen++;
+    m->ov_bound = 0;
+    HIPCHK(hipMemsetAsync(m->ov_count, 0, sizeof(uint32_t), st));
+  }
 
   // geometry of the new grid: the latest geometry (recomputed when auto extents grew)
   std::vector<gw::Geom> geo = m->grid[og].h_geom;
@@ -643,7 +881,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     if (m->n_leaves)
       HIPCHK(hipMemcpyAsync(m->d_leaves, m->h_leaves, m->n_leaves * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   }
-  gw::ApplyArgs a;
+  gw::ApplyArgs a{};
   a.n_dev = dev ? m->dv_count : nullptr;
   a.op_slot = dev ? m->dv_slot : m->d_op_slot;
   a.op_x = dev ? m->dv_x : m->d_op_x;
@@ -667,6 +905,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   a.opq = m->opq;
   a.ctr = m->ctr;
   a.rank_cnt = m->rank_cnt;
+  a.ov_rec = nullptr;  // (a full pass: no overlay)
   gw::launch_apply(a, st);
   HIPCHK(hipGetLastError());
   if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
@@ -681,23 +920,30 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   const bool fixed = tile_build(m->grid[ng]) && m->sweep_lds != 0 && m->grid[ng].ntiles;
   const uint32_t F = fixed ? m->grid[ng].ntiles * gw::sweep_ev_lds() : 0u;
   if (m->tmp_cap < F + 4096u) RCHK(ensure_events(m, m->ev_cap, F + 4096u, keep, false));
-  // events: expected count is small; grow and re-run the (pure) sweep on overflow
-  bool rebuild = false;
+  // events: expected count is small; grow and re-run the (pure) sweep on overflow. Three causes of a
+  // re-run, each with its own bound: the one-pass build's plan did not hold (build_rr), the event buffers
+  // were too small (ev_rr), the sweep listed dense movers while k_sweep_dense was not launched (the
+  // previous pass had none; dense_rr)
+  bool rebuild = false, force_dense = false, force_band = false;
+  int build_rr = 0, ev_rr = 0, dense_rr = 0, band_rr = 0;
   for (int attempt = 0;; ++attempt) {
     if (rebuild) {  // the one-pass build's plan did not hold: the same pass with the counting build
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_BOVF, 0, sizeof(uint32_t), st));
       RCHK(build_grid(m, ng, base, n_ops, a.op_kind, kBuildRerun));
       m->build_reruns++;
+      m->rerun_counting = true;
       rebuild = false;
     }
-    if (attempt) {  // re-run after growing the event buffers: reset what the sweep accumulates
+    if (attempt) {  // re-run: reset what the sweep and the order stage accumulate
       // the scan turned the counts into offsets, and the sweep stores non-zero counts only
       HIPCHK(hipMemsetAsync(m->rank_cnt, 0, ((size_t)n_ops + 1) * sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_DENSE, 0, 2 * sizeof(uint32_t), st));  // + CTR_HOLES
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 3 * sizeof(uint32_t), st));  // + CTR_BAND_ITEMS, _MV
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, 2 * sizeof(uint32_t), st));     // + CTR_BAND_NEXT
     }
-    gw::SweepArgs s;
+    gw::SweepArgs s{};
     const Grid& G = m->grid[ng];
     s.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
     s.ntiles = G.ntiles;
@@ -729,7 +975,17 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.ctr = m->ctr;
     s.dense = m->d_dense;
     s.dense_cap = m->cap;
-    s.dense_hint = attempt ? ~0u : m->last_dense;
+    s.dense_hint = force_dense ? ~0u : m->last_dense;
+    s.band_mv = m->chunked ? m->band_mv : nullptr;
+    s.band_mv_cap = m->band_mv_cap;
+    s.band_items = m->chunked ? m->band_items : nullptr;
+    s.band_items_cap = m->band_items_cap;
+    s.band_hint = force_band ? ~0u : m->last_band;
+#ifndef GW_CHUNK_MAX_RECS  // tiles over this many records (hotspot crowds) keep the wave-per-mover walk:
+#define GW_CHUNK_MAX_RECS 2048  // chunked, skew50 swept in 14.0 ms instead of 5.75 (r04_b2)
+#endif
+    s.chunk_grid = m->chunk_grid;
+    s.chunk_max_recs = GW_CHUNK_MAX_RECS;
     s.tile_walk = tile_build(G) ? m->tile_walk : nullptr;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
@@ -738,7 +994,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     // canonical order; every step is guarded on the device against a buffer overflow, so the host
     // synchronises once, at the end of the pass
     gw::launch_scan(m->scan, m->rank_cnt, n_ops + 1, st);
-    gw::OrderArgs o;
+    gw::OrderArgs o{};
     o.g = {m->ctr, m->tmp_cap - F, keep, m->ev_cap};
     o.ev_tmp = m->ev_tmp + F;
     o.ev_fix = fixed ? m->ev_tmp : nullptr;
@@ -758,12 +1014,20 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     o.opq = m->opq;
     o.base = base;
     o.cap = m->cap;
-    o.check_ops = dev ? 1 : 0;
+    // device batches: every op on a slot of its own, checked from k_bin_tsort's per-tile acted counts
+    // (tile builds) or per op by k_slice_sort
+    const bool tiles_check = dev && tile_build(m->grid[ng]);
+    o.check_ops = dev && !tiles_check ? 1 : 0;
+    o.tile_acted = m->tile_acted;
+    o.ntiles_acted = tiles_check ? m->grid[ng].ntiles : 0u;
     o.n_dev = dev ? m->dv_count : nullptr;
+    o.pub_seq = publish_seq(m, copy_events);
+    o.pub = o.pub_seq ? m->d_pub : nullptr;
+    o.sorted_hint = attempt == 0 && !m->last_unsorted && !o.check_ops ? 1 : 0;
     gw::launch_order(o, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
-    RCHK(finish_pass(m, copy_events));
+    RCHK(finish_pass(m, o.pub_seq));
     if (m->h_ctr[gw::CTR_ERR]) {
       m->broken = true;
       set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
@@ -773,17 +1037,35 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       return GWAOI_ERR_DEVICE_CHECK;
     }
     if (m->h_ctr[gw::CTR_BOVF]) {  // (the sweep saw an empty grid)
-      if (attempt < 3) {
+      if (build_rr++ < 2) {
         rebuild = true;
         continue;
       }
       set_err("tile build overflow persisted");
       return GWAOI_ERR_NOMEM;
     }
+    if (m->h_ctr[gw::CTR_BAND_ITEMS] && s.band_items && !s.band_hint) {  // crowded tiles nobody walked
+      if (band_rr++ < 1) {
+        force_band = true;
+        m->band_reruns++;
+        continue;
+      }
+      set_err("chunked-sweep items left unwalked");
+      return GWAOI_ERR_STATE;
+    }
+    if (m->h_ctr[gw::CTR_DENSE] && !s.dense_hint) {  // dense movers nobody walked: the sweep again, with them
+      if (dense_rr++ < 1) {
+        force_dense = true;
+        m->dense_reruns++;
+        continue;
+      }
+      set_err("dense movers left unwalked");
+      return GWAOI_ERR_STATE;
+    }
     const uint32_t slots = m->h_ctr[gw::CTR_EVENTS], nev = m->h_ctr[gw::CTR_NEV];
     if (slots > m->tmp_cap - F || keep + nev > m->ev_cap) {
       RCHK(ensure_events(m, keep + nev, F + slots, keep, copy_events));
-      if (attempt < 3) continue;
+      if (ev_rr++ < 3) continue;
       set_err("event buffer overflow persisted");
       return GWAOI_ERR_NOMEM;
     }
@@ -796,6 +1078,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       m->tpend.records = m->h_ctr[gw::CTR_RECORDS];
       m->tpend.ncells = m->grid[ng].ncells;
       m->tpend.dense = m->h_ctr[gw::CTR_DENSE];
+      m->tpend.chunked = m->h_ctr[gw::CTR_BAND_MV];
     }
     break;
   }
@@ -814,6 +1097,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->pass_id++;
   if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
   m->last_dense = m->h_ctr[gw::CTR_DENSE];
+  m->last_band = m->h_ctr[gw::CTR_BAND_ITEMS];
+  m->last_unsorted = m->h_ctr[gw::CTR_UNSORTED] != 0;
   m->n_present_dev = m->n_present;
   m->dv_kind = nullptr;
   m->dv_space = nullptr;
@@ -901,7 +1186,7 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_mv, m->band_items, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
                    m->dx_part, m->dx_out};
@@ -988,17 +1273,31 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->d_op_space, C));
   chk(dalloc(&m->d_leaves, C));
   chk(dalloc(&m->d_dense, C));
+  // the chunked sweep's lists: every pass's movers fit (each at most once; items per tile: its movers /
+  // kChunkBlock rounded up, at most one partial item per tile)
+  m->band_mv_cap = (uint32_t)C;
+  chk(dalloc(&m->band_mv, C));
+  m->ov_cap = (uint32_t)std::min<size_t>(C, kOverlayCap);
+  chk(dalloc(&m->ov_tag, C));
+  chk(dalloc(&m->ov_idx, C));
+  chk(dalloc(&m->ov_rec, m->ov_cap));
+  chk(dalloc(&m->ov_count, 1));
+  if (r == GWAOI_OK) chk(hipMemset(m->ov_tag, 0, C * sizeof(uint32_t)) == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP);
+  if (r == GWAOI_OK) chk(hipMemset(m->ov_count, 0, sizeof(uint32_t)) == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP);
   chk(dalloc(&m->d_op_x, C));
   chk(dalloc(&m->d_op_z, C));
   chk(dalloc(&m->d_op_kind, C));
   chk(dalloc(&m->rank_cnt, C + 1));
   m->nblk = (capacity + gw::bin_chunk(capacity) - 1) / gw::bin_chunk(capacity);
   const uint64_t max_tiles = m->max_cells / gw::kTileCells + 1;
+  m->band_items_cap = (uint32_t)std::min<uint64_t>(C / 1024 + max_tiles + 16, 0xffffffffull);
+  chk(dalloc(&m->band_items, m->band_items_cap));
   const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
   chk(dalloc(&m->thist, thist_n));
   chk(dalloc(&m->ttot, 2 * (size_t)gw::kMaxLdsTiles));  // k_bin_tscatter zeroes kMaxLdsTiles of the other buffer
   chk(dalloc(&m->tstart, 2 * ((size_t)gw::kMaxLdsTiles + 1)));
   chk(dalloc(&m->tile_walk, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
+  chk(dalloc(&m->tile_acted, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
   chk(dalloc(&m->tile_ev, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
   chk(dalloc(&m->tile_ent, std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles)));
   // the scan has at most 1024 chunks up to 16.7M items (scan_ipt), more beyond
@@ -1038,7 +1337,13 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   static bool sweep_ready = false;
   if (!sweep_ready) {
     gw::sweep_init();
+    gw::chunk_init();
     sweep_ready = true;
+  }
+  {
+    int cus = 0;
+    m->chunk_grid = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0
+                        ? (uint32_t)cus : 256u;
   }
   if (r == GWAOI_OK)
     r = ensure_events(m, std::max<uint64_t>(1u << 16, C / 2), (uint32_t)std::max<uint64_t>(1u << 16, C / 2), 0, false);
@@ -1102,6 +1407,7 @@ void set_error(const char* fmt, ...) {
 int mgr_view(gwaoi_mgr* m, MgrView* out) {
   RCHK(check_mgr(m));
   RCHK(set_dev(m));
+  if (!(m->n_ops || m->dv_n)) RCHK(ensure_grid_current(m));  // (staged ops: the caller flushes, then asks again)
   const Grid& g = m->grid[m->cur];
   out->device = m->device;
   out->stream = m->stream;
@@ -1386,7 +1692,7 @@ int gwaoi_stage_moves_pinned(gwaoi_mgr* m, uint32_t n) {
     }
     HIPCHK(hipMemcpyAsync(m->d_pin_ext, m->h_pin_ext, m->nspaces * sizeof(float4), hipMemcpyHostToDevice, st));
   }
-  gw::PinCheckArgs a;
+  gw::PinCheckArgs a{};
   a.slot = m->d_op_slot;
   a.x = m->d_op_x;
   a.z = m->d_op_z;
@@ -1586,7 +1892,7 @@ int relation_delta(gwaoi_mgr* m, bool* done) {
     RCHK(dalloc(&m->rel_tmp, want));
     m->rel_tmp_cap = want;
   }
-  gw::RelDeltaArgs a;
+  gw::RelDeltaArgs a{};
   a.ev = m->ev_out;
   a.nev = (uint32_t)nev;
   a.cap = m->cap;
@@ -1688,6 +1994,7 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
     }
   }
   m->rel_valid = false;
+  RCHK(ensure_grid_current(m));  // (after small passes the grid lags their ops: rebuilt from the slots)
   hipStream_t st = m->stream;
   if (!m->rel_rp) RCHK(dalloc(&m->rel_rp, (size_t)m->cap + 1));
   if (!m->rel_tot) RCHK(dalloc(&m->rel_tot, 3));  // [0] entries, [1] longest row, [2] rows to fix
@@ -1723,7 +2030,7 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
     }
   }
   const Grid& g = m->grid[m->cur];
-  gw::RelArgs a;
+  gw::RelArgs a{};
   a.g = {g.rec, g.cs, g.d_geom, g.d_tile_space};
   a.pos_x = m->pos_x;
   a.pos_z = m->pos_z;
@@ -1739,6 +2046,7 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   a.tstat = m->rel_tstat;
   a.slab = m->rel_slab;
   a.slab_s = a.slab ? kSlabS : 0u;
+  a.slab_recs = a.slab ? (uint32_t)std::min<uint64_t>(m->rel_slab_recs, 0xffffffffull) : 0u;
   // count pass, scan, then the row lengths' total is the one value the host must know (allocation)
   HIPCHK(hipMemsetAsync(m->rel_rp, 0, ((size_t)m->cap + 1) * sizeof(uint32_t), st));
   HIPCHK(hipMemsetAsync(m->rel_tot, 0, 3 * sizeof(unsigned long long), st));
@@ -1878,7 +2186,7 @@ int gwaoi_export_relation_delta(gwaoi_mgr* m, gwaoi_event* out, uint64_t cap, ui
   HIPCHK(hipMemsetAsync(m->dx_keys, 0xFF, slots * sizeof(unsigned long long), st));
   HIPCHK(hipMemsetAsync(m->dx_cnt, 0, slots * sizeof(uint32_t), st));
   HIPCHK(hipMemsetAsync(m->dx_last, 0, slots * sizeof(uint32_t), st));
-  gw::DeltaExportArgs a;
+  gw::DeltaExportArgs a{};
   a.ev = m->ev_out;
   a.nev = (uint32_t)nev;
   a.mask = (uint32_t)(slots - 1);
@@ -2033,7 +2341,20 @@ int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
 
 int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
   RCHK(check_mgr(m));
+  // 3: the LDS sweep without the chunked sweep (crowded tiles' movers walk from L2: k_sweep_dense), A/B
+  m->chunked = enable != 3;
   m->sweep_lds = enable < 0 ? 0 : (enable > 2 ? 1 : enable);
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_small_pass(gwaoi_mgr* m, int mode, uint64_t* n_small) {
+  RCHK(check_mgr(m));
+  if (mode > 2) {
+    set_err("debug_set_small_pass: mode %d (0 off, 1 auto, 2 whenever the overlay has room)", mode);
+    return GWAOI_ERR_INVALID;
+  }
+  if (mode >= 0) m->small_mode = mode;
+  if (n_small) *n_small = m->small_passes;
   return GWAOI_OK;
 }
 

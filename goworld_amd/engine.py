@@ -237,6 +237,13 @@ class Engine:
     def debug_set_sweep_lds(self, on: bool):
         check(self._L.gwaoi_debug_set_sweep_lds(self._h, 1 if on else 0))
 
+    def debug_small_pass(self, mode: int = -1) -> int:
+        """Small passes (gwaoi_debug_set_small_pass): mode 0 off, 1 auto, 2 whenever possible, -1 keep;
+        returns the number of small passes run so far."""
+        n = ctypes.c_uint64()
+        check(self._L.gwaoi_debug_set_small_pass(self._h, int(mode), ctypes.byref(n)))
+        return n.value
+
     def debug_set_cells_per_dist(self, v: float):
         check(self._L.gwaoi_debug_set_cells_per_dist(self._h, v))
 

@@ -167,6 +167,7 @@ class StripNode:
         self.eng.set_stream(self.stream.cuda_stream)
         self.eng.set_population_hint(0, max(1, min(n, int(share * 1.05))))
         self.tick_no = 0
+        self.xev = []  # (start, end) hipEvents of timed exchanges (tick_rccl(time_exchange=True))
 
     # ---- raw kernel calls ----
     def _s(self):
@@ -294,11 +295,13 @@ class StripNode:
             return self._emit_and_tick(host_events, self.eng.count()[0] + nin)
 
     def tick_rccl(self, t: int, comm: "StripComm", host_events: bool = False, step: float = 1.0,
-                  moves: Optional[Tuple[torch.Tensor, ...]] = None, peers: Optional[Tuple[int, int]] = None):
+                  moves: Optional[Tuple[torch.Tensor, ...]] = None, peers: Optional[Tuple[int, int]] = None,
+                  time_exchange: bool = False):
         """One whole tick with the halo exchange over RCCL inside libgwaoi (gwaoi_strip_exchange): walk /
         ingest, select, exchange, absorb, emit and the AOI pipeline all enqueued on the node's stream,
         no host round trip before the pipeline's own end-of-pass read. peers = (left, right) rank or -1
-        (default: the neighbouring ranks)."""
+        (default: the neighbouring ranks). time_exchange: hipEvents around the exchange on the node's
+        stream, kept in self.xev (read after a synchronisation: exchange_ms)."""
         if self.left_in is None:
             dev = self.device
             self.left_in = torch.zeros((self.cap, 4), dtype=torch.int32, device=dev)
@@ -322,9 +325,16 @@ class StripNode:
             check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
                                        _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
                                        ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+            if time_exchange:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             check(L.gwaoi_strip_exchange(comm.handle, self._s(), int(peers[0]), int(peers[1]), _ptr(self.left),
                                          _ptr(self.right), _ptr(self.counts), self.cap, _ptr(self.left_in),
                                          _ptr(self.right_in), _ptr(self.counts_in)))
+            if time_exchange:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                self.xev.append((e0, e1))
             for k, recs in enumerate((self.left_in, self.right_in)):
                 if peers[k] >= 0:
                     check(L.gwaoi_strip_absorb_n(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
@@ -332,6 +342,16 @@ class StripNode:
                                                  self.cap, self._err()))
             self.tick_no = t
             return self._emit_and_tick(host_events, self.eng.count()[0] + 2 * self.cap)
+
+    def exchange_ms(self) -> Optional[float]:
+        """Mean device time of the timed exchanges (tick_rccl(time_exchange=True)) since the last call:
+        the RCCL group on the node's stream, including the wait for the neighbours' matching calls."""
+        if not self.xev:
+            return None
+        self.stream.synchronize()
+        ms = sum(a.elapsed_time(b) for a, b in self.xev) / len(self.xev)
+        self.xev = []
+        return ms
 
     def close(self):
         self.eng.close()

@@ -42,7 +42,9 @@ int gwaoi_wl_pack_ingest(int device, const uint8_t* d_ids, const float* d_x, con
  * otherwise runs every ~2^31 ops). */
 struct gwaoi_mgr;
 int gwaoi_debug_set_next_seq(struct gwaoi_mgr* mgr, uint32_t next_seq);
-/* Test hook: 0 = the sweep reads candidates from global memory only (A/B of the LDS-staged path). */
+/* Test hook: 0 = the sweep reads candidates from global memory only (A/B of the LDS-staged path);
+ * 1 = the default (LDS-staged tiles, crowded tiles chunked through LDS); 3 = LDS-staged tiles, crowded
+ * tiles' movers walk from global memory (A/B of the chunked sweep). */
 int gwaoi_debug_set_sweep_lds(struct gwaoi_mgr* mgr, int enable);
 /* Test hook: cell size = D / cells_per_dist for grids built from now on (default 4). */
 int gwaoi_debug_set_cells_per_dist(struct gwaoi_mgr* mgr, float cells_per_dist);
@@ -62,6 +64,10 @@ int gwaoi_debug_set_index_limit(struct gwaoi_mgr* mgr, uint64_t limit);
  * bound, 7 a row with too many changes, 8 inconsistent size). */
 int gwaoi_debug_set_relation_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* n_incremental, uint64_t* n_full,
                                   int* last_rebuild_reason);
+/* Test hook: small passes (a pass with few ops is judged against the last full build's grid plus an
+ * overlay of the slots with ops since, without rebuilding the grid). mode 0 = off, 1 = auto (default),
+ * 2 = whenever the overlay has room; < 0 leaves the mode. *n_small (optional): small passes run. */
+int gwaoi_debug_set_small_pass(struct gwaoi_mgr* mgr, int mode, uint64_t* n_small);
 /* Grid build mode: 0 = the one-pass tile build whenever the previous tile build's starts fit the grid
  * (default; a pass whose plan overflows is re-run with the counting build), 1 = always the counting
  * build; -1 leaves the mode. Reports the builds of each kind and the re-runs since the manager was made. */

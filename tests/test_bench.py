@@ -35,6 +35,18 @@ def test_self_launch_two_ranks_gloo():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["dry_run"] and r["backend"] == "gloo"
     assert abs(r["elapsed"] - 0.002) < 1e-9  # the max over both ranks
+    # the N > 1 line carries the config-4 strips sub-measurement (every rank takes part: collective)
+    st = r["strips"]
+    assert st["workload"] == "strips" and st["n_gpus"] == 2 and st["dry_run"]
+    assert abs(st["elapsed"] - 0.002) < 1e-9
+
+
+def test_watchdog_ends_a_hung_rank():
+    # a rank that outlives its watchdog exits with status 3 (no exec, no hang)
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; bench.arm_watchdog(0.5, 0); time.sleep(30)"
+            % ROOT)
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3 and "watchdog" in p.stderr
 
 
 def test_self_launch_propagates_failure():

@@ -222,6 +222,28 @@ def test_replay_tool_tracks_the_relation(po):
     rs.close()
 
 
+def test_sharded_replay_tool_equals_the_single_sink(po):
+    """tools/replay_sets.c's sharded sink (bench.py replay_ms_sharded: the same set operations split by
+    owning entity over worker threads) stays consistent with the relation, as the single sink does."""
+    import __graft_entry__ as G
+    G.build_tools()
+    from tools.replay import ShardedReplaySets
+    case = H.case_walk(0x5EED0003, 3000, 1200.0, 4, workload=po)
+    orc = po.XZListOracle(100.0, 3000)
+    H.oracle_tick(orc, case["ticks"][0])
+    rp, cols = orc.relation()
+    rs = ShardedReplaySets(2 * len(cols), 5)
+    rs.load_relation(rp, cols)
+    assert rs.size() == 2 * len(cols)
+    for ops in case["ticks"][1:]:
+        ev = np.ascontiguousarray(H.oracle_tick(orc, ops))
+        assert rs.replay(ev.ctypes.data, len(ev)) == 0
+        assert rs.size() == 2 * len(orc.relation()[1])
+    bad = np.ascontiguousarray(ev[-1:])
+    assert rs.replay(bad.ctypes.data, 1) == 4
+    rs.close()
+
+
 def test_delta_rows_tool_tracks_the_relation(po):
     """tools/delta_rows.c (bench.py's relation_delta_apply_ms): per-slot sorted neighbour arrays patched
     with the net changes of a tick (both directions, as gwaoi_export_relation_delta lists them) equal
@@ -246,7 +268,7 @@ def test_delta_rows_tool_tracks_the_relation(po):
         d = [(k >> 32, (k & 0xFFFFFFFF) | 0x80000000) for k in sorted(b - a)] + \
             [(k >> 32, k & 0xFFFFFFFF) for k in sorted(a - b)]
         delta = np.asarray(d, np.uint32).reshape(-1, 2)
-        assert dr.apply(delta) == 0
+        assert dr.apply(delta, threads=1 + len(rel[1]) % 4) == 0  # (single and multi-threaded apply)
         assert dr.diff(*new) == 0
         rel = new
     assert dr.apply(delta[:1]) == 1

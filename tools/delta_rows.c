@@ -7,6 +7,7 @@
  * Counts inconsistent entries (insert of a present col, removal of an absent one): 0 when the delta is
  * exactly the relation's change.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -18,19 +19,27 @@ typedef struct {
   uint32_t** row;
 } dr_sets;
 
+void dr_destroy(dr_sets* s);
+
 dr_sets* dr_create(const uint32_t* row_ptr, const uint32_t* cols, uint32_t nrows) {
   dr_sets* s = calloc(1, sizeof *s);
   if (!s) return NULL;
   s->nrows = nrows;
   s->len = calloc(nrows, sizeof *s->len);
   s->cap = calloc(nrows, sizeof *s->cap);
-  s->row = calloc(nrows, sizeof *s->row);
-  if (!s->len || !s->cap || !s->row) return NULL;
+  s->row = calloc(nrows, sizeof *s->row); /* zeroed: dr_destroy frees only the rows built */
+  if (!s->len || !s->cap || !s->row) {
+    dr_destroy(s);
+    return NULL;
+  }
   for (uint32_t r = 0; r < nrows; ++r) {
     const uint32_t n = row_ptr[r + 1] - row_ptr[r];
     s->cap[r] = n + 8;
     s->row[r] = malloc(s->cap[r] * sizeof(uint32_t));
-    if (!s->row[r]) return NULL;
+    if (!s->row[r]) {
+      dr_destroy(s);
+      return NULL;
+    }
     memcpy(s->row[r], cols + row_ptr[r], n * sizeof(uint32_t));
     s->len[r] = n;
   }
@@ -39,7 +48,8 @@ dr_sets* dr_create(const uint32_t* row_ptr, const uint32_t* cols, uint32_t nrows
 
 void dr_destroy(dr_sets* s) {
   if (!s) return;
-  for (uint32_t r = 0; r < s->nrows; ++r) free(s->row[r]);
+  if (s->row)
+    for (uint32_t r = 0; r < s->nrows; ++r) free(s->row[r]);
   free(s->row);
   free(s->cap);
   free(s->len);
@@ -92,6 +102,57 @@ uint64_t dr_apply(dr_sets* s, const uint32_t* d, uint64_t n) {
       s->len[r] = len - 1;
     }
   }
+  return bad;
+}
+
+/* dr_apply over worker threads: thread k applies the entries of rows r with r % nthreads == k, in entry
+ * order (every row belongs to one thread, so the per-row result equals dr_apply's) */
+typedef struct {
+  dr_sets* s;
+  const uint32_t* d;
+  uint64_t n;
+  uint32_t k, nt;
+  uint64_t bad;
+} dr_job;
+
+static void* dr_run(void* p) {
+  dr_job* j = (dr_job*)p;
+  dr_sets* s = j->s;
+  uint64_t bad = 0;
+  for (uint64_t i = 0; i < j->n; ++i) {
+    const uint32_t r = j->d[2 * i];
+    if (r % j->nt != j->k) continue;
+    const uint64_t b = dr_apply(s, j->d + 2 * i, 1);
+    if (b == ~0ull) {
+      j->bad = ~0ull;
+      return NULL;
+    }
+    bad += b;
+  }
+  j->bad = bad;
+  return NULL;
+}
+
+uint64_t dr_apply_mt(dr_sets* s, const uint32_t* d, uint64_t n, uint32_t nthreads) {
+  if (nthreads < 2) return dr_apply(s, d, n);
+  pthread_t* th = calloc(nthreads, sizeof(pthread_t));
+  dr_job* jb = calloc(nthreads, sizeof(dr_job));
+  uint64_t bad = 0;
+  if (!th || !jb) {
+    free(th);
+    free(jb);
+    return ~0ull;
+  }
+  for (uint32_t k = 0; k < nthreads; ++k) {
+    jb[k] = (dr_job){s, d, n, k, nthreads, 0};
+    if (pthread_create(&th[k], NULL, dr_run, &jb[k])) dr_run(&jb[k]), th[k] = 0;
+  }
+  for (uint32_t k = 0; k < nthreads; ++k) {
+    if (th[k]) pthread_join(th[k], NULL);
+    bad = (bad == ~0ull || jb[k].bad == ~0ull) ? ~0ull : bad + jb[k].bad;
+  }
+  free(th);
+  free(jb);
   return bad;
 }
 

@@ -41,6 +41,40 @@ class ReplaySets:
             self._h = None
 
 
+class ShardedReplaySets:
+    """The same sink split by owning entity over `shards` worker threads (rs_sharded_*)."""
+
+    def __init__(self, expect_entries: int, shards: int):
+        L = ctypes.CDLL(_SO)
+        vp, u64, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32
+        L.rs_sharded_create.argtypes, L.rs_sharded_create.restype = [u64, u32], vp
+        L.rs_sharded_destroy.argtypes = [vp]
+        L.rs_sharded_load_relation.argtypes = [vp, vp, vp, u32]
+        L.rs_sharded_replay.argtypes, L.rs_sharded_replay.restype = [vp, vp, u64], u64
+        L.rs_sharded_size.argtypes, L.rs_sharded_size.restype = [vp], u64
+        self._L = L
+        self.shards = int(shards)
+        self._h = L.rs_sharded_create(int(expect_entries), self.shards)
+        if not self._h:
+            raise MemoryError("rs_sharded_create")
+
+    def load_relation(self, row_ptr: np.ndarray, cols: np.ndarray):
+        rp = np.ascontiguousarray(row_ptr, np.uint32)
+        c = np.ascontiguousarray(cols, np.uint32)
+        self._L.rs_sharded_load_relation(self._h, rp.ctypes.data, c.ctypes.data, len(rp) - 1)
+
+    def replay(self, events_ptr: int, count: int) -> int:
+        return int(self._L.rs_sharded_replay(self._h, ctypes.c_void_p(events_ptr), int(count)))
+
+    def size(self) -> int:
+        return int(self._L.rs_sharded_size(self._h))
+
+    def close(self):
+        if self._h:
+            self._L.rs_sharded_destroy(self._h)
+            self._h = None
+
+
 _DR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_bin", "libdeltarows.so")
 
 
@@ -54,6 +88,7 @@ class DeltaRows:
         L.dr_create.argtypes, L.dr_create.restype = [vp, vp, u32], vp
         L.dr_destroy.argtypes = [vp]
         L.dr_apply.argtypes, L.dr_apply.restype = [vp, vp, u64], u64
+        L.dr_apply_mt.argtypes, L.dr_apply_mt.restype = [vp, vp, u64, u32], u64
         L.dr_diff.argtypes, L.dr_diff.restype = [vp, vp, vp], u64
         self._L = L
         rp = np.ascontiguousarray(row_ptr, np.uint32)
@@ -62,8 +97,11 @@ class DeltaRows:
         if not self._h:
             raise MemoryError("dr_create")
 
-    def apply(self, delta: np.ndarray) -> int:
+    def apply(self, delta: np.ndarray, threads: int = 1) -> int:
+        """Patch the rows with the delta entries; threads > 1: rows split over worker threads."""
         d = np.ascontiguousarray(delta, np.uint32)
+        if threads > 1:
+            return int(self._L.dr_apply_mt(self._h, d.ctypes.data, len(d), int(threads)))
         return int(self._L.dr_apply(self._h, d.ctypes.data, len(d)))
 
     def diff(self, row_ptr: np.ndarray, cols: np.ndarray) -> int:
