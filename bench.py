@@ -251,6 +251,65 @@ def spaces_workload(args, rank):
     raise ValueError(args.workload)
 
 
+def small_pass_leg(eng, n, L, xs, zs, reps, seed):
+    """Passes with few ops into the full manager: the Go wrapper flushes every Enter and
+    Leave as its own pass (gwaoi.go SyncEnterLeave; Space.go:188-251 calls), and a server may flush a
+    handful of Moved calls between ticks. Per repetition: a 1-op Leave of a random present slot, the
+    1-op Enter bringing it back at its position, then a 1,000-op Moved pass (distinct random slots, each
+    moved by <= 1 unit), host-staged through the wrapper's calls, events left in HBM. Run with small
+    passes on (auto: the overlay restarts when ops x overlay grows past its budget, so some 1k passes are
+    full) and off (every pass a full pass), for comparison. Device time = the pass's hipEvents
+    (stats ms_total), host time = stage + gwaoi_tick_ex wall time."""
+    import numpy as np
+    rng = np.random.default_rng(seed ^ 0x5A11)
+    xs, zs = xs.copy(), zs.copy()
+    eng.adopt_device_state()
+    eng.set_timing(True)
+    out = {}
+    for mode, tag in ((1, "small_on"), (0, "small_off")):
+        eng.debug_small_pass(mode)
+        rec = {"leave_1op": [], "enter_1op": [], "moved_1k": []}
+        for _ in range(reps):
+            s = int(rng.integers(n))
+            mv = np.sort(rng.choice(n, 1000, replace=False)).astype(np.uint32)
+
+            def moved():
+                xs[mv] = np.clip(xs[mv] + rng.uniform(-1, 1, mv.size), 0, np.nextafter(np.float32(L), 0))
+                zs[mv] = np.clip(zs[mv] + rng.uniform(-1, 1, mv.size), 0, np.nextafter(np.float32(L), 0))
+                eng.stage_moves(mv, xs[mv], zs[mv])
+
+            for kind, stage in (("leave_1op", lambda: eng.leave(s)),
+                                ("enter_1op", lambda: eng.enter(s, float(xs[s]), float(zs[s]))),
+                                ("moved_1k", moved)):
+                n0 = eng.debug_small_pass()
+                eng.reset_stats()
+                t0 = time.perf_counter()
+                stage()
+                eng.tick_device()
+                dt = time.perf_counter() - t0
+                dev_ms = eng.stats()["ms_total"]
+                rec[kind].append((eng.debug_small_pass() > n0, dev_ms, dt * 1e3, int(eng.last.count)))
+        res = {}
+        for kind, v in rec.items():
+            sm = [r for r in v if r[0]]
+            fu = [r for r in v if not r[0]]
+            res[kind] = {
+                "passes": len(v), "small_passes": len(sm),
+                "device_ms_p50_small": percentile([r[1] for r in sm], 50) if sm else None,
+                "device_ms_p50_full": percentile([r[1] for r in fu], 50) if fu else None,
+                "host_ms_p50": percentile([r[2] for r in v], 50),
+                "events_mean": float(np.mean([r[3] for r in v])),
+            }
+        out[tag] = res
+    eng.debug_small_pass(1)
+    eng.set_timing(False)
+    out["note"] = (
+        f"{reps} repetitions per setting of a 1-op Leave, the 1-op Enter bringing the slot back, and a 1,000-op "
+        "Moved pass (<= 1 unit each), host-staged, events in HBM, into the full manager; device = the pass's "
+        "hipEvents, host = stage + tick wall time; small_passes = passes that took the small path")
+    return out
+
+
 def run_spaces(args, rank, world, dev, sync_all, allmax):
     import ctypes
 
@@ -502,6 +561,13 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             eng.relation()
             reps.append(time.perf_counter() - t0)
         rel_export_ms = sorted(reps)[1] * 1e3
+    small = None
+    if (args.workload in ("config2", "config3") and args.small_reps > 0 and nsp == 1
+            and hasattr(L_, "gwaoi_debug_set_small_pass")):
+        kp = wstate["k"] ^ 1  # the walk's last positions
+        xs = walk.download(np.float32, n, (2 * kp) * 4 * n)
+        zs = walk.download(np.float32, n, (2 * kp + 1) * 4 * n)
+        small = small_pass_leg(eng, n, L, xs, zs, args.small_reps, seed0)
     eng.close()
     walk.free()
     if rank != 0:
@@ -590,6 +656,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         "stage_ms": {k: st[k] / ticks for k in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")},
         "stage_ms_note": f"per-stage hipEvents over {ticks} ticks of the same walk run after the timed region "
                          "(the timed ticks run without them)",
+        "small_pass": small,
         "roofline": {
             "bound": "hbm",
             "kernel": "k_sweep",
@@ -1063,6 +1130,9 @@ def main():
     ap.add_argument("--latency-ticks", type=int, default=200, help="extra ticks with events delivered to host")
     ap.add_argument("--p99-ticks", type=int, default=1000,
                     help="device-resident ticks after the timed region for p50/p99 (SURVEY 8(d): >= 1,000)")
+    ap.add_argument("--small-reps", type=int, default=20,
+                    help="config 2/3: repetitions of the small-pass leg (1-op Leave, 1-op Enter, 1k-op Moved "
+                         "passes into the full manager, small passes on and off); 0 skips it")
     ap.add_argument("--host-staged-ticks", type=int, default=50,
                     help="extra ticks staged from host arrays (gwaoi_stage_moves), events to host, replayed")
     ap.add_argument("--no-replay", dest="replay", action="store_false",

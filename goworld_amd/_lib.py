@@ -263,6 +263,8 @@ def load(path: str = SO_PATH):
                                         ctypes.c_int),
     }
     for name, (args, res) in sig.items():
+        if name in TOOL_SYMBOLS and not hasattr(L, name):
+            continue  # a debug tool newer than this build (A/B runs of older libraries)
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

@@ -24,7 +24,7 @@ done
 if [ -n "$KSTATS" ]; then
   w=${WORKLOADS%% *}
   for v in $(tr ' ' '\n' < variants/LIST | awk '!seen[$0]++'); do
-    (cd /tmp && export TMPDIR=/tmp && GWAOI_LIB=$R/variants/libgwaoi_$v.so timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_${v}_prof -o run -- python3 $R/bench.py --workload $w --steps 100 --latency-ticks 0 --host-staged-ticks 0 --no-replay --p99-ticks 0 --no-cpu-baseline > $R/gpurun_out/${TAG}_${v}_prof.json 2> $R/gpurun_out/${TAG}_${v}_prof.err)
+    (cd /tmp && export TMPDIR=/tmp && GWAOI_LIB=$R/variants/libgwaoi_$v.so timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_${v}_prof -o run -- python3 $R/bench.py --workload $w --steps 100 --latency-ticks 0 --host-staged-ticks 0 --no-replay --p99-ticks 0 --small-reps 0 --no-cpu-baseline > $R/gpurun_out/${TAG}_${v}_prof.json 2> $R/gpurun_out/${TAG}_${v}_prof.err)
     python3 $R/scripts/kstats.py $R/gpurun_out/${TAG}_${v}_prof > $R/gpurun_out/${TAG}_${v}_kstats.txt
     rm -rf $R/gpurun_out/${TAG}_${v}_prof
   done

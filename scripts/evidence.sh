@@ -30,7 +30,7 @@ if has suite; then
 fi
 if has bench; then
   timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_config2.json 2> gpurun_out/${TAG}_config2.err
-  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_config2_prof -o run -- python3 $R/bench.py --steps 300 --latency-ticks 10 --p99-ticks 0 --no-cpu-baseline > $R/gpurun_out/${TAG}_config2_prof.json 2> $R/gpurun_out/${TAG}_config2_prof.err)
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/${TAG}_config2_prof -o run -- python3 $R/bench.py --steps 300 --latency-ticks 10 --p99-ticks 0 --small-reps 0 --no-cpu-baseline > $R/gpurun_out/${TAG}_config2_prof.json 2> $R/gpurun_out/${TAG}_config2_prof.err)
   python3 scripts/kstats.py gpurun_out/${TAG}_config2_prof > gpurun_out/${TAG}_config2_kstats.txt
   cp gpurun_out/${TAG}_config2_prof/run_kernel_stats.csv gpurun_out/${TAG}_config2_kernel_stats.csv 2>/dev/null || true
   rm -rf gpurun_out/${TAG}_config2_prof

@@ -6,7 +6,7 @@ set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out
 TAG=${TAG:-pmc}
-ARGS="--steps 20 --warmup 2 --latency-ticks 0 --no-cpu-baseline ${BENCH_ARGS}"
+ARGS="--steps 20 --warmup 2 --latency-ticks 0 --small-reps 0 --no-cpu-baseline ${BENCH_ARGS}"
 cd /tmp && export TMPDIR=/tmp
 i=0
 PMC_GROUPS=${PMC_GROUPS:-"FETCH_SIZE|WRITE_SIZE"}
