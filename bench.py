@@ -351,6 +351,8 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         eng.debug_set_cell_side(args.cell_side)
     if args.sweep_lds != 1:
         eng._L.gwaoi_debug_set_sweep_lds(eng.handle, args.sweep_lds)
+    if args.chunked:  # A/B: min_recs,max_recs,max_pad of the tiles k_sweep_chunked takes
+        eng.debug_set_chunked(*[int(v) for v in args.chunked.split(",")])
     if args.counting_build:
         eng.debug_build_mode(1)
     # bulk restore (untimed): one device-staged pass of SILENT Enters into their Spaces; the relation
@@ -735,6 +737,9 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
     eng.tick_device()
     kinds.free()
     sy = EntitySync(eng, args.gates)
+    if hasattr(L_, "gwaoi_debug_set_fanout_mode"):
+        sy.debug_fanout_mode(args.fanout)
+    direct = args.fanout == 0 and args.gates <= 8 and hasattr(L_, "gwaoi_debug_set_fanout_mode")
     all_slots = np.arange(n, dtype=np.uint32)
     sy.set_entities(all_slots, ids)
     has_client = (all_slots.astype(np.uint64) * 2654435761 % 1000) < int(args.client_frac * 1000)
@@ -790,6 +795,10 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
     #  gate partition (k_gate_hist + k_gate_scatter): per record the pair (8 B) and its gate (1 B), the
     #    receiver's ClientID (16 B) and the entity's info (32 B) gathered, the 48-B record written;
     #  ingest: payload read (32 B) + hash probe (16 B key + 4 B slot) + staged Moved (12 B) + flag/y/yaw (9 B).
+    #  direct write pass (k_fan_dwrite, n_gates <= 8): per record walked its 16-B binned record, collected
+    #    bits (1 B) and per-gate counts (4 B x gates rounded up to 4); per collected entity gate 2 B +
+    #    EntityID/Y/yaw 24 B; per wire record 48 B written + the receiver's ClientID (16 B) gathered; the
+    #    client sub-grid records (16 B + gate 1 B) staged once.
     nc = max(1, ss["collects"])
     ents = ss["entities"] / nc
     n_client = float(has_client.sum())
@@ -802,14 +811,18 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
     b_gate = (8.0 + 1.0 + 16.0 + 32.0 + 48.0) * recs
     b_ing = (32.0 + 20.0 + 12.0 + 9.0) * n
     gbs = lambda b, d: b / (d * 1e-3) / 1e9 if d > 0 else 0.0
-    stages = {"write_walk": (d_write, b_write, "k_fan_tile<true>"),
-              "gate_partition": (d_gate, b_gate, "k_gate_hist + k_gate_scatter")}
+    if direct:
+        gstride = (args.gates + 3) // 4 * 4
+        b_dwrite = (17.0 + 4.0 * gstride) * rec_grid + 26.0 * ents + 64.0 * recs + 17.0 * n_client
+        stages = {"write_walk": (d_write, b_dwrite, "k_fan_dwrite")}
+    else:
+        stages = {"write_walk": (d_write, b_write, "k_fan_tile<true>"),
+                  "gate_partition": (d_gate, b_gate, "k_gate_hist + k_gate_scatter")}
     dom = max(stages, key=lambda k: stages[k][0])
     dd, db, dk = stages[dom]
     ach = gbs(db, dd)
     lib_v, stamp = lib_stamp(L_)
-    t_bytes, t_note = pmc_traffic("gametick", n, stamp,
-                                  ["k_fan_tile<true>"] if dom == "write_walk" else ["k_gate_hist", "k_gate_scatter"])
+    t_bytes, t_note = pmc_traffic("gametick", n, stamp, [dk] if dom == "write_walk" else ["k_gate_hist", "k_gate_scatter"])
     return {
         "metric": "GoWorld game tick (client position ingest + AOI tick + sync fan-out) entity-updates/s at 1M "
                   "entities per Space",
@@ -842,6 +855,8 @@ def run_gametick(args, rank, world, dev, sync_all, allmax):
         "events_per_tick": st["events"] / ticks,
         "device_stage_ms": {"ingest": d_ing, "client_grid": d_cg, "count_walk": d_count, "write_walk": d_write,
                             "gate_partition": d_gate},
+        "fanout": "direct (records written into the gate packets: k_fan_dcount, scan, k_fan_dwrite)" if direct else
+                  "pair list + gate partition (k_fan_tile, k_gate_hist, k_gate_scatter)",
         "roofline": {
             "bound": "hbm", "kernel": dk, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": ach / HBM_PEAK_GBS, "traffic": gbs(t_bytes, dd) if t_bytes else None,
@@ -1143,6 +1158,10 @@ def main():
     ap.add_argument("--dists", default=None, help="skew workloads: comma list of per-Space D (A/B)")
     ap.add_argument("--cell-side", type=float, default=None, help="absolute cell side for every Space (A/B)")
     ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
+    ap.add_argument("--fanout", type=int, default=0,
+                    help="gametick: 0 = direct fan-out when gates <= 8 (default), 1 = pair list + gate partition (A/B)")
+    ap.add_argument("--chunked", default="",
+                    help="A/B: 'min_recs,max_recs,max_pad' of the over-budget tiles k_sweep_chunked takes (-1 keeps)")
     ap.add_argument("--stage-ticks", type=int, default=200,
                     help="ticks run with per-stage hipEvents after the timed region (stage_ms, roofline)")
     ap.add_argument("--counting-build", action="store_true",

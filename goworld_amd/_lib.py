@@ -42,7 +42,8 @@ TOOL_SYMBOLS = (
     "gwaoi_debug_set_cells_per_dist", "gwaoi_debug_set_cell_side", "gwaoi_debug_set_sweep_lds",
     "gwaoi_debug_read_stamps",
     "gwaoi_debug_sweep_occupancy", "gwaoi_wl_pack_ingest", "gwaoi_debug_set_index_limit",
-    "gwaoi_debug_set_relation_mode", "gwaoi_debug_set_build_mode", "gwaoi_debug_set_small_pass",
+    "gwaoi_debug_set_relation_mode", "gwaoi_debug_set_build_mode", "gwaoi_debug_set_small_pass", "gwaoi_debug_set_fanout_mode",
+    "gwaoi_debug_set_chunked",
 )
 
 
@@ -231,6 +232,8 @@ def load(path: str = SO_PATH):
         "gwaoi_debug_set_build_mode": ([vp, ctypes.c_int, ctypes.POINTER(u64), ctypes.POINTER(u64),
                                         ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_debug_set_small_pass": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
+        "gwaoi_debug_set_fanout_mode": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
+        "gwaoi_debug_set_chunked": ([vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64], ctypes.c_int),
         "gwaoi_strip_init_walk": ([vp, vp, vp, vp, vp, u64, f32], ctypes.c_int),
         "gwaoi_strip_walk": ([vp, vp, vp, vp, vp, vp, vp, u64, u64, f32, f32, vp], ctypes.c_int),
         "gwaoi_strip_ingest": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),

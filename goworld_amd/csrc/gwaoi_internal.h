@@ -25,6 +25,7 @@ enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 
        CTR_UNSORTED = 12,  // set when some op's events were numbered out of canonical order (k_slice_sort sorts)
        CTR_BAND_ITEMS = 13,  // items of k_sweep_chunked listed by k_sweep (crowded tiles)
        CTR_BAND_MV = 14,     // movers in those items
+       CTR_SMALL_OVF = 15,   // k_order_small: the pass's events exceed its LDS (the host re-runs the order stage)
        CTR_BDONE = 16,  // blocks of the one-pass build done (not published)
        CTR_SDONE = 17,  // blocks of k_slice_sort done (the last one publishes the counters)
        CTR_BAND_NEXT = 18,  // k_sweep_chunked's work counter
@@ -115,34 +116,13 @@ struct ApplyArgs {
   Rec* ov_rec;
   uint32_t* ov_count;        // device: overlay entries
   uint32_t ov_cap;
+  // small pass with host ops: op_* are the device aliases of the pinned staging arrays (read over PCIe,
+  // no copies); each op's slot and raw kind byte are written here for the kernels after k_apply
+  uint32_t* cp_slot;
+  uint8_t* cp_kind;
 };
 
-// Small pass: the movers of a pass with few ops judged against the last full build's grid (records of
-// slots without an op since then; their state is the record's end state) plus the overlay (every slot
-// with an op since then, one record each), without rebuilding the grid (k_sweep_small).
-struct SmallArgs {
-  GridView g;                // the grid of the last full build
-  uint32_t base, n_ops;
-  const uint32_t* n_dev;     // device-counted batch (null: n_ops)
-  const uint32_t* op_slot;
-  const uint8_t* op_kind;    // null: all moves
-  const uint32_t* space_of;
-  const float* pos_x;
-  const float* pos_z;
-  const float* old_x;
-  const float* old_z;
-  const uint32_t* old_seq;
-  const uint32_t* opq;
-  uint32_t gen;
-  const uint32_t* ov_tag;
-  const Rec* ov_rec;
-  const uint32_t* ov_count;
-  uint4* ev_tmp;             // shared region (slots from ctr[CTR_EVENTS], reserved per wave)
-  uint32_t ev_cap;
-  uint32_t* rank_cnt;
-  uint32_t* ctr;
-};
-void launch_sweep_small(const SmallArgs& a, hipStream_t st);
+
 
 struct BinArgs {
   const float* pos_x;
@@ -238,7 +218,9 @@ struct SweepArgs {
   uint4* band_items;    // {tile, first mover, movers, 0}
   uint32_t band_items_cap;
   uint32_t band_hint;   // items of the previous pass (0: k_sweep_chunked not launched)
-  uint32_t chunk_max_recs;  // tiles holding more records take the dense walk instead (hotspot crowds)
+  uint32_t chunk_min_recs;  // over-budget tiles with records in [min, max] and halo <= chunk_max_pad cells
+  uint32_t chunk_max_recs;  // take k_sweep_chunked; the others the dense walk
+  uint32_t chunk_max_pad;
   uint32_t chunk_grid;  // its blocks (one per CU)
   const uint32_t* tile_walk;  // per tile: holds a reported mover (null: k_sweep scans the tile's records)
 };
@@ -362,9 +344,50 @@ struct OrderArgs {
                              // the last of which publishes (else one thread per op, then k_publish)
   uint32_t place_blocks;     // k_place's grid (0: 1024)
 };
+// Small pass: the movers of a pass with few ops judged against the last full build's grid (records of
+// slots without an op since then; their state is the record's end state) plus the overlay (every slot
+// with an op since then, one record each), without rebuilding the grid (k_sweep_small).
+struct SmallArgs {
+  GridView g;                // the grid of the last full build
+  uint32_t base, n_ops;
+  const uint32_t* n_dev;     // device-counted batch (null: n_ops)
+  const uint32_t* op_slot;
+  const uint8_t* op_kind;    // null: all moves
+  const uint32_t* space_of;
+  const float* pos_x;
+  const float* pos_z;
+  const float* old_x;
+  const float* old_z;
+  const uint32_t* old_seq;
+  const uint32_t* opq;
+  uint32_t gen;
+  const uint32_t* ov_tag;
+  const Rec* ov_rec;
+  const uint32_t* ov_count;
+  uint4* ev_tmp;             // shared region (slots from ctr[CTR_EVENTS], reserved per wave)
+  uint32_t ev_cap;
+  uint32_t* rank_cnt;
+  uint32_t* ctr;
+  // one_op: a pass of ONE host op (the Go wrapper's flushed Enter or Leave) runs as one kernel: the op
+  // applied (ap; no k_apply launch), swept, and its slice ordered and published (od) from LDS. A slice
+  // over the kernel's LDS, or over the event buffers, leaves the order stage to the host as
+  // k_order_small's overflow does (ctr[CTR_SMALL_OVF] / the buffer re-run); a re-run of the sweep is a
+  // plain k_sweep_small (the op is applied once).
+  int one_op;
+  ApplyArgs ap;
+  OrderArgs od;
+};
+void launch_sweep_small(const SmallArgs& a, hipStream_t st);
 // k_place (+ zeroing side jobs, duplicate-slot check) -> k_slice_sort (+ batch check, publication of
 // the counters by its last block when o.pub) -> k_copy_out (if host_out)
 void launch_order(const OrderArgs& o, hipStream_t st);
+// The order stage of a small pass in one single-block kernel (scan of the per-op counts, placement and
+// slice sort in LDS, publication): when the pass has at most kOrderSmallOps ops. A pass whose events
+// exceed the kernel's LDS sets ctr[CTR_SMALL_OVF] (published); the host then runs launch_order on the
+// scanned counts.
+constexpr uint32_t kOrderSmallOps = 1024;
+void launch_order_small(const OrderArgs& o, hipStream_t st);
+void launch_copy_out(const OrderArgs& o, hipStream_t st);  // k_copy_out alone (host event delivery)
 void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_t st);
 void launch_relation(const RelArgs& a, hipStream_t st);
 // Rows of cols (filled by the fill pass) sorted in place.

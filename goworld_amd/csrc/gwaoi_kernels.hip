@@ -94,7 +94,12 @@ __global__ void __launch_bounds__(kBlock) k_apply(ApplyArgs a) {
   bool ok = live;
   if (live) {
     s = a.op_slot[i];
-    kind = a.op_kind ? (uint8_t)(a.op_kind[i] & OP_KIND) : (uint8_t)OP_MOVE;
+    const uint8_t raw = a.op_kind ? a.op_kind[i] : (uint8_t)OP_MOVE;
+    kind = (uint8_t)(raw & OP_KIND);
+    if (a.cp_slot) {  // host ops read over PCIe: device copies for the kernels after this one
+      a.cp_slot[i] = s;
+      a.cp_kind[i] = raw;
+    }
     if (a.check && s >= a.cap) {
       atomicOr(&a.ctr[CTR_ERR], ERR_BAD_SLOT);
       ok = false;
@@ -1779,8 +1784,9 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     GW_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
                     ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32));
   }
-  if (!lds && a.band_mv && g.pad > 0 &&
-      a.g.cs[(t + 1) << kTileCellShift] - a.g.cs[t << kTileCellShift] <= a.chunk_max_recs) {
+  const uint32_t trecs = a.g.cs[(t + 1) << kTileCellShift] - a.g.cs[t << kTileCellShift];
+  if (!lds && a.band_mv && g.pad > 0 && g.pad <= a.chunk_max_pad && trecs >= a.chunk_min_recs &&
+      trecs <= a.chunk_max_recs) {
     // region over the LDS budget (crowds, large D): the tile's movers (grid indices, in grid order) to
     // k_sweep_chunked, in items of up to kChunkBlock; one atomic per block on each list's counter (the
     // lists are sized so that every pass's movers fit)
@@ -2531,103 +2537,256 @@ __device__ __forceinline__ int judge_small(const Judge& J, uint32_t base, uint32
   return judge(J, ra, rb);
 }
 
-__global__ void __launch_bounds__(kBlock) k_sweep_small(SmallArgs a) {
+// kW waves per op: a block of max(kBlock, 64 kW) threads takes kBlock / 64 ops (kW = 1) or one op (kW > 1);
+// with kW > 1 the op's grid rows and overlay entries are dealt round-robin over its waves, and the
+// mover's event numbering is an LDS counter the waves share (a pass of a single Enter: 16 waves walk its
+// box and a 16k-entry overlay together, instead of one wave's 256 dependent loads).
+// kOne (a pass of one host op, SmallArgs.one_op): thread 0 first applies the op (k_apply's work: no
+// separate launch), the mover's state goes through LDS, the events are also kept in LDS, and after the
+// walk the block orders the slice (rank by key) into ev_out and publishes the counters: one launch for
+// the whole pass.
+constexpr uint32_t kOneEv = 4096;  // kOne: events of the op kept in LDS
+struct OneSmem {
+  uint2 lev[kOneEv];
+  uint32_t st[8];  // slot, raw kind, seq before, space, x0, z0, x1, z1 (float bits)
+};
+template <int kW, bool kOne>
+__global__ void __launch_bounds__(kW == 1 ? kBlock : 64 * kW) k_sweep_small(SmallArgs a) {
+  constexpr int kThreads = kW == 1 ? kBlock : 64 * kW;
+  static_assert(!kOne || kW > 1, "one op per block");
+  __shared__ uint32_t sloc;  // kW > 1: the op's events numbered so far
+  __shared__ __attribute__((aligned(16))) uint32_t one_raw[kOne ? sizeof(OneSmem) / 4 : 1];
+  OneSmem* one = reinterpret_cast<OneSmem*>(one_raw);  // (kOne only)
   const int lane = threadIdx.x & 63;
-  const uint32_t i = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);  // the wave's op
+  const int wv = threadIdx.x >> 6;
+  const uint32_t i = kW == 1 ? blockIdx.x * (kThreads / 64) + wv : blockIdx.x;  // the wave's op
+  const int sub = kW == 1 ? 0 : wv;  // the wave's share of the op's work
   const uint32_t n = a.n_dev ? min(*a.n_dev, a.n_ops) : a.n_ops;
-  if (i >= n) return;  // wave-uniform
-  const uint8_t kind = a.op_kind ? a.op_kind[i] : (uint8_t)OP_MOVE;
-  if (kind & OP_SILENT) return;
-  const uint32_t s = a.op_slot[i];
-  if (a.opq[s] != a.base + i) return;  // (a failed op: the batch is refused anyway)
-  const uint32_t sp = __builtin_amdgcn_readfirstlane(a.space_of[s]);
-  const Geom g = uniform_geom(&a.g.geom[sp]);
-  Mover m;
-  m.slot = s;
-  m.q = a.base + i;
-  m.q0 = a.old_seq[s];
-  m.rank = i;
-  m.valid0 = m.q0 != 0;
-  m.valid1 = (kind & OP_KIND) != OP_LEAVE;
-  m.mx0 = a.old_x[s];
-  m.mz0 = a.old_z[s];
-  m.mx1 = m.valid1 ? a.pos_x[s] : m.mx0;
-  m.mz1 = m.valid1 ? a.pos_z[s] : m.mz0;
-  m.D = g.D;
-  const Judge J = make_judge(m, a.base);
-  const Walk w = make_walk(m, g);
-  const unsigned long long below = (1ull << lane) - 1ull;
-  uint32_t local = 0, nent = 0, cur = 0, left = 0;  // (wave-uniform but local/cur/left)
-  auto emit_round = [&](int ev, uint32_t other) {
-    const unsigned long long em = __ballot(ev != 0);
-    if (!em) return;
-    const uint32_t cnt = (uint32_t)__popcll(em), pre = (uint32_t)__popcll(em & below);
-    uint32_t gi = cur + pre;
-    if (cnt > left) {  // this reservation fills up: the rest goes to a fresh one
-      uint32_t nb = 0;
-      if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
-      nb = __shfl(nb, 0, 64);
-      if (pre >= left) gi = nb + (pre - left);
-      cur = nb + (cnt - left);
-      left = kEvChunk - (cnt - left);
-    } else {
-      cur += cnt;
-      left -= cnt;
+  if (kW > 1 && threadIdx.x == 0) sloc = 0;
+  if (kOne && threadIdx.x == 0) {  // k_apply for the op (host-staged: validated on the host)
+    const ApplyArgs& p = a.ap;
+    // the op over PCIe, all four loads in flight; then the slot's state, all loads in flight
+    const uint32_t s = p.op_slot[0];
+    const uint8_t raw = p.op_kind[0], kind = raw & OP_KIND;
+    const float ox = p.op_x[0], oz = p.op_z[0];
+    const uint32_t osp = p.op_space ? p.op_space[0] : 0u;
+    const uint32_t q = p.base, q0 = p.seq[s], sp0 = p.space_of[s], tag = p.ov_tag[s], oidx = p.ov_idx[s];
+    const float x0 = p.pos_x[s], z0 = p.pos_z[s];
+    p.cp_slot[0] = s;  // (a re-run of the sweep reads the op from the device copies)
+    p.cp_kind[0] = raw;
+    p.ctr[CTR_NOPS] = 1u;
+    p.rank_cnt[0] = 0u;
+    p.rank_cnt[1] = 0u;
+    p.old_x[s] = x0;
+    p.old_z[s] = z0;
+    p.old_seq[s] = q0;
+    p.opq[s] = q;
+    const bool leave = kind == OP_LEAVE;
+    const float x1 = leave ? x0 : ox, z1 = leave ? z0 : oz;
+    const uint32_t sp = kind == OP_ENTER ? osp : sp0;
+    p.seq[s] = leave ? 0u : q;
+    if (!leave) {
+      p.pos_x[s] = x1;
+      p.pos_z[s] = z1;
     }
-    if (ev) {
-      if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
-      nent += ev == 2 ? 1u : 0u;
+    if (kind == OP_ENTER) p.space_of[s] = sp;
+    // overlay_put with the slot's tag already loaded
+    uint32_t e = oidx;
+    if (tag != p.gen) {
+      e = atomicAdd(p.ov_count, 1u);
+      p.ov_tag[s] = p.gen;
+      p.ov_idx[s] = e;
     }
-    local += cnt;
-  };
-  auto cand = [&](uint32_t j, bool on) {  // grid record j (on: a candidate of this lane)
-    int ev = 0;
-    uint32_t o = 0;
-    if (on) {
-      const uint4 ra = a.g.rec[j].a;
-      o = ra.z & REC_SLOT;
-      if (a.ov_tag[o] != a.gen) ev = judge_small(J, a.base, a.n_ops, ra, a.g.rec[j].b);
+    if (e < p.ov_cap) {
+      const uint4 ra = make_uint4(__float_as_uint(leave ? x0 : x1), __float_as_uint(leave ? z0 : z1),
+                                  s | (leave ? REC_GHOST : 0u), q);
+      const uint4 rb = make_uint4(__float_as_uint(q0 ? x0 : x1), __float_as_uint(q0 ? z0 : z1), q0, leave ? 0u : q);
+      p.ov_rec[e] = Rec{ra, rb};
     }
-    emit_round(ev, o);
-  };
-  // the grid: the walk's rows, each row segment's records 64 at a time across the lanes
-  for (int r = w.z0; r <= w.z1; ++r) {
-    int a0, a1, b0, b1;
-    walk_row(w, r, a0, a1, b0, b1);
-    auto seg = [&](int c0, int c1) {
-      row_entries_ranges(g, a.g.cs, r, c0, c1, [&](uint32_t jb, uint32_t je) {
-        for (uint32_t j = jb; j < je; j += 64) cand(j + lane, j + lane < je);
-      });
+    one[0].st[0] = s, one[0].st[1] = raw, one[0].st[2] = q0, one[0].st[3] = sp;
+    one[0].st[4] = __float_as_uint(x0), one[0].st[5] = __float_as_uint(z0);
+    one[0].st[6] = __float_as_uint(x1), one[0].st[7] = __float_as_uint(z1);
+  }
+  if (kW > 1) __syncthreads();
+  bool run = i < n;  // wave-uniform (kW > 1: block-uniform)
+  uint8_t kind = 0;
+  uint32_t s = 0;
+  if (kOne) {
+    kind = (uint8_t)one[0].st[1];
+    s = one[0].st[0];
+  } else if (run) {
+    kind = a.op_kind ? a.op_kind[i] : (uint8_t)OP_MOVE;
+    s = a.op_slot[i];
+    run = a.opq[s] == a.base + i;  // (a failed op: the batch is refused anyway)
+  }
+  run = run && !(kind & OP_SILENT);
+  if (!kOne && !run) return;
+  uint32_t local = 0, nent = 0, cur = 0, left = 0;  // (wave-uniform but nent)
+  if (run) {
+    const uint32_t sp = __builtin_amdgcn_readfirstlane(kOne ? one[0].st[3] : a.space_of[s]);
+    const Geom g = uniform_geom(&a.g.geom[sp]);
+    Mover m;
+    m.slot = s;
+    m.q = a.base + i;
+    m.q0 = kOne ? one[0].st[2] : a.old_seq[s];
+    m.rank = i;
+    m.valid0 = m.q0 != 0;
+    m.valid1 = (kind & OP_KIND) != OP_LEAVE;
+    m.mx0 = kOne ? __uint_as_float(one[0].st[4]) : a.old_x[s];
+    m.mz0 = kOne ? __uint_as_float(one[0].st[5]) : a.old_z[s];
+    m.mx1 = !m.valid1 ? m.mx0 : kOne ? __uint_as_float(one[0].st[6]) : a.pos_x[s];
+    m.mz1 = !m.valid1 ? m.mz0 : kOne ? __uint_as_float(one[0].st[7]) : a.pos_z[s];
+    m.D = g.D;
+    const Judge J = make_judge(m, a.base);
+    const Walk w = make_walk(m, g);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    auto emit_round = [&](int ev, uint32_t other) {
+      const unsigned long long em = __ballot(ev != 0);
+      if (!em) return;
+      const uint32_t cnt = (uint32_t)__popcll(em), pre = (uint32_t)__popcll(em & below);
+      uint32_t lb = local;  // this round's first local index
+      if (kW > 1) {
+        if (lane == 0) lb = atomicAdd(&sloc, cnt);  // LDS atomic
+        lb = __shfl(lb, 0, 64);
+      }
+      uint32_t gi = cur + pre;
+      if (cnt > left) {  // this reservation fills up: the rest goes to a fresh one
+        uint32_t nb = 0;
+        if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
+        nb = __shfl(nb, 0, 64);
+        if (pre >= left) gi = nb + (pre - left);
+        cur = nb + (cnt - left);
+        left = kEvChunk - (cnt - left);
+      } else {
+        cur += cnt;
+        left -= cnt;
+      }
+      if (ev) {
+        const uint32_t ow = other | (ev == 2 ? 0x80000000u : 0u);
+        if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, lb + pre, m.slot, ow);
+        if (kOne && lb + pre < kOneEv) one[0].lev[lb + pre] = make_uint2(m.slot, ow);
+        nent += ev == 2 ? 1u : 0u;
+      }
+      local += cnt;
     };
-    seg(a0, a1);
-    seg(b0, b1);
-  }
-  // the overlay
-  const uint32_t nov = *a.ov_count;
-  for (uint32_t e = 0; e < nov; e += 64) {
-    int ev = 0;
-    uint32_t o = 0;
-    if (e + lane < nov) {
-      const Rec r = a.ov_rec[e + lane];
-      o = r.a.z & REC_SLOT;
-      ev = judge_small(J, a.base, a.n_ops, r.a, r.b);
+    // (o == the mover: never an event; in kOne its overlay tag and entry were written by this block)
+    auto cand = [&](uint32_t j, bool on) {  // grid record j (on: a candidate of this lane)
+      int ev = 0;
+      uint32_t o = 0;
+      if (on) {
+        const uint4 ra = a.g.rec[j].a;
+        o = ra.z & REC_SLOT;
+        if (o != s && a.ov_tag[o] != a.gen) ev = judge_small(J, a.base, a.n_ops, ra, a.g.rec[j].b);
+      }
+      emit_round(ev, o);
+    };
+    // the grid: the walk's rows (this wave's share), each row segment's records 64 at a time across the lanes
+    for (int r = w.z0 + sub; r <= w.z1; r += kW) {
+      int a0, a1, b0, b1;
+      walk_row(w, r, a0, a1, b0, b1);
+      auto seg = [&](int c0, int c1) {
+        row_entries_ranges(g, a.g.cs, r, c0, c1, [&](uint32_t jb, uint32_t je) {
+          for (uint32_t j = jb; j < je; j += 64) cand(j + lane, j + lane < je);
+        });
+      };
+      seg(a0, a1);
+      seg(b0, b1);
     }
-    emit_round(ev, o);
+    // the overlay (this wave's share), four entries per lane in flight
+    const uint32_t nov = __hip_atomic_load(a.ov_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    constexpr uint32_t kStride = 64u * kW;
+    for (uint32_t e0 = 64u * sub; e0 < nov; e0 += 4u * kStride) {
+      Rec r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t e = e0 + k * kStride + lane;
+        if (e < nov) r[k] = a.ov_rec[e];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t e = e0 + k * kStride + lane;
+        int ev = 0;
+        uint32_t o = 0;
+        if (e < nov) {
+          o = r[k].a.z & REC_SLOT;
+          if (o != s) ev = judge_small(J, a.base, a.n_ops, r[k].a, r[k].b);
+        }
+        emit_round(ev, o);
+      }
+    }
+    for (uint32_t k = lane; k < left; k += 64)
+      if (cur + k < a.ev_cap) a.ev_tmp[cur + k] = make_uint4(kEvHole, 0u, 0u, 0u);
+    if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
+    const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);
+    if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
   }
-  if (lane == 0) {
-    put_count(a.rank_cnt, m.rank, local);
-    if (local > 1u) a.ctr[CTR_UNSORTED] = 1u;
+  if (kW == 1) {
+    if (lane == 0) {
+      put_count(a.rank_cnt, i, local);
+      if (local > 1u) a.ctr[CTR_UNSORTED] = 1u;
+    }
+    return;
   }
-  for (uint32_t k = lane; k < left; k += 64)
-    if (cur + k < a.ev_cap) a.ev_tmp[cur + k] = make_uint4(kEvHole, 0u, 0u, 0u);
-  if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
-  const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);
-  if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
+  __syncthreads();  // every wave's events numbered
+  const uint32_t nev = sloc;
+  if (!kOne) {
+    if (threadIdx.x == 0) {
+      put_count(a.rank_cnt, i, nev);
+      if (nev > 1u) a.ctr[CTR_UNSORTED] = 1u;
+    }
+    return;
+  }
+  // kOne: the order stage of the pass (k_order_small's work for one op, the slice in LDS)
+  const OrderArgs& o = a.od;
+  uint32_t* ctr = a.ctr;
+  const uint32_t slots = __hip_atomic_load(&ctr[CTR_EVENTS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool fits = slots <= o.g.tmp_cap && o.g.keep + nev <= o.g.out_cap;
+  if (threadIdx.x == 0) {
+    ctr[CTR_NEV] = nev;  // (also on overflow: the host sizes ev_out by it)
+    a.rank_cnt[1] = nev;  // the scanned form: [0, nev)
+    if (nev > 1u) ctr[CTR_UNSORTED] = 1u;
+  }
+  if (fits) {
+    if (threadIdx.x < CTR_N) o.ctr_next[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) ctr[CTR_RECORDS] = *o.grid_total;
+    if (nev > kOneEv) {
+      if (threadIdx.x == 0) ctr[CTR_SMALL_OVF] = 1u;  // the host orders from ev_tmp
+    } else {
+      for (uint32_t e = threadIdx.x; e < nev; e += kThreads) {
+        const uint2 v = one[0].lev[e];
+        uint32_t pos = 0;
+        for (uint32_t k = 0; k < nev; ++k) {
+          const uint32_t kk = one[0].lev[k].y;
+          pos += (kk < v.y || (kk == v.y && k < e)) ? 1u : 0u;
+        }
+        o.ev_out[pos] = v;
+      }
+    }
+  }
+  if (!o.pub) return;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x < (uint32_t)kPubWords) {
+    __hip_atomic_store(&o.pub[threadIdx.x], atomicAdd(&ctr[threadIdx.x], 0u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&o.pub[kPubWords], o.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+constexpr uint32_t kSmallWideOps = 64;  // passes of at most this many ops: 16 waves per op
 void launch_sweep_small(const SmallArgs& a, hipStream_t st) {
-  if (a.n_ops)
-    hipLaunchKernelGGL(k_sweep_small, dim3((a.n_ops + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0, st, a);
+  if (!a.n_ops) return;
+  if (a.one_op)
+    hipLaunchKernelGGL((k_sweep_small<16, true>), dim3(1), dim3(1024), 0, st, a);
+  else if (a.n_ops <= kSmallWideOps)
+    hipLaunchKernelGGL((k_sweep_small<16, false>), dim3(a.n_ops), dim3(1024), 0, st, a);
+  else if (a.n_ops <= kOrderSmallOps)
+    hipLaunchKernelGGL((k_sweep_small<4, false>), dim3(a.n_ops), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_sweep_small<1, false>), dim3((a.n_ops + kBlock / 64 - 1) / (kBlock / 64)), dim3(kBlock), 0,
+                       st, a);
 }
 
 uint32_t sweep_ev_lds() { return kEvLds; }
@@ -2922,6 +3081,101 @@ void launch_order(const OrderArgs& o, hipStream_t st) {
                      st, o);
   if (o.host_out) hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, o);
   if (o.pub && !o.sorted_hint) launch_publish(o.g.ctr, o.pub, o.pub_seq, st);
+}
+
+// The order stage of a small pass (at most kOrderSmallOps ops) as one block: the per-op counts scanned
+// in LDS (and written back, as launch_scan leaves them), the events placed into LDS by op rank, each
+// op's slice ordered by rank (an event's position = the events of its slice ordered before it: key,
+// then index), written out once, the counters published. Replaces scan + k_place + k_slice_sort (+
+// k_publish): four dependent launches of a pass whose work is a few hundred events. The side jobs of
+// k_place ride along (next pass's counter block, CTR_NEV, CTR_RECORDS); the batch check of k_slice_sort
+// too. A pass with more events than the LDS holds sets CTR_SMALL_OVF and places nothing.
+constexpr int kOrdThreads = 1024;
+constexpr uint32_t kOrdSmallEv = 4096;
+static_assert(kOrderSmallOps <= (uint32_t)kOrdThreads, "one op per thread in the scan");
+__global__ void __launch_bounds__(kOrdThreads) k_order_small(OrderArgs o) {
+  __shared__ uint2 lev[kOrdSmallEv];            // placed events
+  __shared__ uint32_t off[kOrderSmallOps + 1];  // scanned counts
+  __shared__ uint32_t ws[kOrdThreads / 64];
+  const uint32_t t = threadIdx.x;
+  uint32_t* ctr = const_cast<uint32_t*>(o.g.ctr);
+  uint32_t* rank = const_cast<uint32_t*>(o.rank_off);  // counts on entry, offsets on exit
+  const uint32_t nops = o.n_ops;
+  // scan (one op per thread)
+  const uint32_t c = t < nops ? rank[t] : 0u;
+  const uint32_t inc = wave_incl_scan(c);
+  if ((t & 63) == 63) ws[t >> 6] = inc;
+  __syncthreads();
+  uint32_t pre = inc - c, n = 0;
+#pragma unroll
+  for (int k = 0; k < kOrdThreads / 64; ++k) {
+    pre += k < (int)(t >> 6) ? ws[k] : 0u;
+    n += ws[k];
+  }
+  if (t < nops) off[t] = pre, rank[t] = pre;
+  if (t == 0) off[nops] = n, rank[nops] = n;
+  const uint32_t slots = ctr[CTR_EVENTS];
+  const bool fits = slots <= o.g.tmp_cap && o.g.keep + n <= o.g.out_cap;
+  __syncthreads();
+  if (t == 0) ctr[CTR_NEV] = n;  // (also on overflow: the host sizes ev_out by it)
+  if (fits) {
+    if (t < CTR_N) o.ctr_next[t] = 0u;
+    if (t == 0) ctr[CTR_RECORDS] = *o.grid_total;
+    if (o.check_ops) {
+      const uint32_t nr = o.n_dev ? min(*o.n_dev, nops) : nops;
+      if (t < nr) {
+        const uint32_t s = o.op_slot[t];
+        if (s < o.cap && o.opq[s] != o.base + t) atomicOr(&ctr[CTR_ERR], ERR_DUP_SLOT);
+      }
+    }
+    if (n > kOrdSmallEv) {
+      if (t == 0) ctr[CTR_SMALL_OVF] = 1u;
+    } else {
+      for (uint32_t i = t; i < slots; i += kOrdThreads) {
+        const uint4 e = o.ev_tmp[i];
+        if (e.x != kEvHole) lev[off[e.x] + e.y] = make_uint2(e.z, e.w);
+      }
+      __syncthreads();
+      const bool sort = ctr[CTR_UNSORTED] != 0u;  // (written by the sweep kernel before this one)
+      for (uint32_t i = t; i < n; i += kOrdThreads) {
+        const uint2 v = lev[i];
+        uint32_t pos = i;
+        if (sort) {
+          uint32_t lo = 0, hi = nops;  // the op whose slice holds event i: off[r] <= i < off[r + 1]
+          while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (off[mid] <= i) lo = mid;
+            else hi = mid;
+          }
+          const uint32_t b = off[lo], e = off[lo + 1];
+          pos = b;
+          for (uint32_t j = b; j < e; ++j) {
+            const uint32_t kj = lev[j].y;
+            pos += (kj < v.y || (kj == v.y && j < i)) ? 1u : 0u;
+          }
+        }
+        o.ev_out[pos] = v;
+      }
+    }
+  }
+  if (!o.pub) return;
+  __threadfence();  // this kernel's counter stores (CTR_NEV, CTR_RECORDS, ...) reach L2 before they are read
+  __syncthreads();
+  if (t < (uint32_t)kPubWords) {  // one counter per lane (atomics: where the sweep's atomics meet)
+    __hip_atomic_store(&o.pub[t], atomicAdd(&ctr[t], 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(&o.pub[kPubWords], o.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_copy_out(const OrderArgs& o, hipStream_t st) {
+  if (o.host_out) hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, o);
+}
+
+void launch_order_small(const OrderArgs& o, hipStream_t st) {
+  hipLaunchKernelGGL(k_order_small, dim3(1), dim3(kOrdThreads), 0, st, o);
+  if (o.host_out) hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, o);
 }
 
 // End-of-pass publication (when k_slice_sort does not publish): the counters the host reads, then a

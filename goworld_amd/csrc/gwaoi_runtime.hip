@@ -102,6 +102,15 @@ struct Grid {  // one pass's cell-sorted records (two buffers, alternating betwe
 
 }  // namespace
 
+#ifndef GW_CHUNK_MIN_RECS
+#define GW_CHUNK_MIN_RECS 0u
+#endif
+#ifndef GW_CHUNK_MAX_RECS
+#define GW_CHUNK_MAX_RECS 0u  // off by default: slower than the dense walk on skew and skew50 (r04_c3)
+#endif
+#ifndef GW_CHUNK_MAX_PAD
+#define GW_CHUNK_MAX_PAD 32u
+#endif
 struct gwaoi_mgr {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -130,6 +139,13 @@ struct gwaoi_mgr {
   uint8_t* h_op_kind = nullptr;
   uint32_t* h_op_space = nullptr;
   uint32_t* h_leaves = nullptr;
+  // device addresses of the pinned op arrays (small passes read them over PCIe instead of copying them);
+  // null when the runtime gives none
+  const uint32_t* hd_op_slot = nullptr;
+  const float* hd_op_x = nullptr;
+  const float* hd_op_z = nullptr;
+  const uint8_t* hd_op_kind = nullptr;
+  const uint32_t* hd_op_space = nullptr;
   uint32_t n_ops = 0, n_leaves = 0;
   bool geom_dirty = true;
   // device-staged batch
@@ -189,6 +205,9 @@ struct gwaoi_mgr {
   uint32_t* tile_acted = nullptr;  // per tile: slots of the pass's ops (k_bin_tsort; duplicate-slot check)
   bool rerun_counting = false;   // the previous pass re-ran its build: this one uses the counting build
   bool chunked = true;           // crowded tiles take k_sweep_chunked (gwaoi_debug_set_sweep_lds(3): off)
+  // which over-budget tiles k_sweep_chunked takes (gwaoi_debug_set_chunked): records in [min, max], halo
+  // at most max_pad cells; the rest walk from L2 (k_sweep_dense)
+  uint32_t chunk_min_recs = GW_CHUNK_MIN_RECS, chunk_max_recs = GW_CHUNK_MAX_RECS, chunk_max_pad = GW_CHUNK_MAX_PAD;
   uint32_t* tile_ev = nullptr;   // per tile: events k_sweep queued in the tile's region of ev_tmp
   uint32_t* tile_ent = nullptr;  // per tile: their enter events
   uint32_t nblk = 0;
@@ -665,7 +684,10 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
   hipStream_t st = m->stream;
   RCHK(collect_timing(m));
   if (m->timing) HIPCHK(hipEventRecord(m->tev[0], st));
-  if (!dev) {
+  // host ops: k_apply reads them from the pinned arrays over PCIe (five DMA copies cost more than the
+  // whole small pass's kernels) and leaves device copies of slot and kind for the sweep
+  const bool mapped = !dev && m->hd_op_slot;
+  if (!dev && !mapped) {
     HIPCHK(hipMemcpyAsync(m->d_op_slot, m->h_op_slot, n_ops * sizeof(uint32_t), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(m->d_op_x, m->h_op_x, n_ops * sizeof(float), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(m->d_op_z, m->h_op_z, n_ops * sizeof(float), hipMemcpyHostToDevice, st));
@@ -674,11 +696,13 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
   }
   gw::ApplyArgs a{};
   a.n_dev = dev ? m->dv_count : nullptr;
-  a.op_slot = dev ? m->dv_slot : m->d_op_slot;
-  a.op_x = dev ? m->dv_x : m->d_op_x;
-  a.op_z = dev ? m->dv_z : m->d_op_z;
-  a.op_kind = dev ? m->dv_kind : m->d_op_kind;
-  a.op_space = dev ? m->dv_space : m->d_op_space;
+  a.op_slot = dev ? m->dv_slot : mapped ? m->hd_op_slot : m->d_op_slot;
+  a.op_x = dev ? m->dv_x : mapped ? m->hd_op_x : m->d_op_x;
+  a.op_z = dev ? m->dv_z : mapped ? m->hd_op_z : m->d_op_z;
+  a.op_kind = dev ? m->dv_kind : mapped ? m->hd_op_kind : m->d_op_kind;
+  a.op_space = dev ? m->dv_space : mapped ? m->hd_op_space : m->d_op_space;
+  a.cp_slot = mapped ? m->d_op_slot : nullptr;
+  a.cp_kind = mapped ? m->d_op_kind : nullptr;
   a.nspaces = m->nspaces;
   a.leaves = dev_mixed ? m->d_leaves : nullptr;  // (the presence delta of a mixed batch is counted with it)
   a.n_ops = n_ops;
@@ -701,7 +725,9 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
   a.ov_rec = m->ov_rec;
   a.ov_count = m->ov_count;
   a.ov_cap = m->ov_cap;
-  gw::launch_apply(a, st);
+  // a single host op (the Go wrapper's flushed Enter / Leave): applied, swept and ordered by one kernel
+  const bool one_op = mapped && n_ops == 1;
+  if (!one_op) gw::launch_apply(a, st);
   HIPCHK(hipGetLastError());
   if (m->timing) HIPCHK(hipEventRecord(m->tev[1], st));
   if (m->timing) HIPCHK(hipEventRecord(m->tev[2], st));
@@ -714,36 +740,12 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_DENSE, 0, 2 * sizeof(uint32_t), st));  // + CTR_HOLES
-      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 3 * sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 4 * sizeof(uint32_t), st));  // .. CTR_SMALL_OVF
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, 2 * sizeof(uint32_t), st));
     }
-    gw::SmallArgs sa{};
-    sa.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
-    sa.base = base;
-    sa.n_ops = n_ops;
-    sa.n_dev = a.n_dev;
-    sa.op_slot = a.op_slot;
-    sa.op_kind = a.op_kind;
-    sa.space_of = m->space_of;
-    sa.pos_x = m->pos_x;
-    sa.pos_z = m->pos_z;
-    sa.old_x = m->old_x;
-    sa.old_z = m->old_z;
-    sa.old_seq = m->old_seq;
-    sa.opq = m->opq;
-    sa.gen = m->grid_gen;
-    sa.ov_tag = m->ov_tag;
-    sa.ov_rec = m->ov_rec;
-    sa.ov_count = m->ov_count;
-    sa.ev_tmp = m->ev_tmp;
-    sa.ev_cap = m->tmp_cap;
-    sa.rank_cnt = m->rank_cnt;
-    sa.ctr = m->ctr;
-    gw::launch_sweep_small(sa, st);
-    HIPCHK(hipGetLastError());
-    if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
     if (copy_events) RCHK(ensure_host_events(m, m->ev_cap, keep));
-    gw::launch_scan(m->scan, m->rank_cnt, n_ops + 1, st);
+    const bool one = one_op && attempt == 0;  // (a re-run sweeps the op applied by the first attempt)
+    const bool fused = n_ops <= gw::kOrderSmallOps;  // one-block order stage (k_order_small)
     gw::OrderArgs o{};
     o.g = {m->ctr, m->tmp_cap, keep, m->ev_cap};
     o.ev_tmp = m->ev_tmp;
@@ -760,7 +762,7 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
     o.zero_n = 0;
     o.ctr_next = m->ctr_buf + (m->ctr_sel ^ 1) * gw::CTR_N;
     o.grid_total = G.cs + G.ncells;
-    o.op_slot = a.op_slot;
+    o.op_slot = mapped ? m->d_op_slot : a.op_slot;
     o.opq = m->opq;
     o.base = base;
     o.cap = m->cap;
@@ -772,10 +774,57 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
     o.pub = o.pub_seq ? m->d_pub : nullptr;
     o.sorted_hint = !o.check_ops ? 1 : 0;  // few blocks: a small pass sorts few slices
     o.place_blocks = 16;
-    gw::launch_order(o, st);
+    gw::SmallArgs sa{};
+    sa.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
+    sa.base = base;
+    sa.n_ops = n_ops;
+    sa.n_dev = a.n_dev;
+    sa.op_slot = mapped ? m->d_op_slot : a.op_slot;
+    sa.op_kind = mapped ? m->d_op_kind : a.op_kind;
+    sa.space_of = m->space_of;
+    sa.pos_x = m->pos_x;
+    sa.pos_z = m->pos_z;
+    sa.old_x = m->old_x;
+    sa.old_z = m->old_z;
+    sa.old_seq = m->old_seq;
+    sa.opq = m->opq;
+    sa.gen = m->grid_gen;
+    sa.ov_tag = m->ov_tag;
+    sa.ov_rec = m->ov_rec;
+    sa.ov_count = m->ov_count;
+    sa.ev_tmp = m->ev_tmp;
+    sa.ev_cap = m->tmp_cap;
+    sa.rank_cnt = m->rank_cnt;
+    sa.ctr = m->ctr;
+    sa.one_op = one ? 1 : 0;
+    sa.ap = a;
+    sa.od = o;
+    gw::launch_sweep_small(sa, st);
+    HIPCHK(hipGetLastError());
+    if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
+    if (one) {
+      gw::launch_copy_out(o, st);
+    } else {
+      if (!fused) gw::launch_scan(m->scan, m->rank_cnt, n_ops + 1, st);
+      if (fused)
+        gw::launch_order_small(o, st);
+      else
+        gw::launch_order(o, st);
+    }
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
     RCHK(finish_pass(m, o.pub_seq));
+    if ((fused || one) && m->h_ctr[gw::CTR_SMALL_OVF] && !m->h_ctr[gw::CTR_ERR]) {
+      // more events than k_order_small's LDS: the general kernels, on the counts it scanned
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SMALL_OVF, 0, sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, sizeof(uint32_t), st));
+      o.pub_seq = publish_seq(m, copy_events);
+      o.pub = o.pub_seq ? m->d_pub : nullptr;
+      gw::launch_order(o, st);
+      HIPCHK(hipGetLastError());
+      if (m->timing) HIPCHK(hipEventRecord(m->tev[4], st));
+      RCHK(finish_pass(m, o.pub_seq));
+    }
     if (m->h_ctr[gw::CTR_ERR]) {
       m->broken = true;
       set_err("device-staged batch failed validation (flags 0x%x: 1=duplicate slot, 2=absent slot, 4=slot >= "
@@ -981,11 +1030,10 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.band_items = m->chunked ? m->band_items : nullptr;
     s.band_items_cap = m->band_items_cap;
     s.band_hint = force_band ? ~0u : m->last_band;
-#ifndef GW_CHUNK_MAX_RECS  // tiles over this many records (hotspot crowds) keep the wave-per-mover walk:
-#define GW_CHUNK_MAX_RECS 2048  // chunked, skew50 swept in 14.0 ms instead of 5.75 (r04_b2)
-#endif
     s.chunk_grid = m->chunk_grid;
-    s.chunk_max_recs = GW_CHUNK_MAX_RECS;
+    s.chunk_min_recs = m->chunk_min_recs;
+    s.chunk_max_recs = m->chunk_max_recs;
+    s.chunk_max_pad = m->chunk_max_pad;
     s.tile_walk = tile_build(G) ? m->tile_walk : nullptr;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
@@ -1327,6 +1375,22 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(halloc(&m->h_op_kind, C));
   chk(halloc(&m->h_op_space, C));
   chk(halloc(&m->h_leaves, C));
+  if (r == GWAOI_OK) {
+    void *ps = nullptr, *px = nullptr, *pz = nullptr, *pk = nullptr, *pp = nullptr;
+    if (hipHostGetDevicePointer(&ps, m->h_op_slot, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&px, m->h_op_x, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&pz, m->h_op_z, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&pk, m->h_op_kind, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&pp, m->h_op_space, 0) == hipSuccess) {
+      m->hd_op_slot = (const uint32_t*)ps;
+      m->hd_op_x = (const float*)px;
+      m->hd_op_z = (const float*)pz;
+      m->hd_op_kind = (const uint8_t*)pk;
+      m->hd_op_space = (const uint32_t*)pp;
+    } else {
+      (void)hipGetLastError();  // the small pass copies the ops instead
+    }
+  }
   for (int gi = 0; gi < 2; ++gi) {
     Grid& g = m->grid[gi];
     chk(dalloc(&g.rec, 2 * C));
@@ -2344,6 +2408,15 @@ int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
   // 3: the LDS sweep without the chunked sweep (crowded tiles' movers walk from L2: k_sweep_dense), A/B
   m->chunked = enable != 3;
   m->sweep_lds = enable < 0 ? 0 : (enable > 2 ? 1 : enable);
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_chunked(gwaoi_mgr* m, int64_t min_recs, int64_t max_recs, int64_t max_pad) {
+  RCHK(check_mgr(m));
+  auto u32 = [](int64_t v) { return (uint32_t)std::min<int64_t>(v, 0xFFFFFFFFll); };
+  if (min_recs >= 0) m->chunk_min_recs = u32(min_recs);
+  if (max_recs >= 0) m->chunk_max_recs = u32(max_recs);
+  if (max_pad >= 0) m->chunk_max_pad = u32(max_pad);
   return GWAOI_OK;
 }
 

@@ -136,10 +136,21 @@ struct FanArgs {
   const uint4* crec;    // {x, z, seq_end, slot}
   const uint8_t* cgate;
   const uint32_t* cpos;  // scanned sub-grid positions (own client: the entity's own sub-grid record)
+  const uint4* ccid;    // client id of each sub-grid record (direct fan-out)
   const uint4* eid;
   const float* y;
   const float* yaw;
   uint4* info;          // write pass: per grid record of a collected entity {EntityID}, {x, y, z, yaw}
+  // direct fan-out (n_gates <= kDirectGates: k_fan_dcount / k_fan_dwrite)
+  uint32_t n_gates;
+  uint32_t gstride;      // gcnt entries per record (n_gates rounded up to 4)
+  uint32_t* gcnt;        // count pass: pairs of each record per gate, record-major [j * gstride + g]
+  uint8_t* wantj;        // count pass: each record's collected bits (the flags are cleared there)
+  uint32_t* tg;          // count pass: pairs per gate per tile, gate-major [g * ntiles + t] (+ 1 total);
+                         // scanned: the first wire record of each (gate, tile) block
+  uint32_t ntiles;
+  uint4* out;            // write pass: the wire records, 3 uint4 each
+  uint32_t out_cap;      // records out holds (nothing is written past it: the host grows it and re-runs)
 };
 
 struct ClientGridArgs {
@@ -340,6 +351,326 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
       a.tstat[t] = make_uint4((uint32_t)pt, (uint32_t)(pt >> 32), tot, 0u);
     }
   }
+}
+
+// ---- direct fan-out (n_gates <= kDirectGates) ---------------------------------------------------
+// The wire records are written straight into their gate's packet, in grid order, with no pair list and
+// no gate partition: the count pass stores each record's pairs PER GATE (record-major) and each tile's
+// pairs per gate (gate-major); one small scan over the (gate, tile) totals gives every (gate, tile)
+// block its first record, and the gate offsets. The write pass block-scans a round's per-gate counts
+// into per-thread cursors, walks again, and stages the round's records as 4-byte references
+// {receiver, entity, gate} in LDS; the round's records of one gate are one contiguous range of the
+// packet, copied out 16 B per lane over consecutive addresses. Same records and order as the
+// partition path: gates in order, entities in grid order, each entity's run contiguous with its own
+// client's record first.
+constexpr uint32_t kDirectGates = 8;
+constexpr uint32_t kRoundRecs = 4096;   // a round's staged records (16 KB of references)
+constexpr uint32_t kRefSkip = 0xFFFFFFFFu;  // written directly (receiver outside the LDS region)
+constexpr uint32_t kRefOwn = 1u << 28;      // the entity's own client
+
+struct FanGeo {
+  Geom g;
+  int cx0, cx1, cz0, cz1, W, Hh;
+  uint32_t j0, j1;
+};
+
+__device__ __forceinline__ FanGeo fan_geo(const FanArgs& a, uint32_t t) {
+  FanGeo f;
+  const uint32_t sp = __builtin_amdgcn_readfirstlane(a.g.tile_space[t]);
+  f.g = uniform_geom(&a.g.geom[sp]);
+  const int lt = (int)(t - f.g.tile_base);
+  const int tx = lt % f.g.ntx, tz = lt / f.g.ntx;
+  const uint32_t k0 = f.g.base + ((uint32_t)lt << kTileCellShift);
+  f.j0 = a.g.cs[k0];
+  f.j1 = a.g.cs[k0 + kTileCells];
+  const int R = f.g.reach;
+  f.cx0 = max(tx * kTile - R, 0), f.cx1 = min(tx * kTile + kTile - 1 + R, f.g.ncx - 1);
+  f.cz0 = max(tz * kTile - R, 0), f.cz1 = min(tz * kTile + kTile - 1 + R, f.g.ncz - 1);
+  f.W = f.cx1 - f.cx0 + 1, f.Hh = f.cz1 - f.cz0 + 1;
+  return f;
+}
+
+// Every client neighbour of record j's entity (the pair predicate of k_fan_tile): f(gate, lds index
+// or kNone, sub-grid index)
+template <class F>
+__device__ __forceinline__ void fan_pairs(const FanArgs& a, const FanGeo& fg, bool lds, const uint16_t* cst,
+                                          const uint4* crl, const uint8_t* cgl, uint32_t j, uint4 ra, uint32_t s,
+                                          uint16_t gs, F&& f) {
+  const Geom& g = fg.g;
+  const float sx = __uint_as_float(ra.x), sz = __uint_as_float(ra.y);
+  const uint32_t qs = a.g.rec[j].b.w;
+  const CellBox B = qbox(g, sx, sz);
+  if (lds && B.x0 >= fg.cx0 && B.x1 <= fg.cx1 && B.z0 >= fg.cz0 && B.z1 <= fg.cz1) {
+    const float D = g.D;
+    const uint32_t selfq = gs != GWAOI_SYNC_NO_CLIENT ? a.cpos[j] : 0xffffffffu;
+    for (int r = B.z0; r <= B.z1; ++r) {
+      const int rb = (r - fg.cz0) * fg.W - fg.cx0;
+      const uint32_t e = cst[rb + B.x1 + 1];
+      for (uint32_t p = cst[rb + B.x0]; p < e; ++p) {
+        const uint4 cr = crl[p];
+        const float ox = __uint_as_float(cr.x), oz = __uint_as_float(cr.y);
+        const bool in = cr.w != selfq && ((cr.z > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz));
+        if (in) f((uint32_t)cgl[p], p, cr.w);
+      }
+    }
+  } else {
+    client_neighbours(a, s, sx, sz, qs, [&](uint32_t cj, uint8_t cg) { f((uint32_t)cg, kNone, cj); });
+  }
+}
+
+// stage the tile's region of the client sub-grid (and each staged record's gate); false: walk global
+__device__ __forceinline__ bool fan_stage(const FanArgs& a, const FanGeo& fg, uint16_t* cst, uint4* crl, uint8_t* cgl,
+                                          uint32_t* red, uint32_t* tot_sh) {
+  const int ncell = fg.W * fg.Hh;
+  const bool lds = fg.g.reach > 0 && ncell <= kFanRegCells &&
+                   stage_region<kSy, kFanRegCells, kFanLdsRecs>(fg.g, a.ccs, fg.cx0, fg.cz0, fg.W, ncell, cst, crl, red,
+                                                                 tot_sh, [&](uint32_t q) {
+                                                                   const uint4 c = a.crec[q];
+                                                                   return make_uint4(c.x, c.y, c.z, q);
+                                                                 });
+  if (lds) {
+    const uint32_t ns = cst[ncell];
+    for (uint32_t p = threadIdx.x; p < ns; p += kSy) cgl[p] = a.cgate[crl[p].w];
+    __syncthreads();
+  }
+  return lds;
+}
+
+// a gate's per-thread counter / cursor in registers: static indices only (a dynamic index would go
+// through scratch), one select per gate
+__device__ __forceinline__ uint32_t gate_bump(uint32_t (&c)[kDirectGates], uint32_t g) {
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kDirectGates; ++k) {
+    v = g == k ? c[k] : v;
+    c[k] += g == k ? 1u : 0u;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(kSy) k_fan_dcount(FanArgs a) {
+  __shared__ uint16_t cst[kFanRegCells + 1];
+  __shared__ uint4 crl[kFanLdsRecs];
+  __shared__ uint8_t cgl[kFanLdsRecs];
+  __shared__ uint32_t gsum[kDirectGates];
+  __shared__ uint32_t red[kSy / 64];
+  __shared__ uint32_t tot_sh;
+  __shared__ unsigned long long rp[kSy / 64];
+  const uint32_t G = a.n_gates, t = blockIdx.x;
+  if (t == 0 && threadIdx.x == 0) a.tg[G * a.ntiles] = 0u;  // (the scan's total lands there)
+  const FanGeo fg = fan_geo(a, t);
+  if (fg.j0 == fg.j1) {
+    if (threadIdx.x < G) a.tg[threadIdx.x * a.ntiles + t] = 0u;
+    if (threadIdx.x == 0) a.tstat[t] = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
+  if (threadIdx.x < kDirectGates) gsum[threadIdx.x] = 0u;
+  const bool lds = fan_stage(a, fg, cst, crl, cgl, red, &tot_sh);
+  __syncthreads();
+  uint32_t ents = 0;
+  unsigned long long psum = 0;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t jb = fg.j0; jb < fg.j1; jb += kSy) {
+    const uint32_t j = jb + tid;
+    if (j >= fg.j1) continue;
+    uint32_t c[kDirectGates];
+#pragma unroll
+    for (uint32_t g = 0; g < kDirectGates; ++g) c[g] = 0u;
+    const uint4 ra = a.g.rec[j].a;
+    const uint32_t s = ra.z & REC_SLOT;
+    const uint8_t fl = (ra.z & REC_GHOST) ? 0 : a.flags[s];
+    const uint8_t want = fl & (GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
+    if (want) {
+      ++ents;
+      const uint16_t gs = a.gate[s];
+      if ((want & GWAOI_SYNC_OWN_CLIENT) && gs < G) gate_bump(c, gs);
+      if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS)
+        fan_pairs(a, fg, lds, cst, crl, cgl, j, ra, s, gs, [&](uint32_t g, uint32_t, uint32_t) {
+          if (g < G) gate_bump(c, g);
+        });
+      if (a.clear) a.flags[s] = (uint8_t)(fl & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
+    }
+    a.wantj[j] = want;
+    uint4* dst = reinterpret_cast<uint4*>(a.gcnt + (size_t)j * a.gstride);
+    dst[0] = make_uint4(c[0], c[1], c[2], c[3]);
+    if (a.gstride > 4) dst[1] = make_uint4(c[4], c[5], c[6], c[7]);
+#pragma unroll
+    for (uint32_t g = 0; g < kDirectGates; ++g) {
+      psum += c[g];
+      if (c[g]) atomicAdd(&gsum[g], c[g]);  // LDS
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) psum += __shfl_xor(psum, o, 64);
+  for (int o = 32; o > 0; o >>= 1) ents += __shfl_xor(ents, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = ents, rp[tid >> 6] = psum;
+  __syncthreads();
+  if (tid < G) a.tg[tid * a.ntiles + t] = gsum[tid];
+  if (tid == 0) {
+    uint32_t tot = 0;
+    unsigned long long pt = 0;
+    for (int k = 0; k < kSy / 64; ++k) tot += red[k], pt += rp[k];
+    a.tstat[t] = make_uint4((uint32_t)pt, (uint32_t)(pt >> 32), tot, 0u);
+  }
+}
+
+__global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k_fan_dwrite(FanArgs a) {
+  __shared__ uint16_t cst[kFanRegCells + 1];
+  __shared__ uint4 crl[kFanLdsRecs];
+  __shared__ uint8_t cgl[kFanLdsRecs];
+  __shared__ uint32_t gbase[kDirectGates];      // out index of the round's first record of each gate
+  __shared__ uint32_t wred[kDirectGates][kSy / 64];
+  __shared__ uint32_t groff[kDirectGates];      // round position of each gate's first record
+  __shared__ uint32_t gtot[kDirectGates];       // the round's records of each gate
+  __shared__ uint32_t ref[kRoundRecs];
+  __shared__ uint4 ent[kSy][2];                 // the round's entities: EntityID, {x, y, z, yaw}
+  __shared__ uint4 ocid[kSy];                   // and their own client's id
+  __shared__ uint32_t red[kSy / 64];
+  __shared__ uint32_t tot_sh;
+  const uint32_t G = a.n_gates, t = blockIdx.x, tid = threadIdx.x;
+  const FanGeo fg = fan_geo(a, t);
+  if (fg.j0 == fg.j1) return;
+  if (tid < G) gbase[tid] = a.tg[tid * a.ntiles + t];
+  const bool lds = fan_stage(a, fg, cst, crl, cgl, red, &tot_sh);
+  __syncthreads();  // gbase
+  const int lane = tid & 63, w = tid >> 6;
+  for (uint32_t jb = fg.j0; jb < fg.j1; jb += kSy) {  // block-uniform
+    const uint32_t j = jb + tid;
+    const bool live = j < fg.j1;
+    const uint8_t want = live ? a.wantj[j] : 0;
+    uint32_t c[kDirectGates];
+#pragma unroll
+    for (uint32_t g = 0; g < kDirectGates; ++g) c[g] = 0u;
+    if (want) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.gcnt + (size_t)j * a.gstride);
+#pragma unroll
+      for (uint32_t g4 = 0; g4 < kDirectGates; g4 += 4) {
+        if (g4 < a.gstride) {
+          const uint4 v = src[g4 / 4];
+          c[g4] = v.x, c[g4 + 1] = v.y, c[g4 + 2] = v.z, c[g4 + 3] = v.w;
+        }
+      }
+    }
+    // block scan of the per-gate counts: wave scans, then the waves' totals
+    uint32_t inc[kDirectGates];
+#pragma unroll
+    for (uint32_t g = 0; g < kDirectGates; ++g) {
+      uint32_t v = c[g];
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+      }
+      inc[g] = v;
+      if (lane == 63) wred[g][w] = v;
+    }
+    __syncthreads();
+    uint32_t roff = 0;  // round position of gate g's first record
+    uint32_t cur[kDirectGates];  // the thread's next record per gate (round position, or out index)
+    bool staged;
+    {
+      uint32_t R = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < kDirectGates; ++g) {
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < kSy / 64; ++k) {
+          const uint32_t x = wred[g][k];
+          before += k < w ? x : 0u;
+          tot += x;
+        }
+        inc[g] = before + inc[g] - c[g];  // exclusive prefix within the round
+        c[g] = tot;                       // the round's records of gate g
+        R += tot;
+      }
+      staged = R <= kRoundRecs;  // block-uniform
+#pragma unroll
+      for (uint32_t g = 0; g < kDirectGates; ++g) {
+        cur[g] = staged ? roff + inc[g] : gbase[g] + inc[g];
+        if (tid == 0) groff[g] = roff, gtot[g] = c[g];
+        roff += c[g];
+      }
+    }
+    __syncthreads();  // groff / gtot
+    uint4 eid = make_uint4(0, 0, 0, 0), info = make_uint4(0, 0, 0, 0), own = make_uint4(0, 0, 0, 0);
+    uint4 ra = make_uint4(0, 0, 0, 0);
+    uint32_t s = 0;
+    uint16_t gs = GWAOI_SYNC_NO_CLIENT;
+    if (want) {
+      ra = a.g.rec[j].a;
+      s = ra.z & REC_SLOT;
+      gs = a.gate[s];
+      eid = a.eid[s];
+      info = make_uint4(ra.x, __float_as_uint(a.y[s]), ra.y, __float_as_uint(a.yaw[s]));
+      if ((want & GWAOI_SYNC_OWN_CLIENT) && gs < G) own = a.ccid[a.cpos[j]];
+      ent[tid][0] = eid;
+      ent[tid][1] = info;
+      ocid[tid] = own;
+    }
+    auto put_direct = [&](uint32_t dst, const uint4& cid) {
+      if (dst < a.out_cap) {
+        a.out[3 * (size_t)dst] = cid;
+        a.out[3 * (size_t)dst + 1] = eid;
+        a.out[3 * (size_t)dst + 2] = info;
+      }
+    };
+    if (want) {
+      if ((want & GWAOI_SYNC_OWN_CLIENT) && gs < G) {
+        const uint32_t pos = gate_bump(cur, gs);
+        if (!staged) put_direct(pos, own);
+        else if (pos < kRoundRecs) ref[pos] = kRefOwn | (tid << 12) | ((uint32_t)gs << 20);
+      }
+      if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS)
+        fan_pairs(a, fg, lds, cst, crl, cgl, j, ra, s, gs, [&](uint32_t g, uint32_t p, uint32_t q) {
+          if (g >= G) return;
+          const uint32_t pos = gate_bump(cur, g);
+          if (!staged) {
+            put_direct(pos, a.ccid[q]);
+          } else if (pos < kRoundRecs) {
+            if (p != kNone) {
+              ref[pos] = p | (tid << 12) | (g << 20);
+            } else {  // a receiver outside the staged region: written now, skipped by the copy-out
+              ref[pos] = kRefSkip;
+              put_direct(gbase[g] + (pos - groff[g]), a.ccid[q]);
+            }
+          }
+        });
+    }
+    __syncthreads();
+    if (staged) {  // copy-out: record r of the round, 16-B part k, over consecutive addresses per gate;
+                   // four parts per thread in flight (the ClientID gathers are global loads)
+      const uint32_t nq = 3 * roff;
+      constexpr size_t kNoDst = ~(size_t)0;
+      auto fetch = [&](uint32_t i, size_t& dst) -> uint4 {  // part i of the round: its value and out index
+        const bool on = i < nq;
+        const uint32_t r = on ? i / 3 : 0u, k = i - 3 * r;
+        const uint32_t v = on ? ref[r] : kRefSkip;
+        const uint32_t g = (v >> 20) & 0xFFu, owner = (v >> 12) & 0xFFu;
+        const bool live = v != kRefSkip;
+        const uint32_t d = live ? gbase[g] + (r - groff[g]) : 0u;
+        dst = live && d < a.out_cap ? 3 * (size_t)d + k : kNoDst;
+        if (!live) return make_uint4(0, 0, 0, 0);
+        if (k != 0) return ent[owner][k - 1];
+        return (v & kRefOwn) ? ocid[owner] : a.ccid[crl[v & 0xFFFu].w];
+      };
+      for (uint32_t i0 = tid; i0 < nq; i0 += 4 * kSy) {
+        size_t d0, d1, d2, d3;
+        const uint4 v0 = fetch(i0, d0), v1 = fetch(i0 + kSy, d1), v2 = fetch(i0 + 2 * kSy, d2),
+                    v3 = fetch(i0 + 3 * kSy, d3);
+        if (d0 != kNoDst) a.out[d0] = v0;
+        if (d1 != kNoDst) a.out[d1] = v1;
+        if (d2 != kNoDst) a.out[d2] = v2;
+        if (d3 != kNoDst) a.out[d3] = v3;
+      }
+    }
+    __syncthreads();
+    if (tid < G) gbase[tid] += gtot[tid];
+    __syncthreads();
+  }
+}
+
+// gate offsets of the direct fan-out: the scanned (gate, tile) blocks' first records (g = G: the total)
+__global__ void k_fan_goff(const uint32_t* __restrict__ tg, uint32_t ntiles, uint32_t G, uint32_t* goff) {
+  const uint32_t g = threadIdx.x;
+  if (g <= G) goff[g] = tg[(size_t)g * ntiles];
 }
 
 // The count pass's totals: entities collected (n_ent) and pairs in 64 bits (npairs64, the guard against
@@ -660,6 +991,15 @@ struct SyncState {
   uint64_t info_cap = 0;
   uint4* tstat = nullptr;  // per tile count-pass totals
   uint32_t tstat_n = 0;
+  // direct fan-out (k_fan_dcount / k_fan_dwrite)
+  uint32_t* gcnt = nullptr;
+  uint64_t gcnt_cap = 0;
+  uint8_t* wantj = nullptr;
+  uint64_t wantj_cap = 0;
+  uint32_t* tg = nullptr;
+  uint64_t tg_cap = 0;
+  int fan_mode = 0;  // gwaoi_debug_set_fanout_mode: 0 direct when n_gates <= kDirectGates, 1 pair list + partition
+  uint64_t direct_reruns = 0;
   uint2* pairs = nullptr;
   uint64_t pairs_cap = 0;
   uint32_t* ghist = nullptr;
@@ -693,7 +1033,7 @@ struct SyncState {
 void sync_free(SyncState* s) {
   if (!s) return;
   void* p[] = {s->flags, s->gate, s->cid, s->eid, s->y, s->yaw, s->d_hkey, s->d_hval, s->cnt, s->cpos, s->ccs,
-               s->crec, s->cgate, s->ccid, s->info, s->tstat, s->pairs,
+               s->crec, s->cgate, s->ccid, s->info, s->tstat, s->pairs, s->gcnt, s->wantj, s->tg,
                s->ghist, s->out, s->d_goff, s->scan.status, s->d_payload, s->res, s->first, s->ictr, s->bcnt,
                s->op_slot, s->op_x, s->op_z};
   for (void* q : p)
@@ -876,6 +1216,104 @@ int upload_hash(const MgrView& v, SyncState* s) {
                      (uint32_t)idx.size(), s->d_hkey, s->d_hval);
   SCHK(hipGetLastError());
   SCHK(hipStreamSynchronize(v.stream));
+  return GWAOI_OK;
+}
+
+void add_collect_stats(SyncState* s, uint64_t records, uint32_t entities) {
+  float t01, t12, t34, t45;
+  if (hipEventElapsedTime(&t01, s->tev[0], s->tev[1]) != hipSuccess ||
+      hipEventElapsedTime(&t12, s->tev[1], s->tev[2]) != hipSuccess ||
+      hipEventElapsedTime(&t34, s->tev[3], s->tev[4]) != hipSuccess ||
+      hipEventElapsedTime(&t45, s->tev[4], s->tev[5]) != hipSuccess)
+    return;
+  s->stats.collects++;
+  s->stats.ms_client_grid += t01;
+  s->stats.ms_count += t12;
+  s->stats.ms_write += t34;
+  s->stats.ms_gate += t45;
+  s->stats.records += records;
+  s->stats.entities += entities;
+}
+
+// The direct fan-out (n_gates <= kDirectGates), after the client sub-grid: count pass (per-gate counts,
+// flags cleared) -> scan of the (gate, tile) totals -> write pass straight into the gate packets. The
+// packet buffer keeps the previous collect's size: no host round trip between the passes; a collect
+// with more records re-runs the write pass into a grown buffer.
+int collect_direct(const MgrView& v, SyncState* s, FanArgs f, uint32_t opts, gwaoi_sync_out* out) {
+  hipStream_t st = v.stream;
+  const uint32_t ntiles = v.ntiles, G = s->n_gates, bound = v.rec_bound;
+  const uint32_t gstride = (G + 3u) & ~3u;
+  SRCHK(dgrow(&s->gcnt, &s->gcnt_cap, ((uint64_t)bound + 1) * gstride));
+  SRCHK(dgrow(&s->wantj, &s->wantj_cap, (uint64_t)bound + 1));
+  const uint64_t tgn = (uint64_t)G * ntiles + 1;
+  SRCHK(dgrow(&s->tg, &s->tg_cap, tgn));
+  SRCHK(ensure_scan(s, (uint32_t)tgn));
+  if (!s->out) SRCHK(dgrow(&s->out, &s->out_cap, 3u * 65536u));
+  f.n_gates = G;
+  f.gstride = gstride;
+  f.gcnt = s->gcnt;
+  f.wantj = s->wantj;
+  f.tg = s->tg;
+  f.ntiles = ntiles;
+  if (v.timing) SCHK(hipEventRecord(s->tev[1], st));
+  hipLaunchKernelGGL(k_fan_dcount, dim3(ntiles), dim3(kSy), 0, st, f);
+  hipLaunchKernelGGL(k_fan_total, dim3(1), dim3(1024), 0, st, (const uint4*)s->tstat, ntiles, s->ictr + 8,
+                     (unsigned long long*)(s->ictr + 10));
+  launch_scan(s->scan, s->tg, (uint32_t)tgn, st);
+  hipLaunchKernelGGL(k_fan_goff, dim3(1), dim3(kDirectGates + 1), 0, st, (const uint32_t*)s->tg, ntiles, G, s->d_goff);
+  if (v.timing) SCHK(hipEventRecord(s->tev[2], st));
+  auto write = [&]() -> int {
+    f.out = s->out;
+    f.out_cap = (uint32_t)std::min<uint64_t>(s->out_cap / 3, 0xFFFFFFFFull);
+    if (v.timing) SCHK(hipEventRecord(s->tev[3], st));
+    hipLaunchKernelGGL(k_fan_dwrite, dim3(ntiles), dim3(kSy), 0, st, f);
+    if (v.timing) {
+      SCHK(hipEventRecord(s->tev[4], st));
+      SCHK(hipEventRecord(s->tev[5], st));
+    }
+    SCHK(hipGetLastError());
+    SCHK(hipMemcpyAsync(s->h_small + 8, s->d_goff, (G + 1) * 4, hipMemcpyDeviceToHost, st));
+    SCHK(hipMemcpyAsync(s->h_small + 4, s->ictr + 8, 16, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    return GWAOI_OK;
+  };
+  SRCHK(write());
+  uint64_t M64;
+  memcpy(&M64, s->h_small + 6, sizeof M64);
+  if (M64 > v.index_limit) {  // record indices are uint32: the scanned offsets wrapped
+    set_error("collect_sync: %llu records exceed the fan-out's uint32 offsets (limit %llu)", (unsigned long long)M64,
+              (unsigned long long)v.index_limit);
+    return GWAOI_ERR_NOMEM;
+  }
+  const uint32_t M = s->h_small[8 + G];
+  if ((uint64_t)M * 3 > s->out_cap) {  // more records than the previous collect's buffer: grown, written again
+    SRCHK(dgrow(&s->out, &s->out_cap, (uint64_t)M * 3));
+    s->direct_reruns++;
+    SRCHK(write());
+  }
+  out->n_entities = s->h_small[4];
+  for (uint32_t k = 0; k <= G; ++k) s->goff64[k] = s->h_small[8 + k];
+  out->n_records = M;
+  out->d_records = (const uint8_t*)s->out;
+  if (M && (opts & GWAOI_COLLECT_HOST)) {
+    const uint64_t bytes = (uint64_t)M * GWAOI_SYNC_RECORD_BYTES;
+    if (s->h_out_cap < bytes) {
+      if (s->h_out) hipHostFree(s->h_out);
+      s->h_out = nullptr;
+      s->h_out_cap = 0;
+      const uint64_t nb = bytes + bytes / 4;
+      if (hipHostMalloc((void**)&s->h_out, nb, hipHostMallocDefault) != hipSuccess) {
+        s->h_out = nullptr;
+        set_error("collect_sync: hipHostMalloc(%llu) failed", (unsigned long long)nb);
+        return GWAOI_ERR_NOMEM;
+      }
+      s->h_out_cap = nb;
+    }
+    SCHK(hipMemcpyAsync(s->h_out, s->out, bytes, hipMemcpyDeviceToHost, st));
+    SCHK(hipStreamSynchronize(st));
+    out->records = s->h_out;
+  }
+  if (v.timing) add_collect_stats(s, M, out->n_entities);
   return GWAOI_OK;
 }
 
@@ -1204,7 +1642,6 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
     return GWAOI_OK;
   }
   const uint32_t bound = v.rec_bound;
-  SRCHK(gw::dgrow32(&s->cnt, &s->cnt_n, (uint64_t)bound + 1));
   SRCHK(gw::ensure_scan(s, bound + 1));
   // client sub-grid
   SRCHK(gw::dgrow32(&s->cpos, &s->cpos_n, (uint64_t)bound + 1));
@@ -1212,7 +1649,6 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   SRCHK(gw::dgrow32(&s->crec, &s->crec_n, s->cap));
   SRCHK(gw::dgrow32(&s->cgate, &s->cgate_n, s->cap));
   SRCHK(gw::dgrow32(&s->ccid, &s->ccid_n, s->cap));
-  SRCHK(gw::dgrow(&s->info, &s->info_cap, 2 * ((uint64_t)bound + 1)));
   gw::ClientGridArgs cg = {};
   cg.rec = v.g.rec;
   cg.cs = v.g.cs;
@@ -1237,10 +1673,10 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   f.crec = s->crec;
   f.cgate = s->cgate;
   f.cpos = s->cpos;
+  f.ccid = s->ccid;
   f.eid = s->eid;
   f.y = s->y;
   f.yaw = s->yaw;
-  f.info = s->info;
   f.g = v.g;
   f.rec_count = v.rec_count;
   f.rec_bound = bound;
@@ -1250,12 +1686,17 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   f.flags = s->flags;
   f.gate = s->gate;
   f.clear = !(opts & GWAOI_COLLECT_KEEP_FLAGS);
-  f.cnt = s->cnt;
-  SCHK(hipMemsetAsync(s->cnt, 0, ((size_t)bound + 1) * 4, st));
   const uint32_t ntiles = v.ntiles;
   if (!ntiles) return GWAOI_OK;
   SRCHK(gw::dgrow32(&s->tstat, &s->tstat_n, ntiles));
   f.tstat = s->tstat;
+  if (s->n_gates <= gw::kDirectGates && s->fan_mode == 0) return gw::collect_direct(v, s, f, opts, out);
+  // pair list + gate partition
+  SRCHK(gw::dgrow32(&s->cnt, &s->cnt_n, (uint64_t)bound + 1));
+  SRCHK(gw::dgrow(&s->info, &s->info_cap, 2 * ((uint64_t)bound + 1)));
+  f.info = s->info;
+  f.cnt = s->cnt;
+  SCHK(hipMemsetAsync(s->cnt, 0, ((size_t)bound + 1) * 4, st));
   if (v.timing) SCHK(hipEventRecord(s->tev[1], st));
   hipLaunchKernelGGL(gw::k_fan_tile<false>, dim3(ntiles), dim3(gw::kSy), 0, st, f);
   hipLaunchKernelGGL(gw::k_fan_total, dim3(1), dim3(1024), 0, st, (const uint4*)s->tstat, ntiles, s->ictr + 8,
@@ -1476,6 +1917,19 @@ int gwaoi_sync_get_stats(gwaoi_mgr* m, gwaoi_sync_stats* out) {
     return GWAOI_ERR_INVALID;
   }
   *out = s->stats;
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_set_fanout_mode(gwaoi_mgr* m, int mode, uint64_t* direct_reruns) {
+  gw::MgrView v;
+  SyncState* s;
+  SRCHK(gw::get_state(m, &v, &s));
+  if (mode > 1) {
+    gw::set_error("debug_set_fanout_mode: mode %d not in {-1, 0, 1}", mode);
+    return GWAOI_ERR_INVALID;
+  }
+  if (mode >= 0) s->fan_mode = mode;
+  if (direct_reruns) *direct_reruns = s->direct_reruns;
   return GWAOI_OK;
 }
 

@@ -58,6 +58,13 @@ class EntitySync:
     def reset_stats(self):
         check(self._L.gwaoi_sync_reset_stats(self.eng.handle))
 
+    def debug_fanout_mode(self, mode: int = -1) -> int:
+        """gwaoi_debug_set_fanout_mode: 0 direct gate writes when n_gates <= 8, 1 pair list + gate partition,
+        -1 keep; returns the direct collects re-run into a grown packet buffer."""
+        n = ctypes.c_uint64(0)
+        check(self._L.gwaoi_debug_set_fanout_mode(self.eng.handle, int(mode), ctypes.byref(n)))
+        return n.value
+
     @staticmethod
     def _ids(ids, n) -> np.ndarray:
         a = np.ascontiguousarray(np.asarray(ids, dtype=np.uint8).reshape(n, 16))

@@ -73,6 +73,15 @@ int gwaoi_debug_set_small_pass(struct gwaoi_mgr* mgr, int mode, uint64_t* n_smal
  * build; -1 leaves the mode. Reports the builds of each kind and the re-runs since the manager was made. */
 int gwaoi_debug_set_build_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* n_fused, uint64_t* n_counting,
                                uint64_t* n_reruns);
+/* A/B: which tiles over k_sweep's LDS budget take the chunked LDS sweep (k_sweep_chunked): those holding
+ * [min_recs, max_recs] records whose halo is at most max_pad cells; the others walk from L2
+ * (k_sweep_dense). A negative value leaves that bound. */
+int gwaoi_debug_set_chunked(struct gwaoi_mgr* mgr, int64_t min_recs, int64_t max_recs, int64_t max_pad);
+/* Sync fan-out path (gwaoi_collect_sync): 0 = the records written straight into their gate packets when
+ * n_gates <= 8 (default), 1 = always the pair list + gate partition; -1 leaves the mode. *direct_reruns
+ * (optional): direct collects whose packet buffer was too small and were written again. Requires
+ * gwaoi_sync_enable. */
+int gwaoi_debug_set_fanout_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* direct_reruns);
 /* Diagnostics: resident sweep workgroups per CU (HIP occupancy API) and the sweep's LDS bytes. */
 int gwaoi_debug_sweep_occupancy(int device, int* blocks_per_cu, int* lds_bytes);
 

@@ -129,3 +129,36 @@ def test_small_and_full_passes_agree(gpu, po):
     for t, ops in enumerate(case["ticks"]):
         _same(H.gpu_tick(b, ops), H.gpu_tick(a, ops), f"tick {t}")
     assert a.debug_small_pass() == 0
+
+
+def test_small_pass_crowd_overflows_order_lds(gpu, po):
+    """An Enter into a crowd: the single pass has more events than k_order_small's LDS holds (4,096), so
+    the order stage falls back to the general kernels on the scanned counts; then a Leave of the same
+    slot, and a Moved of a crowd member across the crowd (its slice needs the sort)."""
+    from goworld_amd.engine import Engine
+    rng = np.random.default_rng(5)
+    n, D = 6000, 100.0
+    eng = Engine(D, capacity=n + 1, bounds=(0.0, 0.0, 1000.0, 1000.0))
+    eng.debug_small_pass(2)
+    orc = po.XZListOracle(D, n + 1)
+    pos = rng.uniform(450, 550, (n, 2)).astype(np.float32)  # every pair within D
+    ops = [(H.ENTER, int(s), float(pos[s, 0]), float(pos[s, 1])) for s in range(n)]
+    _same(H.gpu_tick(eng, ops), H.oracle_tick(orc, ops), "crowd enter")
+    n0 = eng.debug_small_pass()
+    for t, ops in enumerate([[(H.ENTER, n, 500.0, 500.0)], [(H.LEAVE, n, 0.0, 0.0)],
+                             [(H.MOVE, 7, 451.0, 549.0)], [(H.ENTER, n, 520.0, 480.0), (H.MOVE, 9, 549.5, 450.5)]]):
+        got, want = H.gpu_tick(eng, ops), H.oracle_tick(orc, ops)
+        assert len(want) > 4096 or t == 2
+        _same(got, want, f"crowd pass {t}")
+    assert eng.debug_small_pass() - n0 == 4
+
+
+def test_small_pass_above_fused_order_ops(gpu, po):
+    """A forced small pass of 1,500 ops (mode 2): more ops than k_order_small takes, so the scan and
+    the general order kernels run after k_sweep_small."""
+    case = H.case_random_ops(seed=303, n=4000, nticks=4, ops_per_tick=1500, world=800.0, dist=60.0, dup=False)
+    eng = _engine(case, 2)
+    orc = po.XZListOracle(case["dist"], case["cap"])
+    for t, ops in enumerate(case["ticks"]):
+        _same(H.gpu_tick(eng, ops), H.oracle_tick(orc, ops), f"tick {t}")
+    assert eng.debug_small_pass() >= 3

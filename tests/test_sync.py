@@ -432,3 +432,28 @@ def test_ingest_drops_nonfinite(gpu, oracle_lib):
     fl, _, gy, _ = sy.read_tables()
     assert gy[3] == 9.0 and all(gy[s] == st["y"][s] for s in (1, 2, 4))
     assert all(fl[s] == R.FROM_CLIENT for s in (1, 2, 4))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,L,dist,n_gates,seed,cpd", [
+    (3000, 1200.0, 100.0, 8, 11, None),     # 8 gates (the direct path's maximum)
+    (2500, 900.0, 80.0, 3, 12, None),       # gstride 4 > n_gates
+    (20000, 5000.0, 100.0, 5, 13, 1.0),     # cells of D: regions over the LDS budget walk the global grid
+])
+def test_collect_direct_matches_partition(gpu, oracle_lib, n, L, dist, n_gates, seed, cpd):
+    """The direct fan-out (records written straight into the gate packets, n_gates <= 8) and the pair
+    list + gate partition produce the same bytes in the same order, and both match the oracle."""
+    from goworld_amd.sync import EntitySync
+    eng, orc, x, z = world(oracle_lib, n, L, dist, seed, cells_per_dist=cpd)
+    sy = EntitySync(eng, n_gates)
+    rng = np.random.default_rng(seed)
+    st = fill_sync(sy, rng, n, n_gates)
+    r0 = sy.debug_fanout_mode(0)
+    got, _ = check_collect(sy, orc, st, x, z, n_gates, keep=True)  # direct, flags kept
+    sy.debug_fanout_mode(1)
+    got2, _ = check_collect(sy, orc, st, x, z, n_gates)  # partition path
+    assert sorted(got) == sorted(got2)
+    for g in got:
+        for f in got[g].dtype.names:
+            assert np.array_equal(got[g][f], got2[g][f]), f"gate {g} field {f}: direct and partition differ"
+    assert sy.debug_fanout_mode(0) >= r0
