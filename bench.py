@@ -287,8 +287,9 @@ def small_pass_leg(eng, n, L, xs, zs, reps, seed):
                 stage()
                 eng.tick_device()
                 dt = time.perf_counter() - t0
-                dev_ms = eng.stats()["ms_total"]
-                rec[kind].append((eng.debug_small_pass() > n0, dev_ms, dt * 1e3, int(eng.last.count)))
+                st = eng.stats()
+                rec[kind].append((eng.debug_small_pass() > n0, st["ms_total"], dt * 1e3, int(eng.last.count),
+                                  st["ms_sweep"]))
         res = {}
         for kind, v in rec.items():
             sm = [r for r in v if r[0]]
@@ -297,6 +298,7 @@ def small_pass_leg(eng, n, L, xs, zs, reps, seed):
                 "passes": len(v), "small_passes": len(sm),
                 "device_ms_p50_small": percentile([r[1] for r in sm], 50) if sm else None,
                 "device_ms_p50_full": percentile([r[1] for r in fu], 50) if fu else None,
+                "sweep_stage_ms_p50_small": percentile([r[4] for r in sm], 50) if sm else None,
                 "host_ms_p50": percentile([r[2] for r in v], 50),
                 "events_mean": float(np.mean([r[3] for r in v])),
             }
@@ -306,7 +308,9 @@ def small_pass_leg(eng, n, L, xs, zs, reps, seed):
     out["note"] = (
         f"{reps} repetitions per setting of a 1-op Leave, the 1-op Enter bringing the slot back, and a 1,000-op "
         "Moved pass (<= 1 unit each), host-staged, events in HBM, into the full manager; device = the pass's "
-        "hipEvents, host = stage + tick wall time; small_passes = passes that took the small path")
+        "hipEvents (first to last: the event records between the kernels included), sweep_stage = the hipEvents "
+        "around the sweep kernel (a single op: the whole pass, apply + sweep + order + publication, is that one "
+        "kernel); host = stage + tick wall time; small_passes = passes that took the small path")
     return out
 
 

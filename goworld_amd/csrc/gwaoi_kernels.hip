@@ -2651,12 +2651,15 @@ __global__ void __launch_bounds__(kW == 1 ? kBlock : 64 * kW) k_sweep_small(Smal
       }
       uint32_t gi = cur + pre;
       if (cnt > left) {  // this reservation fills up: the rest goes to a fresh one
+        // (kW > 1: small reservations — a small pass's events are few and spread over many waves, and
+        // every reserved slot is read by the order stage, holes included)
+        const uint32_t res = max(kW > 1 ? 16u : kEvChunk, cnt);
         uint32_t nb = 0;
-        if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
+        if (lane == 0) nb = atomicAdd(&a.ctr[CTR_EVENTS], res);
         nb = __shfl(nb, 0, 64);
         if (pre >= left) gi = nb + (pre - left);
         cur = nb + (cnt - left);
-        left = kEvChunk - (cnt - left);
+        left = res - (cnt - left);
       } else {
         cur += cnt;
         left -= cnt;

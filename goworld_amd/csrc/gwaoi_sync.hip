@@ -104,13 +104,13 @@ __global__ void __launch_bounds__(kSy) k_clear_absent(uint8_t* flags, const uint
       flags[s] = (uint8_t)(flags[s] & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
 }
 
+// the device hash table: one 32-B bucket per entry, {key} then {slot, 0, 0, 0}, so a probe is one line
 __global__ void __launch_bounds__(kSy) k_hash_scatter(const uint32_t* __restrict__ idx, const uint4* __restrict__ key,
-                                                      const uint32_t* __restrict__ val, uint32_t n, uint4* hkey,
-                                                      uint32_t* hval) {
+                                                      const uint32_t* __restrict__ val, uint32_t n, uint4* hb) {
   const uint32_t i = blockIdx.x * kSy + threadIdx.x;
   if (i >= n) return;
-  hkey[idx[i]] = key[i];
-  hval[idx[i]] = val[i];
+  hb[2 * (size_t)idx[i]] = key[i];
+  hb[2 * (size_t)idx[i] + 1] = make_uint4(val[i], 0u, 0u, 0u);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -364,7 +364,9 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
 // partition path: gates in order, entities in grid order, each entity's run contiguous with its own
 // client's record first.
 constexpr uint32_t kDirectGates = 8;
-constexpr uint32_t kRoundRecs = 4096;   // a round's staged records (16 KB of references)
+constexpr uint32_t kRoundRecs = 3072;   // a round's staged records (12 KB of references)
+constexpr int kDirLdsRecs = 512;        // staged sub-grid records of the direct kernels (config 2: ~210 per
+                                        // region); smaller LDS: 4 blocks per CU instead of 3
 constexpr uint32_t kRefSkip = 0xFFFFFFFFu;  // written directly (receiver outside the LDS region)
 constexpr uint32_t kRefOwn = 1u << 28;      // the entity's own client
 
@@ -423,7 +425,7 @@ __device__ __forceinline__ bool fan_stage(const FanArgs& a, const FanGeo& fg, ui
                                           uint32_t* red, uint32_t* tot_sh) {
   const int ncell = fg.W * fg.Hh;
   const bool lds = fg.g.reach > 0 && ncell <= kFanRegCells &&
-                   stage_region<kSy, kFanRegCells, kFanLdsRecs>(fg.g, a.ccs, fg.cx0, fg.cz0, fg.W, ncell, cst, crl, red,
+                   stage_region<kSy, kFanRegCells, kDirLdsRecs>(fg.g, a.ccs, fg.cx0, fg.cz0, fg.W, ncell, cst, crl, red,
                                                                  tot_sh, [&](uint32_t q) {
                                                                    const uint4 c = a.crec[q];
                                                                    return make_uint4(c.x, c.y, c.z, q);
@@ -450,8 +452,8 @@ __device__ __forceinline__ uint32_t gate_bump(uint32_t (&c)[kDirectGates], uint3
 
 __global__ void __launch_bounds__(kSy) k_fan_dcount(FanArgs a) {
   __shared__ uint16_t cst[kFanRegCells + 1];
-  __shared__ uint4 crl[kFanLdsRecs];
-  __shared__ uint8_t cgl[kFanLdsRecs];
+  __shared__ uint4 crl[kDirLdsRecs];
+  __shared__ uint8_t cgl[kDirLdsRecs];
   __shared__ uint32_t gsum[kDirectGates];
   __shared__ uint32_t red[kSy / 64];
   __shared__ uint32_t tot_sh;
@@ -515,8 +517,8 @@ __global__ void __launch_bounds__(kSy) k_fan_dcount(FanArgs a) {
 
 __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k_fan_dwrite(FanArgs a) {
   __shared__ uint16_t cst[kFanRegCells + 1];
-  __shared__ uint4 crl[kFanLdsRecs];
-  __shared__ uint8_t cgl[kFanLdsRecs];
+  __shared__ uint4 crl[kDirLdsRecs];
+  __shared__ uint8_t cgl[kDirLdsRecs];
   __shared__ uint32_t gbase[kDirectGates];      // out index of the round's first record of each gate
   __shared__ uint32_t wred[kDirectGates][kSy / 64];
   __shared__ uint32_t groff[kDirectGates];      // round position of each gate's first record
@@ -814,8 +816,7 @@ struct IngArgs {
   uint32_t n;        // records in the payload
   uint32_t seg;      // first record of this batch
   uint32_t hmask;
-  const uint4* hkey;
-  const uint32_t* hval;
+  const uint4* hb;       // buckets: [2b] key, [2b + 1].x slot (kHEmpty / kHTomb)
   const uint32_t* seq;
   uint8_t* flags;
   float* y;
@@ -842,9 +843,10 @@ __global__ void __launch_bounds__(kSy) k_ing_resolve(IngArgs a) {
     const uint4 id = a.rec[2 * i];
     uint32_t b = id_hash(id) & a.hmask, slot = kNone;
     for (;;) {
-      const uint32_t v = a.hval[b];
+      const uint4 k = a.hb[2 * (size_t)b];  // key and slot of a bucket: one 32-B line, both loads together
+      const uint32_t v = a.hb[2 * (size_t)b + 1].x;
       if (v == kHEmpty) break;
-      if (v != kHTomb && id_eq(a.hkey[b], id)) {
+      if (v != kHTomb && id_eq(k, id)) {
         slot = v;
         break;
       }
@@ -964,8 +966,7 @@ struct SyncState {
   float* yaw = nullptr;
   // EntityID -> slot: host-owned open addressing table, mirrored to HBM
   uint32_t hcap = 0, n_tomb = 0;
-  uint4* d_hkey = nullptr;
-  uint32_t* d_hval = nullptr;
+  uint4* d_hb = nullptr;  // 2 x hcap: the buckets (k_ing_resolve)
   std::vector<uint4> h_hkey;
   std::vector<uint32_t> h_hval;
   std::vector<uint4> h_id_of;      // slot -> registered id (zero: none)
@@ -1032,7 +1033,7 @@ struct SyncState {
 
 void sync_free(SyncState* s) {
   if (!s) return;
-  void* p[] = {s->flags, s->gate, s->cid, s->eid, s->y, s->yaw, s->d_hkey, s->d_hval, s->cnt, s->cpos, s->ccs,
+  void* p[] = {s->flags, s->gate, s->cid, s->eid, s->y, s->yaw, s->d_hb, s->cnt, s->cpos, s->ccs,
                s->crec, s->cgate, s->ccid, s->info, s->tstat, s->pairs, s->gcnt, s->wantj, s->tg,
                s->ghist, s->out, s->d_goff, s->scan.status, s->d_payload, s->res, s->first, s->ictr, s->bcnt,
                s->op_slot, s->op_x, s->op_z};
@@ -1188,9 +1189,12 @@ void rehash(SyncState* s) {
 
 int upload_hash(const MgrView& v, SyncState* s) {
   if (s->dirty_all) {
-    SCHK(hipMemcpyAsync(s->d_hkey, s->h_hkey.data(), (size_t)s->hcap * sizeof(uint4), hipMemcpyHostToDevice, v.stream));
-    SCHK(hipMemcpyAsync(s->d_hval, s->h_hval.data(), (size_t)s->hcap * sizeof(uint32_t), hipMemcpyHostToDevice,
-                        v.stream));
+    std::vector<uint4> hb(2 * (size_t)s->hcap);
+    for (uint32_t b = 0; b < s->hcap; ++b) {
+      hb[2 * (size_t)b] = s->h_hkey[b];
+      hb[2 * (size_t)b + 1] = make_uint4(s->h_hval[b], 0u, 0u, 0u);
+    }
+    SCHK(hipMemcpyAsync(s->d_hb, hb.data(), hb.size() * sizeof(uint4), hipMemcpyHostToDevice, v.stream));
     SCHK(hipStreamSynchronize(v.stream));
     for (uint32_t b : s->dirty) s->is_dirty[b] = 0;
     s->dirty.clear();
@@ -1213,7 +1217,7 @@ int upload_hash(const MgrView& v, SyncState* s) {
   SRCHK(up.put(val, &d_val));
   SRCHK(up.put(key, &d_key));
   hipLaunchKernelGGL(k_hash_scatter, dim3(blocks_for(idx.size())), dim3(kSy), 0, v.stream, d_idx, d_key, d_val,
-                     (uint32_t)idx.size(), s->d_hkey, s->d_hval);
+                     (uint32_t)idx.size(), s->d_hb);
   SCHK(hipGetLastError());
   SCHK(hipStreamSynchronize(v.stream));
   return GWAOI_OK;
@@ -1346,8 +1350,7 @@ int gwaoi_sync_enable(gwaoi_mgr* m, uint32_t n_gates) {
   bool ok = hipMalloc((void**)&s->flags, C) == hipSuccess && hipMalloc((void**)&s->gate, C * 2) == hipSuccess &&
             hipMalloc((void**)&s->cid, C * 16) == hipSuccess && hipMalloc((void**)&s->eid, C * 16) == hipSuccess &&
             hipMalloc((void**)&s->y, C * 4) == hipSuccess && hipMalloc((void**)&s->yaw, C * 4) == hipSuccess &&
-            hipMalloc((void**)&s->d_hkey, (size_t)s->hcap * 16) == hipSuccess &&
-            hipMalloc((void**)&s->d_hval, (size_t)s->hcap * 4) == hipSuccess &&
+            hipMalloc((void**)&s->d_hb, (size_t)s->hcap * 32) == hipSuccess &&
             hipMalloc((void**)&s->first, C * 4) == hipSuccess && hipMalloc((void**)&s->ictr, 64) == hipSuccess &&
             hipHostMalloc((void**)&s->h_small, (8 + GWAOI_SYNC_MAX_GATES + 1) * 4, hipHostMallocDefault) == hipSuccess &&
             hipMalloc((void**)&s->d_goff, (GWAOI_SYNC_MAX_GATES + 1) * 4) == hipSuccess;
@@ -1358,7 +1361,7 @@ int gwaoi_sync_enable(gwaoi_mgr* m, uint32_t n_gates) {
          hipMemsetAsync(s->eid, 0, C * 16, v.stream) == hipSuccess &&
          hipMemsetAsync(s->y, 0, C * 4, v.stream) == hipSuccess && hipMemsetAsync(s->yaw, 0, C * 4, v.stream) == hipSuccess &&
          hipMemsetAsync(s->first, 0xFF, C * 4, v.stream) == hipSuccess &&
-         hipMemsetAsync(s->d_hval, 0xFF, (size_t)s->hcap * 4, v.stream) == hipSuccess &&
+         hipMemsetAsync(s->d_hb, 0xFF, (size_t)s->hcap * 32, v.stream) == hipSuccess &&
          hipStreamSynchronize(v.stream) == hipSuccess;
   }
   if (!ok) {
@@ -1845,8 +1848,7 @@ int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes,
   a.rec = (const uint4*)src;
   a.n = n;
   a.hmask = s->hcap - 1;
-  a.hkey = s->d_hkey;
-  a.hval = s->d_hval;
+  a.hb = s->d_hb;
   a.seq = v.seq;
   a.flags = s->flags;
   a.y = s->y;
