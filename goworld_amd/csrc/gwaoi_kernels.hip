@@ -2066,7 +2066,6 @@ k_sweep_dense(SweepArgs a) {
   const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
   const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t nent = 0;
-  bool uns = false;  // a mover of this wave has events numbered in walk order (wave-uniform)
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
   __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the wave's batch of movers: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
 #if GW_STAMPS
@@ -2209,7 +2208,6 @@ k_sweep_dense(SweepArgs a) {
         }
       }
       if (lane == 0) put_count(a.rank_cnt, m.rank, local);
-      uns |= local > 1u;
     }
     __builtin_amdgcn_wave_barrier();  // every read of the batch before the next batch is written
   }
@@ -2218,7 +2216,10 @@ k_sweep_dense(SweepArgs a) {
   if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
   const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);  // one add per wave, not per lane
   if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
-  if (lane == 0 && uns) a.ctr[CTR_UNSORTED] = 1u;
+  // (a dense mover's events are numbered in walk order: the slices are sorted whenever the list is not
+  // empty. Flagging only the movers with two or more events, a per-mover flag in the walk loop, made
+  // this kernel 66% slower on strips_skew: 484 -> 803 us, r04_c8)
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nd) a.ctr[CTR_UNSORTED] = 1u;
 #if GW_STAMPS
   if (lane == 0)
     for (int k = 0; k < 16; ++k) atomicAdd(&gw_stamps[kStampWords * 16383 + k], dph[k]);

@@ -454,7 +454,7 @@ __global__ void __launch_bounds__(kSy) k_fan_dcount(FanArgs a) {
   __shared__ uint16_t cst[kFanRegCells + 1];
   __shared__ uint4 crl[kDirLdsRecs];
   __shared__ uint8_t cgl[kDirLdsRecs];
-  __shared__ uint32_t gsum[kDirectGates];
+  __shared__ uint32_t gred[kDirectGates][kSy / 64];
   __shared__ uint32_t red[kSy / 64];
   __shared__ uint32_t tot_sh;
   __shared__ unsigned long long rp[kSy / 64];
@@ -466,11 +466,13 @@ __global__ void __launch_bounds__(kSy) k_fan_dcount(FanArgs a) {
     if (threadIdx.x == 0) a.tstat[t] = make_uint4(0u, 0u, 0u, 0u);
     return;
   }
-  if (threadIdx.x < kDirectGates) gsum[threadIdx.x] = 0u;
   const bool lds = fan_stage(a, fg, cst, crl, cgl, red, &tot_sh);
   __syncthreads();
   uint32_t ents = 0;
   unsigned long long psum = 0;
+  uint32_t gtot[kDirectGates];  // the thread's pairs per gate over its rounds (reduced once per tile)
+#pragma unroll
+  for (uint32_t g = 0; g < kDirectGates; ++g) gtot[g] = 0u;
   const uint32_t tid = threadIdx.x;
   for (uint32_t jb = fg.j0; jb < fg.j1; jb += kSy) {
     const uint32_t j = jb + tid;
@@ -490,7 +492,6 @@ __global__ void __launch_bounds__(kSy) k_fan_dcount(FanArgs a) {
         fan_pairs(a, fg, lds, cst, crl, cgl, j, ra, s, gs, [&](uint32_t g, uint32_t, uint32_t) {
           if (g < G) gate_bump(c, g);
         });
-      if (a.clear) a.flags[s] = (uint8_t)(fl & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
     }
     a.wantj[j] = want;
     uint4* dst = reinterpret_cast<uint4*>(a.gcnt + (size_t)j * a.gstride);
@@ -499,14 +500,26 @@ __global__ void __launch_bounds__(kSy) k_fan_dcount(FanArgs a) {
 #pragma unroll
     for (uint32_t g = 0; g < kDirectGates; ++g) {
       psum += c[g];
-      if (c[g]) atomicAdd(&gsum[g], c[g]);  // LDS
+      gtot[g] += c[g];
     }
+  }
+  // tile totals per gate: wave sums, then the block's (one LDS word per wave and gate)
+#pragma unroll
+  for (uint32_t g = 0; g < kDirectGates; ++g) {
+    uint32_t v = gtot[g];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((tid & 63) == 0) gred[g][tid >> 6] = v;
   }
   for (int o = 32; o > 0; o >>= 1) psum += __shfl_xor(psum, o, 64);
   for (int o = 32; o > 0; o >>= 1) ents += __shfl_xor(ents, o, 64);
   if ((tid & 63) == 0) red[tid >> 6] = ents, rp[tid >> 6] = psum;
   __syncthreads();
-  if (tid < G) a.tg[tid * a.ntiles + t] = gsum[tid];
+  if (tid < G) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < kSy / 64; ++k) v += gred[tid][k];
+    a.tg[tid * a.ntiles + t] = v;
+  }
   if (tid == 0) {
     uint32_t tot = 0;
     unsigned long long pt = 0;
@@ -667,6 +680,22 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
     if (tid < G) gbase[tid] += gtot[tid];
     __syncthreads();
   }
+}
+
+// direct fan-out: the sync bits of EVERY slot cleared after the count pass read them (a collected
+// entity's bits clear, and so do an absent slot's: k_clear_absent's contract), one coalesced pass
+// instead of a random byte write per collected entity
+__global__ void __launch_bounds__(kSy) k_clear_sync_bits(uint8_t* flags, uint32_t cap) {
+  const uint32_t n16 = cap / 16;
+  constexpr uint32_t kMask = 0x01010101u * (uint32_t)(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
+  uint4* f4 = reinterpret_cast<uint4*>(flags);
+  for (uint32_t i = blockIdx.x * kSy + threadIdx.x; i < n16; i += gridDim.x * kSy) {
+    uint4 v = f4[i];
+    v.x &= ~kMask, v.y &= ~kMask, v.z &= ~kMask, v.w &= ~kMask;
+    f4[i] = v;
+  }
+  for (uint32_t s = 16 * n16 + blockIdx.x * kSy + threadIdx.x; s < cap; s += gridDim.x * kSy)
+    flags[s] = (uint8_t)(flags[s] & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
 }
 
 // gate offsets of the direct fan-out: the scanned (gate, tile) blocks' first records (g = G: the total)
@@ -1261,6 +1290,9 @@ int collect_direct(const MgrView& v, SyncState* s, FanArgs f, uint32_t opts, gwa
   f.ntiles = ntiles;
   if (v.timing) SCHK(hipEventRecord(s->tev[1], st));
   hipLaunchKernelGGL(k_fan_dcount, dim3(ntiles), dim3(kSy), 0, st, f);
+  if (f.clear)
+    hipLaunchKernelGGL(k_clear_sync_bits, dim3(std::min<uint32_t>(blocks_for(s->cap / 16 + 1), 2048)), dim3(kSy), 0, st,
+                       s->flags, s->cap);
   hipLaunchKernelGGL(k_fan_total, dim3(1), dim3(1024), 0, st, (const uint4*)s->tstat, ntiles, s->ictr + 8,
                      (unsigned long long*)(s->ictr + 10));
   launch_scan(s->scan, s->tg, (uint32_t)tgn, st);
@@ -1635,7 +1667,8 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   s->goff64.assign(s->n_gates + 1, 0);
   out->gate_off = s->goff64.data();
   hipStream_t st = v.stream;
-  if (!(opts & GWAOI_COLLECT_KEEP_FLAGS)) {  // absent slots: their sync bits clear without records
+  const bool direct = s->n_gates <= gw::kDirectGates && s->fan_mode == 0 && v.g.rec && v.ntiles;
+  if (!(opts & GWAOI_COLLECT_KEEP_FLAGS) && !direct) {  // absent slots: their sync bits clear without records
     hipLaunchKernelGGL(gw::k_clear_absent, dim3(std::min<uint32_t>(gw::blocks_for(s->cap), 4096)), dim3(gw::kSy), 0, st,
                        s->flags, v.seq, s->cap);
     SCHK(hipGetLastError());
@@ -1693,7 +1726,7 @@ int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   if (!ntiles) return GWAOI_OK;
   SRCHK(gw::dgrow32(&s->tstat, &s->tstat_n, ntiles));
   f.tstat = s->tstat;
-  if (s->n_gates <= gw::kDirectGates && s->fan_mode == 0) return gw::collect_direct(v, s, f, opts, out);
+  if (direct) return gw::collect_direct(v, s, f, opts, out);
   // pair list + gate partition
   SRCHK(gw::dgrow32(&s->cnt, &s->cnt_n, (uint64_t)bound + 1));
   SRCHK(gw::dgrow(&s->info, &s->info_cap, 2 * ((uint64_t)bound + 1)));
