@@ -2218,7 +2218,7 @@ k_sweep_dense(SweepArgs a) {
   if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
   // (a dense mover's events are numbered in walk order: the slices are sorted whenever the list is not
   // empty. Flagging only the movers with two or more events, a per-mover flag in the walk loop, made
-  // this kernel 66% slower on strips_skew: 484 -> 803 us, r04_c8)
+  // this kernel 66% slower on strips_skew: 484 -> 803 us, r04_c9)
   if (blockIdx.x == 0 && threadIdx.x == 0 && nd) a.ctr[CTR_UNSORTED] = 1u;
 #if GW_STAMPS
   if (lane == 0)
