@@ -364,9 +364,9 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
 // partition path: gates in order, entities in grid order, each entity's run contiguous with its own
 // client's record first.
 constexpr uint32_t kDirectGates = 8;
-constexpr uint32_t kRoundRecs = 3072;   // a round's staged records (12 KB of references)
-constexpr int kDirLdsRecs = 512;        // staged sub-grid records of the direct kernels (config 2: ~210 per
-                                        // region); smaller LDS: 4 blocks per CU instead of 3
+constexpr uint32_t kRoundRecs = 2560;   // a round's staged records (10 KB of references)
+constexpr int kDirLdsRecs = 384;        // staged sub-grid records of the direct kernels (config 2: ~210 per
+                                        // region); with the write pass's ClientIDs, 4 blocks per CU
 constexpr uint32_t kRefSkip = 0xFFFFFFFFu;  // written directly (receiver outside the LDS region)
 constexpr uint32_t kRefOwn = 1u << 28;      // the entity's own client
 
@@ -422,7 +422,7 @@ __device__ __forceinline__ void fan_pairs(const FanArgs& a, const FanGeo& fg, bo
 
 // stage the tile's region of the client sub-grid (and each staged record's gate); false: walk global
 __device__ __forceinline__ bool fan_stage(const FanArgs& a, const FanGeo& fg, uint16_t* cst, uint4* crl, uint8_t* cgl,
-                                          uint32_t* red, uint32_t* tot_sh) {
+                                          uint32_t* red, uint32_t* tot_sh, uint4* cidl = nullptr) {
   const int ncell = fg.W * fg.Hh;
   const bool lds = fg.g.reach > 0 && ncell <= kFanRegCells &&
                    stage_region<kSy, kFanRegCells, kDirLdsRecs>(fg.g, a.ccs, fg.cx0, fg.cz0, fg.W, ncell, cst, crl, red,
@@ -432,7 +432,11 @@ __device__ __forceinline__ bool fan_stage(const FanArgs& a, const FanGeo& fg, ui
                                                                  });
   if (lds) {
     const uint32_t ns = cst[ncell];
-    for (uint32_t p = threadIdx.x; p < ns; p += kSy) cgl[p] = a.cgate[crl[p].w];
+    for (uint32_t p = threadIdx.x; p < ns; p += kSy) {
+      const uint32_t q = crl[p].w;
+      cgl[p] = a.cgate[q];
+      if (cidl) cidl[p] = a.ccid[q];  // (write pass: the receivers' ClientIDs, gathered once per region)
+    }
     __syncthreads();
   }
   return lds;
@@ -537,6 +541,7 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
   __shared__ uint32_t groff[kDirectGates];      // round position of each gate's first record
   __shared__ uint32_t gtot[kDirectGates];       // the round's records of each gate
   __shared__ uint32_t ref[kRoundRecs];
+  __shared__ uint4 cidl[kDirLdsRecs];           // the staged receivers' ClientIDs
   __shared__ uint4 ent[kSy][2];                 // the round's entities: EntityID, {x, y, z, yaw}
   __shared__ uint4 ocid[kSy];                   // and their own client's id
   __shared__ uint32_t red[kSy / 64];
@@ -545,7 +550,7 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
   const FanGeo fg = fan_geo(a, t);
   if (fg.j0 == fg.j1) return;
   if (tid < G) gbase[tid] = a.tg[tid * a.ntiles + t];
-  const bool lds = fan_stage(a, fg, cst, crl, cgl, red, &tot_sh);
+  const bool lds = fan_stage(a, fg, cst, crl, cgl, red, &tot_sh, cidl);
   __syncthreads();  // gbase
   const int lane = tid & 63, w = tid >> 6;
   for (uint32_t jb = fg.j0; jb < fg.j1; jb += kSy) {  // block-uniform
@@ -664,7 +669,7 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
         dst = live && d < a.out_cap ? 3 * (size_t)d + k : kNoDst;
         if (!live) return make_uint4(0, 0, 0, 0);
         if (k != 0) return ent[owner][k - 1];
-        return (v & kRefOwn) ? ocid[owner] : a.ccid[crl[v & 0xFFFu].w];
+        return (v & kRefOwn) ? ocid[owner] : cidl[v & 0xFFFu];
       };
       for (uint32_t i0 = tid; i0 < nq; i0 += 4 * kSy) {
         size_t d0, d1, d2, d3;
