@@ -570,6 +570,19 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
         }
       }
     }
+    // the entity's record and slot state: issued before the scan below, whose barriers then overlap them
+    uint4 eid = make_uint4(0, 0, 0, 0), info = make_uint4(0, 0, 0, 0), own = make_uint4(0, 0, 0, 0);
+    uint4 ra = make_uint4(0, 0, 0, 0);
+    uint32_t s = 0;
+    uint16_t gs = GWAOI_SYNC_NO_CLIENT;
+    if (want) {
+      ra = a.g.rec[j].a;
+      s = ra.z & REC_SLOT;
+      gs = a.gate[s];
+      eid = a.eid[s];
+      info = make_uint4(ra.x, __float_as_uint(a.y[s]), ra.y, __float_as_uint(a.yaw[s]));
+      if ((want & GWAOI_SYNC_OWN_CLIENT) && gs < G) own = a.ccid[a.cpos[j]];
+    }
     // block scan of the per-gate counts: wave scans, then the waves' totals
     uint32_t inc[kDirectGates];
 #pragma unroll
@@ -609,22 +622,12 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
         roff += c[g];
       }
     }
-    __syncthreads();  // groff / gtot
-    uint4 eid = make_uint4(0, 0, 0, 0), info = make_uint4(0, 0, 0, 0), own = make_uint4(0, 0, 0, 0);
-    uint4 ra = make_uint4(0, 0, 0, 0);
-    uint32_t s = 0;
-    uint16_t gs = GWAOI_SYNC_NO_CLIENT;
-    if (want) {
-      ra = a.g.rec[j].a;
-      s = ra.z & REC_SLOT;
-      gs = a.gate[s];
-      eid = a.eid[s];
-      info = make_uint4(ra.x, __float_as_uint(a.y[s]), ra.y, __float_as_uint(a.yaw[s]));
-      if ((want & GWAOI_SYNC_OWN_CLIENT) && gs < G) own = a.ccid[a.cpos[j]];
+    if (want) {  // (the previous round's copy-out read ent / ocid before its last barrier)
       ent[tid][0] = eid;
       ent[tid][1] = info;
       ocid[tid] = own;
     }
+    __syncthreads();  // groff / gtot
     auto put_direct = [&](uint32_t dst, const uint4& cid) {
       if (dst < a.out_cap) {
         a.out[3 * (size_t)dst] = cid;
@@ -638,21 +641,21 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
         if (!staged) put_direct(pos, own);
         else if (pos < kRoundRecs) ref[pos] = kRefOwn | (tid << 12) | ((uint32_t)gs << 20);
       }
-      if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS)
-        fan_pairs(a, fg, lds, cst, crl, cgl, j, ra, s, gs, [&](uint32_t g, uint32_t p, uint32_t q) {
-          if (g >= G) return;
-          const uint32_t pos = gate_bump(cur, g);
-          if (!staged) {
-            put_direct(pos, a.ccid[q]);
-          } else if (pos < kRoundRecs) {
-            if (p != kNone) {
-              ref[pos] = p | (tid << 12) | (g << 20);
-            } else {  // a receiver outside the staged region: written now, skipped by the copy-out
-              ref[pos] = kRefSkip;
-              put_direct(gbase[g] + (pos - groff[g]), a.ccid[q]);
-            }
+      auto pair = [&](uint32_t g, uint32_t p, uint32_t q) {
+        if (g >= G) return;
+        const uint32_t pos = gate_bump(cur, g);
+        if (!staged) {
+          put_direct(pos, p != kNone ? cidl[p] : a.ccid[q]);
+        } else if (pos < kRoundRecs) {
+          if (p != kNone) {
+            ref[pos] = p | (tid << 12) | (g << 20);
+          } else {  // a receiver outside the staged region: written now, skipped by the copy-out
+            ref[pos] = kRefSkip;
+            put_direct(gbase[g] + (pos - groff[g]), a.ccid[q]);
           }
-        });
+        }
+      };
+      if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS) fan_pairs(a, fg, lds, cst, crl, cgl, j, ra, s, gs, pair);
     }
     __syncthreads();
     if (staged) {  // copy-out: record r of the round, 16-B part k, over consecutive addresses per gate;
@@ -701,6 +704,15 @@ __global__ void __launch_bounds__(kSy) k_clear_sync_bits(uint8_t* flags, uint32_
   }
   for (uint32_t s = 16 * n16 + blockIdx.x * kSy + threadIdx.x; s < cap; s += gridDim.x * kSy)
     flags[s] = (uint8_t)(flags[s] & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
+}
+
+// two small device ranges into the mapped host words the host reads after the stream synchronises (no
+// DMA copy per range: each cost a copy-engine round trip on the collect / ingest critical path)
+__global__ void k_to_host(const uint32_t* __restrict__ a, uint32_t na, uint32_t oa, const uint32_t* __restrict__ b,
+                          uint32_t nb, uint32_t ob, uint32_t* h) {
+  for (uint32_t i = threadIdx.x; i < na; i += blockDim.x) h[oa + i] = a[i];
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) h[ob + i] = b[i];
+  __threadfence_system();
 }
 
 // gate offsets of the direct fan-out: the scanned (gate, tile) blocks' first records (g = G: the total)
@@ -1044,7 +1056,8 @@ struct SyncState {
   uint8_t* h_out = nullptr;
   uint64_t h_out_cap = 0;
   uint32_t* d_goff = nullptr;
-  uint32_t* h_small = nullptr;  // pinned: [0..3] counters, [4..] gate offsets
+  uint32_t* h_small = nullptr;  // pinned (mapped): [0..3] counters, [4..] gate offsets
+  uint32_t* d_small = nullptr;  // its device address (k_to_host), null: DMA copies instead
   std::vector<uint64_t> goff64;
   ScanCtx scan;
   uint32_t scan_words = 0;
@@ -1313,8 +1326,13 @@ int collect_direct(const MgrView& v, SyncState* s, FanArgs f, uint32_t opts, gwa
       SCHK(hipEventRecord(s->tev[5], st));
     }
     SCHK(hipGetLastError());
-    SCHK(hipMemcpyAsync(s->h_small + 8, s->d_goff, (G + 1) * 4, hipMemcpyDeviceToHost, st));
-    SCHK(hipMemcpyAsync(s->h_small + 4, s->ictr + 8, 16, hipMemcpyDeviceToHost, st));
+    if (s->d_small) {
+      hipLaunchKernelGGL(k_to_host, dim3(1), dim3(64), 0, st, (const uint32_t*)s->d_goff, G + 1, 8u,
+                         (const uint32_t*)(s->ictr + 8), 4u, 4u, s->d_small);
+    } else {
+      SCHK(hipMemcpyAsync(s->h_small + 8, s->d_goff, (G + 1) * 4, hipMemcpyDeviceToHost, st));
+      SCHK(hipMemcpyAsync(s->h_small + 4, s->ictr + 8, 16, hipMemcpyDeviceToHost, st));
+    }
     SCHK(hipStreamSynchronize(st));
     return GWAOI_OK;
   };
@@ -1389,7 +1407,8 @@ int gwaoi_sync_enable(gwaoi_mgr* m, uint32_t n_gates) {
             hipMalloc((void**)&s->y, C * 4) == hipSuccess && hipMalloc((void**)&s->yaw, C * 4) == hipSuccess &&
             hipMalloc((void**)&s->d_hb, (size_t)s->hcap * 32) == hipSuccess &&
             hipMalloc((void**)&s->first, C * 4) == hipSuccess && hipMalloc((void**)&s->ictr, 64) == hipSuccess &&
-            hipHostMalloc((void**)&s->h_small, (8 + GWAOI_SYNC_MAX_GATES + 1) * 4, hipHostMallocDefault) == hipSuccess &&
+            hipHostMalloc((void**)&s->h_small, (8 + GWAOI_SYNC_MAX_GATES + 1) * 4,
+                          hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
             hipMalloc((void**)&s->d_goff, (GWAOI_SYNC_MAX_GATES + 1) * 4) == hipSuccess;
   if (ok) {
     ok = hipMemsetAsync(s->flags, 0, C, v.stream) == hipSuccess &&
@@ -1400,6 +1419,11 @@ int gwaoi_sync_enable(gwaoi_mgr* m, uint32_t n_gates) {
          hipMemsetAsync(s->first, 0xFF, C * 4, v.stream) == hipSuccess &&
          hipMemsetAsync(s->d_hb, 0xFF, (size_t)s->hcap * 32, v.stream) == hipSuccess &&
          hipStreamSynchronize(v.stream) == hipSuccess;
+  }
+  if (ok) {
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, s->h_small, 0) == hipSuccess) s->d_small = (uint32_t*)dp;
+    else (void)hipGetLastError();
   }
   if (!ok) {
     gw::set_error("sync_enable: device allocation failed");
@@ -1917,8 +1941,13 @@ int gwaoi_ingest_positions(gwaoi_mgr* m, const uint8_t* payload, uint64_t bytes,
     SCHK(hipGetLastError());
     const uint32_t bound = std::min<uint32_t>(n - seg, s->cap);
     SRCHK(gw::mgr_stage_moves_device_n(m, s->op_slot, s->op_x, s->op_z, s->bcnt + nseg, bound));
-    SCHK(hipMemcpyAsync(s->h_small, s->ictr, 16, hipMemcpyDeviceToHost, st));
-    SCHK(hipMemcpyAsync(s->h_small + 4, s->bcnt + nseg, 4, hipMemcpyDeviceToHost, st));
+    if (s->d_small) {
+      hipLaunchKernelGGL(gw::k_to_host, dim3(1), dim3(64), 0, st, (const uint32_t*)s->ictr, 4u, 0u,
+                         (const uint32_t*)(s->bcnt + nseg), 1u, 4u, s->d_small);
+    } else {
+      SCHK(hipMemcpyAsync(s->h_small, s->ictr, 16, hipMemcpyDeviceToHost, st));
+      SCHK(hipMemcpyAsync(s->h_small + 4, s->bcnt + nseg, 4, hipMemcpyDeviceToHost, st));
+    }
     SCHK(hipStreamSynchronize(st));
     if (v.timing) {
       float t;
