@@ -162,3 +162,33 @@ def test_small_pass_above_fused_order_ops(gpu, po):
     for t, ops in enumerate(case["ticks"]):
         _same(H.gpu_tick(eng, ops), H.oracle_tick(orc, ops), f"tick {t}")
     assert eng.debug_small_pass() >= 3
+
+
+def test_single_op_pass_over_the_event_buffers(gpu, po):
+    """A single Enter into a crowd of 70,000 (restored silently from a device batch): its 70,000 events
+    exceed the event buffers, so the one-kernel pass (apply, sweep, order) overflows and the pass is
+    re-run as a plain k_sweep_small without applying the op again; then the Leave of the same slot."""
+    from goworld_amd import _lib
+    from goworld_amd.engine import DeviceBuffer, Engine
+    rng = np.random.default_rng(23)
+    n, D = 70000, 100.0
+    bounds = (0.0, 0.0, 1000.0, 1000.0)
+    x = rng.uniform(450, 550, n).astype(np.float32)
+    z = rng.uniform(450, 550, n).astype(np.float32)
+    eng = Engine(D, capacity=n + 1, bounds=bounds)
+    bs, bx, bz, bk = DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(n)
+    bs.upload(np.arange(n, dtype=np.uint32))
+    bx.upload(x)
+    bz.upload(z)
+    bk.upload(np.full(n, _lib.GWAOI_OP_ENTER | _lib.GWAOI_OP_SILENT, np.uint8))
+    eng.stage_ops_device(bs.ptr, bx.ptr, bz.ptr, bk.ptr, n)
+    assert len(eng.tick()) == 0
+    eng.adopt_device_state()
+    orc = po.GridOracle(D, n + 1, bounds)
+    orc.bulk_enter(np.arange(n, dtype=np.uint32), x, z)
+    n0 = eng.debug_small_pass()
+    for op in [(H.ENTER, n, 500.0, 500.0), (H.LEAVE, n, 0.0, 0.0)]:
+        got, want = H.gpu_tick(eng, [op]), H.oracle_tick(orc, [op])
+        assert len(want) == n
+        _same(got, want, f"op {op[0]}")
+    assert eng.debug_small_pass() - n0 == 2
