@@ -151,6 +151,7 @@ struct FanArgs {
   uint32_t ntiles;
   uint4* out;            // write pass: the wire records, 3 uint4 each
   uint32_t out_cap;      // records out holds (nothing is written past it: the host grows it and re-runs)
+  const uint4* pk;       // direct passes: per slot {EntityID}, {y, yaw, gate | flags << 16, 0} (k_sync_pack)
 };
 
 struct ClientGridArgs {
@@ -363,7 +364,34 @@ __global__ void __launch_bounds__(kSy) k_fan_tile(FanArgs a) {
 // packet, copied out 16 B per lane over consecutive addresses. Same records and order as the
 // partition path: gates in order, entities in grid order, each entity's run contiguous with its own
 // client's record first.
+#ifndef GW_FAN_UNROLL  // candidates of a row judged per step of the pair walk (loads in flight together)
+#define GW_FAN_UNROLL 2
+#endif
+#ifndef GW_ABL_FAN  // ablation (timing only), write pass without: 1 its copy-out, 2 + its pair walk, 3 + the region
+                    // staging, 4 + the entities' loads
+#define GW_ABL_FAN 0
+#endif
 constexpr uint32_t kDirectGates = 8;
+
+// The per-slot fields the direct passes read for each collected entity, packed into one 32-B record per
+// slot at the start of the collect: {EntityID}, {y, yaw, gate | flags << 16, 0}. The passes visit the
+// entities in grid order, i.e. at random slots: one 32-B gather per entity instead of a line fetched
+// per field (54 of the write pass's 217 us were those gathers, r04_c17). (On a side stream beside the
+// count pass instead, both ran slower: tick 0.66 -> 0.69 ms, r04_c21.) With `clear`, the sync bits of
+// EVERY slot are cleared here, once packed (a collected entity's bits clear, and so do an absent slot's:
+// k_clear_absent's contract); nothing after the pack reads them.
+__global__ void __launch_bounds__(kSy) k_sync_pack(uint8_t* __restrict__ flags, const uint16_t* __restrict__ gate,
+                                                   const uint4* __restrict__ eid, const float* __restrict__ y,
+                                                   const float* __restrict__ yaw, uint32_t cap, int clear,
+                                                   uint4* __restrict__ pk) {
+  for (uint32_t s = blockIdx.x * kSy + threadIdx.x; s < cap; s += gridDim.x * kSy) {
+    const uint8_t fl = flags[s];
+    pk[2 * (size_t)s] = eid[s];
+    pk[2 * (size_t)s + 1] = make_uint4(__float_as_uint(y[s]), __float_as_uint(yaw[s]),
+                                       (uint32_t)gate[s] | ((uint32_t)fl << 16), 0u);
+    if (clear) flags[s] = fl & (uint8_t)~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
+  }
+}
 constexpr uint32_t kRoundRecs = 2560;   // a round's staged records (10 KB of references)
 constexpr int kDirLdsRecs = 384;        // staged sub-grid records of the direct kernels (config 2: ~210 per
                                         // region); with the write pass's ClientIDs, 4 blocks per CU
@@ -392,28 +420,38 @@ __device__ __forceinline__ FanGeo fan_geo(const FanArgs& a, uint32_t t) {
   return f;
 }
 
-// Every client neighbour of record j's entity (the pair predicate of k_fan_tile): f(gate, lds index
-// or kNone, sub-grid index)
+// Every client neighbour of the entity of main record ra (the pair predicate of k_fan_tile): f(gate, lds
+// index or kNone, sub-grid index). qs: the record's seq_end, selfq: the entity's own sub-grid record or
+// 0xffffffff (loaded by the caller, ahead of the walk).
 template <class F>
 __device__ __forceinline__ void fan_pairs(const FanArgs& a, const FanGeo& fg, bool lds, const uint16_t* cst,
-                                          const uint4* crl, const uint8_t* cgl, uint32_t j, uint4 ra, uint32_t s,
-                                          uint16_t gs, F&& f) {
+                                          const uint4* crl, const uint8_t* cgl, uint32_t qs, uint32_t selfq, uint4 ra,
+                                          uint32_t s, F&& f) {
   const Geom& g = fg.g;
   const float sx = __uint_as_float(ra.x), sz = __uint_as_float(ra.y);
-  const uint32_t qs = a.g.rec[j].b.w;
   const CellBox B = qbox(g, sx, sz);
   if (lds && B.x0 >= fg.cx0 && B.x1 <= fg.cx1 && B.z0 >= fg.cz0 && B.z1 <= fg.cz1) {
     const float D = g.D;
-    const uint32_t selfq = gs != GWAOI_SYNC_NO_CLIENT ? a.cpos[j] : 0xffffffffu;
+    auto test = [&](const uint4 cr, uint32_t p) {
+      const float ox = __uint_as_float(cr.x), oz = __uint_as_float(cr.y);
+      const bool in = cr.w != selfq && ((cr.z > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz));
+      if (in) f((uint32_t)cgl[p], p, cr.w);
+    };
     for (int r = B.z0; r <= B.z1; ++r) {
       const int rb = (r - fg.cz0) * fg.W - fg.cx0;
       const uint32_t e = cst[rb + B.x1 + 1];
-      for (uint32_t p = cst[rb + B.x0]; p < e; ++p) {
-        const uint4 cr = crl[p];
-        const float ox = __uint_as_float(cr.x), oz = __uint_as_float(cr.y);
-        const bool in = cr.w != selfq && ((cr.z > qs) ? inbox(ox, oz, D, sx, sz) : inbox(sx, sz, D, ox, oz));
-        if (in) f((uint32_t)cgl[p], p, cr.w);
+#if GW_FAN_UNROLL > 1
+      for (uint32_t p = cst[rb + B.x0]; p < e; p += GW_FAN_UNROLL) {
+        uint4 cr[GW_FAN_UNROLL];
+#pragma unroll
+        for (int k = 0; k < GW_FAN_UNROLL; ++k) cr[k] = crl[min(p + k, e - 1)];
+#pragma unroll
+        for (int k = 0; k < GW_FAN_UNROLL; ++k)
+          if (p + k < e) test(cr[k], p + k);
       }
+#else
+      for (uint32_t p = cst[rb + B.x0]; p < e; ++p) test(crl[p], p);
+#endif
     }
   } else {
     client_neighbours(a, s, sx, sz, qs, [&](uint32_t cj, uint8_t cg) { f((uint32_t)cg, kNone, cj); });
@@ -486,16 +524,17 @@ __global__ void __launch_bounds__(kSy) k_fan_dcount(FanArgs a) {
     for (uint32_t g = 0; g < kDirectGates; ++g) c[g] = 0u;
     const uint4 ra = a.g.rec[j].a;
     const uint32_t s = ra.z & REC_SLOT;
-    const uint8_t fl = (ra.z & REC_GHOST) ? 0 : a.flags[s];
-    const uint8_t want = fl & (GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
+    const uint32_t pw = (ra.z & REC_GHOST) ? 0u : a.pk[2 * (size_t)s + 1].z;  // gate | flags << 16
+    const uint8_t want = (uint8_t)(pw >> 16) & (GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
     if (want) {
       ++ents;
-      const uint16_t gs = a.gate[s];
+      const uint16_t gs = (uint16_t)pw;
       if ((want & GWAOI_SYNC_OWN_CLIENT) && gs < G) gate_bump(c, gs);
       if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS)
-        fan_pairs(a, fg, lds, cst, crl, cgl, j, ra, s, gs, [&](uint32_t g, uint32_t, uint32_t) {
-          if (g < G) gate_bump(c, g);
-        });
+        fan_pairs(a, fg, lds, cst, crl, cgl, a.g.rec[j].b.w, gs != GWAOI_SYNC_NO_CLIENT ? a.cpos[j] : 0xffffffffu, ra,
+                  s, [&](uint32_t g, uint32_t, uint32_t) {
+                    if (g < G) gate_bump(c, g);
+                  });
     }
     a.wantj[j] = want;
     uint4* dst = reinterpret_cast<uint4*>(a.gcnt + (size_t)j * a.gstride);
@@ -550,48 +589,71 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
   const FanGeo fg = fan_geo(a, t);
   if (fg.j0 == fg.j1) return;
   if (tid < G) gbase[tid] = a.tg[tid * a.ntiles + t];
-  const bool lds = fan_stage(a, fg, cst, crl, cgl, red, &tot_sh, cidl);
+  const bool lds = GW_ABL_FAN < 3 && fan_stage(a, fg, cst, crl, cgl, red, &tot_sh, cidl);
   __syncthreads();  // gbase
   const int lane = tid & 63, w = tid >> 6;
-  for (uint32_t jb = fg.j0; jb < fg.j1; jb += kSy) {  // block-uniform
-    const uint32_t j = jb + tid;
+  // A round's per-entity inputs. The next round's are loaded during this one (software pipelined:
+  // the record-order loads at the round's start, the slot gathers after its walk, the own client's id
+  // after its copy-out), so each round's walk and copy-out cover the gathers' latency.
+  struct RoundIn {
+    uint32_t want, qs, cp, c[kDirectGates];
+    uint4 ra, eid, pw, own;
+  };
+  auto load_rec = [&](uint32_t j, RoundIn& in) {  // record order: coalesced
     const bool live = j < fg.j1;
-    const uint8_t want = live ? a.wantj[j] : 0;
-    uint32_t c[kDirectGates];
+    in.want = live ? a.wantj[j] : 0u;
 #pragma unroll
-    for (uint32_t g = 0; g < kDirectGates; ++g) c[g] = 0u;
-    if (want) {
+    for (uint32_t g = 0; g < kDirectGates; ++g) in.c[g] = 0u;
+    in.ra = make_uint4(0, 0, 0, 0);
+    in.qs = in.cp = 0u;
+    if (live) {
       const uint4* src = reinterpret_cast<const uint4*>(a.gcnt + (size_t)j * a.gstride);
 #pragma unroll
       for (uint32_t g4 = 0; g4 < kDirectGates; g4 += 4) {
         if (g4 < a.gstride) {
           const uint4 v = src[g4 / 4];
-          c[g4] = v.x, c[g4 + 1] = v.y, c[g4 + 2] = v.z, c[g4 + 3] = v.w;
+          in.c[g4] = v.x, in.c[g4 + 1] = v.y, in.c[g4 + 2] = v.z, in.c[g4 + 3] = v.w;
         }
       }
+      in.ra = a.g.rec[j].a;
+      in.qs = a.g.rec[j].b.w;
+      in.cp = a.cpos[j];
     }
-    // the entity's record and slot state: issued before the scan below, whose barriers then overlap them
-    uint4 eid = make_uint4(0, 0, 0, 0), info = make_uint4(0, 0, 0, 0), own = make_uint4(0, 0, 0, 0);
-    uint4 ra = make_uint4(0, 0, 0, 0);
-    uint32_t s = 0;
-    uint16_t gs = GWAOI_SYNC_NO_CLIENT;
-    if (want) {
-      ra = a.g.rec[j].a;
-      s = ra.z & REC_SLOT;
-      gs = a.gate[s];
-      eid = a.eid[s];
-      info = make_uint4(ra.x, __float_as_uint(a.y[s]), ra.y, __float_as_uint(a.yaw[s]));
-      if ((want & GWAOI_SYNC_OWN_CLIENT) && gs < G) own = a.ccid[a.cpos[j]];
+  };
+  auto load_slot = [&](RoundIn& in) {  // the entity's slot: one 32-B gather
+    in.eid = in.pw = make_uint4(0, 0, 0, 0);
+    in.pw.z = GWAOI_SYNC_NO_CLIENT;
+    if (GW_ABL_FAN < 4 && in.want) {
+      const size_t s2 = 2 * (size_t)(in.ra.z & REC_SLOT);
+      in.eid = a.pk[s2];
+      in.pw = a.pk[s2 + 1];
     }
+  };
+  auto load_own = [&](RoundIn& in) {
+    in.own = make_uint4(0, 0, 0, 0);
+    if ((in.want & GWAOI_SYNC_OWN_CLIENT) && (in.pw.z & 0xFFFFu) < G) in.own = a.ccid[in.cp];
+  };
+  RoundIn rin, rnx;
+  load_rec(fg.j0 + tid, rin);
+  load_slot(rin);
+  load_own(rin);
+  for (uint32_t jb = fg.j0; jb < fg.j1; jb += kSy) {  // block-uniform
+    const uint32_t j = jb + tid;
+    const bool more = jb + kSy < fg.j1;  // block-uniform
+    if (more) load_rec(j + kSy, rnx);
+    const uint32_t want = rin.want;
+    uint32_t c[kDirectGates];
+#pragma unroll
+    for (uint32_t g = 0; g < kDirectGates; ++g) c[g] = rin.c[g];
+    const uint4 ra = rin.ra, eid = rin.eid, own = rin.own;
+    const uint4 info = make_uint4(ra.x, rin.pw.x, ra.y, rin.pw.y);
+    const uint32_t s = ra.z & REC_SLOT;
+    const uint16_t gs = (uint16_t)rin.pw.z;
     // block scan of the per-gate counts: wave scans, then the waves' totals
     uint32_t inc[kDirectGates];
 #pragma unroll
     for (uint32_t g = 0; g < kDirectGates; ++g) {
-      uint32_t v = c[g];
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
-      }
+      const uint32_t v = wave_incl_scan(c[g]);  // (DPP; every lane of the block reaches it)
       inc[g] = v;
       if (lane == 63) wred[g][w] = v;
     }
@@ -655,10 +717,12 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
           }
         }
       };
-      if (want & GWAOI_SYNC_NEIGHBOR_CLIENTS) fan_pairs(a, fg, lds, cst, crl, cgl, j, ra, s, gs, pair);
+      if (GW_ABL_FAN < 2 && (want & GWAOI_SYNC_NEIGHBOR_CLIENTS))
+        fan_pairs(a, fg, lds, cst, crl, cgl, rin.qs, gs != GWAOI_SYNC_NO_CLIENT ? rin.cp : 0xffffffffu, ra, s, pair);
     }
+    if (more) load_slot(rnx);
     __syncthreads();
-    if (staged) {  // copy-out: record r of the round, 16-B part k, over consecutive addresses per gate;
+    if (staged && GW_ABL_FAN == 0) {  // copy-out: record r of the round, 16-B part k, over consecutive addresses per gate;
                    // four parts per thread in flight (the ClientID gathers are global loads)
       const uint32_t nq = 3 * roff;
       constexpr size_t kNoDst = ~(size_t)0;
@@ -684,26 +748,12 @@ __global__ void __launch_bounds__(kSy) __attribute__((amdgpu_waves_per_eu(3))) k
         if (d3 != kNoDst) a.out[d3] = v3;
       }
     }
+    if (more) load_own(rnx);
     __syncthreads();
     if (tid < G) gbase[tid] += gtot[tid];
     __syncthreads();
+    rin = rnx;
   }
-}
-
-// direct fan-out: the sync bits of EVERY slot cleared after the count pass read them (a collected
-// entity's bits clear, and so do an absent slot's: k_clear_absent's contract), one coalesced pass
-// instead of a random byte write per collected entity
-__global__ void __launch_bounds__(kSy) k_clear_sync_bits(uint8_t* flags, uint32_t cap) {
-  const uint32_t n16 = cap / 16;
-  constexpr uint32_t kMask = 0x01010101u * (uint32_t)(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS);
-  uint4* f4 = reinterpret_cast<uint4*>(flags);
-  for (uint32_t i = blockIdx.x * kSy + threadIdx.x; i < n16; i += gridDim.x * kSy) {
-    uint4 v = f4[i];
-    v.x &= ~kMask, v.y &= ~kMask, v.z &= ~kMask, v.w &= ~kMask;
-    f4[i] = v;
-  }
-  for (uint32_t s = 16 * n16 + blockIdx.x * kSy + threadIdx.x; s < cap; s += gridDim.x * kSy)
-    flags[s] = (uint8_t)(flags[s] & ~(GWAOI_SYNC_OWN_CLIENT | GWAOI_SYNC_NEIGHBOR_CLIENTS));
 }
 
 // two small device ranges into the mapped host words the host reads after the stream synchronises (no
@@ -1033,6 +1083,7 @@ struct SyncState {
   uint8_t* cgate = nullptr;
   uint32_t crec_n = 0, cgate_n = 0;
   uint4* ccid = nullptr;
+  uint4* pk = nullptr;  // [2 cap]: k_sync_pack (direct fan-out)
   uint32_t ccid_n = 0;
   uint4* info = nullptr;
   uint64_t info_cap = 0;
@@ -1083,7 +1134,7 @@ void sync_free(SyncState* s) {
   void* p[] = {s->flags, s->gate, s->cid, s->eid, s->y, s->yaw, s->d_hb, s->cnt, s->cpos, s->ccs,
                s->crec, s->cgate, s->ccid, s->info, s->tstat, s->pairs, s->gcnt, s->wantj, s->tg,
                s->ghist, s->out, s->d_goff, s->scan.status, s->d_payload, s->res, s->first, s->ictr, s->bcnt,
-               s->op_slot, s->op_x, s->op_z};
+               s->op_slot, s->op_x, s->op_z, s->pk};
   for (void* q : p)
     if (q) hipFree(q);
   if (s->h_out) hipHostFree(s->h_out);
@@ -1300,6 +1351,14 @@ int collect_direct(const MgrView& v, SyncState* s, FanArgs f, uint32_t opts, gwa
   SRCHK(dgrow(&s->tg, &s->tg_cap, tgn));
   SRCHK(ensure_scan(s, (uint32_t)tgn));
   if (!s->out) SRCHK(dgrow(&s->out, &s->out_cap, 3u * 65536u));
+  if (!s->pk) {
+    if (hipMalloc((void**)&s->pk, (size_t)s->cap * 32) != hipSuccess) {
+      s->pk = nullptr;
+      set_error("collect_sync: hipMalloc(%llu) failed", (unsigned long long)s->cap * 32);
+      return GWAOI_ERR_NOMEM;
+    }
+  }
+  f.pk = s->pk;
   f.n_gates = G;
   f.gstride = gstride;
   f.gcnt = s->gcnt;
@@ -1307,10 +1366,10 @@ int collect_direct(const MgrView& v, SyncState* s, FanArgs f, uint32_t opts, gwa
   f.tg = s->tg;
   f.ntiles = ntiles;
   if (v.timing) SCHK(hipEventRecord(s->tev[1], st));
+  hipLaunchKernelGGL(k_sync_pack, dim3(std::min<uint32_t>(blocks_for(s->cap), 4096)), dim3(kSy), 0, st, s->flags,
+                     (const uint16_t*)s->gate, (const uint4*)s->eid, (const float*)s->y, (const float*)s->yaw, s->cap,
+                     f.clear, s->pk);
   hipLaunchKernelGGL(k_fan_dcount, dim3(ntiles), dim3(kSy), 0, st, f);
-  if (f.clear)
-    hipLaunchKernelGGL(k_clear_sync_bits, dim3(std::min<uint32_t>(blocks_for(s->cap / 16 + 1), 2048)), dim3(kSy), 0, st,
-                       s->flags, s->cap);
   hipLaunchKernelGGL(k_fan_total, dim3(1), dim3(1024), 0, st, (const uint4*)s->tstat, ntiles, s->ictr + 8,
                      (unsigned long long*)(s->ictr + 10));
   launch_scan(s->scan, s->tg, (uint32_t)tgn, st);

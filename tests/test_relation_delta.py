@@ -56,8 +56,10 @@ def test_delta_random_ops_vs_oracle(gpu, oracle_lib, seed):
 
 
 def test_delta_walk_and_states(gpu, oracle_lib):
-    """A 100k walk (config-2 density) tick by tick; the export is refused before any tick and once a
-    later pass has overwritten the tick's events."""
+    """A 100k walk (config-2 density) tick by tick against oracle (ii) run in lockstep: the delta is the
+    difference of the ORACLE's relations before and after each tick, and the GPU relation equals the
+    oracle's. The export is refused before any tick and once a later pass has overwritten the tick's
+    events."""
     from goworld_amd import _lib
     from goworld_amd.engine import Engine
     po = oracle_lib
@@ -68,15 +70,21 @@ def test_delta_walk_and_states(gpu, oracle_lib):
         eng.relation_delta()
     assert e.value.code == _lib.GWAOI_ERR_STATE
     slots = np.arange(n, dtype=np.uint32)
+    orc = po.GridOracle(100.0, n, (0.0, 0.0, L, L))
+    orc.bulk_enter(slots, x, z)
     eng.stage_enters(slots, x, z)
     eng.tick()
-    before = pairs(eng.relation())
+    before = pairs(orc.relation())
+    assert pairs(eng.relation()) == before
     for t in range(1, 4):
         po.workload_step(seed, t, x, z, L, 1.0)
+        orc.moved_batch(slots, x, z)
+        orc.take_events()
         eng.stage_moves(slots, x, z)
         ev = eng.tick()
         d = eng.relation_delta()
-        after = pairs(eng.relation())  # (runs no pass: the tick's events stay exportable)
+        after = pairs(orc.relation())
+        assert pairs(eng.relation()) == after, f"walk tick {t}: relation"  # (runs no pass)
         check_delta(d, before, after, f"walk tick {t}")
         assert 0 < len(d) <= 2 * len(ev)  # both members moving: a leave then an enter can cancel
         assert np.array_equal(eng.relation_delta(), d)  # repeatable until the next pass
