@@ -391,6 +391,49 @@ __global__ void __launch_bounds__(kBlock) k_scan_apply(uint32_t* __restrict__ d,
   }
 }
 
+// Short arrays (n <= kScanOneMax: tile totals, block counts) in ONE kernel of one 1024-thread block,
+// 32 items per thread: a launch less than the two-kernel scan, whose second kernel alone costs a
+// dispatch (~4.7 us of a tick's stream time each, r04_c24 kernel stats).
+#ifndef GW_SCAN_ONE_MAX
+#define GW_SCAN_ONE_MAX 8192  // (32768, i.e. the fan-out's tile totals too: count stage +2.5 us, r04_c27)
+#endif
+constexpr int kScanOneThreads = 1024, kScanOneIpt = 32;
+constexpr uint32_t kScanOneMax = GW_SCAN_ONE_MAX;
+static_assert(kScanOneMax <= (uint32_t)kScanOneThreads * kScanOneIpt, "one block's items");
+
+__global__ void __launch_bounds__(kScanOneThreads) k_scan_one(uint32_t* __restrict__ d, uint32_t n) {
+  __shared__ uint32_t ws[kScanOneThreads / 64];
+  const uint32_t b0 = threadIdx.x * kScanOneIpt;
+  uint32_t v[kScanOneIpt];
+  scan_load<kScanOneIpt>(d, n, b0, v);
+  uint32_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < kScanOneIpt; ++k) sum += v[k];
+  const uint32_t inc = wave_incl_scan(sum);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t pre = inc - sum;
+  for (int k = 0; k < w; ++k) pre += ws[k];
+  if (b0 + kScanOneIpt <= n) {
+#pragma unroll
+    for (int k = 0; k < kScanOneIpt; k += 4) {
+      uint4 q;
+      q.x = pre, pre += v[k];
+      q.y = pre, pre += v[k + 1];
+      q.z = pre, pre += v[k + 2];
+      q.w = pre, pre += v[k + 3];
+      *reinterpret_cast<uint4*>(d + b0 + k) = q;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanOneIpt; ++k) {
+      if (b0 + k < n) d[b0 + k] = pre;
+      pre += v[k];
+    }
+  }
+}
+
 static uint32_t scan_ipt(uint32_t n) {
   for (uint32_t ipt : {4u, 16u})
     if ((n + kBlock * ipt - 1) / (kBlock * ipt) <= kScanMaxChunks) return ipt;
@@ -410,6 +453,10 @@ static void scan_ipt_launch(ScanCtx& c, uint32_t* d, uint32_t n, uint32_t nb, hi
 
 void launch_scan(ScanCtx& c, uint32_t* d, uint32_t n, hipStream_t st) {
   if (!n) return;
+  if (n <= kScanOneMax) {
+    hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(kScanOneThreads), 0, st, d, n);
+    return;
+  }
   const uint32_t ipt = scan_ipt(n);
   const uint32_t nb = (n + kBlock * ipt - 1) / (kBlock * ipt);
   if (ipt == 4)
