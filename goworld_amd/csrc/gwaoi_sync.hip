@@ -185,9 +185,12 @@ __global__ void __launch_bounds__(kSy) k_cg_build(ClientGridArgs a) {
   const uint32_t nrec = *a.rec_count;
   const uint32_t nth = gridDim.x * kSy;
   for (uint32_t j = blockIdx.x * kSy + threadIdx.x; j < nrec; j += nth) {
-    if (!cg_take(a, j, nrec)) continue;
+    // taken iff the exclusive scan steps at j (j < nrec <= rec_bound: cpos[j + 1] exists): two coalesced
+    // words instead of the record and its slot's gate again
+    const uint32_t p = a.cpos[j];
+    if (a.cpos[j + 1] == p) continue;
     const Rec r = a.rec[j];
-    const uint32_t s = r.a.z & REC_SLOT, p = a.cpos[j];
+    const uint32_t s = r.a.z & REC_SLOT;
     a.crec[p] = make_uint4(r.a.x, r.a.y, r.b.w, s);
     a.cgate[p] = (uint8_t)a.gate[s];
     a.ccid[p] = a.cid[s];
