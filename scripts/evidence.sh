@@ -17,7 +17,7 @@ if has pmc; then
   PMC_GROUPS="FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU|SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
     BENCH_ARGS="--host-staged-ticks 0 --no-replay --p99-ticks 0" TAG=${TAG}_config2 bash scripts/pmc.sh
   python3 scripts/make_pmc_latest.py gpurun_out/${TAG}_config2_pmc config2 profiles/pmc_latest.json > gpurun_out/${TAG}_config2_pmc_latest.txt
-  for w in ${PMC_WORKLOADS:-skew50 skew strips gametick config3}; do
+  for w in ${PMC_WORKLOADS:-skew50 skew strips strips_skew gametick config3}; do
     PMC_GROUPS="FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE" \
       BENCH_ARGS="--workload $w --steps 8 --warmup 2 --stage-ticks 4 --host-staged-ticks 0 --no-replay --p99-ticks 0" \
       TAG=${TAG}_$w bash scripts/pmc.sh
