@@ -330,7 +330,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     W, K, H = args.warmup, args.steps, args.latency_ticks
     HS = args.host_staged_ticks
     S = min(K, args.stage_ticks)  # instrumented ticks (per-stage hipEvents) after the timed region
-    T = W + K + S + H + HS + 1
+    T = W + K + S + H + 1  # (the host-staged and p99 loops generate their positions as they go)
     L_ = _lib.load()
 
     # ---- untimed setup: positions for every tick generated on the device ----
@@ -355,8 +355,8 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         eng.debug_set_cell_side(args.cell_side)
     if args.sweep_lds != 1:
         eng._L.gwaoi_debug_set_sweep_lds(eng.handle, args.sweep_lds)
-    if args.chunked:  # A/B: min_recs,max_recs,max_pad of the tiles k_sweep_chunked takes
-        eng.debug_set_chunked(*[int(v) for v in args.chunked.split(",")])
+    if args.band != 1:  # A/B: the band walk of the global-memory movers off (their whole rings)
+        eng.debug_set_band(args.band)
     if args.counting_build:
         eng.debug_build_mode(1)
     # bulk restore (untimed): one device-staged pass of SILENT Enters into their Spaces; the relation
@@ -416,9 +416,22 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         eng.tick_raw()
         lat_host.append(time.perf_counter() - ts)
 
-    # ---- SURVEY 8(d) latency: from gwaoi_stage_moves with HOST arrays (the cgo wrapper's one call per
-    # tick) to the events in the pinned host buffer; then the events replayed into per-entity hash sets
-    # (tools/replay_sets.c: Entity.interest/uninterest, 4 set ops per pair event, Entity.go:227-246) ----
+    # the walk continues after the staged ticks, each tick's positions generated on the device (and
+    # synchronised) before its clock starts: two [x|z][n] tick slots, ping-pong
+    walk = DeviceBuffer(2 * 2 * 4 * n, dev)
+    wstate = {"prev": (px(T - 1), pz(T - 1)), "t": T, "k": 0}
+
+    def walk_next():
+        k = wstate["k"]
+        bx, bz = walk.ptr + (2 * k) * 4 * n, walk.ptr + (2 * k + 1) * 4 * n
+        wl_step_spaces(dev, *wstate["prev"], bx, bz, n_per, nsp, seed0, wstate["t"], L, 1.0)
+        wstate.update(prev=(bx, bz), t=wstate["t"] + 1, k=k ^ 1)
+        return bx, bz
+
+    # ---- SURVEY 8(d) p99, the headline: from the positions in host memory through the cgo wrapper's one
+    # staging call per tick to the events in the pinned host buffer, over HS >= 1,000 ticks; the first
+    # --replay-ticks of them also replayed into per-entity hash sets (tools/replay_sets.c:
+    # Entity.interest/uninterest, 4 set ops per pair event, Entity.go:227-246) ----
     lat_hs, stage_hs, replay_s, replay_bad = [], [], [], 0
     replay_sh_s, replay_sh_bad = [], 0
     rs = rss = None
@@ -452,11 +465,12 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         pin_s[:n] = slots_h
     copyin = min(10, HS // 2)
     stage_ci = []
-    for t in range(W + K + S + H + 1, T):
-        use_pin = t < T - copyin
+    for i in range(HS + copyin):
+        use_pin = i < HS
         dx, dz = (pin_x, pin_z) if use_pin else (xh, zh)
-        _lib.check(L_.gwaoi_dev_dtoh(dev, dx.ctypes.data, ctypes.c_void_p(px(t)), 4 * n))  # untimed
-        _lib.check(L_.gwaoi_dev_dtoh(dev, dz.ctypes.data, ctypes.c_void_p(pz(t)), 4 * n))
+        bx, bz = walk_next()  # untimed: the tick's positions into the host arrays
+        _lib.check(L_.gwaoi_dev_dtoh(dev, dx.ctypes.data, ctypes.c_void_p(bx), 4 * n))
+        _lib.check(L_.gwaoi_dev_dtoh(dev, dz.ctypes.data, ctypes.c_void_p(bz), 4 * n))
         ts = time.perf_counter()
         if use_pin:
             eng.stage_moves_pinned(n)
@@ -478,24 +492,19 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             tr = time.perf_counter()
             replay_sh_bad += rss.replay(ctypes.cast(ev.events, ctypes.c_void_p).value, int(ev.count))
             replay_sh_s.append(time.perf_counter() - tr)
+        if (rs is not None or rss is not None) and i + 1 >= args.replay_ticks:  # the sets stop following here
+            if rs is not None:
+                rs.close()
+            if rss is not None:
+                rss.close()
+            rs = rss = None
     if rs is not None:
         rs.close()
     if rss is not None:
         rss.close()
 
-    # ---- a fixed loop of P device-resident ticks (events left in HBM), independent of
-    # --steps; the walk continues from the last staged tick, each tick's positions generated (and
-    # synchronised) before its clock starts ----
-    walk = DeviceBuffer(2 * 2 * 4 * n, dev)  # two [x|z][n] tick slots, ping-pong
-    wstate = {"prev": (px(T - 1), pz(T - 1)), "t": T, "k": 0}
-
-    def walk_next():
-        k = wstate["k"]
-        bx, bz = walk.ptr + (2 * k) * 4 * n, walk.ptr + (2 * k + 1) * 4 * n
-        wl_step_spaces(dev, *wstate["prev"], bx, bz, n_per, nsp, seed0, wstate["t"], L, 1.0)
-        wstate.update(prev=(bx, bz), t=wstate["t"] + 1, k=k ^ 1)
-        return bx, bz
-
+    # ---- device-resident p50/p99 (p99_tick_ms_device): a fixed loop of P ticks (events left in HBM),
+    # independent of --steps ----
     lat_p = []
     for _ in range(args.p99_ticks):
         bx, bz = walk_next()
@@ -614,18 +623,23 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "seed": hex(seed0 - rank * (nsp if nsp > 1 else 1)),
             "parallelism": "independent Spaces, one manager per GPU, no data-path collective" if world > 1 else "1 GPU",
         },
-        "p50_tick_ms": percentile(lat_p or lat, 50) * 1e3,
-        "p99_tick_ms": percentile(lat_p or lat, 99) * 1e3,
-        "p99_samples": len(lat_p or lat),
-        "p99_note": (f"host wall time of {len(lat_p)} device-resident ticks (stage_moves_device -> events ordered in "
-                     "HBM, count on the host) run after the timed region, each tick's positions generated before "
-                     "its clock starts" if lat_p else "over the timed ticks"),
+        "p50_tick_ms": percentile(lat_hs or lat_p or lat, 50) * 1e3,
+        "p99_tick_ms": percentile(lat_hs or lat_p or lat, 99) * 1e3,
+        "p99_samples": len(lat_hs or lat_p or lat),
+        "p99_note": (f"SURVEY 8(d): host wall time from the positions in host memory to the events in host memory, "
+                     f"{len(lat_hs)} ticks after the timed region (the tick's positions written into the manager's "
+                     "pinned staging arrays, untimed; gwaoi_stage_moves_pinned + gwaoi_tick = one DMA copy in, the "
+                     "pipeline, the events copied into pinned host memory by the GPU)" if lat_hs else
+                     f"host wall time of {len(lat_p)} device-resident ticks" if lat_p else "over the timed ticks"),
+        "p50_tick_ms_device": percentile(lat_p, 50) * 1e3 if lat_p else None,
+        "p99_tick_ms_device": percentile(lat_p, 99) * 1e3 if lat_p else None,
+        "p99_device_note": (f"host wall time of {len(lat_p)} device-resident ticks (stage_moves_device -> events "
+                            "ordered in HBM, count on the host), each tick's positions generated before its clock "
+                            "starts") if lat_p else None,
         "p50_tick_ms_timed": percentile(lat, 50) * 1e3,
         "p99_tick_ms_timed": percentile(lat, 99) * 1e3,
         "p50_tick_ms_host_events": percentile(lat_host, 50) * 1e3 if lat_host else None,
         "p99_tick_ms_host_events": percentile(lat_host, 99) * 1e3 if lat_host else None,
-        "p50_tick_ms_host_staged": percentile(lat_hs, 50) * 1e3 if lat_hs else None,
-        "p99_tick_ms_host_staged": percentile(lat_hs, 99) * 1e3 if lat_hs else None,
         "host_stage_ms": percentile(stage_hs, 50) * 1e3 if stage_hs else None,
         "host_stage_copyin_ms": percentile(stage_ci, 50) * 1e3 if stage_ci else None,
         "replay_ms": percentile(replay_s, 50) * 1e3 if replay_s else None,
@@ -677,10 +691,11 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "grid_records_per_tick": rec_per_tick,
             "grid_cells": cells,
             "dense_movers_per_tick": st["dense_movers"] / ticks,
-            "chunked_movers_per_tick": st["chunked_movers"] / ticks,
+            "band_movers_per_tick": st["band_movers"] / ticks,
             "avg_launch_ms": sweep_ms,
-            "kernels_timed": "k_sweep" + (" + k_sweep_chunked" if st["chunked_movers"] else "") +
+            "kernels_timed": "k_sweep" +
                              (" + k_sweep_dense" if st["dense_movers"] else "") +
+                             (" + k_band_keys + k_band_rank" if st["band_movers"] else "") +
                              " (the pass's sweep stage, hipEvents on the manager's stream)",
             "survey_formula": None if b_survey is None else {
                 "bytes_per_tick": b_survey,
@@ -1152,7 +1167,9 @@ def main():
     ap.add_argument("--small-reps", type=int, default=20,
                     help="config 2/3: repetitions of the small-pass leg (1-op Leave, 1-op Enter, 1k-op Moved "
                          "passes into the full manager, small passes on and off); 0 skips it")
-    ap.add_argument("--host-staged-ticks", type=int, default=50,
+    ap.add_argument("--replay-ticks", type=int, default=20,
+                    help="host-staged ticks whose events are also replayed into the hash-set sink (replay_ms)")
+    ap.add_argument("--host-staged-ticks", type=int, default=1000,
                     help="extra ticks staged from host arrays (gwaoi_stage_moves), events to host, replayed")
     ap.add_argument("--no-replay", dest="replay", action="store_false",
                     help="skip the C replay of events into per-entity hash sets")
@@ -1164,8 +1181,8 @@ def main():
     ap.add_argument("--sweep-lds", type=int, default=1, help="0: global-memory sweep path (A/B)")
     ap.add_argument("--fanout", type=int, default=0,
                     help="gametick: 0 = direct fan-out when gates <= 8 (default), 1 = pair list + gate partition (A/B)")
-    ap.add_argument("--chunked", default="",
-                    help="A/B: 'min_recs,max_recs,max_pad' of the over-budget tiles k_sweep_chunked takes (-1 keeps)")
+    ap.add_argument("--band", type=int, default=1,
+                    help="A/B: the band walk of the global-memory movers (1 on, 0 off: their whole rings)")
     ap.add_argument("--stage-ticks", type=int, default=200,
                     help="ticks run with per-stage hipEvents after the timed region (stage_ms, roofline)")
     ap.add_argument("--counting-build", action="store_true",

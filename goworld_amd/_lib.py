@@ -43,7 +43,7 @@ TOOL_SYMBOLS = (
     "gwaoi_debug_read_stamps",
     "gwaoi_debug_sweep_occupancy", "gwaoi_wl_pack_ingest", "gwaoi_debug_set_index_limit",
     "gwaoi_debug_set_relation_mode", "gwaoi_debug_set_build_mode", "gwaoi_debug_set_small_pass", "gwaoi_debug_set_fanout_mode",
-    "gwaoi_debug_set_chunked",
+    "gwaoi_debug_set_band",
 )
 
 
@@ -152,7 +152,7 @@ class Stats(ctypes.Structure):
         ("grid_records", ctypes.c_uint64),
         ("grid_cells", ctypes.c_uint64),
         ("dense_movers", ctypes.c_uint64),
-        ("chunked_movers", ctypes.c_uint64),
+        ("band_movers", ctypes.c_uint64),
     ]
 
 
@@ -233,7 +233,7 @@ def load(path: str = SO_PATH):
                                         ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_debug_set_small_pass": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_debug_set_fanout_mode": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
-        "gwaoi_debug_set_chunked": ([vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64], ctypes.c_int),
+        "gwaoi_debug_set_band": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_strip_init_walk": ([vp, vp, vp, vp, vp, u64, f32], ctypes.c_int),
         "gwaoi_strip_walk": ([vp, vp, vp, vp, vp, vp, vp, u64, u64, f32, f32, vp], ctypes.c_int),
         "gwaoi_strip_ingest": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),

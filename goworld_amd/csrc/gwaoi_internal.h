@@ -23,12 +23,11 @@ enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 
        CTR_BOVF = 10,   // the one-pass build overflowed a tile's bucket: the pass is re-run (counting build)
        CTR_NEV = 11,    // events of the pass (scan total of the per-op counts; k_place)
        CTR_UNSORTED = 12,  // set when some op's events were numbered out of canonical order (k_slice_sort sorts)
-       CTR_BAND_ITEMS = 13,  // items of k_sweep_chunked listed by k_sweep (crowded tiles)
-       CTR_BAND_MV = 14,     // movers in those items
+       CTR_DENSE2 = 13,   // dense movers k_sweep_band hands to the ring walk (dense2)
+       CTR_BAND_MV = 14,     // dense movers that took the band walk (k_sweep_dense)
        CTR_SMALL_OVF = 15,   // k_order_small: the pass's events exceed its LDS (the host re-runs the order stage)
        CTR_BDONE = 16,  // blocks of the one-pass build done (not published)
        CTR_SDONE = 17,  // blocks of k_slice_sort done (the last one publishes the counters)
-       CTR_BAND_NEXT = 18,  // k_sweep_chunked's work counter
        CTR_N = 32 };
 constexpr int kPubWords = 16;  // counters [0, 16) are what the host reads after a pass
 // CTR_EVENTS counts SLOTS of ev_tmp's shared region (after the per-tile regions, SweepArgs.ev_fix);
@@ -61,7 +60,7 @@ struct Geom {
   uint32_t base;      // first cell key of this Space
   uint32_t tile_base; // first tile index of this Space (base / kTileCells)
   int32_t reach;      // halo (cells) staged around a tile in the sweep (0: the region does not fit k_sweep)
-  uint32_t pad;       // halo of the chunked sweep (k_sweep_chunked; 0: none, the dense walk instead)
+  uint32_t pad;
 };
 
 // The pass's grid: every record sorted by cell key (counting sort). Per slot: a MAIN record at its
@@ -194,7 +193,7 @@ struct SweepArgs {
   uint32_t n_rec;      // upper bound on records in the grid (flat variant grid size)
   uint32_t ncells;     // cells of the grid (cs[ncells] = record count)
   uint32_t ntiles;     // tiles of the grid: blocks [0, ntiles) take one tile each, the rest Leave ops
-  int use_lds;         // 1: LDS-staged sweep; 0: flat global-memory sweep (A/B); 2: staging only (timing)
+  int use_lds;         // 1: LDS-staged sweep; 0: every mover to k_sweep_dense (tests); 2: staging only (timing)
   const uint32_t* op_slot;    // for the leave path
   const uint8_t* op_kind;     // per op (null: all moves); OP_SILENT movers are applied, not walked
   const uint32_t* leave_ops;  // op indices of OP_LEAVE ops
@@ -211,19 +210,40 @@ struct SweepArgs {
   uint32_t* rank_cnt;
   uint32_t* ctr;
   uint32_t* dense;      // slots of movers for k_sweep_dense (boxes beyond the tile's LDS region)
+  uint32_t* dense2;     // band walk on: the movers k_sweep_band leaves to the ring walk
   uint32_t dense_cap;
   uint32_t dense_hint;  // dense movers of the previous pass (0: k_sweep_dense not launched)
-  uint32_t* band_mv;    // k_sweep_chunked: movers (grid indices) of crowded tiles, null: no chunked sweep
-  uint32_t band_mv_cap;
-  uint4* band_items;    // {tile, first mover, movers, 0}
-  uint32_t band_items_cap;
-  uint32_t band_hint;   // items of the previous pass (0: k_sweep_chunked not launched)
-  uint32_t chunk_min_recs;  // over-budget tiles with records in [min, max] and halo <= chunk_max_pad cells
-  uint32_t chunk_max_recs;  // take k_sweep_chunked; the others the dense walk
-  uint32_t chunk_max_pad;
-  uint32_t chunk_grid;  // its blocks (one per CU)
   const uint32_t* tile_walk;  // per tile: holds a reported mover (null: k_sweep scans the tile's records)
+  // the band walk of k_sweep_dense: the grid's records sorted per cell by search key (null:
+  // not built this pass, every dense mover walks its ring), and per Space the key spread
+  const float* band_xk;   // x key of each record (the grid's records sorted by x key inside each cell)
+  const float* band_zk;   // per cell by z key: the key, and
+  const uint32_t* band_zi;  // the record
+  const uint32_t* band_hd;
 };
+
+// Band keys of the pass's grid for k_sweep_dense's band walk. A record's judge position p is
+// its binned position, or, for a main record without a ghost whose entity acted, its start OR its end
+// position (both in the binned cell), depending on the mover. Its search key is the midpoint of the two
+// (the binned position otherwise), and hd bounds |p - key| per Space and axis, so a band of p values is a
+// window of keys widened by hd.
+struct BandArgs {
+  GridView g;
+  const uint32_t* space_of;
+  uint32_t nspaces;
+  uint32_t rec_bound;    // launch bound on the grid's records
+  const uint32_t* nrec;  // device: the grid's records (cs[ncells])
+  float2* key2;          // [records] per record {x key, z key}
+  Rec* rec_out;          // [records] the grid's records sorted by x key inside each cell (cells over
+                         // kBandCellMax records copied as they are); replaces the grid's records
+  float* xk;             // [records] their x keys, in rec_out order
+  float* zk;             // [records] per cell by z key: the key,
+  uint32_t* zi;          // and the record's index in rec_out
+  uint32_t* hd;          // [2 nspaces] per Space: max |p - key| (float bits; zeroed by the caller), x then z
+};
+// cells of more records than this are not sorted: the band walk reads them whole
+constexpr uint32_t kBandCellMax = 256;
+void launch_band_keys(const BandArgs& b, hipStream_t st);
 
 struct RelArgs {
   GridView g;
@@ -301,8 +321,6 @@ uint32_t sweep_ev_lds();  // events queued per tile block (the per-tile region s
 size_t sweep_lds_bytes();
 uint32_t sweep_block();  // threads per sweep block
 void sweep_init();  // once per process (dynamic LDS limit of the sweep)
-void chunk_init();  // once per process (dynamic LDS limit of the chunked sweep)
-size_t chunk_lds_bytes();
 int read_stamps(void* host, size_t bytes);
 int sweep_occupancy(int* blocks);  // resident sweep blocks per CU (HIP occupancy API)  // GW_STAMPS diagnostic builds only (else -1)
 // Event ordering runs without a host round trip: each step checks on the device that the sweep's
@@ -456,6 +474,7 @@ struct MgrView {
 struct gwaoi_mgr;
 namespace gw {
 int mgr_view(gwaoi_mgr* m, MgrView* out);
+int mgr_grid_current(gwaoi_mgr* m);  // bring the grid up to date after small passes (readers of the grid)
 int mgr_flush(gwaoi_mgr* m);  // run the staged ops now (their events are kept for the next gwaoi_tick)
 // stage a device-counted batch of moves (*d_n <= n_max ops; slots distinct and present, checked on device)
 int mgr_stage_moves_device_n(gwaoi_mgr* m, const uint32_t* d_slots, const float* d_x, const float* d_z,

@@ -966,7 +966,6 @@ void launch_bin_tiles(const BinArgs& a, hipStream_t st) {
 #ifndef GW_SWEEP_WAVES_PER_EU
 #define GW_SWEEP_WAVES_PER_EU 6
 #endif
-constexpr int kChunkBlock = 1024;  // k_sweep_chunked: threads per block = movers per item
 constexpr int kSweepBlock = GW_SWEEP_BLOCK;  // 8 waves: a config-2 tile holds ~520 movers (one round, a few twice)
 #ifndef GW_EV_LDS
 #define GW_EV_LDS 256
@@ -1809,36 +1808,8 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     GW_STAMP(6, (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
                     ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32));
   }
-  const uint32_t trecs = a.g.cs[(t + 1) << kTileCellShift] - a.g.cs[t << kTileCellShift];
-  if (!lds && a.band_mv && g.pad > 0 && g.pad <= a.chunk_max_pad && trecs >= a.chunk_min_recs &&
-      trecs <= a.chunk_max_recs) {
-    // region over the LDS budget (crowds, large D): the tile's movers (grid indices, in grid order) to
-    // k_sweep_chunked, in items of up to kChunkBlock; one atomic per block on each list's counter (the
-    // lists are sized so that every pass's movers fit)
-    const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
-    uint32_t mine = 0;
-    for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) mine += is_walker(a, a.g.rec[j].a) ? 1u : 0u;
-    uint32_t tot;
-    const uint32_t pre = block_excl_scan_big(mine, sm.ws, &tot);
-    const uint32_t nit = (tot + kChunkBlock - 1) / kChunkBlock;
-    if (threadIdx.x == 0) {
-      sm.base = tot ? atomicAdd(&a.ctr[CTR_BAND_MV], tot) : 0u;
-      sm.item = nit ? atomicAdd(&a.ctr[CTR_BAND_ITEMS], nit) : 0u;
-    }
-    __syncthreads();
-    const uint32_t mb = sm.base, ib = sm.item;
-    uint32_t di = mb + pre;
-    for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock)
-      if (is_walker(a, a.g.rec[j].a)) {
-        if (di < a.band_mv_cap) a.band_mv[di] = j;
-        ++di;
-      }
-    for (uint32_t i = threadIdx.x; i < nit; i += kSweepBlock)
-      if (ib + i < a.band_items_cap)
-        a.band_items[ib + i] = make_uint4(t, mb + i * kChunkBlock, min((uint32_t)kChunkBlock, tot - i * kChunkBlock), 0u);
-  } else if (!lds) {
-    // region over the LDS budget, no chunked sweep (its halo is wider than a tile): every mover of the
-    // tile to k_sweep_dense (the tile's entries reserved by ONE atomic per block: an append per wave on
+  if (!lds) {
+    // region over the LDS budget (or the LDS path off, use_lds 0): every mover of the tile to k_sweep_dense (the tile's entries reserved by ONE atomic per block: an append per wave on
     // the one counter serialised at the memory side, ~48k of them per skew50 launch)
     const uint32_t e0 = a.g.cs[t << kTileCellShift], e1 = a.g.cs[(t + 1) << kTileCellShift];
     uint32_t mine = 0;
@@ -1952,55 +1923,11 @@ void sweep_init() {
                             (int)sizeof(SweepSmem));
 }
 
-// Flat variant (use_lds == 0): one thread per record in key (tile-major) order, 256-thread blocks
-// and only the event queue in LDS, i.e. full occupancy; candidates come through L1/L2.
+// The event queue of the one-thread-per-op global walks (k_sweep_leaves): only the queue in LDS.
 struct FlatQ {
   uint32_t n, enter, base, flags;
   uint4 ev[kEvLds];
 };
-
-__global__ void __launch_bounds__(kBlock) k_sweep_flat(SweepArgs a) {
-  __shared__ FlatQ q;
-  uint32_t nent = 0;
-  if (threadIdx.x == 0) {
-    q.n = 0;
-    q.enter = 0;
-    q.flags = 0;
-  }
-  __syncthreads();
-  const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  const uint32_t n_rec = a.g.cs[a.ncells];
-  uint32_t cnt = 0;
-  if (t < n_rec) {
-    const uint4 ra = a.g.rec[t].a;
-    if (is_walker(a, ra)) {
-      const uint32_t slot = ra.z & REC_SLOT;
-      const Geom g = a.g.geom[a.space_of[slot]];
-      const Mover m = mover_of(ra, a.g.rec[t].b, a.base, g.D);
-      put_count(a.rank_cnt, m.rank, cnt = sweep_global(a, q, m, g, nent));
-    }
-  } else if (t >= a.n_rec && t < a.n_rec + (a.n_leaves_dev ? *a.n_leaves_dev : a.n_leaves) &&
-             !(a.op_kind && (a.op_kind[a.leave_ops[t - a.n_rec]] & OP_SILENT))) {
-    const uint32_t i = a.leave_ops[t - a.n_rec];
-    const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
-    const Mover m = leaver(a, i, g.D);
-    put_count(a.rank_cnt, i, cnt = sweep_global(a, q, m, g, nent));
-  }
-  if (cnt > 1u) q.flags = 1u;  // numbered in walk order: k_slice_sort sorts
-  if (nent) atomicAdd(&q.enter, nent);
-  __syncthreads();
-  const uint32_t nq = min(q.n, (uint32_t)kEvLds);
-  if (threadIdx.x == 0) {
-    q.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
-    if (q.enter) atomicAdd(&a.ctr[CTR_ENTER], q.enter);
-    if (q.flags) a.ctr[CTR_UNSORTED] = 1u;
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
-    const uint32_t gi = q.base + i;
-    if (gi < a.ev_cap) a.ev_tmp[gi] = q.ev[i];
-  }
-}
 
 // Leaves of a mixed device batch (or host-staged Leaves): each leaver's old neighbours through the
 // global-memory walk, one thread per leaver.
@@ -2036,6 +1963,145 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
     const uint32_t gi = q.base + i;
     if (gi < a.ev_cap) a.ev_tmp[gi] = q.ev[i];
   }
+}
+
+// ---- Band keys (k_sweep_dense's band walk) -------------------------------------------
+// A candidate can only change state for a mover m if its judge position p lies in the symmetric difference
+// of m's old and new boxes: p.x within the band between the two left (or the two right) box edges, or p.z
+// between the two bottom (top) edges. In a crowd those bands are ~1 unit wide while a cell is 12.5-25, so
+// the records of a ring cell are sorted by search key (x, and separately z) and the walk binary-searches
+// the window of keys that can hold p in the band, instead of reading the whole cell.
+//
+// Search key of a record: its binned position, except for a main record without a ghost whose entity
+// acted in this pass and was present at the start: judge() then meets it at its start OR its end position
+// (which one depends on the mover's rank), both in the binned cell, and the key is their midpoint; hd
+// (per Space and axis) bounds |p - key| over all records.
+__device__ __forceinline__ void band_key(const uint4 ra, const uint4 rb, float& kx, float& kz, float& hx, float& hz) {
+  const float bx = __uint_as_float(ra.x), bz = __uint_as_float(ra.y);
+  kx = bx, kz = bz, hx = 0.0f, hz = 0.0f;
+  if ((ra.z & (REC_GHOST | REC_HASG)) || rb.z == 0u || (rb.x == ra.x && rb.y == ra.y)) return;
+  const float sx = __uint_as_float(rb.x), sz = __uint_as_float(rb.y);
+  const float mx = 0.5f * sx + 0.5f * bx, mz = 0.5f * sz + 0.5f * bz;  // (no overflow for finite coordinates)
+  kx = mx, kz = mz;
+  hx = fmaxf(fabsf(sx - mx), fabsf(bx - mx));
+  hz = fmaxf(fabsf(sz - mz), fabsf(bz - mz));
+}
+
+// keys in record order and the per-Space spread: grid-stride over the records; the spread is reduced per
+// block in LDS (a Space's records are contiguous in grid order) and raised in global memory once per block,
+// Space and axis, only when it exceeds the current value (one atomic or read per wave on the same two
+// words serialised at the memory side: 1.49 ms, then 0.25 ms per skew50 pass)
+constexpr uint32_t kBandKeyBlocks = 1024;
+__global__ void __launch_bounds__(kBlock) k_band_keys(BandArgs a) {
+  __shared__ uint32_t bh[2 * kLdsGeoms];
+  const bool lds = a.nspaces <= kLdsGeoms;
+  if (lds)
+    for (uint32_t i = threadIdx.x; i < 2 * a.nspaces; i += kBlock) bh[i] = 0u;
+  __syncthreads();
+  const uint32_t n = min(*a.nrec, a.rec_bound);
+  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < n; j += gridDim.x * kBlock) {
+    const Rec r = a.g.rec[j];
+    float kx, kz, hx, hz;
+    band_key(r.a, r.b, kx, kz, hx, hz);
+    a.key2[j] = make_float2(kx, kz);
+    if (hx > 0.0f || hz > 0.0f) {
+      const uint32_t sp = a.space_of[r.a.z & REC_SLOT];
+      uint32_t* w = lds ? &bh[2 * sp] : &a.hd[2 * sp];
+      if (hx > 0.0f) atomicMax(&w[0], __float_as_uint(hx));
+      if (hz > 0.0f) atomicMax(&w[1], __float_as_uint(hz));
+    }
+  }
+  if (!lds) return;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < 2 * a.nspaces; i += kBlock) {
+    const uint32_t v = bh[i];
+    if (v && v > __hip_atomic_load(&a.hd[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&a.hd[i], v);
+  }
+}
+
+// per record: its ranks by x key and by z key among its cell's records (ties by record index), from
+// which it writes itself into the two sorted arrays. Cells over kBandCellMax records are left unsorted
+// (the walk reads them whole).
+__global__ void __launch_bounds__(kBlock) k_band_rank(BandArgs a) {
+  __shared__ Geom gs[kLdsGeoms];
+  if (a.nspaces <= kLdsGeoms)
+    for (uint32_t i = threadIdx.x; i < a.nspaces; i += kBlock) gs[i] = a.g.geom[i];
+  __syncthreads();
+  const uint32_t n = min(*a.nrec, a.rec_bound);
+  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const uint4 ra = a.g.rec[j].a;
+  const uint32_t sp = a.space_of[ra.z & REC_SLOT];
+  const float bx = __uint_as_float(ra.x), bz = __uint_as_float(ra.y);
+  const uint32_t key = a.nspaces <= kLdsGeoms ? cell_key_of(gs[sp], bx, bz) : cell_key_of(a.g.geom[sp], bx, bz);
+  const uint32_t s = a.g.cs[key], e = a.g.cs[key + 1];
+  const Rec r = a.g.rec[j];
+  if (e - s > kBandCellMax) {  // copied in place, unsorted (the walk reads the cell whole)
+    a.rec_out[j] = r;
+    return;
+  }
+  const float2 kj = a.key2[j];
+  uint32_t rx = 0, rz = 0;
+  for (uint32_t i = s; i < e; ++i) {
+    const float2 ki = a.key2[i];
+    rx += (ki.x < kj.x || (ki.x == kj.x && i < j)) ? 1u : 0u;
+    rz += (ki.y < kj.y || (ki.y == kj.y && i < j)) ? 1u : 0u;
+  }
+  a.rec_out[s + rx] = r;
+  a.xk[s + rx] = kj.x;
+  a.zk[s + rz] = kj.y;
+  a.zi[s + rz] = s + rx;
+}
+
+void launch_band_keys(const BandArgs& b, hipStream_t st) {
+  if (!b.rec_bound) return;
+  const uint32_t nb = (b.rec_bound + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_band_keys, dim3(std::min(nb, kBandKeyBlocks)), dim3(kBlock), 0, st, b);
+  hipLaunchKernelGGL(k_band_rank, dim3(nb), dim3(kBlock), 0, st, b);
+}
+
+// The band walk's plan for one mover (wave-uniform): the union box's cells, the cell columns that can
+// hold p.x in the left / right band and the rows that can hold p.z in the bottom / top band, and per band
+// the window of keys that can belong to such a p. False: no band walk (an Enter, or bands so wide that the
+// left and right (bottom and top) columns meet: the ring walk instead).
+struct BandPlan {
+  int x0, x1, z0, z1;      // union box (cells)
+  int cl0, cl1, cr0, cr1;  // x-strip columns: left band, right band
+  int rb0, rb1, rt0, rt1;  // z-strip rows: bottom band, top band
+  float wl0, wl1, wr0, wr1, wb0, wb1, wt0, wt1;  // key windows
+};
+
+__device__ __forceinline__ bool band_plan(const Mover& m, const Geom& g, const Judge& J, float hdx, float hdz,
+                                          BandPlan& P) {
+  if (!(m.valid0 && m.valid1)) return false;
+  const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
+  P.x0 = min(A0.x0, A1.x0), P.x1 = max(A0.x1, A1.x1);
+  P.z0 = min(A0.z0, A1.z0), P.z1 = max(A0.z1, A1.z1);
+  const float D = m.D;
+  // the core bands: p outside them on both axes is on the same side of every box edge before and after
+  // (by more than judge()'s near margin eps, so the symmetric test decides and no event is possible)
+  const float mg = 4.0f * J.eps;
+  const float xa = fminf(m.mx0, m.mx1), xb = fmaxf(m.mx0, m.mx1);
+  const float za = fminf(m.mz0, m.mz1), zb = fmaxf(m.mz0, m.mz1);
+  const float l0 = (xa - D) - mg, l1 = (xb - D) + mg, r0 = (xa + D) - mg, r1 = (xb + D) + mg;
+  const float b0 = (za - D) - mg, b1 = (zb - D) + mg, t0 = (za + D) - mg, t1 = (zb + D) + mg;
+  // key windows: |p - key| <= hd (widened for the rounding of hd and of the window bounds)
+  const float wx = hdx * 1.001f + mg, wz = hdz * 1.001f + mg;
+  P.wl0 = l0 - wx, P.wl1 = l1 + wx, P.wr0 = r0 - wx, P.wr1 = r1 + wx;
+  P.wb0 = b0 - wz, P.wb1 = b1 + wz, P.wt0 = t0 - wz, P.wt1 = t1 + wz;
+  P.cl0 = max(P.x0, cellc(l0, g.x0, g.inv_c, g.ncx)), P.cl1 = min(P.x1, cellc_hi(l1, g.x0, g.inv_c, g.ncx));
+  P.cr0 = max(P.x0, cellc(r0, g.x0, g.inv_c, g.ncx)), P.cr1 = min(P.x1, cellc_hi(r1, g.x0, g.inv_c, g.ncx));
+  P.rb0 = max(P.z0, cellc(b0, g.z0, g.inv_c, g.ncz)), P.rb1 = min(P.z1, cellc_hi(b1, g.z0, g.inv_c, g.ncz));
+  P.rt0 = max(P.z0, cellc(t0, g.z0, g.inv_c, g.ncz)), P.rt1 = min(P.z1, cellc_hi(t1, g.z0, g.inv_c, g.ncz));
+  return P.cl1 < P.cr0 && P.rb1 < P.rt0;
+}
+
+// a wave-uniform plan pinned to scalar registers
+__device__ __forceinline__ void band_pin(BandPlan& P) {
+  auto u = [](int& v) { v = __builtin_amdgcn_readfirstlane(v); };
+  auto uf = [](float& v) { v = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+  u(P.x0), u(P.x1), u(P.z0), u(P.z1), u(P.cl0), u(P.cl1), u(P.cr0), u(P.cr1), u(P.rb0), u(P.rb1), u(P.rt0), u(P.rt1);
+  uf(P.wl0), uf(P.wl1), uf(P.wr0), uf(P.wr1), uf(P.wb0), uf(P.wb1), uf(P.wt0), uf(P.wt1);
 }
 
 // Dense movers: one WAVE per mover (k_sweep lists them: boxes beyond the tile's LDS region, tiles whose
@@ -2080,6 +2146,8 @@ constexpr uint32_t kEvChunk = GW_EV_CHUNK;  // event slots a wave reserves at a 
   } while (0)
 #endif
 
+// kRing: the list of the movers k_sweep_band handed over (dense2), else k_sweep's dense list
+template <bool kRing>
 __global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_DENSE_WPE)))
 k_sweep_dense(SweepArgs a) {
   const int lane = threadIdx.x & 63;
@@ -2088,7 +2156,8 @@ k_sweep_dense(SweepArgs a) {
   // and share that XCD's L2 (skew50: dense walk 6.84 -> 6.57 ms with the batch below)
   const uint32_t wv = threadIdx.x >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
   const uint32_t wave = ((blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u) * (kDenseBlock / 64) + wv;
-  const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
+  const uint32_t* list = kRing ? a.dense2 : a.dense;
+  const uint32_t nd = min(a.ctr[kRing ? CTR_DENSE2 : CTR_DENSE], a.dense_cap);
   const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t nent = 0;
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
@@ -2103,7 +2172,7 @@ k_sweep_dense(SweepArgs a) {
   for (uint32_t b0 = 0; wave + b0 * nwaves < nd; b0 += 64u) {
     const uint32_t di = wave + (b0 + (uint32_t)lane) * nwaves;
     if (di < nd) {
-      const uint32_t ls = a.dense[di];
+      const uint32_t ls = list[di];
       mb[wv][lane][0] = make_uint4(ls, a.space_of[ls], a.opq[ls], a.old_seq[ls]);
       mb[wv][lane][1] = make_uint4(__float_as_uint(a.old_x[ls]), __float_as_uint(a.old_z[ls]),
                                    __float_as_uint(a.pos_x[ls]), __float_as_uint(a.pos_z[ls]));
@@ -2134,7 +2203,6 @@ k_sweep_dense(SweepArgs a) {
       m.mz1 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.w));
       m.D = g.D;
       const Judge J = make_judge(m, a.base);
-      const Walk w = make_walk(m, g);
       uint32_t local = 0;  // wave-uniform
       GW_DCNT(8);
       GW_DPH(1);
@@ -2163,6 +2231,7 @@ k_sweep_dense(SweepArgs a) {
         }
         local += cnt;
       };
+      const Walk w = make_walk(m, g);
       // the parts of up to 64 lanes: ranges in one round trip, then the candidates 128 at a time (two
       // loads in flight per lane); candidate k belongs to the first part whose inclusive prefix exceeds
       // k (a binary search over the lanes' prefixes)
@@ -2251,296 +2320,271 @@ k_sweep_dense(SweepArgs a) {
 #endif
 }
 
-// ---- Chunked sweep: tiles whose LDS region does not fit k_sweep's budget ----------------------------
-// (crowds: a hotspot tile's region holds thousands of records; large D: a Space whose region is wider
-// than k_sweep's cell tables). k_sweep lists such a tile's movers (grid indices, in grid order, i.e. by
-// cell) and cuts them into items of up to kChunkBlock movers. One 1024-thread block per CU takes items
-// from a work counter; per item, one thread per mover (its state, walk and judge kept in registers):
-//   - the union of the item's walks (rows zu0..zu1, columns xu0..xu1 of the tile's region: movers that
-//     are neighbours in the grid walk neighbouring rings, so the union is small even in a crowd);
-//   - that window cut into chunks of whole rows, each at most kChunkCap records and kChunkCells cells;
-//   - per chunk: its records staged into LDS (row-major cell order: a box row's cells are one contiguous
-//     LDS range), then every mover walks the rows of its walk inside the chunk (judge_stream: the
-//     candidates 64 at a time, hit masks, events queued in LDS).
-// Each region record is read from L2 once per item and chunk, instead of once per candidate mover as
-// k_sweep_dense does (config 5: ~10^9 candidates per tick at 32 B each). Events go out per block through
-// ev_tmp slots reserved kChunkEvRes at a time (holes marked, skipped by k_place): no per-wave atomics on
-// the shared counter. A mover's events are numbered in walk order over several chunks (k_slice_sort
-// sorts). A mover whose boxes leave the region (teleports), and every mover of an item whose window has
-// a row over kChunkCap records, goes to the dense list (k_sweep_dense).
-constexpr int kChunkCap = 3584;
-constexpr int kChunkCells = 4096;
-constexpr int kChunkRows = 96;          // region rows at most (tile + 2 reach, reach <= 32)
-constexpr uint32_t kChunkEvRes = 2048;  // ev_tmp slots a block reserves at a time
-constexpr int kChunkCellsPT = kChunkCells / kChunkBlock;
-
-struct ChunkSmem {
-  static constexpr uint32_t kEv = 2048;  // event queue entries
-  uint32_t n, enter, unsorted, item;
-  uint32_t cur, left, fcur, hole_cur;
-  uint32_t hole_n, nchunk, crowded, pad;
-  int bx[4];                    // window: zu0, zu1, xu0, xu1 (block reduction)
-  uint32_t ws[16];
-  uint32_t rc[kChunkRows];      // records per window row
-  uint16_t cb[kChunkRows + 1];  // chunk k: window rows [cb[k], cb[k + 1])
-  uint4 ev[kEv];
-  uint16_t lcs[kChunkCells + 8];  // chunk cells, row-major: LDS start (+ total)
-  uint4 rp[kChunkCap];
-  uint2 rm[kChunkCap];
-  uint32_t rslot[kChunkCap];  // slot; while staging: global record index
-};
-static_assert(sizeof(ChunkSmem) <= 163840, "chunked sweep LDS");
-
-size_t chunk_lds_bytes() { return sizeof(ChunkSmem); }
-
-// exclusive scan of v over a kChunkBlock-thread block; *total = block sum (LDS scratch ws[16])
-__device__ __forceinline__ uint32_t chunk_block_scan(uint32_t v, uint32_t* ws, uint32_t* total) {
-  constexpr int NW = kChunkBlock / 64;
-  const uint32_t inc = wave_incl_scan(v);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 63) ws[w] = inc;
-  __syncthreads();
-  uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int k = 0; k < NW; ++k) {
-    const uint32_t x = ws[k];
-    pre += k < w ? x : 0u;
-    tot += x;
-  }
-  __syncthreads();
-  *total = tot;
-  return pre + inc - v;
-}
-
-// flush the block's LDS event queue into ev_tmp through the block's reserved slots (every thread)
-__device__ __forceinline__ void chunk_flush(const SweepArgs& a, ChunkSmem& sm) {
-  __syncthreads();
-  const uint32_t n = min(sm.n, ChunkSmem::kEv);
-  if (n == 0u) return;  // block-uniform
-  if (threadIdx.x == 0) {
-    sm.hole_n = 0;
-    if (sm.left < n) {  // the rest of the current reservation becomes holes; a fresh one
-      sm.hole_cur = sm.cur;
-      sm.hole_n = sm.left;
-      const uint32_t need = max(kChunkEvRes, n);
-      sm.cur = atomicAdd(&a.ctr[CTR_EVENTS], need);
-      sm.left = need;
-      if (sm.hole_n) atomicAdd(&a.ctr[CTR_HOLES], sm.hole_n);
-    }
-    sm.fcur = sm.cur;
-    sm.cur += n;
-    sm.left -= n;
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < sm.hole_n; i += kChunkBlock)
-    if (sm.hole_cur + i < a.ev_cap) a.ev_tmp[sm.hole_cur + i] = make_uint4(kEvHole, 0u, 0u, 0u);
-  for (uint32_t i = threadIdx.x; i < n; i += kChunkBlock)
-    if (sm.fcur + i < a.ev_cap) a.ev_tmp[sm.fcur + i] = sm.ev[i];
-  __syncthreads();
-  if (threadIdx.x == 0) sm.n = 0;
-  __syncthreads();
-}
-
-// block min (k = 0, 2) / max (k = 1, 3) of four ints into sm.bx (every thread)
-__device__ __forceinline__ void chunk_window(ChunkSmem& sm, int z0, int z1, int x0, int x1) {
-  if (threadIdx.x < 4) sm.bx[threadIdx.x] = (threadIdx.x & 1) ? INT_MIN : INT_MAX;
-  __syncthreads();
-  for (int o = 32; o > 0; o >>= 1) {
-    z0 = min(z0, __shfl_xor(z0, o, 64));
-    z1 = max(z1, __shfl_xor(z1, o, 64));
-    x0 = min(x0, __shfl_xor(x0, o, 64));
-    x1 = max(x1, __shfl_xor(x1, o, 64));
-  }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMin(&sm.bx[0], z0);
-    atomicMax(&sm.bx[1], z1);
-    atomicMin(&sm.bx[2], x0);
-    atomicMax(&sm.bx[3], x1);
-  }
-  __syncthreads();
-}
-
-__global__ void __launch_bounds__(kChunkBlock) k_sweep_chunked(SweepArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  ChunkSmem& sm = *reinterpret_cast<ChunkSmem*>(smem_raw);
-  const uint32_t nitems = min(a.ctr[CTR_BAND_ITEMS], a.band_items_cap);
-  if (threadIdx.x == 0) {
-    sm.n = 0;
-    sm.enter = 0;
-    sm.unsorted = 0;
-    sm.cur = 0;
-    sm.left = 0;
-  }
-  uint32_t nent = 0;
-  for (;;) {
-    __syncthreads();
-    if (threadIdx.x == 0) sm.item = atomicAdd(&a.ctr[CTR_BAND_NEXT], 1u);
-    __syncthreads();
-    const uint32_t item = sm.item;
-    if (item >= nitems) break;  // block-uniform
-    const uint4 it = a.band_items[item];
-    const uint32_t t = __builtin_amdgcn_readfirstlane(it.x), first = it.y, count = it.z;
-    const uint32_t sp = __builtin_amdgcn_readfirstlane(a.g.tile_space[t]);
-    const Geom g = uniform_geom(&a.g.geom[sp]);
-    const int reach = (int)g.pad;
-    const uint32_t tl = t - g.tile_base;
-    const int tz = __builtin_amdgcn_readfirstlane((int)(tl / (uint32_t)g.ntx));
-    const int tx = __builtin_amdgcn_readfirstlane((int)(tl - (uint32_t)tz * (uint32_t)g.ntx));
-    Region R;
-    R.zr0 = max(0, tz * kTile - reach);
-    R.zr1 = min(g.ncz - 1, tz * kTile + kTile - 1 + reach);
-    R.xr0 = max(0, tx * kTile - reach);
-    R.xr1 = min(g.ncx - 1, tx * kTile + kTile - 1 + reach);
-    // this thread's mover: state, walk and judge in registers for the whole item
-    bool act = false;
-    Mover m;
-    Walk w;
-    int wx0 = INT_MAX, wx1 = INT_MIN, wz0 = INT_MAX, wz1 = INT_MIN;
-    if (threadIdx.x < count) {
-      const uint32_t j = a.band_mv[first + threadIdx.x];
-      m = mover_of(a.g.rec[j].a, a.g.rec[j].b, a.base, g.D);
-      const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
-      act = R.holds(A1) && (!m.valid0 || R.holds(A0));
-      if (act) {
-        w = make_walk(m, g, A0, A1);
-        wz0 = w.z0, wz1 = w.z1;
-        wx0 = w.ring ? w.ax0 : min(w.ax0, w.bx0);  // (ring: a = the union's columns, b = the inner ones)
-        wx1 = w.ring ? w.ax1 : max(w.ax1, w.bx1);
-      }
-    }
-    // (a mover outside the region: the dense list, as k_sweep does)
-    {
-      const bool out = threadIdx.x < count && !act;
-      const uint32_t di = wave_append(&a.ctr[CTR_DENSE], out);
-      if (out && di < a.dense_cap) a.dense[di] = m.slot;  // (sized to the capacity: every mover fits)
-    }
-    chunk_window(sm, wz0, wz1, wx0, wx1);
-    const int zu0 = sm.bx[0], zu1 = sm.bx[1], xu0 = sm.bx[2], xu1 = sm.bx[3];
-    if (zu0 > zu1) continue;  // no mover to walk (block-uniform)
-    const int W = xu1 - xu0 + 1, nrows = zu1 - zu0 + 1;
-    // records per window row: the row's cells [xu0, xu1] are one contiguous range per tile crossed
-    for (int r = threadIdx.x; r < nrows; r += kChunkBlock) {
-      uint32_t c = 0;
-      row_entries_ranges(g, a.g.cs, zu0 + r, xu0, xu1, [&](uint32_t b, uint32_t e) { c += e - b; });
-      sm.rc[r] = c;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // chunks of whole rows (sequential: at most kChunkRows rows)
-      uint32_t k = 0, sum = 0, rows = 0;
-      sm.crowded = 0;
-      sm.cb[0] = 0;
-      for (int r = 0; r < nrows; ++r) {
-        const uint32_t c = sm.rc[r];
-        if (c > (uint32_t)kChunkCap) sm.crowded = 1;
-        if (rows && (sum + c > (uint32_t)kChunkCap || (int)(rows + 1) * W > kChunkCells)) {
-          sm.cb[++k] = (uint16_t)r;
-          sum = 0, rows = 0;
-        }
-        sum += c, ++rows;
-      }
-      sm.cb[++k] = (uint16_t)nrows;
-      sm.nchunk = k;
-    }
-    __syncthreads();
-    if (sm.crowded) {  // a row of the window holds more than a chunk: every mover to the dense list
-      const uint32_t di = wave_append(&a.ctr[CTR_DENSE], act);
-      if (act && di < a.dense_cap) a.dense[di] = m.slot;
-      continue;
-    }
-    uint32_t local = 0;
-    const uint32_t nchunk = sm.nchunk;
-    for (uint32_t ck = 0; ck < nchunk; ++ck) {
-      const int c0 = zu0 + sm.cb[ck], c1 = zu0 + sm.cb[ck + 1] - 1;
-      const int ncell = (c1 - c0 + 1) * W;
-      // ---- stage: cell starts (kChunkCellsPT consecutive cells per thread), block scan, source map,
-      // then one 32-B gather per record into the LDS form ----
-      {
-        uint32_t n[kChunkCellsPT], s0[kChunkCellsPT], sum = 0;
-        const int cc0 = threadIdx.x * kChunkCellsPT;
-        const int rr0 = small_div(cc0, W);
-        int rr = rr0, col = cc0 - rr0 * W;
-#pragma unroll
-        for (int k = 0; k < kChunkCellsPT; ++k) {
-          n[k] = 0, s0[k] = 0;
-          if (cc0 + k < ncell) {
-            const uint32_t key = cell_key(g, xu0 + col, c0 + rr);
-            s0[k] = a.g.cs[key];
-            n[k] = a.g.cs[key + 1] - s0[k];
-          }
-          sum += n[k];
-          if (++col == W) col = 0, ++rr;
-        }
-        uint32_t total;
-        uint32_t pre = chunk_block_scan(sum, sm.ws, &total);
-#pragma unroll
-        for (int k = 0; k < kChunkCellsPT; ++k) {
-          if (cc0 + k < ncell) {
-            sm.lcs[cc0 + k] = (uint16_t)pre;
-            for (uint32_t q = 0; q < n[k]; ++q) sm.rslot[pre + q] = s0[k] + q;
-          }
-          pre += n[k];
-        }
-        if (threadIdx.x == 0) sm.lcs[ncell] = (uint16_t)total;
-        __syncthreads();
-        // entry i of the source map is read and then overwritten by the same thread only: no barrier in
-        // between; two gathers in flight per thread (the mover state held across the item leaves room
-        // for no more)
-        for (uint32_t i = threadIdx.x; i < total; i += 2 * kChunkBlock) {
-          const uint32_t i2 = i + kChunkBlock;
-          const uint32_t s1 = sm.rslot[i], s2 = i2 < total ? sm.rslot[i2] : s1;
-          const Rec r1 = a.g.rec[s1], r2 = a.g.rec[s2];
-          lds_record(r1.a, r1.b, a.base, a.n_ops, sm.rp[i], sm.rm[i], sm.rslot[i]);
-          if (i2 < total) lds_record(r2.a, r2.b, a.base, a.n_ops, sm.rp[i2], sm.rm[i2], sm.rslot[i2]);
-        }
-        __syncthreads();
-      }
-      // ---- walk: this mover's rows inside the chunk ----
-      const Judge J = make_judge(m, a.base);  // (recomputed per chunk: not held across the staging)
-      const int r0 = act ? max(w.z0, c0) : 1, r1 = act ? min(w.z1, c1) : 0;
-      const int h = r1 - r0;
-      for (int rel = 0; __any(rel <= h); ++rel) {  // wave-uniform trip count
-        const int r = r0 + rel;
-        int a0 = 1, a1 = 0, b0 = 1, b1 = 0;
-        if (rel <= h) walk_row(w, r, a0, a1, b0, b1);
-        const int rb = (r - c0) * W - xu0;
-        auto seg = [&](int x0, int x1) {
-          const uint32_t jb = x0 <= x1 ? (uint32_t)sm.lcs[rb + x0] : 0u;
-          const uint32_t je = x0 <= x1 ? (uint32_t)sm.lcs[rb + x1 + 1] : 0u;
-          judge_stream(a, sm, J, m, je - jb, [&](uint32_t k) { return jb + k; }, local, nent);
+// ---- The band walk --------------------------------------------------------------------
+// k_sweep_dense's list walked by the band walk: one wave per mover as there, but for an ordinary move
+// only the cells that can hold a judge position in the symmetric difference of the two boxes (the x-strip
+// columns of the left / right band over the union's rows, the z-strip rows of the bottom / top band over
+// its columns), and in each such cell only the window of search keys that can (two binary searches per
+// cell, lane-parallel over the cells; k_band_keys / k_band_rank sorted the cells' records). A hotspot
+// cell of ~50 records yields ~3 candidates instead of all 50. The movers without a band plan (Enters,
+// moves whose bands meet) are handed to k_sweep_dense<true> (dense2), which walks their rings.
+#ifndef GW_BAND_WPE
+#define GW_BAND_WPE 6
+#endif
+#ifndef GW_BAND_TRIPS  // the cost model's trips per round of 64 band cells (0: every plan takes the band walk)
+#define GW_BAND_TRIPS 3.0f
+#endif
+constexpr float kBandTrips = GW_BAND_TRIPS;
+__global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_BAND_WPE)))
+k_sweep_band(SweepArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wv = threadIdx.x >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
+  const uint32_t wave = ((blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u) * (kDenseBlock / 64) + wv;
+  const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t nent = 0, nband = 0;  // nband: movers of the wave that took the band walk (wave-uniform)
+  uint32_t cur = 0, left = 0;    // the wave's current chunk of event slots (wave-uniform)
+  __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the wave's batch: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
+#if GW_STAMPS
+  unsigned long long dph[16] = {}, dt0 = __builtin_amdgcn_s_memtime();
+#endif
+  for (uint32_t b0 = 0; wave + b0 * nwaves < nd; b0 += 64u) {
+    const uint32_t di = wave + (b0 + (uint32_t)lane) * nwaves;
+    bool elig = false;
+    uint32_t ls = 0;
+    if (di < nd) {
+      ls = a.dense[di];
+      const uint32_t sp = a.space_of[ls];
+      const uint4 u0 = make_uint4(ls, sp, a.opq[ls], a.old_seq[ls]);
+      const uint4 u1 = make_uint4(__float_as_uint(a.old_x[ls]), __float_as_uint(a.old_z[ls]),
+                                  __float_as_uint(a.pos_x[ls]), __float_as_uint(a.pos_z[ls]));
+      mb[wv][lane][0] = u0;
+      mb[wv][lane][1] = u1;
+      // this lane's mover: a band plan? (else the ring walk, k_sweep_dense<true>)
+      Mover m;
+      m.slot = ls, m.q = u0.z, m.q0 = u0.w, m.rank = m.q - a.base;
+      m.valid0 = m.q0 != 0, m.valid1 = true;
+      m.mx0 = __uint_as_float(u1.x), m.mz0 = __uint_as_float(u1.y);
+      m.mx1 = __uint_as_float(u1.z), m.mz1 = __uint_as_float(u1.w);
+      const Geom gl = a.g.geom[sp];
+      m.D = gl.D;
+      BandPlan P;
+      elig = band_plan(m, gl, make_judge(m, a.base), __uint_as_float(a.band_hd[2 * sp]),
+                       __uint_as_float(a.band_hd[2 * sp + 1]), P);
+      if (elig && kBandTrips > 0.0f) {
+        // cost model (memory round trips of the wave): the ring walk reads ~all records of the ring cells,
+        // 128 per trip, after one trip per 64 row parts; the band walk takes ~kBandTrips trips per 64 cells
+        // (cell starts, two search levels) and reads the window's share of the ring's records, 64 per trip.
+        // The ring's records from the cells at the four edge midpoints: a hotspot mover's edges are crowded,
+        // a large-D mover's in the sparse world around it (there the band walk only adds trips)
+        const int cz = (P.z0 + P.z1) >> 1, cx = (P.x0 + P.x1) >> 1;
+        auto cnt = [&](int c, int r) {
+          const uint32_t k = cell_key(gl, c, r);
+          return (float)(a.g.cs[k + 1] - a.g.cs[k]);
         };
-        seg(a0, a1);
-        seg(b0, b1);
+        const float nl = cnt(P.cl0, cz), nr = cnt(P.cr1, cz), nb = cnt(cx, P.rb0), nt = cnt(cx, P.rt1);
+        const float H = (float)(P.z1 - P.z0 + 1), W = (float)(P.x1 - P.x0 + 1);
+        const float ring = H * (nl + nr) + W * (nb + nt);
+        const float cells = (float)(max(0, P.cl1 - P.cl0 + 1) + max(0, P.cr1 - P.cr0 + 1)) * H +
+                            (float)(max(0, P.rb1 - P.rb0 + 1) + max(0, P.rt1 - P.rt0 + 1)) * W;
+        const float f = fminf(1.0f, (P.wl1 - P.wl0) * gl.inv_c);
+        const float ring_trips = ceilf((2.0f * H + 2.0f) * (1.0f / 64.0f)) + ring * (1.0f / 128.0f);
+        const float band_trips = ceilf(cells * (1.0f / 64.0f)) * kBandTrips + ring * f * (1.0f / 64.0f);
+        elig = band_trips < ring_trips;
       }
-      __syncthreads();  // the chunk's LDS records are read by every walk before the next staging
-      if (sm.n >= ChunkSmem::kEv / 2) chunk_flush(a, sm);  // block-uniform
     }
-    if (act) {
-      put_count(a.rank_cnt, m.rank, local);
-      if (local > 1u) sm.unsorted = 1u;  // numbered in walk order over the chunks
+    {
+      const bool ring = di < nd && !elig;
+      const uint32_t ri = wave_append(&a.ctr[CTR_DENSE2], ring);
+      if (ring && ri < a.dense_cap) a.dense2[ri] = ls;
     }
+    unsigned long long todo = __ballot(elig);  // the batch's movers that take the band walk
+    __builtin_amdgcn_wave_barrier();  // the wave's LDS ops stay in program order
+    GW_DPH(0);
+    uint32_t gsp = ~0u;
+    Geom g;
+    float hdx = 0.0f, hdz = 0.0f;  // the Space's key spread
+    while (todo) {
+      const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
+      todo &= todo - 1ull;
+      const uint4 u0 = mb[wv][k][0], u1 = mb[wv][k][1];
+      const uint32_t sp = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.y);
+      if (sp != gsp) {  // wave-uniform: neighbouring list entries are mostly one Space
+        g = uniform_geom(&a.g.geom[sp]);
+        gsp = sp;
+        hdx = __int_as_float(__builtin_amdgcn_readfirstlane((int)a.band_hd[2 * sp]));
+        hdz = __int_as_float(__builtin_amdgcn_readfirstlane((int)a.band_hd[2 * sp + 1]));
+      }
+      Mover m;
+      m.slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.x);
+      m.q = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.z);
+      m.q0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.w);
+      m.rank = m.q - a.base;
+      m.valid0 = m.q0 != 0;
+      m.valid1 = true;
+      m.mx0 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.x));
+      m.mz0 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.y));
+      m.mx1 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.z));
+      m.mz1 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.w));
+      m.D = g.D;
+      const Judge J = make_judge(m, a.base);
+      uint32_t local = 0;  // wave-uniform
+      GW_DCNT(8);
+      GW_DPH(1);
+      // one sub-round's events (as k_sweep_dense): a ballot prefix on top of the running count, slots from
+      // the wave's current chunk of ev_tmp
+      auto emit_round = [&](int ev, uint32_t other) {
+        const unsigned long long em = __ballot(ev != 0);
+        if (!em) return;
+        const uint32_t cnt = (uint32_t)__popcll(em);
+        const uint32_t pre = (uint32_t)__popcll(em & below);
+        uint32_t gi = cur + pre;
+        if (cnt > left) {
+          uint32_t nbk = 0;
+          if (lane == 0) nbk = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
+          nbk = __shfl(nbk, 0, 64);
+          if (pre >= left) gi = nbk + (pre - left);
+          cur = nbk + (cnt - left);
+          left = kEvChunk - (cnt - left);
+        } else {
+          cur += cnt;
+          left -= cnt;
+        }
+        if (ev) {
+          if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
+          nent += ev == 2 ? 1u : 0u;
+        }
+        local += cnt;
+      };
+      // ---- the band walk: only the cells that can hold a position in the symmetric
+      // difference of the two boxes, and in each only the window of keys that can (binary search) ----
+      BandPlan P;
+      band_plan(m, g, J, hdx, hdz, P);
+      band_pin(P);
+      {
+        const int H = P.z1 - P.z0 + 1, W = P.x1 - P.x0 + 1;
+        const int nxl = max(0, P.cl1 - P.cl0 + 1), nxr = max(0, P.cr1 - P.cr0 + 1);
+        const int nzb = max(0, P.rb1 - P.rb0 + 1), nzt = max(0, P.rt1 - P.rt0 + 1);
+        const uint32_t NX = (uint32_t)((nxl + nxr) * H), N = NX + (uint32_t)((nzb + nzt) * W);
+        for (uint32_t ib = 0; ib < N; ib += 64) {
+          // this lane's cell: x-strip cells (columns of the left / right band over the union's rows: keys
+          // by x), then z-strip cells (rows of the bottom / top band over the union's columns: keys by z;
+          // dd marks a column that is also in an x-strip, whose records with their x key in that strip's
+          // window were judged there)
+          const uint32_t it = ib + (uint32_t)lane;
+          uint32_t p0 = 0, p1 = 0;
+          int kind = 0;  // 0: x keys (the records in x order), 1: z keys, 2: the cell's records (an unsorted cell)
+          int dd = 0;
+          float w0 = 0.0f, w1 = 0.0f;
+          if (it < N) {
+            int c, r;
+            if (it < NX) {
+              const int ci = small_div((int)it, H);
+              r = P.z0 + (int)it - ci * H;
+              const bool left = ci < nxl;
+              c = left ? P.cl0 + ci : P.cr0 + ci - nxl;
+              w0 = left ? P.wl0 : P.wr0;
+              w1 = left ? P.wl1 : P.wr1;
+            } else {
+              const int i2 = (int)(it - NX), ri = small_div(i2, W);
+              c = P.x0 + i2 - ri * W;
+              const bool bot = ri < nzb;
+              r = bot ? P.rb0 + ri : P.rt0 + ri - nzb;
+              w0 = bot ? P.wb0 : P.wt0;
+              w1 = bot ? P.wb1 : P.wt1;
+              kind = 1;
+              dd = (c >= P.cl0 && c <= P.cl1 ? 1 : 0) | (c >= P.cr0 && c <= P.cr1 ? 2 : 0);
+            }
+            const uint32_t ck = cell_key(g, c, r);
+            p0 = a.g.cs[ck];
+            p1 = a.g.cs[ck + 1];
+            if (p1 - p0 > kBandCellMax) {  // unsorted: read whole, once (by its x-strip item when it has one)
+              kind = 2;
+              if (dd) p1 = p0;
+            }
+          }
+          {  // the key window [w0, w1] of a sorted cell: lower and upper bound together, fanout 8 (a cell of
+             // <= 64 records in two round trips, all of a round's probes in flight together)
+            const float* arr = kind == 1 ? a.band_zk : a.band_xk;
+            uint32_t ll = p0, lh = kind < 2 ? p1 : p0, ul = ll, uh = lh;  // lb in [ll, lh], ub in [ul, uh]
+            while (__any(lh > ll || uh > ul)) {
+              const uint32_t sl = (lh - ll + 7) >> 3, su = (uh - ul + 7) >> 3;
+              float kl[8], ku[8];
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                const uint32_t ql = ll + (uint32_t)(q + 1) * sl - 1, qu = ul + (uint32_t)(q + 1) * su - 1;
+                kl[q] = (sl && ql < lh) ? arr[ql] : __builtin_inff();
+                ku[q] = (su && qu < uh) ? arr[qu] : __builtin_inff();
+              }
+              uint32_t cl = 0, cu = 0;  // probes below the bound (a prefix: the keys are sorted)
+#pragma unroll
+              for (int q = 0; q < 8; ++q) {
+                cl += kl[q] < w0 ? 1u : 0u;
+                cu += ku[q] <= w1 ? 1u : 0u;
+              }
+              if (sl) {
+                const uint32_t nll = ll + cl * sl, qc = ll + (cl + 1) * sl - 1;
+                lh = min(lh, qc), ll = min(nll, lh);
+              }
+              if (su) {
+                const uint32_t nul = ul + cu * su, qc = ul + (cu + 1) * su - 1;
+                uh = min(uh, qc), ul = min(nul, uh);
+              }
+            }
+            if (kind < 2) p0 = ll, p1 = max(ul, ll);
+          }
+          GW_DPH(3);
+          const uint32_t cnt = p1 - p0;
+          const uint32_t incl = wave_incl_scan(cnt), excl = incl - cnt;
+          const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+          for (uint32_t b = 0; b < total; b += 64) {
+            const uint32_t kc = b + (uint32_t)lane;
+            int lo = 0, hi = 63;  // the lane holding candidate kc: first inclusive prefix above kc
+#pragma unroll
+            for (int st = 0; st < 6; ++st) {
+              const int mid = (lo + hi) >> 1;
+              if (__shfl(incl, mid, 64) > kc) hi = mid;
+              else lo = mid + 1;
+            }
+            const uint32_t pos = __shfl(p0, lo, 64) + (kc - __shfl(excl, lo, 64));
+            const int kd = __shfl(kind, lo, 64), dl = __shfl(dd, lo, 64);
+            int ev = 0;
+            uint32_t other = 0;
+            if (kc < total) {
+              const uint32_t j = kd == 1 ? a.band_zi[pos] : pos;
+              const uint4 ra = a.g.rec[j].a, rb = a.g.rec[j].b;
+              bool dup = false;
+              if (dl) {
+                float kx, kz, hx, hz;
+                band_key(ra, rb, kx, kz, hx, hz);
+                dup = ((dl & 1) && kx >= P.wl0 && kx <= P.wl1) || ((dl & 2) && kx >= P.wr0 && kx <= P.wr1);
+              }
+              if (!dup) ev = judge(J, ra, rb);
+              other = ra.z & REC_SLOT;
+            }
+            emit_round(ev, other);
+            GW_DCNT(10);
+          }
+          GW_DPH(4);
+        }
+        if (lane == 0) put_count(a.rank_cnt, m.rank, local);
+        ++nband;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // every read of the batch before the next batch is written
   }
-  chunk_flush(a, sm);
-  if (threadIdx.x == 0 && sm.left) {  // the unused rest of the last reservation: holes
-    sm.hole_cur = sm.cur;
-    sm.hole_n = sm.left;
-    atomicAdd(&a.ctr[CTR_HOLES], sm.left);
-  } else if (threadIdx.x == 0) {
-    sm.hole_n = 0;
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < sm.hole_n; i += kChunkBlock)
-    if (sm.hole_cur + i < a.ev_cap) a.ev_tmp[sm.hole_cur + i] = make_uint4(kEvHole, 0u, 0u, 0u);
-  if (nent) atomicAdd(&sm.enter, nent);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (sm.enter) atomicAdd(&a.ctr[CTR_ENTER], sm.enter);
-    if (sm.unsorted) a.ctr[CTR_UNSORTED] = 1u;
-  }
-}
-
-void chunk_init() {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep_chunked),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ChunkSmem));
+  for (uint32_t i = lane; i < left; i += 64)
+    if (cur + i < a.ev_cap) a.ev_tmp[cur + i] = make_uint4(kEvHole, 0u, 0u, 0u);
+  if (lane == 0 && left) atomicAdd(&a.ctr[CTR_HOLES], left);
+  const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);
+  if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
+  if (lane == 0 && nband) atomicAdd(&a.ctr[CTR_BAND_MV], nband);
+  // (events numbered in walk order: the slices are sorted whenever the list is not empty)
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nd) a.ctr[CTR_UNSORTED] = 1u;
+#if GW_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 16; ++k) atomicAdd(&gw_stamps[kStampWords * 16383 + k], dph[k]);
+#endif
 }
 
 // ---- Small pass (k_sweep_small) ---------------------------------------------------------------------
@@ -2821,23 +2865,21 @@ void launch_sweep_small(const SmallArgs& a, hipStream_t st) {
 uint32_t sweep_ev_lds() { return kEvLds; }
 
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
-  if (a.use_lds == 0) {  // (the host passes no per-tile regions for this variant)
-    const uint32_t n = a.n_rec + (a.n_leaves_dev ? a.n_ops : a.n_leaves);
-    if (n) hipLaunchKernelGGL(k_sweep_flat, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, a);
-    return;
-  }
   if (a.ntiles) hipLaunchKernelGGL(k_sweep, dim3(a.ntiles), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
   if (a.leave_blocks)
     hipLaunchKernelGGL(k_sweep_leaves, dim3(a.leave_blocks * ((kSweepBlock + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        st, a);
-  // crowded tiles' items: one block per CU pulling items; launched when the previous pass had some (the
-  // host re-runs the sweep when this one lists items after all, as for the dense list)
-  if (a.band_items && a.band_hint)
-    hipLaunchKernelGGL(k_sweep_chunked, dim3(a.chunk_grid), dim3(kChunkBlock), sizeof(ChunkSmem), st, a);
   // the dense list's length is on the device: a fixed grid that exits at once when it is empty. Not
   // launched at all when the previous pass had no dense mover (an empty launch cost 4.8 us per config-2
   // tick): if this pass lists some after all, the host re-runs the sweep with it (run_pass)
-  if (a.dense && a.dense_hint) hipLaunchKernelGGL(k_sweep_dense, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
+  if (a.dense && a.dense_hint) {
+    if (a.band_xk && a.dense2) {  // the band walk, then the ring walk of the movers it hands over
+      hipLaunchKernelGGL(k_sweep_band, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
+      hipLaunchKernelGGL(k_sweep_dense<true>, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
+    } else {
+      hipLaunchKernelGGL(k_sweep_dense<false>, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
+    }
+  }
 }
 
 // Canonical order: events bucketed by the mover's op rank (scan of per-rank counts), then each

@@ -102,15 +102,6 @@ struct Grid {  // one pass's cell-sorted records (two buffers, alternating betwe
 
 }  // namespace
 
-#ifndef GW_CHUNK_MIN_RECS
-#define GW_CHUNK_MIN_RECS 0u
-#endif
-#ifndef GW_CHUNK_MAX_RECS
-#define GW_CHUNK_MAX_RECS 0u  // off by default: slower than the dense walk on skew and skew50 (r04_c3)
-#endif
-#ifndef GW_CHUNK_MAX_PAD
-#define GW_CHUNK_MAX_PAD 32u
-#endif
 struct gwaoi_mgr {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -204,10 +195,16 @@ struct gwaoi_mgr {
   uint32_t* tile_walk = nullptr; // tile-bucketed build: per tile of the pass's grid, holds a reported mover
   uint32_t* tile_acted = nullptr;  // per tile: slots of the pass's ops (k_bin_tsort; duplicate-slot check)
   bool rerun_counting = false;   // the previous pass re-ran its build: this one uses the counting build
-  bool chunked = true;           // crowded tiles take k_sweep_chunked (gwaoi_debug_set_sweep_lds(3): off)
-  // which over-budget tiles k_sweep_chunked takes (gwaoi_debug_set_chunked): records in [min, max], halo
-  // at most max_pad cells; the rest walk from L2 (k_sweep_dense)
-  uint32_t chunk_min_recs = GW_CHUNK_MIN_RECS, chunk_max_recs = GW_CHUNK_MAX_RECS, chunk_max_pad = GW_CHUNK_MAX_PAD;
+  // the band walk of k_sweep_dense: the grid's records sorted per cell by search key, built
+  // after the grid of every pass that launches k_sweep_dense (gwaoi_debug_set_band: 0 off)
+  int band_mode = 1;
+  float2* band_key2 = nullptr;
+  float *band_xk = nullptr, *band_zk = nullptr;
+  uint32_t* band_zi = nullptr;
+  uint32_t* band_hd = nullptr;   // [2 nspaces]
+  uint32_t* band_dense2 = nullptr;  // [cap] the dense movers the band walk leaves to the ring walk
+  uint64_t band_cap = 0;         // records the arrays hold (0: not allocated)
+  uint64_t band_builds = 0, band_movers = 0;
   uint32_t* tile_ev = nullptr;   // per tile: events k_sweep queued in the tile's region of ev_tmp
   uint32_t* tile_ent = nullptr;  // per tile: their enter events
   uint32_t nblk = 0;
@@ -219,11 +216,6 @@ struct gwaoi_mgr {
   uint32_t* d_pub = nullptr;     // its device address
   uint32_t pub_seq = 0;
   uint32_t last_dense = ~0u;     // dense movers of the last pass (k_sweep_dense launched when non-zero)
-  uint32_t last_band = ~0u;      // chunked-sweep items of the last pass (k_sweep_chunked launched when non-zero)
-  uint32_t* band_mv = nullptr;   // k_sweep_chunked's movers (grid indices) and items
-  uint4* band_items = nullptr;
-  uint32_t band_mv_cap = 0, band_items_cap = 0, chunk_grid = 256;
-  uint64_t band_reruns = 0;
   bool last_unsorted = true;     // the last pass needed k_slice_sort (its grid: one thread per op)
   // small passes (run_small_pass): the overlay of slots with an op since the grid was last built
   uint32_t* ov_tag = nullptr;    // [cap] grid generation in which the slot joined the overlay
@@ -237,7 +229,7 @@ struct gwaoi_mgr {
   uint64_t small_passes = 0;
   struct {                       // the last timed pass, collected once its events are complete
     bool pending = false;
-    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0, chunked = 0;
+    uint32_t n_ops = 0, nev = 0, records = 0, ncells = 0, dense = 0, band = 0;
   } tpend;
   // events
   uint4* ev_tmp = nullptr;
@@ -402,9 +394,7 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
                                   std::fabs((double)z1)});
     const double span = ((double)sh.desc.dist * (1.0 + 1e-5) + (maxc + sh.desc.dist) * 1e-6) / c;
     int reach = (int)std::ceil(span) + 1;
-    // the chunked sweep (crowded tiles, and every tile of a Space whose region is over k_sweep's budget)
-    // takes halos up to one tile wide; wider ones walk from L2 (k_sweep_dense)
-    g.pad = reach <= gw::kTile ? (uint32_t)reach : 0u;
+    g.pad = 0;
     if ((gw::kTile + 2 * reach) * (gw::kTile + 2 * reach) > gw::kSweepRegCells) reach = 0;  // LDS path off for this Space
     g.reach = reach;
     base += (uint32_t)(tx * tz) * gw::kTileCells;
@@ -473,6 +463,50 @@ int ensure_events(gwaoi_mgr* m, uint64_t need_out, uint32_t need_tmp, uint64_t k
     m->ev_cap = nc;
   }
   if (host) RCHK(ensure_host_events(m, m->ev_cap, keep));
+  return GWAOI_OK;
+}
+
+// The band walk's keys over grid gi (records <= bound): per record its {x, z} search keys, per cell the
+// records sorted by each, per Space the keys' spread. The arrays are allocated on first use for
+// the grid's largest size (2 records per slot); without the memory the dense walk reads whole rings.
+int build_band_keys(gwaoi_mgr* m, int gi, uint32_t bound, bool* built) {
+  *built = false;
+  Grid& G = m->grid[gi];
+  if (!G.ntiles || !bound) return GWAOI_OK;
+  if (!m->band_cap) {
+    const uint64_t n = 2 * (uint64_t)m->cap;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < n * 20 + 4ull * m->cap + (64ull << 20)) return GWAOI_OK;
+    if (dalloc(&m->band_key2, n) || dalloc(&m->band_xk, n) || dalloc(&m->band_zk, n) || dalloc(&m->band_zi, n) ||
+        dalloc(&m->band_hd, 2 * (size_t)m->nspaces) || dalloc(&m->band_dense2, m->cap)) {  // (no room: the ring walk)
+      for (void* p : {(void*)m->band_key2, (void*)m->band_xk, (void*)m->band_zk, (void*)m->band_zi, (void*)m->band_hd,
+                      (void*)m->band_dense2})
+        if (p) hipFree(p);
+      m->band_key2 = nullptr, m->band_xk = m->band_zk = nullptr, m->band_zi = m->band_hd = m->band_dense2 = nullptr;
+      return GWAOI_OK;
+    }
+    m->band_cap = n;
+  }
+  HIPCHK(hipMemsetAsync(m->band_hd, 0, 2 * (size_t)m->nspaces * sizeof(uint32_t), m->stream));
+  gw::BandArgs b{};
+  b.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
+  b.space_of = m->space_of;
+  b.nspaces = m->nspaces;
+  b.rec_bound = (uint32_t)std::min<uint64_t>(bound, m->band_cap);
+  b.nrec = G.cs + G.ncells;
+  b.key2 = m->band_key2;
+  // the records sorted by x key inside their cells go into the other grid's record buffer (this pass does
+  // not read it: it was the build's bucket buffer), which then becomes this grid's
+  b.rec_out = m->grid[gi ^ 1].rec;
+  b.xk = m->band_xk;
+  b.zk = m->band_zk;
+  b.zi = m->band_zi;
+  b.hd = m->band_hd;
+  gw::launch_band_keys(b, m->stream);
+  HIPCHK(hipGetLastError());
+  std::swap(G.rec, m->grid[gi ^ 1].rec);
+  m->band_builds++;
+  *built = true;
   return GWAOI_OK;
 }
 
@@ -582,6 +616,11 @@ int renormalise(gwaoi_mgr* m) {
   HIPCHK(hipMemcpy(m->seq, q.data(), m->cap * sizeof(uint32_t), hipMemcpyHostToDevice));
   HIPCHK(hipMemsetAsync(m->opq, 0, (size_t)m->cap * sizeof(uint32_t), m->stream));  // stale op seqs
   RCHK(build_grid(m, m->cur, 0, 0, nullptr, kBuildCounting));
+  // the grid now holds every slot's current state with the new seqs: the overlay (copies of records
+  // with the old seqs) starts over, as after any full build
+  m->grid_gen++;
+  m->ov_bound = 0;
+  HIPCHK(hipMemsetAsync(m->ov_count, 0, sizeof(uint32_t), m->stream));
   m->next_seq = (uint32_t)v.size() + 1;
   HIPCHK(hipStreamSynchronize(m->stream));
   return GWAOI_OK;
@@ -616,7 +655,7 @@ int collect_timing(gwaoi_mgr* m) {
   m->stats.grid_records += m->tpend.records;
   m->stats.grid_cells += m->tpend.ncells;
   m->stats.dense_movers += m->tpend.dense;
-  m->stats.chunked_movers += m->tpend.chunked;
+  m->stats.band_movers += m->tpend.band;
   return GWAOI_OK;
 }
 
@@ -849,7 +888,7 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
       m->tpend.records = 0;
       m->tpend.ncells = 0;
       m->tpend.dense = 0;
-      m->tpend.chunked = 0;
+      m->tpend.band = 0;
     }
     break;
   }
@@ -871,7 +910,7 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
   m->dv_kind = nullptr;
   m->dv_space = nullptr;
   m->dv_count = nullptr;
-  return GWAOI_OK;  // (last_unsorted and the dense / chunked hints stay the last full pass's)
+  return GWAOI_OK;  // (last_unsorted and the dense hint stay the last full pass's)
 }
 
 // The grid of the last full build plus an overlay is current for the sweep, not for readers of the grid
@@ -973,8 +1012,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   // re-run, each with its own bound: the one-pass build's plan did not hold (build_rr), the event buffers
   // were too small (ev_rr), the sweep listed dense movers while k_sweep_dense was not launched (the
   // previous pass had none; dense_rr)
-  bool rebuild = false, force_dense = false, force_band = false;
-  int build_rr = 0, ev_rr = 0, dense_rr = 0, band_rr = 0;
+  bool rebuild = false, force_dense = false, keys = false;  // keys: band keys built for this pass's grid
+  int build_rr = 0, ev_rr = 0, dense_rr = 0;
   for (int attempt = 0;; ++attempt) {
     if (rebuild) {  // the one-pass build's plan did not hold: the same pass with the counting build
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_BOVF, 0, sizeof(uint32_t), st));
@@ -982,6 +1021,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       m->build_reruns++;
       m->rerun_counting = true;
       rebuild = false;
+      keys = false;
     }
     if (attempt) {  // re-run: reset what the sweep and the order stage accumulate
       // the scan turned the counts into offsets, and the sweep stores non-zero counts only
@@ -989,8 +1029,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_DENSE, 0, 2 * sizeof(uint32_t), st));  // + CTR_HOLES
-      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 3 * sizeof(uint32_t), st));  // + CTR_BAND_ITEMS, _MV
-      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, 2 * sizeof(uint32_t), st));     // + CTR_BAND_NEXT
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 3 * sizeof(uint32_t), st));  // + 13, CTR_BAND_MV
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, sizeof(uint32_t), st));
     }
     gw::SweepArgs s{};
     const Grid& G = m->grid[ng];
@@ -1025,16 +1065,17 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.dense = m->d_dense;
     s.dense_cap = m->cap;
     s.dense_hint = force_dense ? ~0u : m->last_dense;
-    s.band_mv = m->chunked ? m->band_mv : nullptr;
-    s.band_mv_cap = m->band_mv_cap;
-    s.band_items = m->chunked ? m->band_items : nullptr;
-    s.band_items_cap = m->band_items_cap;
-    s.band_hint = force_band ? ~0u : m->last_band;
-    s.chunk_grid = m->chunk_grid;
-    s.chunk_min_recs = m->chunk_min_recs;
-    s.chunk_max_recs = m->chunk_max_recs;
-    s.chunk_max_pad = m->chunk_max_pad;
     s.tile_walk = tile_build(G) ? m->tile_walk : nullptr;
+    // the band walk's keys: built over this grid when k_sweep_dense runs (the previous pass had dense
+    // movers, or this is the re-run that walks them)
+    if (s.dense_hint && m->band_mode && !keys) RCHK(build_band_keys(m, ng, s.n_rec, &keys));
+    // (after build_band_keys: it allocates the arrays, dense2 included, on first use)
+    s.dense2 = keys ? m->band_dense2 : nullptr;
+    s.g.rec = G.rec;  // (build_band_keys replaced it by the records sorted by x key inside each cell)
+    s.band_xk = keys ? m->band_xk : nullptr;
+    s.band_zk = keys ? m->band_zk : nullptr;
+    s.band_zi = keys ? m->band_zi : nullptr;
+    s.band_hd = keys ? m->band_hd : nullptr;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
@@ -1092,15 +1133,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       set_err("tile build overflow persisted");
       return GWAOI_ERR_NOMEM;
     }
-    if (m->h_ctr[gw::CTR_BAND_ITEMS] && s.band_items && !s.band_hint) {  // crowded tiles nobody walked
-      if (band_rr++ < 1) {
-        force_band = true;
-        m->band_reruns++;
-        continue;
-      }
-      set_err("chunked-sweep items left unwalked");
-      return GWAOI_ERR_STATE;
-    }
     if (m->h_ctr[gw::CTR_DENSE] && !s.dense_hint) {  // dense movers nobody walked: the sweep again, with them
       if (dense_rr++ < 1) {
         force_dense = true;
@@ -1126,7 +1158,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       m->tpend.records = m->h_ctr[gw::CTR_RECORDS];
       m->tpend.ncells = m->grid[ng].ncells;
       m->tpend.dense = m->h_ctr[gw::CTR_DENSE];
-      m->tpend.chunked = m->h_ctr[gw::CTR_BAND_MV];
+      m->tpend.band = m->h_ctr[gw::CTR_BAND_MV];
     }
     break;
   }
@@ -1145,7 +1177,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   m->pass_id++;
   if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
   m->last_dense = m->h_ctr[gw::CTR_DENSE];
-  m->last_band = m->h_ctr[gw::CTR_BAND_ITEMS];
+  m->band_movers += m->h_ctr[gw::CTR_BAND_MV];
   m->last_unsorted = m->h_ctr[gw::CTR_UNSORTED] != 0;
   m->n_present_dev = m->n_present;
   m->dv_kind = nullptr;
@@ -1234,7 +1266,7 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_mv, m->band_items, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_key2, m->band_xk, m->band_zk, m->band_zi, m->band_hd, m->band_dense2, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
                    m->dx_part, m->dx_out};
@@ -1321,10 +1353,6 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->d_op_space, C));
   chk(dalloc(&m->d_leaves, C));
   chk(dalloc(&m->d_dense, C));
-  // the chunked sweep's lists: every pass's movers fit (each at most once; items per tile: its movers /
-  // kChunkBlock rounded up, at most one partial item per tile)
-  m->band_mv_cap = (uint32_t)C;
-  chk(dalloc(&m->band_mv, C));
   m->ov_cap = (uint32_t)std::min<size_t>(C, kOverlayCap);
   chk(dalloc(&m->ov_tag, C));
   chk(dalloc(&m->ov_idx, C));
@@ -1338,8 +1366,6 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->rank_cnt, C + 1));
   m->nblk = (capacity + gw::bin_chunk(capacity) - 1) / gw::bin_chunk(capacity);
   const uint64_t max_tiles = m->max_cells / gw::kTileCells + 1;
-  m->band_items_cap = (uint32_t)std::min<uint64_t>(C / 1024 + max_tiles + 16, 0xffffffffull);
-  chk(dalloc(&m->band_items, m->band_items_cap));
   const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
   chk(dalloc(&m->thist, thist_n));
   chk(dalloc(&m->ttot, 2 * (size_t)gw::kMaxLdsTiles));  // k_bin_tscatter zeroes kMaxLdsTiles of the other buffer
@@ -1401,13 +1427,7 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   static bool sweep_ready = false;
   if (!sweep_ready) {
     gw::sweep_init();
-    gw::chunk_init();
     sweep_ready = true;
-  }
-  {
-    int cus = 0;
-    m->chunk_grid = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0
-                        ? (uint32_t)cus : 256u;
   }
   if (r == GWAOI_OK)
     r = ensure_events(m, std::max<uint64_t>(1u << 16, C / 2), (uint32_t)std::max<uint64_t>(1u << 16, C / 2), 0, false);
@@ -1471,7 +1491,6 @@ void set_error(const char* fmt, ...) {
 int mgr_view(gwaoi_mgr* m, MgrView* out) {
   RCHK(check_mgr(m));
   RCHK(set_dev(m));
-  if (!(m->n_ops || m->dv_n)) RCHK(ensure_grid_current(m));  // (staged ops: the caller flushes, then asks again)
   const Grid& g = m->grid[m->cur];
   out->device = m->device;
   out->stream = m->stream;
@@ -1491,6 +1510,16 @@ int mgr_view(gwaoi_mgr* m, MgrView* out) {
   out->index_limit = m->index_limit;
   out->timing = m->timing;
   return GWAOI_OK;
+}
+
+// Readers of the grid itself (the sync fan-out) call this before mgr_view: after small passes the grid
+// lags their ops and is rebuilt from the slots' state. mgr_view stays free of side effects, so the sync
+// setters and stats calls between single-op passes never rebuild it.
+int mgr_grid_current(gwaoi_mgr* m) {
+  RCHK(check_mgr(m));
+  RCHK(set_dev(m));
+  if (m->n_ops || m->dv_n) return GWAOI_OK;  // (staged ops: the caller flushes, then asks again)
+  return ensure_grid_current(m);
 }
 
 int mgr_flush(gwaoi_mgr* m) {
@@ -2405,18 +2434,20 @@ int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
 
 int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
   RCHK(check_mgr(m));
-  // 3: the LDS sweep without the chunked sweep (crowded tiles' movers walk from L2: k_sweep_dense), A/B
-  m->chunked = enable != 3;
+  // 0: every mover walks from global memory (k_sweep lists them all for k_sweep_dense); 1: the default;
+  // 2: staging only (timing)
   m->sweep_lds = enable < 0 ? 0 : (enable > 2 ? 1 : enable);
   return GWAOI_OK;
 }
 
-int gwaoi_debug_set_chunked(gwaoi_mgr* m, int64_t min_recs, int64_t max_recs, int64_t max_pad) {
+int gwaoi_debug_set_band(gwaoi_mgr* m, int mode, uint64_t* n_band_movers) {
   RCHK(check_mgr(m));
-  auto u32 = [](int64_t v) { return (uint32_t)std::min<int64_t>(v, 0xFFFFFFFFll); };
-  if (min_recs >= 0) m->chunk_min_recs = u32(min_recs);
-  if (max_recs >= 0) m->chunk_max_recs = u32(max_recs);
-  if (max_pad >= 0) m->chunk_max_pad = u32(max_pad);
+  if (mode > 1) {
+    set_err("debug_set_band: mode %d (0 off: every dense mover walks its ring, 1 on)", mode);
+    return GWAOI_ERR_INVALID;
+  }
+  if (mode >= 0) m->band_mode = mode;
+  if (n_band_movers) *n_band_movers = m->band_movers;
   return GWAOI_OK;
 }
 

@@ -1777,6 +1777,7 @@ int gwaoi_sync_mark(gwaoi_mgr* m, const uint32_t* slots, const float* y, const f
 int gwaoi_collect_sync(gwaoi_mgr* m, uint32_t opts, gwaoi_sync_out* out) {
   gw::MgrView v;
   SyncState* s;
+  SRCHK(gw::mgr_grid_current(m));  // the walks read the grid
   SRCHK(gw::get_state(m, &v, &s));
   if (!out) return GWAOI_ERR_INVALID;
   if (v.pending) {

@@ -237,10 +237,12 @@ class Engine:
     def debug_set_sweep_lds(self, on: bool):
         check(self._L.gwaoi_debug_set_sweep_lds(self._h, 1 if on else 0))
 
-    def debug_set_chunked(self, min_recs: int = -1, max_recs: int = -1, max_pad: int = -1):
-        """gwaoi_debug_set_chunked: over-budget tiles with records in [min_recs, max_recs] and a halo of at
-        most max_pad cells take k_sweep_chunked, the rest k_sweep_dense (-1 keeps a bound)."""
-        check(self._L.gwaoi_debug_set_chunked(self._h, int(min_recs), int(max_recs), int(max_pad)))
+    def debug_set_band(self, mode: int = -1) -> int:
+        """gwaoi_debug_set_band: the band walk of the global-memory movers on (1, default) or off (0: their
+        whole rings); returns the movers that took the band walk so far."""
+        n = ctypes.c_uint64()
+        check(self._L.gwaoi_debug_set_band(self._h, int(mode), ctypes.byref(n)))
+        return int(n.value)
 
     def debug_small_pass(self, mode: int = -1) -> int:
         """Small passes (gwaoi_debug_set_small_pass): mode 0 off, 1 auto, 2 whenever possible, -1 keep;

@@ -211,8 +211,8 @@ typedef struct {
   uint64_t grid_records;   /* records of the passes' cell-sorted grids (main + ghost) */
   uint64_t grid_cells;     /* cells of those grids */
   uint64_t dense_movers;   /* movers swept one wave each (boxes beyond their tile's LDS region) */
-  uint64_t chunked_movers; /* movers of crowded tiles swept through LDS in chunks (k_sweep_chunked); this
-                              * was the reserved refined_cells word of ABI 2 (always 0 there): same layout */
+  uint64_t band_movers;    /* of the dense movers, those that took the band walk; this was
+                              * the reserved refined_cells word of ABI 2 (always 0 there): same layout */
 } gwaoi_stats;
 int gwaoi_set_timing(gwaoi_mgr* mgr, int enable);
 int gwaoi_get_stats(const gwaoi_mgr* mgr, gwaoi_stats* out);

@@ -42,9 +42,9 @@ int gwaoi_wl_pack_ingest(int device, const uint8_t* d_ids, const float* d_x, con
  * otherwise runs every ~2^31 ops). */
 struct gwaoi_mgr;
 int gwaoi_debug_set_next_seq(struct gwaoi_mgr* mgr, uint32_t next_seq);
-/* Test hook: 0 = the sweep reads candidates from global memory only (A/B of the LDS-staged path);
- * 1 = the default (LDS-staged tiles, crowded tiles chunked through LDS); 3 = LDS-staged tiles, crowded
- * tiles' movers walk from global memory (A/B of the chunked sweep). */
+/* Test hook: 0 = every mover walks from global memory (k_sweep_dense: the band walk, else its ring),
+ * the A/B of the LDS-staged path; 1 = the default (LDS-staged tiles; movers of tiles over the LDS budget
+ * walk from global memory). */
 int gwaoi_debug_set_sweep_lds(struct gwaoi_mgr* mgr, int enable);
 /* Test hook: cell size = D / cells_per_dist for grids built from now on (default 4). */
 int gwaoi_debug_set_cells_per_dist(struct gwaoi_mgr* mgr, float cells_per_dist);
@@ -73,10 +73,12 @@ int gwaoi_debug_set_small_pass(struct gwaoi_mgr* mgr, int mode, uint64_t* n_smal
  * build; -1 leaves the mode. Reports the builds of each kind and the re-runs since the manager was made. */
 int gwaoi_debug_set_build_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* n_fused, uint64_t* n_counting,
                                uint64_t* n_reruns);
-/* A/B: which tiles over k_sweep's LDS budget take the chunked LDS sweep (k_sweep_chunked): those holding
- * [min_recs, max_recs] records whose halo is at most max_pad cells; the others walk from L2
- * (k_sweep_dense). A negative value leaves that bound. */
-int gwaoi_debug_set_chunked(struct gwaoi_mgr* mgr, int64_t min_recs, int64_t max_recs, int64_t max_pad);
+/* The band walk of the global-memory movers (k_sweep_dense): 1 = on (default: per pass that
+ * walks from global memory, the grid's records are sorted per cell by search key and each ordinary move
+ * reads only the key windows of the two boxes' symmetric difference), 0 = off (every such mover reads its
+ * whole ring of cells); -1 leaves the mode. *n_band_movers (optional): movers that took the band walk
+ * since the manager was made. */
+int gwaoi_debug_set_band(struct gwaoi_mgr* mgr, int mode, uint64_t* n_band_movers);
 /* Sync fan-out path (gwaoi_collect_sync): 0 = the records written straight into their gate packets when
  * n_gates <= 8 (default), 1 = always the pair list + gate partition; -1 leaves the mode. *direct_reruns
  * (optional): direct collects whose packet buffer was too small and were written again. Requires

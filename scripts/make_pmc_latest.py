@@ -61,7 +61,7 @@ for k, cs in vals.items():
         e["wait_any_frac"] = d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]
     kern[k] = e
 # the workload's roofline kernel(s), as bench.py times them (the pass's sweep stage)
-dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_chunked", "k_sweep_dense"])
+dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_dense", "k_band_keys", "k_band_rank"])
 summed = [k for k in dominant if "bytes" in kern.get(k, {})]
 entry = {"lib_src": lib.pop(), "n": n.pop(), "source": prefix, "kernels": kern, "kernels_summed": summed,
          "bytes_per_launch": sum(kern[k]["bytes"] for k in summed) if summed else None}

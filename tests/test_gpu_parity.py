@@ -352,21 +352,22 @@ def test_config2_full_size_two_ticks(gpu, po):
     assert eng.debug_relation_mode()[0] == 4, eng.debug_relation_mode()  # every moving tick: updated
 
 
-@pytest.mark.parametrize("path", ["chunked", "dense"])
+@pytest.mark.parametrize("path", ["band", "ring", "all_global"])
 def test_skewed_crowd_dense_path(gpu, po, path):
     """Config 5 in miniature: a small-D Space with Gaussian hotspots (~100x the mean
     density) and a large-D Space in one manager. Hotspot tiles and every D=400 tile exceed the sweep's
-    LDS region: their movers take the wave-per-mover path (k_sweep_dense, the default) with its reserved
-    event slots, or, switched on for every over-budget tile, the chunked LDS sweep (k_sweep_chunked);
-    relation after the enter tick and the last tick, events every tick, against oracle (ii)."""
+    LDS region: their movers take the wave-per-mover path (k_sweep_dense) with its reserved event slots,
+    by the band walk (the default: per-cell key windows of the boxes' symmetric difference), by their whole
+    rings (band off), or with every mover of the world on that path (LDS sweep off); relation after the
+    enter tick and the last tick, events every tick, against oracle (ii)."""
     from goworld_amd.engine import Engine
     n, L = 60000, 8500.0  # the mean density of config 5 (1M in 35,000^2)
     spaces = [(50.0, 0x5EED0050), (400.0, 0x5EED0400)]
     eng = Engine(capacity=n * len(spaces), spaces=[(d, (0.0, 0.0, L, L)) for d, _ in spaces])
-    if path == "dense":
-        eng._L.gwaoi_debug_set_sweep_lds(eng.handle, 3)
-    else:
-        eng.debug_set_chunked(0, 2**32 - 1, 32)
+    if path == "ring":
+        eng.debug_set_band(0)
+    elif path == "all_global":
+        eng.debug_set_sweep_lds(False)
     eng.set_timing(True)
     pos, orcs = [], []
     for k, (d, seed) in enumerate(spaces):
@@ -400,7 +401,8 @@ def test_skewed_crowd_dense_path(gpu, po, path):
         assert len(want) > 1000
     check_relation("last tick")
     st = eng.stats()
-    assert st["chunked_movers" if path == "chunked" else "dense_movers"] > n  # the path under test was taken
+    assert st["dense_movers"] > n  # the global-memory path was taken
+    assert (st["band_movers"] > n) == (path != "ring")
 
 
 @pytest.mark.parametrize("seed", range(3))

@@ -192,3 +192,23 @@ def test_single_op_pass_over_the_event_buffers(gpu, po):
         assert len(want) == n
         _same(got, want, f"op {op[0]}")
     assert eng.debug_small_pass() - n0 == 2
+
+
+def test_seq_renormalise_with_live_overlay(gpu, po):
+    """a small pass that crosses the seq limit renormalises the seqs while the overlay holds
+    copies of records with the old seqs. The overlay must start over (the grid is rebuilt from the
+    slots' state), so the exact near-boundary tests read the renumbered seqs. Boundary-heavy world
+    (snapped coordinates, D = 10 on a 1-unit lattice), small passes forced, bit-exact against oracle (i)
+    before, across and after the renormalisation, and the relation after it."""
+    case = H.case_random_ops(seed=8123, n=400, nticks=12, ops_per_tick=20, world=60.0, dist=10.0, snap=True)
+    eng = _engine(case, 2)
+    orc = po.XZListOracle(case["dist"], case["cap"])
+    n0 = None
+    for t, ops in enumerate(case["ticks"]):
+        if t == 6:  # the overlay is non-empty here (small passes since tick 1): the next pass crosses the limit
+            n0 = eng.debug_small_pass()
+            eng.debug_set_next_seq(0x7ff00000 - 5)
+        _same(H.gpu_tick(eng, ops), H.oracle_tick(orc, ops), f"tick {t}")
+    assert eng.debug_small_pass() > n0  # small passes ran after the renormalisation too
+    rg, ro = eng.relation(), orc.relation()
+    assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1])
