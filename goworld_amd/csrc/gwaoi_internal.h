@@ -23,7 +23,6 @@ enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 
        CTR_BOVF = 10,   // the one-pass build overflowed a tile's bucket: the pass is re-run (counting build)
        CTR_NEV = 11,    // events of the pass (scan total of the per-op counts; k_place)
        CTR_UNSORTED = 12,  // set when some op's events were numbered out of canonical order (k_slice_sort sorts)
-       CTR_DENSE2 = 13,   // dense movers k_sweep_band hands to the ring walk (dense2)
        CTR_BAND_MV = 14,     // dense movers that took the band walk (k_sweep_dense)
        CTR_SMALL_OVF = 15,   // k_order_small: the pass's events exceed its LDS (the host re-runs the order stage)
        CTR_BDONE = 16,  // blocks of the one-pass build done (not published)
@@ -49,6 +48,9 @@ constexpr int kTileCells = kTile * kTile;    // 1024
 #define GW_REG_CELLS 2304
 #endif
 constexpr int kSweepRegCells = GW_REG_CELLS;  // 48 x 48
+// the big LDS sweep (one 1024-thread block per CU): regions of up to 68 x 68 cells
+constexpr int kSweepBigRows = 68;
+constexpr int kSweepBigCells = kSweepBigRows * kSweepBigRows;
 
 // Cell geometry of one Space inside one grid snapshot.
 struct Geom {
@@ -60,7 +62,7 @@ struct Geom {
   uint32_t base;      // first cell key of this Space
   uint32_t tile_base; // first tile index of this Space (base / kTileCells)
   int32_t reach;      // halo (cells) staged around a tile in the sweep (0: the region does not fit k_sweep)
-  uint32_t pad;
+  uint32_t pad;       // reach 0: the halo of the big sweep (k_sweep<SwBig>; 0: neither, the dense walk)
 };
 
 // The pass's grid: every record sorted by cell key (counting sort). Per slot: a MAIN record at its
@@ -193,6 +195,7 @@ struct SweepArgs {
   uint32_t n_rec;      // upper bound on records in the grid (flat variant grid size)
   uint32_t ncells;     // cells of the grid (cs[ncells] = record count)
   uint32_t ntiles;     // tiles of the grid: blocks [0, ntiles) take one tile each, the rest Leave ops
+  uint32_t big_t0, big_n;  // the tiles of the Spaces of the big sweep (Geom.pad): [big_t0, big_t0 + big_n)
   int use_lds;         // 1: LDS-staged sweep; 0: every mover to k_sweep_dense (tests); 2: staging only (timing)
   const uint32_t* op_slot;    // for the leave path
   const uint8_t* op_kind;     // per op (null: all moves); OP_SILENT movers are applied, not walked
@@ -220,6 +223,7 @@ struct SweepArgs {
   const float* band_zk;   // per cell by z key: the key, and
   const uint32_t* band_zi;  // the record
   const uint32_t* band_hd;
+  int band_all;           // 1: every mover with a band plan takes the band walk (cost model off; tests)
 };
 
 // Band keys of the pass's grid for k_sweep_dense's band walk. A record's judge position p is

@@ -971,33 +971,51 @@ constexpr int kSweepBlock = GW_SWEEP_BLOCK;  // 8 waves: a config-2 tile holds ~
 #define GW_EV_LDS 256
 #endif
 constexpr int kEvLds = GW_EV_LDS;      // events staged per block before spilling to global atomics
-constexpr int kRegCells = kSweepRegCells;  // max cells of a staged region (48 x 48)
 #ifndef GW_CAP
 #define GW_CAP 1200
 #endif
-constexpr int kCap = GW_CAP;  // max records staged (config 2: ~1030 +- 32 in a 44 x 44 region)
+// GW_CAP: records the small sweep stages at most (config 2: ~1030 +- 32 in a 44 x 44 region)
 constexpr int kMaxRows = 48;
+// The LDS sweep in two sizes: the small one (three 512-thread blocks per CU, a region of 48 x 48 cells and
+// 1,200 records: config 2's tiles) and the big one for Spaces whose region needs more (large D at fine
+// cells: config 5's D = 200 / 400 Spaces, ~1,300 / ~2,200 records in 50 x 50 / 66 x 66 cells): one
+// 1024-thread block per CU. A Space takes one of them (Geom.reach: small, Geom.pad: big) or neither.
+template <int kB, int kCapT, int kCellsT, int kRowsT, int kWpeT>
+struct SwCfg {
+  static constexpr int kBlk = kB, kCap = kCapT, kCells = kCellsT, kRows = kRowsT, kWpe = kWpeT;
+  static constexpr int kCellsPT = (kCells + kB - 1) / kB;  // region cells per thread (staging)
+  static constexpr int kIters = (kCap + kB - 1) / kB;      // staged records per thread
+  static constexpr bool kBig = kB > 512;
+};
+using SwSmall = SwCfg<kSweepBlock, GW_CAP, kSweepRegCells, kMaxRows, GW_SWEEP_WAVES_PER_EU>;
+#ifndef GW_BIG_CAP
+#define GW_BIG_CAP 2800
+#endif
+using SwBig = SwCfg<1024, GW_BIG_CAP, kSweepBigCells, kSweepBigRows, 4>;
 constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
-struct SweepSmem {  // dynamic LDS (16-B aligned carve)
+template <class C>
+struct SweepSmemT {  // dynamic LDS (16-B aligned carve)
   static constexpr uint32_t kEv = kEvLds;  // event queue entries
   uint32_t n, enter, base, item;
   uint32_t nmv, unsorted, pad1, pad2;  // nmv: movers in mv; unsorted: a mover's events left unsorted
   uint32_t ws[16];                 // block-scan scratch
   uint4 ev[kEvLds];             // event queue
-  uint16_t lcs[kRegCells + 8];  // row-major: LDS start of each region cell (+ total)
-  uint16_t ccs[kRegCells + 8];  // column-major: start in cidx of each region cell (+ total)
-  uint16_t cidx[kCap];          // column-major order of the staged records (LDS record indices)
-  uint16_t mv[kCap];            // the tile's movers (LDS record indices)
-  uint4 rp[kCap];      // staged record, LDS form: {x_start, z_start, x_end, z_end} (float bits)
-  uint2 rm[kCap];      // {r | G, seq_start | A}: op rank (kNoRank: no op) and the validity mode (lds_record)
-  uint32_t rslot[kCap];  // slot (read only when an event is emitted); while staging: grid index | kCoreBit
+  uint16_t lcs[C::kCells + 8];  // row-major: LDS start of each region cell (+ total)
+  uint16_t ccs[C::kCells + 8];  // column-major: start in cidx of each region cell (+ total)
+  uint16_t cidx[C::kCap];          // column-major order of the staged records (LDS record indices)
+  uint16_t mv[C::kCap];            // the tile's movers (LDS record indices)
+  uint4 rp[C::kCap];      // staged record, LDS form: {x_start, z_start, x_end, z_end} (float bits)
+  uint2 rm[C::kCap];      // {r | G, seq_start | A}: op rank (kNoRank: no op) and the validity mode (lds_record)
+  uint32_t rslot[C::kCap];  // slot (read only when an event is emitted); while staging: grid index | kCoreBit
 };
+using SweepSmem = SweepSmemT<SwSmall>;
 // 24 waves per CU (160 KiB of LDS): three 512-thread blocks, or four 384-thread blocks
 #ifndef GW_SWEEP_BLOCKS_PER_CU
 #define GW_SWEEP_BLOCKS_PER_CU 3
 #endif
 static_assert(sizeof(SweepSmem) <= 163840 / GW_SWEEP_BLOCKS_PER_CU - 512, "sweep LDS budget per block");
+static_assert(sizeof(SweepSmemT<SwBig>) <= 163840 - 512, "big sweep: one block per CU");
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
 uint32_t sweep_block() { return kSweepBlock; }
@@ -1292,7 +1310,8 @@ __device__ __forceinline__ uint32_t stream_at(const RingStream& S, uint32_t k) {
   return k + S.d0 + (k >= S.p1 ? S.d1 : 0u) + (k >= S.p2 ? S.d2 : 0u) + (k >= S.p3 ? S.d3 : 0u);
 }
 
-__device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const SweepSmem& sm, RingStream& Rs,
+template <class S>
+__device__ __forceinline__ bool ring_plan(const Walk& w, const Region& R, const S& sm, RingStream& Rs,
                                           RingStream& Cs) {
   if (!w.ring || w.bz0 > w.bz1 || w.bx0 > w.bx1) return false;
   if (w.bz0 - w.z0 > 2 || w.z1 - w.bz1 > 2 || w.bx0 - w.ax0 > 2 || w.ax1 - w.bx1 > 2) return false;
@@ -1483,7 +1502,8 @@ __device__ unsigned long long gw_stamps[kStampWords * 16384];
   do {            \
   } while (0)
 #endif
-__device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm, const Mover& m, const Walk& w,
+template <class S>
+__device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, S& sm, const Mover& m, const Walk& w,
                                               const Region& R, const Geom& g, uint32_t& nent) {
 #if GW_STAMPS
   unsigned long long st0 = __builtin_amdgcn_s_memtime();
@@ -1524,9 +1544,10 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, SweepSmem& sm,
   return local;
 }
 
-// exclusive scan of v over a kSweepBlock-thread block; *total = block sum (LDS scratch `ws`)
+// exclusive scan of v over a kB-thread block; *total = block sum (LDS scratch `ws`)
+template <int kB = kSweepBlock>
 __device__ __forceinline__ uint32_t block_excl_scan_big(uint32_t v, uint32_t* ws, uint32_t* total) {
-  constexpr int NW = kSweepBlock / 64;
+  constexpr int NW = kB / 64;
   const uint32_t inc = wave_incl_scan(v);
   const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 63) ws[w] = inc;
@@ -1544,8 +1565,6 @@ __device__ __forceinline__ uint32_t block_excl_scan_big(uint32_t v, uint32_t* ws
 }
 
 
-constexpr int kCellsPerThread = (kRegCells + kSweepBlock - 1) / kSweepBlock;
-constexpr int kStageIters = (kCap + kSweepBlock - 1) / kSweepBlock;  // staged records per thread
 constexpr uint32_t kCoreBit = 0x80000000u;  // staging map: the record lies in the tile itself, not its halo
 
 __device__ __forceinline__ bool is_walker(const SweepArgs& a, const uint4 ra);
@@ -1559,8 +1578,10 @@ __device__ __forceinline__ bool is_walker(const SweepArgs& a, const uint4 ra);
 // issued together), LDS form. The tile's reported movers are listed in mv (unordered), or, when
 // their boxes leave the region, appended to the dense list (k_sweep_dense). Returns the staged count
 // (block-uniform); a count > kCap means "does not fit" and nothing was staged.
+template <class C>
 __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, const Region& R, int tcx, int tcz,
-                                          SweepSmem& sm) {
+                                          SweepSmemT<C>& sm) {
+  constexpr int kCellsPerThread = C::kCellsPT, kStageIters = C::kIters, kSweepBlock = C::kBlk, kCap = C::kCap;
   uint32_t n[kCellsPerThread], s0[kCellsPerThread];
   uint32_t sum = 0;
   const int c0 = threadIdx.x * kCellsPerThread;
@@ -1582,7 +1603,7 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
     }
   }
   uint32_t total;
-  uint32_t pre = block_excl_scan_big(sum, sm.ws, &total);
+  uint32_t pre = block_excl_scan_big<kSweepBlock>(sum, sm.ws, &total);
   GW_STAMP(8, __builtin_amdgcn_s_memrealtime());  // cell starts loaded and scanned
   if (total > (uint32_t)kCap) return total;
   {
@@ -1629,7 +1650,7 @@ __device__ __forceinline__ uint32_t stage(const SweepArgs& a, const Geom& g, con
       if (++rr == R.nrows) rr = 0, ++cc;
     }
     uint32_t tot2;
-    uint32_t pre2 = block_excl_scan_big(sum2, sm.ws, &tot2);
+    uint32_t pre2 = block_excl_scan_big<kSweepBlock>(sum2, sm.ws, &tot2);
 #pragma unroll
     for (int k = 0; k < kCellsPerThread; ++k) {
       if (c0 + k < R.ncells) sm.ccs[c0 + k] = (uint16_t)pre2;
@@ -1740,7 +1761,8 @@ __device__ __forceinline__ bool is_walker(const SweepArgs& a, const uint4 ra) {
 }
 
 // a mover from its staged LDS record (lds_record's form; movers are main records of this pass's ops)
-__device__ __forceinline__ Mover lds_mover(const SweepSmem& sm, uint32_t i, uint32_t base, float D) {
+template <class S>
+__device__ __forceinline__ Mover lds_mover(const S& sm, uint32_t i, uint32_t base, float D) {
   const uint4 p = sm.rp[i];
   const uint2 q = sm.rm[i];
   Mover m;
@@ -1761,12 +1783,20 @@ __device__ __forceinline__ Mover lds_mover(const SweepSmem& sm, uint32_t i, uint
 // One work item of k_sweep: a tile. Stage its region (which lists the tile's movers); walk them, one
 // thread per mover, consecutive rounds of the block in alternating direction (a tile holds ~520
 // movers for 512 threads). The block's LDS event queue is flushed with one global atomic at the end.
-__device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, const uint32_t item) {
+template <class C>
+__device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmemT<C>& sm, const uint32_t item) {
+  constexpr int kSweepBlock = C::kBlk, kCap = C::kCap;
   uint32_t nent = 0;  // enter events of this thread's movers
   const uint32_t t = item;
   auto no_events = [&]() {
     if (a.ev_fix && threadIdx.x == 0) a.tile_ev[t] = 0u, a.tile_ent[t] = 0u;
   };
+  // block-uniform: a scalar index, so the Space's geometry comes in with scalar loads
+  const uint32_t sp = __builtin_amdgcn_readfirstlane(a.g.tile_space[t]);
+  const Geom g = uniform_geom(&a.g.geom[sp]);
+  // a Space takes the small sweep (reach), the big one (pad) or neither; a tile of the other kernel's
+  // Space is left alone entirely (that kernel stores its events and counts)
+  if (C::kBig ? !(g.reach == 0 && g.pad > 0) : (g.reach == 0 && g.pad > 0 && a.use_lds)) return;
   if (a.tile_walk) {
     if (!a.tile_walk[t]) return no_events();  // block-uniform: no reported mover in the tile (k_bin_tsort)
   } else {
@@ -1775,10 +1805,8 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_walker(a, a.g.rec[j].a);
     if (!__syncthreads_or(mine)) return no_events();  // nothing queued: the caller's barrier follows
   }
-  // block-uniform: a scalar index, so the Space's geometry comes in with scalar loads
-  const uint32_t sp = __builtin_amdgcn_readfirstlane(a.g.tile_space[t]);
-  const Geom g = uniform_geom(&a.g.geom[sp]);
-  bool lds = a.use_lds && g.reach > 0;
+  const int reach = C::kBig ? (int)g.pad : g.reach;
+  bool lds = a.use_lds && reach > 0;
   Region R;
   int tcx = 0, tcz = 0;
   if (lds) {
@@ -1787,20 +1815,20 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     // bounds, to scalar registers (in VGPRs they were spilled once per mover)
     const int tz = __builtin_amdgcn_readfirstlane((int)(tl / (uint32_t)g.ntx));
     const int tx = __builtin_amdgcn_readfirstlane((int)(tl - (uint32_t)tz * (uint32_t)g.ntx));
-    R.zr0 = max(0, tz * kTile - g.reach);
-    R.zr1 = min(g.ncz - 1, tz * kTile + kTile - 1 + g.reach);
-    R.xr0 = max(0, tx * kTile - g.reach);
-    R.xr1 = min(g.ncx - 1, tx * kTile + kTile - 1 + g.reach);
+    R.zr0 = max(0, tz * kTile - reach);
+    R.zr1 = min(g.ncz - 1, tz * kTile + kTile - 1 + reach);
+    R.xr0 = max(0, tx * kTile - reach);
+    R.xr1 = min(g.ncx - 1, tx * kTile + kTile - 1 + reach);
     R.ncols = R.xr1 - R.xr0 + 1;
     R.nrows = R.zr1 - R.zr0 + 1;
     R.ncells = R.nrows * R.ncols;
     tcx = tx * kTile - R.xr0;
     tcz = tz * kTile - R.zr0;
-    lds = R.ncells <= kRegCells && R.nrows <= kMaxRows && R.ncols <= 3 * kTile;
+    lds = R.ncells <= C::kCells && R.nrows <= C::kRows && R.ncols <= C::kRows;
   }
   if (lds) {
     GW_STAMP(1, __builtin_amdgcn_s_memrealtime());
-    const uint32_t nst = stage(a, g, R, tcx, tcz, sm);
+    const uint32_t nst = stage<C>(a, g, R, tcx, tcz, sm);
     lds = nst <= (uint32_t)kCap;  // block-uniform
     __syncthreads();
     GW_STAMP(2, __builtin_amdgcn_s_memrealtime());
@@ -1815,7 +1843,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
     uint32_t mine = 0;
     for (uint32_t j = e0 + threadIdx.x; j < e1; j += kSweepBlock) mine += is_walker(a, a.g.rec[j].a) ? 1u : 0u;
     uint32_t tot;
-    const uint32_t pre = block_excl_scan_big(mine, sm.ws, &tot);
+    const uint32_t pre = block_excl_scan_big<kSweepBlock>(mine, sm.ws, &tot);
     if (threadIdx.x == 0) sm.base = tot ? atomicAdd(&a.ctr[CTR_DENSE], tot) : 0u;
     __syncthreads();
     uint32_t di = sm.base + pre;
@@ -1883,23 +1911,26 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmem& sm, co
 // 3 blocks x 8 waves per CU (49 KB of LDS each) = 6 waves per SIMD: at most 80 VGPRs. (A VGPR count
 // that allows fewer waves per SIMD than the blocks need loses a whole block per CU, whatever the
 // occupancy API reports.)
-__global__ void __launch_bounds__(kSweepBlock) __attribute__((amdgpu_waves_per_eu(GW_SWEEP_WAVES_PER_EU)))
+template <class C>
+__global__ void __launch_bounds__(C::kBlk) __attribute__((amdgpu_waves_per_eu(C::kWpe)))
 k_sweep(SweepArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  SweepSmem& sm = *reinterpret_cast<SweepSmem*>(smem_raw);
-  // one block per tile, tiles mapped XCD-aware by block index
+  SweepSmemT<C>& sm = *reinterpret_cast<SweepSmemT<C>*>(smem_raw);
+  // one block per tile of [t0, t0 + n) (all tiles; the big sweep: the range of its Spaces' tiles), tiles
+  // mapped XCD-aware by block index
+  const uint32_t t0 = C::kBig ? a.big_t0 : 0u, nt = C::kBig ? a.big_n : a.ntiles;
   if (threadIdx.x == 0) {
     const uint32_t xcd = blockIdx.x % kXcds;
-    const uint32_t per = a.ntiles / kXcds, rem = a.ntiles % kXcds;
+    const uint32_t per = nt / kXcds, rem = nt % kXcds;
     const uint32_t b = blockIdx.x;
-    sm.item = xcd * per + min(xcd, rem) + b / kXcds;
+    sm.item = t0 + xcd * per + min(xcd, rem) + b / kXcds;
     sm.n = 0;
     sm.enter = 0;
     sm.unsorted = 0;
   }
   __syncthreads();
   GW_STAMP(0, __builtin_amdgcn_s_memrealtime());
-  sweep_item(a, sm, __builtin_amdgcn_readfirstlane(sm.item));
+  sweep_item<C>(a, sm, __builtin_amdgcn_readfirstlane(sm.item));
 }
 
 int read_stamps(void* host, size_t bytes) {
@@ -1914,13 +1945,15 @@ int read_stamps(void* host, size_t bytes) {
 }
 
 int sweep_occupancy(int* blocks) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void*>(&k_sweep), kSweepBlock,
-                                                      sizeof(SweepSmem)) == hipSuccess ? 0 : -3;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, reinterpret_cast<const void*>(&k_sweep<SwSmall>),
+                                                      kSweepBlock, sizeof(SweepSmem)) == hipSuccess ? 0 : -3;
 }
 
 void sweep_init() {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sizeof(SweepSmem));
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep<SwSmall>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SweepSmem));
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep<SwBig>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SweepSmemT<SwBig>));
 }
 
 // The event queue of the one-thread-per-op global walks (k_sweep_leaves): only the queue in LDS.
@@ -2156,8 +2189,10 @@ k_sweep_dense(SweepArgs a) {
   // and share that XCD's L2 (skew50: dense walk 6.84 -> 6.57 ms with the batch below)
   const uint32_t wv = threadIdx.x >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
   const uint32_t wave = ((blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u) * (kDenseBlock / 64) + wv;
+  // (kRing: dense2 runs parallel to the dense list, the band walk's movers marked kNoKey, so the ring walk
+  // visits the rest in the same grid order: handed over compacted, its waves lost their L2 locality)
   const uint32_t* list = kRing ? a.dense2 : a.dense;
-  const uint32_t nd = min(a.ctr[kRing ? CTR_DENSE2 : CTR_DENSE], a.dense_cap);
+  const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
   const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t nent = 0;
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
@@ -2171,18 +2206,20 @@ k_sweep_dense(SweepArgs a) {
   // wave + (b0 + i) nwaves), so a batch costs one dependent chain of loads instead of one per mover.
   for (uint32_t b0 = 0; wave + b0 * nwaves < nd; b0 += 64u) {
     const uint32_t di = wave + (b0 + (uint32_t)lane) * nwaves;
-    if (di < nd) {
-      const uint32_t ls = list[di];
+    const uint32_t ls = di < nd ? list[di] : kNoKey;
+    if (ls != kNoKey) {
       mb[wv][lane][0] = make_uint4(ls, a.space_of[ls], a.opq[ls], a.old_seq[ls]);
       mb[wv][lane][1] = make_uint4(__float_as_uint(a.old_x[ls]), __float_as_uint(a.old_z[ls]),
                                    __float_as_uint(a.pos_x[ls]), __float_as_uint(a.pos_z[ls]));
     }
+    unsigned long long todo = __ballot(ls != kNoKey);  // the batch's movers
     __builtin_amdgcn_wave_barrier();  // the wave's LDS ops stay in program order
     GW_DPH(0);
-    const uint32_t nb = min(64u, (nd - wave + nwaves - 1) / nwaves - b0);  // entries of this wave left
     uint32_t gsp = ~0u;
     Geom g;
-    for (uint32_t k = 0; k < nb; ++k) {
+    while (todo) {
+      const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
+      todo &= todo - 1ull;
       // the mover's state from the wave's batch (uniform LDS address: one broadcast read per half)
       const uint4 u0 = mb[wv][k][0], u1 = mb[wv][k][1];
       const uint32_t sp = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.y);
@@ -2371,7 +2408,7 @@ k_sweep_band(SweepArgs a) {
       BandPlan P;
       elig = band_plan(m, gl, make_judge(m, a.base), __uint_as_float(a.band_hd[2 * sp]),
                        __uint_as_float(a.band_hd[2 * sp + 1]), P);
-      if (elig && kBandTrips > 0.0f) {
+      if (elig && kBandTrips > 0.0f && !a.band_all) {
         // cost model (memory round trips of the wave): the ring walk reads ~all records of the ring cells,
         // 128 per trip, after one trip per 64 row parts; the band walk takes ~kBandTrips trips per 64 cells
         // (cell starts, two search levels) and reads the window's share of the ring's records, 64 per trip.
@@ -2393,11 +2430,7 @@ k_sweep_band(SweepArgs a) {
         elig = band_trips < ring_trips;
       }
     }
-    {
-      const bool ring = di < nd && !elig;
-      const uint32_t ri = wave_append(&a.ctr[CTR_DENSE2], ring);
-      if (ring && ri < a.dense_cap) a.dense2[ri] = ls;
-    }
+    if (di < nd) a.dense2[di] = elig ? kNoKey : ls;  // the ring walk's list, in the same order
     unsigned long long todo = __ballot(elig);  // the batch's movers that take the band walk
     __builtin_amdgcn_wave_barrier();  // the wave's LDS ops stay in program order
     GW_DPH(0);
@@ -2503,6 +2536,7 @@ k_sweep_band(SweepArgs a) {
               if (dd) p1 = p0;
             }
           }
+          GW_DPH(2);
           {  // the key window [w0, w1] of a sorted cell: lower and upper bound together, fanout 8 (a cell of
              // <= 64 records in two round trips, all of a round's probes in flight together)
             const float* arr = kind == 1 ? a.band_zk : a.band_xk;
@@ -2865,7 +2899,9 @@ void launch_sweep_small(const SmallArgs& a, hipStream_t st) {
 uint32_t sweep_ev_lds() { return kEvLds; }
 
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
-  if (a.ntiles) hipLaunchKernelGGL(k_sweep, dim3(a.ntiles), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
+  if (a.ntiles) hipLaunchKernelGGL(k_sweep<SwSmall>, dim3(a.ntiles), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
+  if (a.big_n && a.use_lds)
+    hipLaunchKernelGGL(k_sweep<SwBig>, dim3(a.big_n), dim3(SwBig::kBlk), sizeof(SweepSmemT<SwBig>), st, a);
   if (a.leave_blocks)
     hipLaunchKernelGGL(k_sweep_leaves, dim3(a.leave_blocks * ((kSweepBlock + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        st, a);
@@ -3448,11 +3484,7 @@ __global__ void __launch_bounds__(kBlock) k_row_sort(const uint32_t* __restrict_
   const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t b = s < cap ? row_ptr[s] : 0u, len = s < cap ? row_ptr[s + 1] - b : 0u;
   const bool long_row = __syncthreads_or(len > kRowNetMax) != 0;
-#ifdef GW_RS_FALLBACK  // A/B knob: every block takes the segmented sort
-  if (true) {
-#else
   if (long_row) {  // block-uniform
-#endif
     seg_sort(cols, tmp, b, len, &w[0][0], ss.bigq, &ss.nbig);
     return;
   }

@@ -197,7 +197,8 @@ struct gwaoi_mgr {
   bool rerun_counting = false;   // the previous pass re-ran its build: this one uses the counting build
   // the band walk of k_sweep_dense: the grid's records sorted per cell by search key, built
   // after the grid of every pass that launches k_sweep_dense (gwaoi_debug_set_band: 0 off)
-  int band_mode = 1;
+  bool big_sweep = true;  // Spaces over the small LDS sweep's region budget take the big one (debug_set_sweep_lds 3: off)
+  int band_mode = 1;  // 0 off, 1 on (cost model per mover), 2 every mover with a band plan (tests)
   float2* band_key2 = nullptr;
   float *band_xk = nullptr, *band_zk = nullptr;
   uint32_t* band_zi = nullptr;
@@ -301,6 +302,7 @@ void space_extent(const SpaceHost& sh, float* x0, float* z0, float* x1, float* z
   *z1 = sh.seen_maxz + 0.125f * wz + D;
 }
 
+constexpr double kBigPlanRecs = 2400.0;  // planned records of a big-sweep region at most (GW_BIG_CAP 2800 staged)
 constexpr double kCellOccupancy = 0.5;  // planned entities per cell (config 2: 1M in 35,000^2, cells of 25)
 #ifndef GW_TILE_MOVERS
 #define GW_TILE_MOVERS 440.0
@@ -395,7 +397,16 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
     const double span = ((double)sh.desc.dist * (1.0 + 1e-5) + (maxc + sh.desc.dist) * 1e-6) / c;
     int reach = (int)std::ceil(span) + 1;
     g.pad = 0;
-    if ((gw::kTile + 2 * reach) * (gw::kTile + 2 * reach) > gw::kSweepRegCells) reach = 0;  // LDS path off for this Space
+    const int rw = gw::kTile + 2 * reach;  // region width (cells)
+    if (rw * rw > gw::kSweepRegCells) {  // the small LDS sweep's region budget: not this Space
+      // the big sweep (one 1024-thread block per CU) when its region fits and the planned population of
+      // a region does too (a larger one would only overflow every tile into the dense walk)
+      const double area = ((double)x1 - x0) * ((double)z1 - z0);
+      const double pop = sh.pop_hint ? (double)sh.pop_hint : (double)m->cap / std::max<uint32_t>(1, m->nspaces);
+      const double per_cell = pop * c * c / std::max(1.0, area);
+      if (m->big_sweep && rw <= gw::kSweepBigRows && (double)(rw * rw) * per_cell <= kBigPlanRecs) g.pad = (uint32_t)reach;
+      reach = 0;  // (the small LDS path off for this Space)
+    }
     g.reach = reach;
     base += (uint32_t)(tx * tz) * gw::kTileCells;
     sh.gx0 = x0;
@@ -1036,6 +1047,16 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     const Grid& G = m->grid[ng];
     s.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
     s.ntiles = G.ntiles;
+    {  // the tiles of the big sweep's Spaces, as one range
+      uint32_t b0 = ~0u, b1 = 0;
+      for (const gw::Geom& sg : G.h_geom)
+        if (sg.reach == 0 && sg.pad > 0) {
+          b0 = std::min(b0, sg.tile_base);
+          b1 = std::max(b1, sg.tile_base + (uint32_t)(sg.ntx * sg.ntz));
+        }
+      s.big_t0 = b1 > b0 ? b0 : 0u;
+      s.big_n = b1 > b0 ? b1 - b0 : 0u;
+    }
     s.ncells = G.ncells;
     s.n_rec = dev_mixed ? n_start + n_ops : n_start + n_new;  // upper bound on records (main + ghost)
     s.use_lds = m->sweep_lds;
@@ -1076,6 +1097,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.band_zk = keys ? m->band_zk : nullptr;
     s.band_zi = keys ? m->band_zi : nullptr;
     s.band_hd = keys ? m->band_hd : nullptr;
+    s.band_all = m->band_mode == 2 ? 1 : 0;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
@@ -2435,15 +2457,19 @@ int gwaoi_debug_set_next_seq(gwaoi_mgr* m, uint32_t next_seq) {
 int gwaoi_debug_set_sweep_lds(gwaoi_mgr* m, int enable) {
   RCHK(check_mgr(m));
   // 0: every mover walks from global memory (k_sweep lists them all for k_sweep_dense); 1: the default;
-  // 2: staging only (timing)
+  // 2: staging only (timing); 3: the default without the big sweep (grids built from now on)
   m->sweep_lds = enable < 0 ? 0 : (enable > 2 ? 1 : enable);
+  if (enable == 3 || enable == 1) {
+    m->big_sweep = enable == 1;
+    m->geom_dirty = true;
+  }
   return GWAOI_OK;
 }
 
 int gwaoi_debug_set_band(gwaoi_mgr* m, int mode, uint64_t* n_band_movers) {
   RCHK(check_mgr(m));
-  if (mode > 1) {
-    set_err("debug_set_band: mode %d (0 off: every dense mover walks its ring, 1 on)", mode);
+  if (mode > 2) {
+    set_err("debug_set_band: mode %d (0 off: every dense mover walks its ring, 1 on, 2 every band plan)", mode);
     return GWAOI_ERR_INVALID;
   }
   if (mode >= 0) m->band_mode = mode;

@@ -6,12 +6,14 @@
 #   suite     the GPU test suite (pytest -m gpu)
 #   bench     the default bench line (config 2, CPU baseline) and its rocprofv3 kernel stats
 #   workloads every workload in WORKLOADS: bench line + rocprofv3 kernel stats
+#   loopback  an 8-strip world of 2M per strip on one GPU (scripts/strips_loopback_bench.py): every strip's
+#             pipeline and the halo records it sends per tick
 # Outputs: gpurun_out/${TAG}_*; copy what is judged into profiles/.
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out
 TAG=${TAG:-ev}
-SEL=${STEPS_SEL:-pmc suite bench workloads}
+SEL=${STEPS_SEL:-pmc suite bench workloads loopback}
 has() { [[ " $SEL " == *" $1 "* ]]; }
 if has pmc; then
   PMC_GROUPS="FETCH_SIZE|WRITE_SIZE|SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU|SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
@@ -37,4 +39,7 @@ if has bench; then
 fi
 if has workloads; then
   STEPS=${WSTEPS:-100} WORKLOADS="${WORKLOADS:-config3 skew skew50 strips strips_skew gametick}" TAG=$TAG bash scripts/workloads_prof.sh
+fi
+if has loopback; then
+  timeout -k 10 600 python -u scripts/strips_loopback_bench.py 8 2000000 20 > gpurun_out/${TAG}_strips_loopback.json 2> gpurun_out/${TAG}_strips_loopback.err
 fi

@@ -33,16 +33,27 @@ for nd in nodes:
     nd.eng.set_timing(True)
     nd.eng.reset_stats()
 torch.cuda.synchronize()
+halo = [0] * world
+t0 = time.perf_counter()
 for t in range(4, 4 + ticks):
-    ins = LoopbackExchange.exchange([nd.prepare(t) for nd in nodes])
+    outs = [nd.prepare(t) for nd in nodes]
+    for r, (lo, ro) in enumerate(outs):  # records this strip sends its neighbours (its halo on their side)
+        halo[r] += int(lo.shape[0]) + int(ro.shape[0])
+    ins = LoopbackExchange.exchange(outs)
     for nd, i in zip(nodes, ins):
         nd.finish(*i)
 torch.cuda.synchronize()
+wall = (time.perf_counter() - t0) / ticks * 1e3
 rows = []
 for nd in nodes:
     st = nd.eng.stats()
     k = max(1, st["ticks"])
     rows.append({key: round(st[key] / k, 4) for key in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")})
     rows[-1]["ops"] = nd.last_ops
+    rows[-1]["halo_records_sent_per_tick"] = halo[nd.rank] / ticks
     nd.close()
-print(json.dumps({"world": world, "per_gpu": per, "ticks": ticks, "per_strip": rows}))
+print(json.dumps({"world": world, "per_gpu": per, "ticks": ticks, "halo_records_per_tick": sum(halo) / ticks,
+                  "wall_ms_per_tick_all_strips": wall,
+                  "note": "W strips of one world on ONE GPU, halo records handed over in-process (LoopbackExchange); "
+                          "per strip: its pipeline stages (hipEvents) and the records it sends its neighbours",
+                  "per_strip": rows}))
