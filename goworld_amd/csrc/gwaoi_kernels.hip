@@ -2358,20 +2358,80 @@ k_sweep_dense(SweepArgs a) {
 }
 
 // ---- The band walk --------------------------------------------------------------------
-// k_sweep_dense's list walked by the band walk: one wave per mover as there, but for an ordinary move
-// only the cells that can hold a judge position in the symmetric difference of the two boxes (the x-strip
-// columns of the left / right band over the union's rows, the z-strip rows of the bottom / top band over
-// its columns), and in each such cell only the window of search keys that can (two binary searches per
-// cell, lane-parallel over the cells; k_band_keys / k_band_rank sorted the cells' records). A hotspot
-// cell of ~50 records yields ~3 candidates instead of all 50. The movers without a band plan (Enters,
-// moves whose bands meet) are handed to k_sweep_dense<true> (dense2), which walks their rings.
-#ifndef GW_BAND_WPE
-#define GW_BAND_WPE 6
+// k_sweep_dense's list walked by the band walk. For an ordinary move only the cells that can hold a judge
+// position in the symmetric difference of the two boxes are read (the x-strip columns of the left / right
+// band over the union's rows, the z-strip rows of the bottom / top band over its columns), and in each
+// such cell only the window of search keys that can (a fanout-8 search per cell: k_band_keys /
+// k_band_rank sorted the cells' records). A hotspot cell of ~50 records yields ~3 candidates instead of 50.
+//
+// Every global round trip costs ~3.5k cycles under this load (GW_STAMPS phases, r05_b6), so the walk is
+// flat over the wave's batch of 64 movers: the batch's cells form ONE item stream (2 per lane per round:
+// cell starts, then two search levels, all lanes' loads in flight together), whose candidates form one
+// candidate stream (2 per lane per round), whatever mover they belong to. A mover's plan is recomputed
+// from the batch's LDS copy wherever it is needed (VALU is idle here); its judge data, dedupe windows
+// and event count live in LDS. (One mover per wave at a time, as k_sweep_dense: ~6 trips per mover,
+// no faster than the ring walk, r05_b5.) The movers without a band plan (Enters, moves whose bands meet)
+// or for which the cost model prefers the ring walk are left to k_sweep_dense<true> (dense2).
+#ifndef GW_BAND_WPE  // 4 waves per SIMD: 118 VGPRs (two cells and two candidates per lane in flight)
+#define GW_BAND_WPE 4
 #endif
-#ifndef GW_BAND_TRIPS  // the cost model's trips per round of 64 band cells (0: every plan takes the band walk)
+#ifndef GW_BAND_TRIPS  // the cost model's trips per round of 128 band cells (0: every plan takes the band walk)
 #define GW_BAND_TRIPS 3.0f
 #endif
 constexpr float kBandTrips = GW_BAND_TRIPS;
+#ifndef GW_BAND_SEARCH_MIN  // cells of fewer records are read whole instead of searched
+#define GW_BAND_SEARCH_MIN 8u
+#endif
+constexpr uint32_t kBandSearchMin = GW_BAND_SEARCH_MIN;
+
+// the cell of item li of a band plan: x-strip cells (columns of the left / right band over the union's
+// rows, keys by x), then z-strip cells (rows of the bottom / top band over the union's columns, keys by z;
+// dd marks a column that is also in an x-strip, whose records with their x key in that strip's window
+// were judged there)
+__device__ __forceinline__ void band_item(const BandPlan& P, uint32_t li, int& c, int& r, float& w0, float& w1,
+                                          int& kind, int& dd) {
+  const int H = P.z1 - P.z0 + 1, W = P.x1 - P.x0 + 1;
+  const int nxl = max(0, P.cl1 - P.cl0 + 1), nzb = max(0, P.rb1 - P.rb0 + 1);
+  const uint32_t NX = (uint32_t)((nxl + max(0, P.cr1 - P.cr0 + 1)) * H);
+  if (li < NX) {
+    const int ci = small_div((int)li, H);
+    r = P.z0 + (int)li - ci * H;
+    const bool left = ci < nxl;
+    c = left ? P.cl0 + ci : P.cr0 + ci - nxl;
+    w0 = left ? P.wl0 : P.wr0;
+    w1 = left ? P.wl1 : P.wr1;
+    kind = 0;
+    dd = 0;
+  } else {
+    const int i2 = (int)(li - NX), ri = small_div(i2, W);
+    c = P.x0 + i2 - ri * W;
+    const bool bot = ri < nzb;
+    r = bot ? P.rb0 + ri : P.rt0 + ri - nzb;
+    w0 = bot ? P.wb0 : P.wt0;
+    w1 = bot ? P.wb1 : P.wt1;
+    kind = 1;
+    dd = (c >= P.cl0 && c <= P.cl1 ? 1 : 0) | (c >= P.cr0 && c <= P.cr1 ? 2 : 0);
+  }
+}
+
+__device__ __forceinline__ uint32_t band_items(const BandPlan& P) {
+  const int H = P.z1 - P.z0 + 1, W = P.x1 - P.x0 + 1;
+  return (uint32_t)((max(0, P.cl1 - P.cl0 + 1) + max(0, P.cr1 - P.cr0 + 1)) * H +
+                    (max(0, P.rb1 - P.rb0 + 1) + max(0, P.rt1 - P.rt0 + 1)) * W);
+}
+
+// the lane whose inclusive prefix `incl` is the first above k (every lane of the wave takes part)
+__device__ __forceinline__ int wave_owner(uint32_t incl, uint32_t k) {
+  int lo = 0, hi = 63;
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const int mid = (lo + hi) >> 1;
+    if ((uint32_t)__shfl((int)incl, mid, 64) > k) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
 __global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_BAND_WPE)))
 k_sweep_band(SweepArgs a) {
   const int lane = threadIdx.x & 63;
@@ -2379,16 +2439,21 @@ k_sweep_band(SweepArgs a) {
   const uint32_t wave = ((blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u) * (kDenseBlock / 64) + wv;
   const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
   const unsigned long long below = (1ull << lane) - 1ull;
-  uint32_t nent = 0, nband = 0;  // nband: movers of the wave that took the band walk (wave-uniform)
+  uint32_t nent = 0, nband = 0;  // nband: movers of the wave that took the band walk
   uint32_t cur = 0, left = 0;    // the wave's current chunk of event slots (wave-uniform)
-  __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the wave's batch: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
+  __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the batch: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
+  __shared__ BandPlan pl[kDenseBlock / 64][64];  // per batch mover: its band plan
+  __shared__ uint2 pg[kDenseBlock / 64][64];     // per batch mover: its Space's {base, ntx} (cell keys)
+  __shared__ float2 je[kDenseBlock / 64][64];    // per batch mover: {D, eps} of its judge
+  __shared__ uint32_t lc[kDenseBlock / 64][64];  // per batch mover: its events so far
 #if GW_STAMPS
   unsigned long long dph[16] = {}, dt0 = __builtin_amdgcn_s_memtime();
 #endif
   for (uint32_t b0 = 0; wave + b0 * nwaves < nd; b0 += 64u) {
+    // ---- this lane's mover: state into the batch, a band plan, the cost model, its item count ----
     const uint32_t di = wave + (b0 + (uint32_t)lane) * nwaves;
     bool elig = false;
-    uint32_t ls = 0;
+    uint32_t ls = 0, nit = 0;
     if (di < nd) {
       ls = a.dense[di];
       const uint32_t sp = a.space_of[ls];
@@ -2397,7 +2462,6 @@ k_sweep_band(SweepArgs a) {
                                   __float_as_uint(a.pos_x[ls]), __float_as_uint(a.pos_z[ls]));
       mb[wv][lane][0] = u0;
       mb[wv][lane][1] = u1;
-      // this lane's mover: a band plan? (else the ring walk, k_sweep_dense<true>)
       Mover m;
       m.slot = ls, m.q = u0.z, m.q0 = u0.w, m.rank = m.q - a.base;
       m.valid0 = m.q0 != 0, m.valid1 = true;
@@ -2405,15 +2469,16 @@ k_sweep_band(SweepArgs a) {
       m.mx1 = __uint_as_float(u1.z), m.mz1 = __uint_as_float(u1.w);
       const Geom gl = a.g.geom[sp];
       m.D = gl.D;
+      const Judge J = make_judge(m, a.base);
       BandPlan P;
-      elig = band_plan(m, gl, make_judge(m, a.base), __uint_as_float(a.band_hd[2 * sp]),
-                       __uint_as_float(a.band_hd[2 * sp + 1]), P);
+      elig = band_plan(m, gl, J, __uint_as_float(a.band_hd[2 * sp]), __uint_as_float(a.band_hd[2 * sp + 1]), P);
+      nit = band_items(P);
       if (elig && kBandTrips > 0.0f && !a.band_all) {
-        // cost model (memory round trips of the wave): the ring walk reads ~all records of the ring cells,
-        // 128 per trip, after one trip per 64 row parts; the band walk takes ~kBandTrips trips per 64 cells
-        // (cell starts, two search levels) and reads the window's share of the ring's records, 64 per trip.
-        // The ring's records from the cells at the four edge midpoints: a hotspot mover's edges are crowded,
-        // a large-D mover's in the sparse world around it (there the band walk only adds trips)
+        // cost model (memory round trips): the ring walk reads ~all records of the ring cells, 128 per
+        // trip, after one trip per 64 row parts, for ONE mover at a time; the band walk's cells and
+        // candidates share the batch's rounds of 128 (cells: cell starts + two search levels). The ring's
+        // records from the cells at the four edge midpoints: a hotspot mover's edges are crowded, a large-D
+        // mover's in the sparse world around it (there the band walk only adds work)
         const int cz = (P.z0 + P.z1) >> 1, cx = (P.x0 + P.x1) >> 1;
         auto cnt = [&](int c, int r) {
           const uint32_t k = cell_key(gl, c, r);
@@ -2422,189 +2487,190 @@ k_sweep_band(SweepArgs a) {
         const float nl = cnt(P.cl0, cz), nr = cnt(P.cr1, cz), nb = cnt(cx, P.rb0), nt = cnt(cx, P.rt1);
         const float H = (float)(P.z1 - P.z0 + 1), W = (float)(P.x1 - P.x0 + 1);
         const float ring = H * (nl + nr) + W * (nb + nt);
-        const float cells = (float)(max(0, P.cl1 - P.cl0 + 1) + max(0, P.cr1 - P.cr0 + 1)) * H +
-                            (float)(max(0, P.rb1 - P.rb0 + 1) + max(0, P.rt1 - P.rt0 + 1)) * W;
         const float f = fminf(1.0f, (P.wl1 - P.wl0) * gl.inv_c);
         const float ring_trips = ceilf((2.0f * H + 2.0f) * (1.0f / 64.0f)) + ring * (1.0f / 128.0f);
-        const float band_trips = ceilf(cells * (1.0f / 64.0f)) * kBandTrips + ring * f * (1.0f / 64.0f);
+        const float band_trips = (float)nit * (kBandTrips / 128.0f) + ring * f * (1.5f / 128.0f);
         elig = band_trips < ring_trips;
       }
+      if (elig) {
+        pl[wv][lane] = P;
+        pg[wv][lane] = make_uint2(gl.base, (uint32_t)gl.ntx);
+        je[wv][lane] = make_float2(J.D, J.eps);
+      }
+      lc[wv][lane] = 0u;
     }
     if (di < nd) a.dense2[di] = elig ? kNoKey : ls;  // the ring walk's list, in the same order
-    unsigned long long todo = __ballot(elig);  // the batch's movers that take the band walk
+    if (!elig) nit = 0;
+    nband += (uint32_t)__popcll(__ballot(elig));
+    const uint32_t iincl = wave_incl_scan(nit), iexcl = iincl - nit;
+    const uint32_t N = __builtin_amdgcn_readlane(iincl, 63);  // the batch's band cells
     __builtin_amdgcn_wave_barrier();  // the wave's LDS ops stay in program order
     GW_DPH(0);
-    uint32_t gsp = ~0u;
-    Geom g;
-    float hdx = 0.0f, hdz = 0.0f;  // the Space's key spread
-    while (todo) {
-      const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane(__ffsll((long long)todo) - 1);
-      todo &= todo - 1ull;
-      const uint4 u0 = mb[wv][k][0], u1 = mb[wv][k][1];
-      const uint32_t sp = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.y);
-      if (sp != gsp) {  // wave-uniform: neighbouring list entries are mostly one Space
-        g = uniform_geom(&a.g.geom[sp]);
-        gsp = sp;
-        hdx = __int_as_float(__builtin_amdgcn_readfirstlane((int)a.band_hd[2 * sp]));
-        hdz = __int_as_float(__builtin_amdgcn_readfirstlane((int)a.band_hd[2 * sp + 1]));
+    // ---- item rounds: 2 cells per lane ----
+    for (uint32_t ib = 0; ib < N; ib += 128u) {
+      uint32_t p0[2], p1[2], mk[2];
+      float w0[2], w1[2];
+      int kind[2], dd[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const uint32_t it = ib + (uint32_t)(u * 64 + lane);
+        // (every lane takes part in the lane moves: a source lane outside a divergent branch is inactive)
+        const int k = wave_owner(iincl, min(it, N - 1u));
+        const uint32_t kex = (uint32_t)__shfl((int)iexcl, k, 64);
+        mk[u] = (uint32_t)k;
+        p0[u] = p1[u] = 0u;
+        kind[u] = 3, dd[u] = 0, w0[u] = w1[u] = 0.0f;
+        if (it < N) {
+          const BandPlan P = pl[wv][k];
+          const uint2 sg = pg[wv][k];
+          int c, r;
+          band_item(P, it - kex, c, r, w0[u], w1[u], kind[u], dd[u]);
+          // (cell_key on the Space's base and tile columns)
+          p0[u] = sg.x + ((uint32_t)((r >> kTileShift) * (int)sg.y + (c >> kTileShift)) << kTileCellShift) +
+                  (uint32_t)(((r & (kTile - 1)) << kTileShift) | (c & (kTile - 1)));  // (the key until its starts load)
+        }
       }
-      Mover m;
-      m.slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.x);
-      m.q = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.z);
-      m.q0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0.w);
-      m.rank = m.q - a.base;
-      m.valid0 = m.q0 != 0;
-      m.valid1 = true;
-      m.mx0 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.x));
-      m.mz0 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.y));
-      m.mx1 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.z));
-      m.mz1 = __int_as_float(__builtin_amdgcn_readfirstlane((int)u1.w));
-      m.D = g.D;
-      const Judge J = make_judge(m, a.base);
-      uint32_t local = 0;  // wave-uniform
-      GW_DCNT(8);
       GW_DPH(1);
-      // one sub-round's events (as k_sweep_dense): a ballot prefix on top of the running count, slots from
-      // the wave's current chunk of ev_tmp
-      auto emit_round = [&](int ev, uint32_t other) {
-        const unsigned long long em = __ballot(ev != 0);
-        if (!em) return;
-        const uint32_t cnt = (uint32_t)__popcll(em);
-        const uint32_t pre = (uint32_t)__popcll(em & below);
-        uint32_t gi = cur + pre;
-        if (cnt > left) {
-          uint32_t nbk = 0;
-          if (lane == 0) nbk = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
-          nbk = __shfl(nbk, 0, 64);
-          if (pre >= left) gi = nbk + (pre - left);
-          cur = nbk + (cnt - left);
-          left = kEvChunk - (cnt - left);
-        } else {
-          cur += cnt;
-          left -= cnt;
-        }
-        if (ev) {
-          if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local + pre, m.slot, other | (ev == 2 ? 0x80000000u : 0u));
-          nent += ev == 2 ? 1u : 0u;
-        }
-        local += cnt;
-      };
-      // ---- the band walk: only the cells that can hold a position in the symmetric
-      // difference of the two boxes, and in each only the window of keys that can (binary search) ----
-      BandPlan P;
-      band_plan(m, g, J, hdx, hdz, P);
-      band_pin(P);
-      {
-        const int H = P.z1 - P.z0 + 1, W = P.x1 - P.x0 + 1;
-        const int nxl = max(0, P.cl1 - P.cl0 + 1), nxr = max(0, P.cr1 - P.cr0 + 1);
-        const int nzb = max(0, P.rb1 - P.rb0 + 1), nzt = max(0, P.rt1 - P.rt0 + 1);
-        const uint32_t NX = (uint32_t)((nxl + nxr) * H), N = NX + (uint32_t)((nzb + nzt) * W);
-        for (uint32_t ib = 0; ib < N; ib += 64) {
-          // this lane's cell: x-strip cells (columns of the left / right band over the union's rows: keys
-          // by x), then z-strip cells (rows of the bottom / top band over the union's columns: keys by z;
-          // dd marks a column that is also in an x-strip, whose records with their x key in that strip's
-          // window were judged there)
-          const uint32_t it = ib + (uint32_t)lane;
-          uint32_t p0 = 0, p1 = 0;
-          int kind = 0;  // 0: x keys (the records in x order), 1: z keys, 2: the cell's records (an unsorted cell)
-          int dd = 0;
-          float w0 = 0.0f, w1 = 0.0f;
-          if (it < N) {
-            int c, r;
-            if (it < NX) {
-              const int ci = small_div((int)it, H);
-              r = P.z0 + (int)it - ci * H;
-              const bool left = ci < nxl;
-              c = left ? P.cl0 + ci : P.cr0 + ci - nxl;
-              w0 = left ? P.wl0 : P.wr0;
-              w1 = left ? P.wl1 : P.wr1;
-            } else {
-              const int i2 = (int)(it - NX), ri = small_div(i2, W);
-              c = P.x0 + i2 - ri * W;
-              const bool bot = ri < nzb;
-              r = bot ? P.rb0 + ri : P.rt0 + ri - nzb;
-              w0 = bot ? P.wb0 : P.wt0;
-              w1 = bot ? P.wb1 : P.wt1;
-              kind = 1;
-              dd = (c >= P.cl0 && c <= P.cl1 ? 1 : 0) | (c >= P.cr0 && c <= P.cr1 ? 2 : 0);
-            }
-            const uint32_t ck = cell_key(g, c, r);
-            p0 = a.g.cs[ck];
-            p1 = a.g.cs[ck + 1];
-            if (p1 - p0 > kBandCellMax) {  // unsorted: read whole, once (by its x-strip item when it has one)
-              kind = 2;
-              if (dd) p1 = p0;
-            }
-          }
-          GW_DPH(2);
-          {  // the key window [w0, w1] of a sorted cell: lower and upper bound together, fanout 8 (a cell of
-             // <= 64 records in two round trips, all of a round's probes in flight together)
-            const float* arr = kind == 1 ? a.band_zk : a.band_xk;
-            uint32_t ll = p0, lh = kind < 2 ? p1 : p0, ul = ll, uh = lh;  // lb in [ll, lh], ub in [ul, uh]
-            while (__any(lh > ll || uh > ul)) {
-              const uint32_t sl = (lh - ll + 7) >> 3, su = (uh - ul + 7) >> 3;
-              float kl[8], ku[8];
 #pragma unroll
-              for (int q = 0; q < 8; ++q) {
-                const uint32_t ql = ll + (uint32_t)(q + 1) * sl - 1, qu = ul + (uint32_t)(q + 1) * su - 1;
-                kl[q] = (sl && ql < lh) ? arr[ql] : __builtin_inff();
-                ku[q] = (su && qu < uh) ? arr[qu] : __builtin_inff();
-              }
-              uint32_t cl = 0, cu = 0;  // probes below the bound (a prefix: the keys are sorted)
-#pragma unroll
-              for (int q = 0; q < 8; ++q) {
-                cl += kl[q] < w0 ? 1u : 0u;
-                cu += ku[q] <= w1 ? 1u : 0u;
-              }
-              if (sl) {
-                const uint32_t nll = ll + cl * sl, qc = ll + (cl + 1) * sl - 1;
-                lh = min(lh, qc), ll = min(nll, lh);
-              }
-              if (su) {
-                const uint32_t nul = ul + cu * su, qc = ul + (cu + 1) * su - 1;
-                uh = min(uh, qc), ul = min(nul, uh);
-              }
-            }
-            if (kind < 2) p0 = ll, p1 = max(ul, ll);
-          }
-          GW_DPH(3);
-          const uint32_t cnt = p1 - p0;
-          const uint32_t incl = wave_incl_scan(cnt), excl = incl - cnt;
-          const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-          for (uint32_t b = 0; b < total; b += 64) {
-            const uint32_t kc = b + (uint32_t)lane;
-            int lo = 0, hi = 63;  // the lane holding candidate kc: first inclusive prefix above kc
-#pragma unroll
-            for (int st = 0; st < 6; ++st) {
-              const int mid = (lo + hi) >> 1;
-              if (__shfl(incl, mid, 64) > kc) hi = mid;
-              else lo = mid + 1;
-            }
-            const uint32_t pos = __shfl(p0, lo, 64) + (kc - __shfl(excl, lo, 64));
-            const int kd = __shfl(kind, lo, 64), dl = __shfl(dd, lo, 64);
-            int ev = 0;
-            uint32_t other = 0;
-            if (kc < total) {
-              const uint32_t j = kd == 1 ? a.band_zi[pos] : pos;
-              const uint4 ra = a.g.rec[j].a, rb = a.g.rec[j].b;
-              bool dup = false;
-              if (dl) {
-                float kx, kz, hx, hz;
-                band_key(ra, rb, kx, kz, hx, hz);
-                dup = ((dl & 1) && kx >= P.wl0 && kx <= P.wl1) || ((dl & 2) && kx >= P.wr0 && kx <= P.wr1);
-              }
-              if (!dup) ev = judge(J, ra, rb);
-              other = ra.z & REC_SLOT;
-            }
-            emit_round(ev, other);
-            GW_DCNT(10);
-          }
-          GW_DPH(4);
+      for (int u = 0; u < 2; ++u) {  // cell starts of both cells, loads in flight together
+        if (kind[u] != 3) {
+          const uint32_t ck = p0[u];
+          p0[u] = a.g.cs[ck];
+          p1[u] = a.g.cs[ck + 1];
         }
-        if (lane == 0) put_count(a.rank_cnt, m.rank, local);
-        ++nband;
       }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // a cell that is unsorted (over kBandCellMax records) or small (a search costs more round trips than
+        // reading its few records) is read whole, once: by its x-strip item when it has one (dd: the z-strip
+        // item of a corner cell then reads nothing; the rule depends only on the cell's size, so both
+        // items of a corner cell apply it alike)
+        const uint32_t nc = p1[u] - p0[u];
+        if (kind[u] != 3 && (nc > kBandCellMax || nc < kBandSearchMin)) {
+          kind[u] = 2;
+          if (dd[u]) p1[u] = p0[u];
+        }
+      }
+      GW_DPH(2);
+      {  // key windows of the sorted cells: fanout 8, both bounds of both cells per round trip
+        uint32_t ll[2], lh[2], ul[2], uh[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          ll[u] = ul[u] = p0[u];
+          lh[u] = uh[u] = kind[u] < 2 ? p1[u] : p0[u];
+        }
+        while (__any(lh[0] > ll[0] || uh[0] > ul[0] || lh[1] > ll[1] || uh[1] > ul[1])) {
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const float* arr = kind[u] == 1 ? a.band_zk : a.band_xk;
+            const uint32_t sl = (lh[u] - ll[u] + 7) >> 3, su = (uh[u] - ul[u] + 7) >> 3;
+            uint32_t cl = 0, cu = 0;  // probes below the bound (a prefix: the keys are sorted)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const uint32_t ql = ll[u] + (uint32_t)(q + 1) * sl - 1, qu = ul[u] + (uint32_t)(q + 1) * su - 1;
+              const float kl = (sl && ql < lh[u]) ? arr[ql] : __builtin_inff();
+              const float ku = (su && qu < uh[u]) ? arr[qu] : __builtin_inff();
+              cl += kl < w0[u] ? 1u : 0u;
+              cu += ku <= w1[u] ? 1u : 0u;
+            }
+            if (sl) {
+              const uint32_t nll = ll[u] + cl * sl, qc = ll[u] + (cl + 1) * sl - 1;
+              lh[u] = min(lh[u], qc), ll[u] = min(nll, lh[u]);
+            }
+            if (su) {
+              const uint32_t nul = ul[u] + cu * su, qc = ul[u] + (cu + 1) * su - 1;
+              uh[u] = min(uh[u], qc), ul[u] = min(nul, uh[u]);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          if (kind[u] < 2) p0[u] = ll[u], p1[u] = max(ul[u], ll[u]);
+      }
+      GW_DPH(3);
+      // ---- the round's candidates: one stream over both cells of every lane, 2 per lane per round ----
+      const uint32_t c0 = p1[0] - p0[0], cnt = c0 + (p1[1] - p0[1]);
+      const uint32_t cincl = wave_incl_scan(cnt), cexcl = cincl - cnt;
+      const uint32_t total = __builtin_amdgcn_readlane(cincl, 63);
+      for (uint32_t b = 0; b < total; b += 128u) {
+        uint32_t mo[2], oth[2];
+        int ev[2];
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const uint32_t kc = b + (uint32_t)(v * 64 + lane);
+          const int L = wave_owner(cincl, min(kc, total - 1u));
+          const uint32_t off = kc - (uint32_t)__shfl((int)cexcl, L, 64);
+          const uint32_t lc0 = (uint32_t)__shfl((int)c0, L, 64);
+          const bool second = off >= lc0;
+          const uint32_t pa = (uint32_t)__shfl((int)p0[0], L, 64), pb = (uint32_t)__shfl((int)p0[1], L, 64);
+          const int ka = __shfl(kind[0], L, 64), kb = __shfl(kind[1], L, 64);
+          const int da = __shfl(dd[0], L, 64), db = __shfl(dd[1], L, 64);
+          const uint32_t ma = (uint32_t)__shfl((int)mk[0], L, 64), mbb = (uint32_t)__shfl((int)mk[1], L, 64);
+          const uint32_t pos = second ? pb + (off - lc0) : pa + off;
+          const int kd = second ? kb : ka, dl = second ? db : da;
+          mo[v] = second ? mbb : ma;
+          ev[v] = 0;
+          oth[v] = 0;
+          if (kc < total) {
+            const uint32_t j = kd == 1 ? a.band_zi[pos] : pos;
+            const uint4 ra = a.g.rec[j].a, rb = a.g.rec[j].b;
+            bool dup = false;
+            if (dl) {
+              const float wl0 = pl[wv][mo[v]].wl0, wl1 = pl[wv][mo[v]].wl1;
+              const float wr0 = pl[wv][mo[v]].wr0, wr1 = pl[wv][mo[v]].wr1;
+              float kx, kz, hx, hz;
+              band_key(ra, rb, kx, kz, hx, hz);
+              dup = ((dl & 1) && kx >= wl0 && kx <= wl1) || ((dl & 2) && kx >= wr0 && kx <= wr1);
+            }
+            if (!dup) {
+              const uint4 u0 = mb[wv][mo[v]][0], u1 = mb[wv][mo[v]][1];
+              const float2 e = je[wv][mo[v]];
+              Judge J;
+              J.mx0 = __uint_as_float(u1.x), J.mz0 = __uint_as_float(u1.y);
+              J.mx1 = __uint_as_float(u1.z), J.mz1 = __uint_as_float(u1.w);
+              J.D = e.x, J.eps = e.y;
+              J.lx1 = J.mx1 - J.D, J.hx1 = J.mx1 + J.D, J.lz1 = J.mz1 - J.D, J.hz1 = J.mz1 + J.D;
+              J.v0 = u0.w != 0u, J.v1 = true;
+              J.base = a.base, J.q = u0.z, J.q0 = u0.w, J.rank = u0.z - a.base;
+              ev[v] = judge(J, ra, rb);
+            }
+            oth[v] = ra.z & REC_SLOT;
+          }
+        }
+        GW_DCNT(10);
+        // the round's events: slots from the wave's current chunk of ev_tmp (a ballot prefix), each event
+        // numbered inside its mover by the mover's LDS counter
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const unsigned long long em = __ballot(ev[v] != 0);
+          if (!em) continue;
+          const uint32_t ecnt = (uint32_t)__popcll(em);
+          const uint32_t pre = (uint32_t)__popcll(em & below);
+          uint32_t gi = cur + pre;
+          if (ecnt > left) {  // this chunk fills up: the rest goes to a fresh one
+            uint32_t nbk = 0;
+            if (lane == 0) nbk = atomicAdd(&a.ctr[CTR_EVENTS], kEvChunk);
+            nbk = __shfl(nbk, 0, 64);
+            if (pre >= left) gi = nbk + (pre - left);
+            cur = nbk + (ecnt - left);
+            left = kEvChunk - (ecnt - left);
+          } else {
+            cur += ecnt;
+            left -= ecnt;
+          }
+          if (ev[v]) {
+            const uint32_t local = atomicAdd(&lc[wv][mo[v]], 1u);
+            const uint4 u0 = mb[wv][mo[v]][0];
+            if (gi < a.ev_cap)
+              a.ev_tmp[gi] = make_uint4(u0.z - a.base, local, u0.x, oth[v] | (ev[v] == 2 ? 0x80000000u : 0u));
+            nent += ev[v] == 2 ? 1u : 0u;
+          }
+        }
+      }
+      GW_DPH(4);
     }
+    __builtin_amdgcn_wave_barrier();  // the counters' atomics before their reads
+    if (elig) put_count(a.rank_cnt, mb[wv][lane][0].z - a.base, lc[wv][lane]);
     __builtin_amdgcn_wave_barrier();  // every read of the batch before the next batch is written
   }
   for (uint32_t i = lane; i < left; i += 64)
@@ -2910,7 +2976,7 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
   // tick): if this pass lists some after all, the host re-runs the sweep with it (run_pass)
   if (a.dense && a.dense_hint) {
     if (a.band_xk && a.dense2) {  // the band walk, then the ring walk of the movers it hands over
-      hipLaunchKernelGGL(k_sweep_band, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
+      hipLaunchKernelGGL(k_sweep_band, dim3(256 * GW_BAND_WPE), dim3(kDenseBlock), 0, st, a);
       hipLaunchKernelGGL(k_sweep_dense<true>, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
     } else {
       hipLaunchKernelGGL(k_sweep_dense<false>, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
