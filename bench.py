@@ -224,6 +224,26 @@ def pmc_traffic(workload, n, stamp, kernels=None):
                "WRITE_SIZE, median per launch")
 
 
+def tick_counter_bytes(workload, n, stamp):
+    """HBM bytes per TICK from the same PMC passes (verdict r4): FETCH_SIZE x 2 + WRITE_SIZE summed over
+    every kernel that ran once or more per tick there (at least as many dispatches as k_sweep), i.e. the
+    whole pipeline's counter traffic, beside SURVEY's formula. None when the passes are stale."""
+    p = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(p) as f:
+            w = json.load(f).get("workloads", {}).get(workload)
+    except Exception:
+        return None, None
+    if not w or stamp is None or w.get("lib_src") != stamp or w.get("n") != n:
+        return None, None
+    kt = w.get("kernels", {})
+    per_tick = kt.get("k_sweep", {}).get("dispatches")
+    if not per_tick:
+        return None, None
+    ks = sorted(k for k, e in kt.items() if "bytes" in e and e.get("dispatches", 0) >= per_tick)
+    return sum(kt[k]["bytes"] * round(kt[k]["dispatches"] / per_tick) for k in ks), ks
+
+
 def spaces_workload(args, rank):
     """(name, n_per, nspaces, dists, L, seed0, nhot, sigma, hot_every) of a device-staged, all-moving
     workload."""
@@ -602,6 +622,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     lib_v, stamp = lib_stamp(L_)
     t_bytes, t_note = pmc_traffic(args.workload if not args.dists else None, n, stamp)
     traffic = t_bytes / (sweep_ms * 1e-3) / 1e9 if t_bytes else None  # GB/s, same unit as achieved
+    tick_bytes, tick_kernels = tick_counter_bytes(args.workload if not args.dists else None, n, stamp)
     # SURVEY.md §8(d) whole-tick formula (assumes a CSR-state design; ours keeps no lists)
     b_survey = 24.0 * n + 4.0 * (2 * nnz) + 8.0 * ev_per_tick if nnz is not None else None
     return {
@@ -694,9 +715,14 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "band_movers_per_tick": st["band_movers"] / ticks,
             "avg_launch_ms": sweep_ms,
             "kernels_timed": "k_sweep" +
+                             (" + k_sweep<SwBig>" if args.workload in ("skew", "skew50") else "") +
+                             (" + k_band_keys + k_band_rank + k_sweep_band" if st["band_movers"] else "") +
                              (" + k_sweep_dense" if st["dense_movers"] else "") +
-                             (" + k_band_keys + k_band_rank" if st["band_movers"] else "") +
                              " (the pass's sweep stage, hipEvents on the manager's stream)",
+            "tick_counter_bytes": tick_bytes,
+            "tick_counter_GBps": tick_bytes / (ms_step * 1e-3) / 1e9 if tick_bytes else None,
+            "tick_counter_note": (f"PMC bytes per tick of every per-tick kernel ({len(tick_kernels)}: "
+                                  f"{', '.join(tick_kernels)}) over ms_per_step") if tick_bytes else None,
             "survey_formula": None if b_survey is None else {
                 "bytes_per_tick": b_survey,
                 "achieved_GBps_over_tick": b_survey / (ms_step * 1e-3) / 1e9,

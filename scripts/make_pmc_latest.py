@@ -26,6 +26,13 @@ for f in sorted(glob.glob(prefix + "*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
         name = name.replace("void ", "").replace("gw::", "").strip()
+        # the LDS sweep's two sizes and the ring walk's two lists under stable names
+        if name.startswith("k_sweep<SwCfg<1024"):
+            name = "k_sweep_big"
+        elif name.startswith("k_sweep<SwCfg<"):
+            name = "k_sweep"
+        elif name.startswith("k_sweep_dense<"):
+            name = "k_sweep_dense"
         vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 lib, n = set(), set()
 for f in sorted(glob.glob(prefix + "*.json")):
@@ -61,7 +68,7 @@ for k, cs in vals.items():
         e["wait_any_frac"] = d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]
     kern[k] = e
 # the workload's roofline kernel(s), as bench.py times them (the pass's sweep stage)
-dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_dense", "k_band_keys", "k_band_rank"])
+dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_big", "k_band_keys", "k_band_rank", "k_sweep_band", "k_sweep_dense"])
 summed = [k for k in dominant if "bytes" in kern.get(k, {})]
 entry = {"lib_src": lib.pop(), "n": n.pop(), "source": prefix, "kernels": kern, "kernels_summed": summed,
          "bytes_per_launch": sum(kern[k]["bytes"] for k in summed) if summed else None}
