@@ -22,7 +22,8 @@ enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 
        CTR_DENSE = 7, CTR_HOLES = 8, CTR_NOPS = 9,  // ops of the pass (device-counted batches)
        CTR_BOVF = 10,   // the one-pass build overflowed a tile's bucket: the pass is re-run (counting build)
        CTR_NEV = 11,    // events of the pass (scan total of the per-op counts; k_place)
-       CTR_UNSORTED = 12,  // set when some op's events were numbered out of canonical order (k_slice_sort sorts)
+       CTR_UNSORTED = 12,  // set when ops' events were numbered out of canonical order (k_slice_sort sorts every op)
+       CTR_UNS_SOME = 13,  // set when some ops are flagged in the unsorted bitmask (k_slice_sort sorts those)
        CTR_BAND_MV = 14,     // dense movers that took the band walk (k_sweep_dense)
        CTR_SMALL_OVF = 15,   // k_order_small: the pass's events exceed its LDS (the host re-runs the order stage)
        CTR_BDONE = 16,  // blocks of the one-pass build done (not published)
@@ -211,6 +212,7 @@ struct SweepArgs {
   uint32_t* tile_ev;
   uint32_t* tile_ent;
   uint32_t* rank_cnt;
+  uint32_t* uns;        // [n_ops / 32 + 1] bitmask: ops whose events are out of canonical order (CTR_UNS_SOME)
   uint32_t* ctr;
   uint32_t* dense;      // slots of movers for k_sweep_dense (boxes beyond the tile's LDS region)
   uint32_t* dense2;     // band walk on: the movers k_sweep_band leaves to the ring walk
@@ -344,6 +346,7 @@ struct OrderArgs {
   uint32_t ntiles_fix;
   uint2* scratch;            // k_slice_sort's scratch (the whole ev_tmp: 2 x its slots >= events)
   const uint32_t* rank_off;  // exclusive scan of per-op event counts, [n_ops + 1]
+  uint32_t* uns;             // the sweep's unsorted-op bitmask (CTR_UNS_SOME): k_slice_sort sorts and clears
   uint2* ev_out;             // this pass's slice of the output (offset by g.keep)
   uint2* host_out;           // mapped pinned host slice, or null (events stay in HBM)
   uint32_t n_ops;

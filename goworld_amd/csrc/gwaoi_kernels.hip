@@ -1387,6 +1387,11 @@ __device__ __forceinline__ unsigned long long judge_chunk(const S& sm, const Jud
 // VGPR limit). A lane with more than kSortMax events, or with events past the queue, flags the block
 // (sm.unsorted) instead.
 constexpr uint32_t kSortMax = 8;
+// A mover whose events are numbered in walk order: its op's bit in the unsorted bitmask, for k_slice_sort
+// (the caller's block or wave then sets CTR_UNS_SOME). Only those ops' slices are sorted.
+__device__ __forceinline__ void flag_op(const SweepArgs& a, uint32_t rank) {
+  atomicOr(&a.uns[rank >> 5], 1u << (rank & 31u));
+}
 template <bool kSortLocal, class S, class IdxA, class IdxB>
 __device__ __forceinline__ void emit_masks(const SweepArgs& a, S& sm, const Mover& m, const Judge& J,
                                            unsigned long long hA, IdxA&& ia, unsigned long long hB, IdxB&& ib,
@@ -1453,6 +1458,7 @@ __device__ __forceinline__ void emit_masks(const SweepArgs& a, S& sm, const Move
         sm.ev[p0 + i].y = l0 + rk;
       }
     } else {
+      flag_op(a, m.rank);
       sm.unsorted = 1u;
     }
   }
@@ -1531,7 +1537,7 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, S& sm, const M
     }
     judge_stream(a, sm, J, m, Rs.total, ri, local, nent);
     judge_stream(a, sm, J, m, Cs.total, ci, local, nent);
-    if (local > 1u) sm.unsorted = 1u;  // numbered in walk order
+    if (local > 1u) flag_op(a, m.rank), sm.unsorted = 1u;  // numbered in walk order
     return local;
   }
   walk_cells(w, [&](int r, int c0, int c1) {
@@ -1540,7 +1546,7 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, S& sm, const M
     const uint32_t e = (c0 <= c1) ? (uint32_t)sm.lcs[b + c1 + 1] : j;
     judge_stream(a, sm, J, m, e - j, [&](uint32_t k) { return j + k; }, local, nent);
   });
-  if (local > 1u) sm.unsorted = 1u;
+  if (local > 1u) flag_op(a, m.rank), sm.unsorted = 1u;
   return local;
 }
 
@@ -1857,7 +1863,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmemT<C>& sm
       ++di;
       const Mover m = mover_of(ra, a.g.rec[j].b, a.base, g.D);
       const uint32_t cnt = sweep_global(a, sm, m, g, nent);
-      if (cnt > 1u) sm.unsorted = 1u;  // numbered in walk order
+      if (cnt > 1u) flag_op(a, m.rank), sm.unsorted = 1u;  // numbered in walk order
       put_count(a.rank_cnt, m.rank, cnt);
     }
   } else {
@@ -1888,7 +1894,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmemT<C>& sm
   GW_STAMP(7, __builtin_amdgcn_s_memrealtime());  // thread 0's walk done
   __syncthreads();
   GW_STAMP(3, __builtin_amdgcn_s_memrealtime());
-  if (threadIdx.x == 0 && sm.unsorted) a.ctr[CTR_UNSORTED] = 1u;
+  if (threadIdx.x == 0 && sm.unsorted) a.ctr[CTR_UNS_SOME] = 1u;
   const uint32_t nq = min(sm.n, (uint32_t)kEvLds);
   if (a.ev_fix) {  // the tile's own region: counts stored, no atomics (two per block cost 10 us at config 2)
     if (threadIdx.x == 0) a.tile_ev[t] = nq, a.tile_ent[t] = sm.enter;
@@ -1980,7 +1986,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
     const Geom g = a.g.geom[a.space_of[a.op_slot[i]]];
     const Mover m = leaver(a, i, g.D);
     const uint32_t cnt = sweep_global(a, q, m, g, nent);
-    if (cnt > 1u) q.flags = 1u;  // numbered in walk order: k_slice_sort sorts
+    if (cnt > 1u) flag_op(a, i), q.flags = 1u;  // numbered in walk order: k_slice_sort sorts
     put_count(a.rank_cnt, i, cnt);
   }
   if (nent) atomicAdd(&q.enter, nent);
@@ -1989,7 +1995,7 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
   if (threadIdx.x == 0) {
     q.base = nq ? atomicAdd(&a.ctr[CTR_EVENTS], nq) : 0u;
     if (q.enter) atomicAdd(&a.ctr[CTR_ENTER], q.enter);
-    if (q.flags) a.ctr[CTR_UNSORTED] = 1u;
+    if (q.flags) a.ctr[CTR_UNS_SOME] = 1u;
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nq; i += kBlock) {
@@ -3161,20 +3167,61 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
     for (uint32_t i = 0; i < kSmallSlice; ++i)
       if (i < len) d[b + i] = v[i];
   }
-  // medium segments: the wave, one at a time; each lane holds one element and counts the elements
-  // ordered before it (key, then position: stable)
+  // medium segments (kSmallSlice < len <= 64): the wave's together, in windows of up to kMedWin elements
+  // (whole segments, in lane order) staged in the wave's share of sk with all loads in flight at once; an
+  // element's final index is the count of its segment's elements ordered before it (key, then position:
+  // stable), read from the window (the lanes of one segment read the same element at a time: broadcast).
+  // (One segment at a time, the wave paid a dependent global round trip per segment: skew50's ~1M medium
+  // slices made k_slice_sort 338 us.)
+  constexpr uint32_t kMedWin = kBigChunk / (kBlock / 64);
+  constexpr uint32_t kMedRounds = kMedWin / 64u;
   const uint32_t lane = threadIdx.x & 63u;
-  for (unsigned long long mm = __ballot(len > kSmallSlice && len <= 64u); mm; mm &= mm - 1ull) {
-    const int src = __ffsll((long long)mm) - 1;
-    const uint32_t mb = __shfl(b, src, 64), ml = __shfl(len, src, 64);
-    const T v = lane < ml ? d[mb + lane] : seg_pad<T>();
-    const uint32_t kv = seg_key(v);
-    uint32_t pos = 0;
-    for (uint32_t j = 0; j < ml; ++j) {
-      const uint32_t kj = __shfl(kv, (int)j, 64);
-      pos += (kj < kv || (kj == kv && j < lane)) ? 1u : 0u;
+  T* win = sk + (threadIdx.x >> 6) * kMedWin;
+  const uint32_t lm = (len > kSmallSlice && len <= 64u) ? len : 0u;
+  const uint32_t incl = wave_incl_scan(lm), excl = incl - lm;
+  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  for (uint32_t w0 = 0; w0 < tot;) {  // wave-uniform; each window holds the next segment at least
+    const unsigned long long fit = __ballot(incl <= w0 + kMedWin);  // a prefix of the lanes
+    const int last = __builtin_amdgcn_readfirstlane(63 - __clzll((long long)fit));
+    const uint32_t wend = (uint32_t)__builtin_amdgcn_readlane((int)incl, last);
+    const uint32_t n = wend - w0;
+    T v[kMedRounds];
+#pragma unroll
+    for (uint32_t k = 0; k < kMedRounds; ++k) {
+      const uint32_t i = k * 64u + lane;
+      v[k] = seg_pad<T>();
+      if (k * 64u < n) {  // wave-uniform: every lane takes part in the lane moves
+        const uint32_t g = w0 + min(i, n - 1u);
+        const int L = wave_owner(incl, g);
+        const uint32_t sb = (uint32_t)__shfl((int)b, L, 64), se = (uint32_t)__shfl((int)excl, L, 64);
+        if (i < n) v[k] = d[sb + (g - se)];
+      }
     }
-    if (lane < ml) d[mb + pos] = v;
+#pragma unroll
+    for (uint32_t k = 0; k < kMedRounds; ++k)
+      if (k * 64u + lane < n) win[k * 64u + lane] = v[k];
+    __builtin_amdgcn_wave_barrier();  // the window's writes before its reads
+#pragma unroll
+    for (uint32_t k = 0; k < kMedRounds; ++k) {
+      const uint32_t i = k * 64u + lane;
+      if (k * 64u < n) {
+        const uint32_t g = w0 + min(i, n - 1u);
+        const int L = wave_owner(incl, g);
+        const uint32_t sb = (uint32_t)__shfl((int)b, L, 64), se = (uint32_t)__shfl((int)excl, L, 64);
+        const uint32_t sl = (uint32_t)__shfl((int)lm, L, 64);
+        if (i < n) {
+          const uint32_t kv = seg_key(v[k]), o = g - se, s0 = se - w0;
+          uint32_t pos = 0;
+          for (uint32_t j = 0; j < sl; ++j) {
+            const uint32_t kj = seg_key(win[s0 + j]);
+            pos += (kj < kv || (kj == kv && j < o)) ? 1u : 0u;
+          }
+          d[sb + pos] = v[k];
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the window's reads before the next window's writes
+    w0 = wend;
   }
   // long segments: the whole block
   __syncthreads();
@@ -3193,7 +3240,9 @@ struct SegSmem {
 };
 
 // Grid-stride over the ops (kBlock per block and round). Nothing to sort when every op's events were
-// numbered in canonical order by the sweep (CTR_UNSORTED clear) and no batch check is asked. When the
+// numbered in canonical order by the sweep (CTR_UNSORTED and CTR_UNS_SOME clear) and no batch check is
+// asked; with CTR_UNS_SOME only, only the ops flagged in o.uns (the walks that number a mover's events in
+// walk order flag that mover's op), whose flag words are cleared here for the next pass. When the
 // previous pass needed no sort either (o.sorted_hint), the kernel runs as kSortFewBlocks blocks and the
 // last one to finish (a ticket) publishes the pass's counters to mapped host memory (o.pub): no separate
 // one-thread kernel (3.8 us per pass at config 2). (A ticket per block of the one-thread-per-op grid,
@@ -3206,7 +3255,9 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
   __shared__ uint32_t last;
   uint32_t slots, n;
   const bool fits = ev_fits(o, &slots, &n);
-  const bool sort = fits && o.g.ctr[CTR_UNSORTED] != 0u;  // grid-uniform
+  const bool sort_all = fits && o.g.ctr[CTR_UNSORTED] != 0u;  // grid-uniform
+  const bool flagged = fits && o.g.ctr[CTR_UNS_SOME] != 0u;
+  const bool sort = sort_all || flagged;
   if (sort || o.check_ops) {
     const uint32_t nr = o.n_dev ? min(*o.n_dev, o.n_ops) : o.n_ops;
     for (uint32_t r0 = blockIdx.x * kBlock; r0 < o.n_ops; r0 += gridDim.x * kBlock) {  // block-uniform
@@ -3217,9 +3268,13 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
         if (s < o.cap && o.opq[s] != o.base + r) atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
       }
       if (!sort) continue;
-      const uint32_t b = op ? o.rank_off[r] : 0u, len = op ? o.rank_off[r + 1] - b : 0u;
+      uint32_t fw = 0;  // the op's flag word (read before the clear below)
+      if (flagged && r < o.n_ops) fw = o.uns[r >> 5];
+      const bool mine = op && (sort_all || ((fw >> (r & 31u)) & 1u));
+      const uint32_t b = mine ? o.rank_off[r] : 0u, len = mine ? o.rank_off[r + 1] - b : 0u;
       // ev_tmp is free once k_place has run; its uint2 view has 2 x (tile regions + slots) >= n entries
       seg_sort(o.ev_out, o.scratch, b, len, sk, ss.bigq, &ss.nbig);
+      if (flagged && r < o.n_ops && (r & 31u) == 0u && fw) o.uns[r >> 5] = 0u;
     }
   }
   if (!o.pub || !o.sorted_hint) return;

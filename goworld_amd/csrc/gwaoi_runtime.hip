@@ -179,6 +179,7 @@ struct gwaoi_mgr {
   int cur = 0;  // grid holding the current state
   uint32_t next_seq = 1;
   uint32_t* rank_cnt = nullptr;  // [cap + 1]
+  uint32_t* uns = nullptr;       // [cap / 32 + 2]: ops whose events are out of canonical order (zero between passes)
   int sweep_lds = 1;             // 0: global-memory sweep path only (A/B)
   uint32_t* part = nullptr;     // scan chunk sums
   uint32_t part_words = 0;
@@ -805,6 +806,7 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
     o.ntiles_fix = 0;
     o.scratch = reinterpret_cast<uint2*>(m->ev_tmp);
     o.rank_off = m->rank_cnt;
+    o.uns = m->uns;
     o.ev_out = m->ev_out + keep;
     o.host_out = copy_events ? m->d_hev + keep : nullptr;
     o.n_ops = n_ops;
@@ -1040,7 +1042,9 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_EVENTS, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_ENTER, 0, sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_DENSE, 0, 2 * sizeof(uint32_t), st));  // + CTR_HOLES
-      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 3 * sizeof(uint32_t), st));  // + 13, CTR_BAND_MV
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 3 * sizeof(uint32_t), st));  // + UNS_SOME, BAND_MV
+      // (an overflowing order stage returned before k_slice_sort cleared the flags it would have read)
+      HIPCHK(hipMemsetAsync(m->uns, 0, ((size_t)n_ops / 32 + 1) * sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, sizeof(uint32_t), st));
     }
     gw::SweepArgs s{};
@@ -1082,6 +1086,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.tile_ev = m->tile_ev;
     s.tile_ent = m->tile_ent;
     s.rank_cnt = m->rank_cnt;
+    s.uns = m->uns;
     s.ctr = m->ctr;
     s.dense = m->d_dense;
     s.dense_cap = m->cap;
@@ -1114,6 +1119,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     o.ntiles_fix = fixed ? m->grid[ng].ntiles : 0u;
     o.scratch = reinterpret_cast<uint2*>(m->ev_tmp);
     o.rank_off = m->rank_cnt;
+    o.uns = m->uns;
     o.ev_out = m->ev_out + keep;
     o.host_out = copy_events ? m->d_hev + keep : nullptr;
     o.n_ops = n_ops;
@@ -1200,7 +1206,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   if (dev_mixed) m->n_present += m->h_ctr[gw::CTR_PRESENT];  // signed delta, two's complement
   m->last_dense = m->h_ctr[gw::CTR_DENSE];
   m->band_movers += m->h_ctr[gw::CTR_BAND_MV];
-  m->last_unsorted = m->h_ctr[gw::CTR_UNSORTED] != 0;
+  m->last_unsorted = m->h_ctr[gw::CTR_UNSORTED] != 0 || m->h_ctr[gw::CTR_UNS_SOME] != 0;
   m->n_present_dev = m->n_present;
   m->dv_kind = nullptr;
   m->dv_space = nullptr;
@@ -1287,7 +1293,7 @@ void free_all(gwaoi_mgr* m) {
   m->sync = nullptr;
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
-                   m->d_op_kind, m->rank_cnt, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
+                   m->d_op_kind, m->rank_cnt, m->uns, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
                    m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_key2, m->band_xk, m->band_zk, m->band_zi, m->band_hd, m->band_dense2, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
@@ -1386,6 +1392,8 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   chk(dalloc(&m->d_op_z, C));
   chk(dalloc(&m->d_op_kind, C));
   chk(dalloc(&m->rank_cnt, C + 1));
+  chk(dalloc(&m->uns, C / 32 + 2));
+  if (r == GWAOI_OK) chk(hipMemset(m->uns, 0, (C / 32 + 2) * sizeof(uint32_t)) == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP);
   m->nblk = (capacity + gw::bin_chunk(capacity) - 1) / gw::bin_chunk(capacity);
   const uint64_t max_tiles = m->max_cells / gw::kTileCells + 1;
   const uint64_t thist_n = std::min<uint64_t>(max_tiles, gw::kMaxLdsTiles) * m->nblk + 1;
