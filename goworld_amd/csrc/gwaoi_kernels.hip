@@ -857,11 +857,23 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
     if (on2) atomicAdd(&cnt[c2], 1u), walk |= bin_walker(a, a2), acted += bin_acted(a, a2, b2);
     if (on3) atomicAdd(&cnt[c3], 1u), walk |= bin_walker(a, a3), acted += bin_acted(a, a3, b3);
   } else {
-    for (uint32_t j = b + threadIdx.x; j < e; j += kBlock) {
-      const uint4 ra = a.trec[j].a;
-      atomicAdd(&cnt[tile_cell(g, __uint_as_float(ra.x), __uint_as_float(ra.y))], 1u);
-      walk |= bin_walker(a, ra);
-      acted += bin_acted(a, ra, a.trec[j].b);
+    // crowded tiles (a config-5 hotspot: thousands of records): four records per thread and round, all
+    // loads issued before any is used (one round trip per round instead of one per record: these
+    // blocks set the kernel's tail)
+    // (the small path's registers a0..a3 / b0..b3 are reused: separate arrays spilled)
+    for (uint32_t j = b + threadIdx.x; j < e; j += 4u * kBlock) {
+      a0 = a.trec[j].a;
+      a1 = a.trec[min(j + kBlock, last)].a;
+      a2 = a.trec[min(j + 2u * kBlock, last)].a;
+      a3 = a.trec[min(j + 3u * kBlock, last)].a;
+      auto one = [&](const uint4& ra, uint32_t jj) {
+        if (jj >= e) return;
+        atomicAdd(&cnt[tile_cell(g, __uint_as_float(ra.x), __uint_as_float(ra.y))], 1u);
+        walk |= bin_walker(a, ra);
+        // (bin_acted; the end seq is read only for a ghost of this pass's op)
+        if ((ra.w - a.base) < a.n_ops) acted += (!(ra.z & REC_GHOST) || a.trec[jj].b.w == 0u) ? 1u : 0u;
+      };
+      one(a0, j), one(a1, j + kBlock), one(a2, j + 2u * kBlock), one(a3, j + 3u * kBlock);
     }
   }
   const int any_walker = __syncthreads_or(walk);
@@ -911,10 +923,17 @@ __global__ void __launch_bounds__(kBlock) k_bin_tsort(BinArgs a) {
       o->a = a3, o->b = b3;
     }
   } else {
-    for (uint32_t j = b + threadIdx.x; j < e; j += kBlock) {
-      const uint4 ra = a.trec[j].a, rb = a.trec[j].b;
-      Rec* o = &a.rec[atomicAdd(&cnt[tile_cell(g, __uint_as_float(ra.x), __uint_as_float(ra.y))], 1u)];
-      o->a = ra, o->b = rb;
+    for (uint32_t j = b + threadIdx.x; j < e; j += 4u * kBlock) {
+      a0 = a.trec[j].a, b0 = a.trec[j].b;
+      a1 = a.trec[min(j + kBlock, last)].a, b1 = a.trec[min(j + kBlock, last)].b;
+      a2 = a.trec[min(j + 2u * kBlock, last)].a, b2 = a.trec[min(j + 2u * kBlock, last)].b;
+      a3 = a.trec[min(j + 3u * kBlock, last)].a, b3 = a.trec[min(j + 3u * kBlock, last)].b;
+      auto put = [&](const uint4& ra, const uint4& rb, uint32_t jj) {
+        if (jj >= e) return;
+        Rec* o = &a.rec[atomicAdd(&cnt[tile_cell(g, __uint_as_float(ra.x), __uint_as_float(ra.y))], 1u)];
+        o->a = ra, o->b = rb;
+      };
+      put(a0, b0, j), put(a1, b1, j + kBlock), put(a2, b2, j + 2u * kBlock), put(a3, b3, j + 3u * kBlock);
     }
   }
 }
@@ -2386,9 +2405,13 @@ k_sweep_dense(SweepArgs a) {
 #endif
 constexpr float kBandTrips = GW_BAND_TRIPS;
 #ifndef GW_BAND_SEARCH_MIN  // cells of fewer records are read whole instead of searched
-#define GW_BAND_SEARCH_MIN 8u
+#define GW_BAND_SEARCH_MIN 4u
 #endif
 constexpr uint32_t kBandSearchMin = GW_BAND_SEARCH_MIN;
+#ifndef GW_BAND_FAN
+#define GW_BAND_FAN 4
+#endif
+constexpr uint32_t kBandFan = GW_BAND_FAN;  // probes per search level (cells of up to kBandFan keys: one level)
 
 // the cell of item li of a band plan: x-strip cells (columns of the left / right band over the union's
 // rows, keys by x), then z-strip cells (rows of the bottom / top band over the union's columns, keys by z;
@@ -2511,6 +2534,10 @@ k_sweep_band(SweepArgs a) {
     const uint32_t iincl = wave_incl_scan(nit), iexcl = iincl - nit;
     const uint32_t N = __builtin_amdgcn_readlane(iincl, 63);  // the batch's band cells
     __builtin_amdgcn_wave_barrier();  // the wave's LDS ops stay in program order
+#if GW_STAMPS
+    dph[11] += N;
+    dph[15] += (uint32_t)__popcll(__ballot(elig));
+#endif
     GW_DPH(0);
     // ---- item rounds: 2 cells per lane ----
     for (uint32_t ib = 0; ib < N; ib += 128u) {
@@ -2557,8 +2584,15 @@ k_sweep_band(SweepArgs a) {
           if (dd[u]) p1[u] = p0[u];
         }
       }
+#if GW_STAMPS
+      for (int u = 0; u < 2; ++u) {
+        dph[12] += (uint32_t)__popcll(__ballot(kind[u] < 2));
+        dph[13] += (uint32_t)__popcll(__ballot(kind[u] == 2));
+      }
+#endif
       GW_DPH(2);
-      {  // key windows of the sorted cells: fanout 8, both bounds of both cells per round trip
+      {  // key windows of the sorted cells: fanout kBandFan, both bounds of both cells per round trip; while
+         // both bounds are still in the same key range (a narrow window: mostly), one set of probes serves both
         uint32_t ll[2], lh[2], ul[2], uh[2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -2569,16 +2603,19 @@ k_sweep_band(SweepArgs a) {
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const float* arr = kind[u] == 1 ? a.band_zk : a.band_xk;
-            const uint32_t sl = (lh[u] - ll[u] + 7) >> 3, su = (uh[u] - ul[u] + 7) >> 3;
-            uint32_t cl = 0, cu = 0;  // probes below the bound (a prefix: the keys are sorted)
+            const uint32_t sl = (lh[u] - ll[u] + kBandFan - 1) / kBandFan, su = (uh[u] - ul[u] + kBandFan - 1) / kBandFan;
+            const bool same = ll[u] == ul[u] && lh[u] == uh[u];
+            uint32_t cl = 0, cu = 0, cs = 0;  // probes below the bound (a prefix: the keys are sorted)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const uint32_t ql = ll[u] + (uint32_t)(q + 1) * sl - 1, qu = ul[u] + (uint32_t)(q + 1) * su - 1;
+            for (uint32_t q = 0; q < kBandFan; ++q) {
+              const uint32_t ql = ll[u] + (q + 1) * sl - 1, qu = ul[u] + (q + 1) * su - 1;
               const float kl = (sl && ql < lh[u]) ? arr[ql] : __builtin_inff();
-              const float ku = (su && qu < uh[u]) ? arr[qu] : __builtin_inff();
+              const float ku = (!same && su && qu < uh[u]) ? arr[qu] : __builtin_inff();
               cl += kl < w0[u] ? 1u : 0u;
+              cs += kl <= w1[u] ? 1u : 0u;
               cu += ku <= w1[u] ? 1u : 0u;
             }
+            if (same) cu = cs;
             if (sl) {
               const uint32_t nll = ll[u] + cl * sl, qc = ll[u] + (cl + 1) * sl - 1;
               lh[u] = min(lh[u], qc), ll[u] = min(nll, lh[u]);
@@ -2598,6 +2635,9 @@ k_sweep_band(SweepArgs a) {
       const uint32_t c0 = p1[0] - p0[0], cnt = c0 + (p1[1] - p0[1]);
       const uint32_t cincl = wave_incl_scan(cnt), cexcl = cincl - cnt;
       const uint32_t total = __builtin_amdgcn_readlane(cincl, 63);
+#if GW_STAMPS
+      dph[14] += total;
+#endif
       for (uint32_t b = 0; b < total; b += 128u) {
         uint32_t mo[2], oth[2];
         int ev[2];
@@ -2689,7 +2729,7 @@ k_sweep_band(SweepArgs a) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && nd) a.ctr[CTR_UNSORTED] = 1u;
 #if GW_STAMPS
   if (lane == 0)
-    for (int k = 0; k < 16; ++k) atomicAdd(&gw_stamps[kStampWords * 16383 + k], dph[k]);
+    for (int k = 0; k < 16; ++k) atomicAdd(&gw_stamps[kStampWords * 16381 + k], dph[k]);
 #endif
 }
 
