@@ -132,6 +132,48 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   return v;
 }
 
+// Inclusive wave64 max-scan (the same DPP lane moves as wave_incl_scan). Every lane must be active.
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  const int lane = threadIdx.x & 63, rl = lane & 15;
+  int t;
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  if (rl >= 1) v = max(v, (uint32_t)t);
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  if (rl >= 2) v = max(v, (uint32_t)t);
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  if (rl >= 4) v = max(v, (uint32_t)t);
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  if (rl >= 8) v = max(v, (uint32_t)t);
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x142, 0xf, 0xf, false);  // row_bcast:15
+  if ((lane & 31) >= 16) v = max(v, (uint32_t)t);
+  t = __builtin_amdgcn_mov_dpp((int)v, 0x143, 0xf, 0xf, false);  // row_bcast:31
+  if (lane >= 32) v = max(v, (uint32_t)t);
+  return v;
+}
+
+// Owners of positions w0 + lane and w0 + 64 + lane of a stream that the lanes' ranges [excl, excl + cnt)
+// concatenate in lane order (positions past the stream get the last lane with a range): each lane whose
+// range starts inside the window marks its start in the wave's LDS row (128 words), then a max-scan over
+// the marks in lane order; positions before the first mark belong to the lane holding position w0. Two LDS
+// writes, two reads and two DPP scans instead of two binary searches of six dependent lane moves.
+// Every lane must be active.
+__device__ __forceinline__ void stream_owners(uint32_t* row, uint32_t excl, uint32_t cnt, uint32_t w0, int& o0,
+                                              int& o1) {
+  const int lane = threadIdx.x & 63;
+  row[lane] = 0u;
+  row[64 + lane] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  if (cnt && excl >= w0 && excl < w0 + 128u) row[excl - w0] = (uint32_t)lane + 1u;  // (starts are distinct)
+  __builtin_amdgcn_wave_barrier();
+  const unsigned long long before = __ballot(cnt != 0u && excl <= w0);
+  const uint32_t carry = before ? (uint32_t)(64 - __clzll((long long)before)) : 1u;  // lane + 1
+  const uint32_t s0 = wave_incl_max(row[lane]), s1 = wave_incl_max(row[64 + lane]);
+  const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)s0, 63);
+  o0 = (int)max(carry, s0) - 1;
+  o1 = (int)max(max(carry, m0), s1) - 1;
+  __builtin_amdgcn_wave_barrier();  // the row's reads before its next writes
+}
+
 // q = n / d for 0 <= n < 2^20, 1 <= d < 2^11 (region cell indices): float reciprocal, then one
 // correction step each way (exact; avoids the ~30-instruction integer division sequence)
 __device__ __forceinline__ int small_div(int n, int d) {

@@ -2154,6 +2154,38 @@ __device__ __forceinline__ bool band_plan(const Mover& m, const Geom& g, const J
   return P.cl1 < P.cr0 && P.rb1 < P.rt0;
 }
 
+// A plan as the band walk keeps it in LDS (60 B instead of 80: five blocks per CU): the cell bounds as
+// 16-bit offsets from the union box's corner (band_plan sends boxes too wide for them to the ring walk).
+struct BandPlanL {
+  int x0, z0;
+  short o[10];  // x1, cl0, cl1, cr0, cr1 (from x0); z1, rb0, rb1, rt0, rt1 (from z0)
+  float w[8];   // wl0, wl1, wr0, wr1, wb0, wb1, wt0, wt1
+};
+__device__ __forceinline__ void plan_store(BandPlanL& L, const BandPlan& P) {
+  L.x0 = P.x0, L.z0 = P.z0;
+  L.o[0] = (short)(P.x1 - P.x0), L.o[1] = (short)(P.cl0 - P.x0), L.o[2] = (short)(P.cl1 - P.x0);
+  L.o[3] = (short)(P.cr0 - P.x0), L.o[4] = (short)(P.cr1 - P.x0);
+  L.o[5] = (short)(P.z1 - P.z0), L.o[6] = (short)(P.rb0 - P.z0), L.o[7] = (short)(P.rb1 - P.z0);
+  L.o[8] = (short)(P.rt0 - P.z0), L.o[9] = (short)(P.rt1 - P.z0);
+  L.w[0] = P.wl0, L.w[1] = P.wl1, L.w[2] = P.wr0, L.w[3] = P.wr1;
+  L.w[4] = P.wb0, L.w[5] = P.wb1, L.w[6] = P.wt0, L.w[7] = P.wt1;
+}
+__device__ __forceinline__ BandPlan plan_load(const BandPlanL& L) {
+  BandPlan P;
+  P.x0 = L.x0, P.z0 = L.z0;
+  P.x1 = P.x0 + L.o[0], P.cl0 = P.x0 + L.o[1], P.cl1 = P.x0 + L.o[2], P.cr0 = P.x0 + L.o[3], P.cr1 = P.x0 + L.o[4];
+  P.z1 = P.z0 + L.o[5], P.rb0 = P.z0 + L.o[6], P.rb1 = P.z0 + L.o[7], P.rt0 = P.z0 + L.o[8], P.rt1 = P.z0 + L.o[9];
+  P.wl0 = L.w[0], P.wl1 = L.w[1], P.wr0 = L.w[2], P.wr1 = L.w[3];
+  P.wb0 = L.w[4], P.wb1 = L.w[5], P.wt0 = L.w[6], P.wt1 = L.w[7];
+  return P;
+}
+// every cell bound of the plan within a 16-bit offset of the union box's corner
+__device__ __forceinline__ bool plan_fits(const BandPlan& P) {
+  auto ok = [](int v) { return v >= -32000 && v <= 32000; };
+  return ok(P.x1 - P.x0) && ok(P.cl0 - P.x0) && ok(P.cl1 - P.x0) && ok(P.cr0 - P.x0) && ok(P.cr1 - P.x0) &&
+         ok(P.z1 - P.z0) && ok(P.rb0 - P.z0) && ok(P.rb1 - P.z0) && ok(P.rt0 - P.z0) && ok(P.rt1 - P.z0);
+}
+
 // a wave-uniform plan pinned to scalar registers
 __device__ __forceinline__ void band_pin(BandPlan& P) {
   auto u = [](int& v) { v = __builtin_amdgcn_readfirstlane(v); };
@@ -2222,6 +2254,7 @@ k_sweep_dense(SweepArgs a) {
   uint32_t nent = 0;
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
   __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the wave's batch of movers: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
+  __shared__ uint32_t orow[kDenseBlock / 64][128];  // stream_owners' marks
 #if GW_STAMPS
   unsigned long long dph[16] = {}, dt0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2308,21 +2341,16 @@ k_sweep_dense(SweepArgs a) {
         const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
         GW_DCNT(9);
         GW_DPH(3);
-        auto locate = [&](uint32_t k) -> uint32_t {  // record index of candidate k
-          int lo = 0, hi = 63;  // first lane whose inclusive prefix exceeds k
-#pragma unroll
-          for (int st = 0; st < 6; ++st) {
-            const int mid = (lo + hi) >> 1;
-            if (__shfl(incl, mid, 64) > k) hi = mid;
-            else lo = mid + 1;
-          }
+        auto locate = [&](uint32_t k, int lo) -> uint32_t {  // record index of candidate k (owner lane lo)
           return __shfl(rs, lo, 64) + (k - __shfl(excl, lo, 64));
         };
         for (uint32_t b = 0; b < total; b += 128) {
           const uint32_t kA = b + lane, kB = b + 64 + lane;
-          const uint32_t jA = locate(kA);
+          int oA, oB;
+          stream_owners(orow[wv], excl, rl, b, oA, oB);
+          const uint32_t jA = locate(kA, oA);
           const bool hasB = b + 64 < total;  // wave-uniform
-          const uint32_t jB = hasB ? locate(kB) : 0u;
+          const uint32_t jB = hasB ? locate(kB, oB) : 0u;
           uint4 aA = make_uint4(0, 0, 0, 0), bA = aA, aB = aA, bB = aA;
           if (kA < total) aA = a.g.rec[jA].a, bA = a.g.rec[jA].b;
           if (hasB && kB < total) aB = a.g.rec[jB].a, bB = a.g.rec[jB].b;
@@ -2398,7 +2426,7 @@ k_sweep_dense(SweepArgs a) {
 // no faster than the ring walk, r05_b5.) The movers without a band plan (Enters, moves whose bands meet)
 // or for which the cost model prefers the ring walk are left to k_sweep_dense<true> (dense2).
 #ifndef GW_BAND_WPE  // 4 waves per SIMD: 118 VGPRs (two cells and two candidates per lane in flight)
-#define GW_BAND_WPE 4
+#define GW_BAND_WPE 5
 #endif
 #ifndef GW_BAND_TRIPS  // the cost model's trips per round of 128 band cells (0: every plan takes the band walk)
 #define GW_BAND_TRIPS 3.0f
@@ -2471,10 +2499,11 @@ k_sweep_band(SweepArgs a) {
   uint32_t nent = 0, nband = 0;  // nband: movers of the wave that took the band walk
   uint32_t cur = 0, left = 0;    // the wave's current chunk of event slots (wave-uniform)
   __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the batch: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
-  __shared__ BandPlan pl[kDenseBlock / 64][64];  // per batch mover: its band plan
+  __shared__ BandPlanL pl[kDenseBlock / 64][64];  // per batch mover: its band plan
   __shared__ uint2 pg[kDenseBlock / 64][64];     // per batch mover: its Space's {base, ntx} (cell keys)
   __shared__ float2 je[kDenseBlock / 64][64];    // per batch mover: {D, eps} of its judge
   __shared__ uint32_t lc[kDenseBlock / 64][64];  // per batch mover: its events so far
+  __shared__ uint32_t orow[kDenseBlock / 64][128];  // stream_owners' marks
 #if GW_STAMPS
   unsigned long long dph[16] = {}, dt0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2500,7 +2529,8 @@ k_sweep_band(SweepArgs a) {
       m.D = gl.D;
       const Judge J = make_judge(m, a.base);
       BandPlan P;
-      elig = band_plan(m, gl, J, __uint_as_float(a.band_hd[2 * sp]), __uint_as_float(a.band_hd[2 * sp + 1]), P);
+      elig = band_plan(m, gl, J, __uint_as_float(a.band_hd[2 * sp]), __uint_as_float(a.band_hd[2 * sp + 1]), P) &&
+             plan_fits(P);
       nit = band_items(P);
       if (elig && kBandTrips > 0.0f && !a.band_all) {
         // cost model (memory round trips): the ring walk reads ~all records of the ring cells, 128 per
@@ -2522,7 +2552,7 @@ k_sweep_band(SweepArgs a) {
         elig = band_trips < ring_trips;
       }
       if (elig) {
-        pl[wv][lane] = P;
+        plan_store(pl[wv][lane], P);
         pg[wv][lane] = make_uint2(gl.base, (uint32_t)gl.ntx);
         je[wv][lane] = make_float2(J.D, J.eps);
       }
@@ -2543,18 +2573,19 @@ k_sweep_band(SweepArgs a) {
     for (uint32_t ib = 0; ib < N; ib += 128u) {
       uint32_t p0[2], p1[2], mk[2];
       float w0[2], w1[2];
-      int kind[2], dd[2];
+      int kind[2], dd[2], iow[2];
+      stream_owners(orow[wv], iexcl, nit, ib, iow[0], iow[1]);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const uint32_t it = ib + (uint32_t)(u * 64 + lane);
         // (every lane takes part in the lane moves: a source lane outside a divergent branch is inactive)
-        const int k = wave_owner(iincl, min(it, N - 1u));
+        const int k = iow[u];
         const uint32_t kex = (uint32_t)__shfl((int)iexcl, k, 64);
         mk[u] = (uint32_t)k;
         p0[u] = p1[u] = 0u;
         kind[u] = 3, dd[u] = 0, w0[u] = w1[u] = 0.0f;
         if (it < N) {
-          const BandPlan P = pl[wv][k];
+          const BandPlan P = plan_load(pl[wv][k]);
           const uint2 sg = pg[wv][k];
           int c, r;
           band_item(P, it - kex, c, r, w0[u], w1[u], kind[u], dd[u]);
@@ -2638,23 +2669,26 @@ k_sweep_band(SweepArgs a) {
 #if GW_STAMPS
       dph[14] += total;
 #endif
+      // what a candidate's lane needs of its owner: stream position -> record position of each cell
+      // (cb0 / cb1), the first position of the second cell, and kind | dd | mover of both cells, packed
+      const uint32_t cb0 = p0[0] - cexcl, cb1 = p0[1] - (cexcl + c0), csplit = cexcl + c0;
+      const uint32_t cpk = (uint32_t)kind[0] | ((uint32_t)dd[0] << 2) | (mk[0] << 4) | ((uint32_t)kind[1] << 10) |
+                           ((uint32_t)dd[1] << 12) | (mk[1] << 14);
       for (uint32_t b = 0; b < total; b += 128u) {
         uint32_t mo[2], oth[2];
-        int ev[2];
+        int ev[2], cow[2];
+        stream_owners(orow[wv], cexcl, cnt, b, cow[0], cow[1]);
 #pragma unroll
         for (int v = 0; v < 2; ++v) {
           const uint32_t kc = b + (uint32_t)(v * 64 + lane);
-          const int L = wave_owner(cincl, min(kc, total - 1u));
-          const uint32_t off = kc - (uint32_t)__shfl((int)cexcl, L, 64);
-          const uint32_t lc0 = (uint32_t)__shfl((int)c0, L, 64);
-          const bool second = off >= lc0;
-          const uint32_t pa = (uint32_t)__shfl((int)p0[0], L, 64), pb = (uint32_t)__shfl((int)p0[1], L, 64);
-          const int ka = __shfl(kind[0], L, 64), kb = __shfl(kind[1], L, 64);
-          const int da = __shfl(dd[0], L, 64), db = __shfl(dd[1], L, 64);
-          const uint32_t ma = (uint32_t)__shfl((int)mk[0], L, 64), mbb = (uint32_t)__shfl((int)mk[1], L, 64);
-          const uint32_t pos = second ? pb + (off - lc0) : pa + off;
-          const int kd = second ? kb : ka, dl = second ? db : da;
-          mo[v] = second ? mbb : ma;
+          const int L = cow[v];
+          // (five lane moves: the owner's cell bases relative to the stream, its split and packed fields)
+          const bool second = kc >= (uint32_t)__shfl((int)csplit, L, 64);
+          const uint32_t ob0 = (uint32_t)__shfl((int)cb0, L, 64), ob1 = (uint32_t)__shfl((int)cb1, L, 64);
+          const uint32_t pos = kc + (second ? ob1 : ob0);
+          const uint32_t sel = (uint32_t)__shfl((int)cpk, L, 64) >> (second ? 10 : 0);
+          const int kd = (int)(sel & 3u), dl = (int)((sel >> 2) & 3u);
+          mo[v] = (sel >> 4) & 63u;
           ev[v] = 0;
           oth[v] = 0;
           if (kc < total) {
@@ -2662,8 +2696,8 @@ k_sweep_band(SweepArgs a) {
             const uint4 ra = a.g.rec[j].a, rb = a.g.rec[j].b;
             bool dup = false;
             if (dl) {
-              const float wl0 = pl[wv][mo[v]].wl0, wl1 = pl[wv][mo[v]].wl1;
-              const float wr0 = pl[wv][mo[v]].wr0, wr1 = pl[wv][mo[v]].wr1;
+              const float wl0 = pl[wv][mo[v]].w[0], wl1 = pl[wv][mo[v]].w[1];
+              const float wr0 = pl[wv][mo[v]].w[2], wr1 = pl[wv][mo[v]].w[3];
               float kx, kz, hx, hz;
               band_key(ra, rb, kx, kz, hx, hz);
               dup = ((dl & 1) && kx >= wl0 && kx <= wl1) || ((dl & 2) && kx >= wr0 && kx <= wr1);
