@@ -2127,6 +2127,7 @@ struct BandPlan {
   int cl0, cl1, cr0, cr1;  // x-strip columns: left band, right band
   int rb0, rb1, rt0, rt1;  // z-strip rows: bottom band, top band
   float wl0, wl1, wr0, wr1, wb0, wb1, wt0, wt1;  // key windows
+  int zrun;                // z-strips in runs (a sparse edge): see band_item
 };
 
 __device__ __forceinline__ bool band_plan(const Mover& m, const Geom& g, const Judge& J, float hdx, float hdz,
@@ -2151,6 +2152,7 @@ __device__ __forceinline__ bool band_plan(const Mover& m, const Geom& g, const J
   P.cr0 = max(P.x0, cellc(r0, g.x0, g.inv_c, g.ncx)), P.cr1 = min(P.x1, cellc_hi(r1, g.x0, g.inv_c, g.ncx));
   P.rb0 = max(P.z0, cellc(b0, g.z0, g.inv_c, g.ncz)), P.rb1 = min(P.z1, cellc_hi(b1, g.z0, g.inv_c, g.ncz));
   P.rt0 = max(P.z0, cellc(t0, g.z0, g.inv_c, g.ncz)), P.rt1 = min(P.z1, cellc_hi(t1, g.z0, g.inv_c, g.ncz));
+  P.zrun = 0;
   return P.cl1 < P.cr0 && P.rb1 < P.rt0;
 }
 
@@ -2160,6 +2162,7 @@ struct BandPlanL {
   int x0, z0;
   short o[10];  // x1, cl0, cl1, cr0, cr1 (from x0); z1, rb0, rb1, rt0, rt1 (from z0)
   float w[8];   // wl0, wl1, wr0, wr1, wb0, wb1, wt0, wt1
+  int zrun;
 };
 __device__ __forceinline__ void plan_store(BandPlanL& L, const BandPlan& P) {
   L.x0 = P.x0, L.z0 = P.z0;
@@ -2169,6 +2172,7 @@ __device__ __forceinline__ void plan_store(BandPlanL& L, const BandPlan& P) {
   L.o[8] = (short)(P.rt0 - P.z0), L.o[9] = (short)(P.rt1 - P.z0);
   L.w[0] = P.wl0, L.w[1] = P.wl1, L.w[2] = P.wr0, L.w[3] = P.wr1;
   L.w[4] = P.wb0, L.w[5] = P.wb1, L.w[6] = P.wt0, L.w[7] = P.wt1;
+  L.zrun = P.zrun;
 }
 __device__ __forceinline__ BandPlan plan_load(const BandPlanL& L) {
   BandPlan P;
@@ -2177,6 +2181,7 @@ __device__ __forceinline__ BandPlan plan_load(const BandPlanL& L) {
   P.z1 = P.z0 + L.o[5], P.rb0 = P.z0 + L.o[6], P.rb1 = P.z0 + L.o[7], P.rt0 = P.z0 + L.o[8], P.rt1 = P.z0 + L.o[9];
   P.wl0 = L.w[0], P.wl1 = L.w[1], P.wr0 = L.w[2], P.wr1 = L.w[3];
   P.wb0 = L.w[4], P.wb1 = L.w[5], P.wt0 = L.w[6], P.wt1 = L.w[7];
+  P.zrun = L.zrun;
   return P;
 }
 // every cell bound of the plan within a 16-bit offset of the union box's corner
@@ -2440,16 +2445,39 @@ constexpr uint32_t kBandSearchMin = GW_BAND_SEARCH_MIN;
 #define GW_BAND_FAN 4
 #endif
 constexpr uint32_t kBandFan = GW_BAND_FAN;  // probes per search level (cells of up to kBandFan keys: one level)
+#ifndef GW_BAND_RUN
+#define GW_BAND_RUN 4.0f
+#endif
+constexpr float kBandRun = GW_BAND_RUN;  // z-strips in runs when the bottom / top edge cells hold fewer records
 
-// the cell of item li of a band plan: x-strip cells (columns of the left / right band over the union's
-// rows, keys by x), then z-strip cells (rows of the bottom / top band over the union's columns, keys by z;
-// dd marks a column that is also in an x-strip, whose records with their x key in that strip's window
-// were judged there)
+// z-strip runs (BandPlan.zrun, a mover whose bottom / top edges lie in a sparse part of the world): a z-strip
+// row is one item per cell of the x-strip columns (searched, or read whole, with the corner-cell dedupe as
+// usual) plus one item per tile-row piece of the columns outside them, read whole: a piece's cells are
+// consecutive cell keys, so its records are ONE range (two cell-start loads for up to 32 cells, where the
+// per-cell items cost a decode, two loads and a search each, for a handful of records)
+__device__ __forceinline__ int seg_pieces(int a, int b) { return a <= b ? (b >> kTileShift) - (a >> kTileShift) + 1 : 0; }
+__device__ __forceinline__ void run_cols(const BandPlan& P, int& xl0, int& xl1, int& xr0, int& xr1) {
+  // the x-strip column sets, an empty one moved to the end of the row it lies at
+  const bool el = P.cl1 < P.cl0, er = P.cr1 < P.cr0;
+  xl0 = el ? P.x0 : P.cl0, xl1 = el ? P.x0 - 1 : P.cl1;
+  xr0 = er ? P.x1 + 1 : P.cr0, xr1 = er ? P.x1 : P.cr1;
+}
+__device__ __forceinline__ int run_row_items(const BandPlan& P) {
+  int xl0, xl1, xr0, xr1;
+  run_cols(P, xl0, xl1, xr0, xr1);
+  return (xl1 - xl0 + 1) + (xr1 - xr0 + 1) + seg_pieces(P.x0, xl0 - 1) + seg_pieces(xl1 + 1, xr0 - 1) +
+         seg_pieces(xr1 + 1, P.x1);
+}
+// the cell of item li of a band plan: x-strip cells (columns of the left / right band over the union's rows,
+// keys by x), then z-strip cells (rows of the bottom / top band over the union's columns, keys by z; dd marks
+// a column that is also in an x-strip, whose records with their x key in that strip's window were judged
+// there); in run mode a z-strip piece [c, c + span] of one tile row is kind 4 (read whole)
 __device__ __forceinline__ void band_item(const BandPlan& P, uint32_t li, int& c, int& r, float& w0, float& w1,
-                                          int& kind, int& dd) {
+                                          int& kind, int& dd, int& span) {
   const int H = P.z1 - P.z0 + 1, W = P.x1 - P.x0 + 1;
   const int nxl = max(0, P.cl1 - P.cl0 + 1), nzb = max(0, P.rb1 - P.rb0 + 1);
   const uint32_t NX = (uint32_t)((nxl + max(0, P.cr1 - P.cr0 + 1)) * H);
+  span = 0;
   if (li < NX) {
     const int ci = small_div((int)li, H);
     r = P.z0 + (int)li - ci * H;
@@ -2459,22 +2487,45 @@ __device__ __forceinline__ void band_item(const BandPlan& P, uint32_t li, int& c
     w1 = left ? P.wl1 : P.wr1;
     kind = 0;
     dd = 0;
-  } else {
-    const int i2 = (int)(li - NX), ri = small_div(i2, W);
-    c = P.x0 + i2 - ri * W;
-    const bool bot = ri < nzb;
-    r = bot ? P.rb0 + ri : P.rt0 + ri - nzb;
-    w0 = bot ? P.wb0 : P.wt0;
-    w1 = bot ? P.wb1 : P.wt1;
-    kind = 1;
-    dd = (c >= P.cl0 && c <= P.cl1 ? 1 : 0) | (c >= P.cr0 && c <= P.cr1 ? 2 : 0);
+    return;
   }
+  const int i2 = (int)(li - NX);
+  const int Wz = P.zrun ? run_row_items(P) : W;
+  const int ri = small_div(i2, Wz), k = i2 - ri * Wz;
+  const bool bot = ri < nzb;
+  r = bot ? P.rb0 + ri : P.rt0 + ri - nzb;
+  w0 = bot ? P.wb0 : P.wt0;
+  w1 = bot ? P.wb1 : P.wt1;
+  kind = 1;
+  if (!P.zrun) {
+    c = P.x0 + k;
+  } else {
+    int xl0, xl1, xr0, xr1;
+    run_cols(P, xl0, xl1, xr0, xr1);
+    const int kl = xl1 - xl0 + 1, kc = kl + (xr1 - xr0 + 1);
+    if (k < kc) {
+      c = k < kl ? xl0 + k : xr0 + (k - kl);
+    } else {  // a piece of the segments left of, between and right of the x-strip columns
+      int j = k - kc, a = P.x0, b = xl0 - 1;
+      const int p1 = seg_pieces(a, b);
+      if (j >= p1) {
+        j -= p1, a = xl1 + 1, b = xr0 - 1;
+        const int p2 = seg_pieces(a, b);
+        if (j >= p2) j -= p2, a = xr1 + 1, b = P.x1;
+      }
+      c = j == 0 ? a : ((a >> kTileShift) + j) << kTileShift;
+      span = min(b, (((a >> kTileShift) + j + 1) << kTileShift) - 1) - c;
+      kind = 4;
+      dd = 0;
+      return;
+    }
+  }
+  dd = (c >= P.cl0 && c <= P.cl1 ? 1 : 0) | (c >= P.cr0 && c <= P.cr1 ? 2 : 0);
 }
-
 __device__ __forceinline__ uint32_t band_items(const BandPlan& P) {
   const int H = P.z1 - P.z0 + 1, W = P.x1 - P.x0 + 1;
   return (uint32_t)((max(0, P.cl1 - P.cl0 + 1) + max(0, P.cr1 - P.cr0 + 1)) * H +
-                    (max(0, P.rb1 - P.rb0 + 1) + max(0, P.rt1 - P.rt0 + 1)) * W);
+                    (max(0, P.rb1 - P.rb0 + 1) + max(0, P.rt1 - P.rt0 + 1)) * (P.zrun ? run_row_items(P) : W));
 }
 
 // the lane whose inclusive prefix `incl` is the first above k (every lane of the wave takes part)
@@ -2531,25 +2582,31 @@ k_sweep_band(SweepArgs a) {
       BandPlan P;
       elig = band_plan(m, gl, J, __uint_as_float(a.band_hd[2 * sp]), __uint_as_float(a.band_hd[2 * sp + 1]), P) &&
              plan_fits(P);
-      nit = band_items(P);
-      if (elig && kBandTrips > 0.0f && !a.band_all) {
-        // cost model (memory round trips): the ring walk reads ~all records of the ring cells, 128 per
-        // trip, after one trip per 64 row parts, for ONE mover at a time; the band walk's cells and
-        // candidates share the batch's rounds of 128 (cells: cell starts + two search levels). The ring's
-        // records from the cells at the four edge midpoints: a hotspot mover's edges are crowded, a large-D
-        // mover's in the sparse world around it (there the band walk only adds work)
+      if (elig) {
+        // The ring's records from the cells at the four edge midpoints: a hotspot mover's edges are crowded,
+        // a large-D mover's in the sparse world around it. Sparse bottom and top edges: z-strips in runs.
         const int cz = (P.z0 + P.z1) >> 1, cx = (P.x0 + P.x1) >> 1;
         auto cnt = [&](int c, int r) {
           const uint32_t k = cell_key(gl, c, r);
           return (float)(a.g.cs[k + 1] - a.g.cs[k]);
         };
         const float nl = cnt(P.cl0, cz), nr = cnt(P.cr1, cz), nb = cnt(cx, P.rb0), nt = cnt(cx, P.rt1);
-        const float H = (float)(P.z1 - P.z0 + 1), W = (float)(P.x1 - P.x0 + 1);
-        const float ring = H * (nl + nr) + W * (nb + nt);
-        const float f = fminf(1.0f, (P.wl1 - P.wl0) * gl.inv_c);
-        const float ring_trips = ceilf((2.0f * H + 2.0f) * (1.0f / 64.0f)) + ring * (1.0f / 128.0f);
-        const float band_trips = (float)nit * (kBandTrips / 128.0f) + ring * f * (1.5f / 128.0f);
-        elig = band_trips < ring_trips;
+        P.zrun = kBandRun > 0.0f && nb + nt < 2.0f * kBandRun ? 1 : 0;
+        nit = band_items(P);
+        if (kBandTrips > 0.0f && !a.band_all) {
+          // cost model (memory round trips): the ring walk reads ~all records of the ring cells, 128 per
+          // trip, after one trip per 64 row parts, for ONE mover at a time; the band walk's cells and
+          // candidates share the batch's rounds of 128 (cells: cell starts + two search levels; runs: their
+          // whole rows' records)
+          const float H = (float)(P.z1 - P.z0 + 1), W = (float)(P.x1 - P.x0 + 1);
+          const float ring = H * (nl + nr) + W * (nb + nt);
+          const float f = fminf(1.0f, (P.wl1 - P.wl0) * gl.inv_c);
+          const float zr = (float)(max(0, P.rb1 - P.rb0 + 1) + max(0, P.rt1 - P.rt0 + 1));
+          const float ring_trips = ceilf((2.0f * H + 2.0f) * (1.0f / 64.0f)) + ring * (1.0f / 128.0f);
+          const float band_trips = (float)nit * (kBandTrips / 128.0f) + ring * f * (1.5f / 128.0f) +
+                                   (P.zrun ? zr * W * (nb + nt) * (0.5f / 128.0f) : 0.0f);
+          elig = band_trips < ring_trips;
+        }
       }
       if (elig) {
         plan_store(pl[wv][lane], P);
@@ -2573,7 +2630,7 @@ k_sweep_band(SweepArgs a) {
     for (uint32_t ib = 0; ib < N; ib += 128u) {
       uint32_t p0[2], p1[2], mk[2];
       float w0[2], w1[2];
-      int kind[2], dd[2], iow[2];
+      int kind[2], dd[2], iow[2], span[2];
       stream_owners(orow[wv], iexcl, nit, ib, iow[0], iow[1]);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -2583,12 +2640,12 @@ k_sweep_band(SweepArgs a) {
         const uint32_t kex = (uint32_t)__shfl((int)iexcl, k, 64);
         mk[u] = (uint32_t)k;
         p0[u] = p1[u] = 0u;
-        kind[u] = 3, dd[u] = 0, w0[u] = w1[u] = 0.0f;
+        kind[u] = 3, dd[u] = 0, span[u] = 0, w0[u] = w1[u] = 0.0f;
         if (it < N) {
           const BandPlan P = plan_load(pl[wv][k]);
           const uint2 sg = pg[wv][k];
           int c, r;
-          band_item(P, it - kex, c, r, w0[u], w1[u], kind[u], dd[u]);
+          band_item(P, it - kex, c, r, w0[u], w1[u], kind[u], dd[u], span[u]);
           // (cell_key on the Space's base and tile columns)
           p0[u] = sg.x + ((uint32_t)((r >> kTileShift) * (int)sg.y + (c >> kTileShift)) << kTileCellShift) +
                   (uint32_t)(((r & (kTile - 1)) << kTileShift) | (c & (kTile - 1)));  // (the key until its starts load)
@@ -2600,7 +2657,7 @@ k_sweep_band(SweepArgs a) {
         if (kind[u] != 3) {
           const uint32_t ck = p0[u];
           p0[u] = a.g.cs[ck];
-          p1[u] = a.g.cs[ck + 1];
+          p1[u] = a.g.cs[ck + 1 + (uint32_t)span[u]];  // (a run: its last cell's end)
         }
       }
 #pragma unroll
@@ -2610,7 +2667,9 @@ k_sweep_band(SweepArgs a) {
         // item of a corner cell then reads nothing; the rule depends only on the cell's size, so both
         // items of a corner cell apply it alike)
         const uint32_t nc = p1[u] - p0[u];
-        if (kind[u] != 3 && (nc > kBandCellMax || nc < kBandSearchMin)) {
+        if (kind[u] == 4) {
+          kind[u] = 2;  // a run: read whole (no x-strip column in it: no dedupe)
+        } else if (kind[u] != 3 && (nc > kBandCellMax || nc < kBandSearchMin)) {
           kind[u] = 2;
           if (dd[u]) p1[u] = p0[u];
         }
@@ -3373,6 +3432,9 @@ __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
 __global__ void __launch_bounds__(kBlock) k_copy_out(OrderArgs o) {
   uint32_t slots, n;
   if (!ev_fits(o, &slots, &n)) return;
+  // a small pass whose events overflowed k_order_small's LDS placed nothing: the host zeroes the flag and
+  // runs the general order stage, whose own copy delivers them
+  if (o.g.ctr[CTR_SMALL_OVF]) return;
   for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) o.host_out[i] = o.ev_out[i];
 }
 

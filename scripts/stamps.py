@@ -6,8 +6,14 @@ import sys
 import numpy as np
 
 a = np.load(sys.argv[1]).astype(np.int64)
-n = int(sys.argv[2]) if len(sys.argv) > 2 else int((a[:, 0] > 0).sum())
-a = a[:n]
+# optional item range [lo, hi) (tile indices: e.g. the big sweep's Spaces), else the first n items
+if len(sys.argv) > 3:
+    a = a[int(sys.argv[2]):int(sys.argv[3])]
+    a = a[a[:, 0] > 0]
+    n = a.shape[0]
+else:
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else int((a[:, 0] > 0).sum())
+    a = a[:n]
 t0 = a[:, 0].min()
 us = lambda v: v / 100.0  # 100 MHz -> us
 print(f"blocks {n}; kernel span {us(a[:, 4].max() - t0):.1f} us")

@@ -456,4 +456,10 @@ def test_collect_direct_matches_partition(gpu, oracle_lib, n, L, dist, n_gates, 
     for g in got:
         for f in got[g].dtype.names:
             assert np.array_equal(got[g][f], got2[g][f]), f"gate {g} field {f}: direct and partition differ"
-    assert sy.debug_fanout_mode(0) >= r0
+    reruns = sy.debug_fanout_mode(0) - r0
+    # the direct path's first packet buffer holds 65,536 records: a larger collect is grown and written again
+    # (the bytes compared above are the rewrite's)
+    if sum(len(v) for v in got.values()) > 65536:
+        assert reruns >= 1
+    else:
+        assert reruns >= 0
