@@ -240,8 +240,9 @@ def tick_counter_bytes(workload, n, stamp):
     per_tick = kt.get("k_sweep", {}).get("dispatches")
     if not per_tick:
         return None, None
-    ks = sorted(k for k, e in kt.items() if "bytes" in e and e.get("dispatches", 0) >= per_tick)
-    return sum(kt[k]["bytes"] * round(kt[k]["dispatches"] / per_tick) for k in ks), ks
+    # (>= 3/4 of k_sweep's dispatches: the first pass of a run, the bulk Enter, launches no global walk)
+    ks = sorted(k for k, e in kt.items() if "bytes" in e and e.get("dispatches", 0) >= 0.75 * per_tick)
+    return sum(kt[k]["bytes"] * max(1, round(kt[k]["dispatches"] / per_tick)) for k in ks), ks
 
 
 def spaces_workload(args, rank):

@@ -69,7 +69,10 @@ for k, cs in vals.items():
     kern[k] = e
 # the workload's roofline kernel(s), as bench.py times them (the pass's sweep stage)
 dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_big", "k_band_keys", "k_band_rank", "k_sweep_band", "k_sweep_dense"])
-summed = [k for k in dominant if "bytes" in kern.get(k, {})]
+# (only kernels that ran (nearly) every tick of the passes, >= 3/4 of k_sweep's dispatches: a band walk launched once
+# in a config-2 run, for the bulk Enter pass, is not the tick's)
+per_tick = kern.get("k_sweep", {}).get("dispatches", 0)
+summed = [k for k in dominant if "bytes" in kern.get(k, {}) and kern[k].get("dispatches", 0) >= 0.75 * per_tick]
 entry = {"lib_src": lib.pop(), "n": n.pop(), "source": prefix, "kernels": kern, "kernels_summed": summed,
          "bytes_per_launch": sum(kern[k]["bytes"] for k in summed) if summed else None}
 res = {}
