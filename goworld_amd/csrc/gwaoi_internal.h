@@ -28,6 +28,7 @@ enum { CTR_EVENTS = 0, CTR_ERR = 1, CTR_ENTER = 2, CTR_UNITS = 3, CTR_RECORDS = 
        CTR_SMALL_OVF = 15,   // k_order_small: the pass's events exceed its LDS (the host re-runs the order stage)
        CTR_BDONE = 16,  // blocks of the one-pass build done (not published)
        CTR_SDONE = 17,  // blocks of k_slice_sort done (the last one publishes the counters)
+       CTR_RING_MV = 18,  // movers k_sweep_band handed to the ring walk (k_sweep_dense<true> exits at 0)
        CTR_N = 32 };
 constexpr int kPubWords = 16;  // counters [0, 16) are what the host reads after a pass
 // CTR_EVENTS counts SLOTS of ev_tmp's shared region (after the per-tile regions, SweepArgs.ev_fix);
@@ -225,7 +226,6 @@ struct SweepArgs {
   const float* band_zk;   // per cell by z key: the key, and
   const uint32_t* band_zi;  // the record
   const uint32_t* band_hd;
-  int band_all;           // 1: every mover with a band plan takes the band walk (cost model off; tests)
 };
 
 // Band keys of the pass's grid for k_sweep_dense's band walk. A record's judge position p is

@@ -2254,7 +2254,9 @@ k_sweep_dense(SweepArgs a) {
   // (kRing: dense2 runs parallel to the dense list, the band walk's movers marked kNoKey, so the ring walk
   // visits the rest in the same grid order: handed over compacted, its waves lost their L2 locality)
   const uint32_t* list = kRing ? a.dense2 : a.dense;
-  const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
+  // (kRing: nothing handed over, the usual case now that every mover with a band plan takes it: the list
+  // is not scanned)
+  const uint32_t nd = kRing && a.ctr[CTR_RING_MV] == 0u ? 0u : min(a.ctr[CTR_DENSE], a.dense_cap);
   const unsigned long long below = (1ull << lane) - 1ull;
   uint32_t nent = 0;
   uint32_t cur = 0, left = 0;  // the wave's current chunk of event slots (wave-uniform)
@@ -2433,10 +2435,6 @@ k_sweep_dense(SweepArgs a) {
 #ifndef GW_BAND_WPE  // 4 waves per SIMD: 118 VGPRs (two cells and two candidates per lane in flight)
 #define GW_BAND_WPE 5
 #endif
-#ifndef GW_BAND_TRIPS  // the cost model's trips per round of 128 band cells (0: every plan takes the band walk)
-#define GW_BAND_TRIPS 3.0f
-#endif
-constexpr float kBandTrips = GW_BAND_TRIPS;
 #ifndef GW_BAND_SEARCH_MIN  // cells of fewer records are read whole instead of searched
 #define GW_BAND_SEARCH_MIN 4u
 #endif
@@ -2547,7 +2545,7 @@ k_sweep_band(SweepArgs a) {
   const uint32_t wave = ((blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u) * (kDenseBlock / 64) + wv;
   const uint32_t nd = min(a.ctr[CTR_DENSE], a.dense_cap);
   const unsigned long long below = (1ull << lane) - 1ull;
-  uint32_t nent = 0, nband = 0;  // nband: movers of the wave that took the band walk
+  uint32_t nent = 0, nband = 0, nring = 0;  // the wave's movers that took the band walk / were handed over
   uint32_t cur = 0, left = 0;    // the wave's current chunk of event slots (wave-uniform)
   __shared__ uint4 mb[kDenseBlock / 64][64][2];  // the batch: {slot, Space, opq, seq0}, {x0, z0, x1, z1}
   __shared__ BandPlanL pl[kDenseBlock / 64][64];  // per batch mover: its band plan
@@ -2583,30 +2581,18 @@ k_sweep_band(SweepArgs a) {
       elig = band_plan(m, gl, J, __uint_as_float(a.band_hd[2 * sp]), __uint_as_float(a.band_hd[2 * sp + 1]), P) &&
              plan_fits(P);
       if (elig) {
-        // The ring's records from the cells at the four edge midpoints: a hotspot mover's edges are crowded,
-        // a large-D mover's in the sparse world around it. Sparse bottom and top edges: z-strips in runs.
-        const int cz = (P.z0 + P.z1) >> 1, cx = (P.x0 + P.x1) >> 1;
+        // the records of the cells at the bottom / top edge midpoints: a hotspot mover's edges are crowded,
+        // a large-D mover's in the sparse world around it; sparse bottom and top edges: z-strips in runs
+        const int cx = (P.x0 + P.x1) >> 1;
         auto cnt = [&](int c, int r) {
           const uint32_t k = cell_key(gl, c, r);
           return (float)(a.g.cs[k + 1] - a.g.cs[k]);
         };
-        const float nl = cnt(P.cl0, cz), nr = cnt(P.cr1, cz), nb = cnt(cx, P.rb0), nt = cnt(cx, P.rt1);
+        const float nb = cnt(cx, P.rb0), nt = cnt(cx, P.rt1);
         P.zrun = kBandRun > 0.0f && nb + nt < 2.0f * kBandRun ? 1 : 0;
         nit = band_items(P);
-        if (kBandTrips > 0.0f && !a.band_all) {
-          // cost model (memory round trips): the ring walk reads ~all records of the ring cells, 128 per
-          // trip, after one trip per 64 row parts, for ONE mover at a time; the band walk's cells and
-          // candidates share the batch's rounds of 128 (cells: cell starts + two search levels; runs: their
-          // whole rows' records)
-          const float H = (float)(P.z1 - P.z0 + 1), W = (float)(P.x1 - P.x0 + 1);
-          const float ring = H * (nl + nr) + W * (nb + nt);
-          const float f = fminf(1.0f, (P.wl1 - P.wl0) * gl.inv_c);
-          const float zr = (float)(max(0, P.rb1 - P.rb0 + 1) + max(0, P.rt1 - P.rt0 + 1));
-          const float ring_trips = ceilf((2.0f * H + 2.0f) * (1.0f / 64.0f)) + ring * (1.0f / 128.0f);
-          const float band_trips = (float)nit * (kBandTrips / 128.0f) + ring * f * (1.5f / 128.0f) +
-                                   (P.zrun ? zr * W * (nb + nt) * (0.5f / 128.0f) : 0.0f);
-          elig = band_trips < ring_trips;
-        }
+        // (every mover with a band plan takes the band walk: a per-mover cost model choosing the ring walk
+        // for the movers it rated cheaper there lost on skew50, skew and strips_skew alike, r05_c17 / c18)
       }
       if (elig) {
         plan_store(pl[wv][lane], P);
@@ -2618,6 +2604,7 @@ k_sweep_band(SweepArgs a) {
     if (di < nd) a.dense2[di] = elig ? kNoKey : ls;  // the ring walk's list, in the same order
     if (!elig) nit = 0;
     nband += (uint32_t)__popcll(__ballot(elig));
+    nring += (uint32_t)__popcll(__ballot(di < nd && !elig));
     const uint32_t iincl = wave_incl_scan(nit), iexcl = iincl - nit;
     const uint32_t N = __builtin_amdgcn_readlane(iincl, 63);  // the batch's band cells
     __builtin_amdgcn_wave_barrier();  // the wave's LDS ops stay in program order
@@ -2818,6 +2805,7 @@ k_sweep_band(SweepArgs a) {
   const uint32_t went = __shfl(wave_incl_scan(nent), 63, 64);
   if (lane == 0 && went) atomicAdd(&a.ctr[CTR_ENTER], went);
   if (lane == 0 && nband) atomicAdd(&a.ctr[CTR_BAND_MV], nband);
+  if (lane == 0 && nring) atomicAdd(&a.ctr[CTR_RING_MV], nring);
   // (events numbered in walk order: the slices are sorted whenever the list is not empty)
   if (blockIdx.x == 0 && threadIdx.x == 0 && nd) a.ctr[CTR_UNSORTED] = 1u;
 #if GW_STAMPS

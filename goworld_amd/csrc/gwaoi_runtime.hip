@@ -199,7 +199,7 @@ struct gwaoi_mgr {
   // the band walk of k_sweep_dense: the grid's records sorted per cell by search key, built
   // after the grid of every pass that launches k_sweep_dense (gwaoi_debug_set_band: 0 off)
   bool big_sweep = true;  // Spaces over the small LDS sweep's region budget take the big one (debug_set_sweep_lds 3: off)
-  int band_mode = 1;  // 0 off, 1 on (cost model per mover), 2 every mover with a band plan (tests)
+  int band_mode = 1;  // 0 off, 1 (or 2) on: every mover with a band plan
   float2* band_key2 = nullptr;
   float *band_xk = nullptr, *band_zk = nullptr;
   uint32_t* band_zi = nullptr;
@@ -1045,7 +1045,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
       HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_UNSORTED, 0, 3 * sizeof(uint32_t), st));  // + UNS_SOME, BAND_MV
       // (an overflowing order stage returned before k_slice_sort cleared the flags it would have read)
       HIPCHK(hipMemsetAsync(m->uns, 0, ((size_t)n_ops / 32 + 1) * sizeof(uint32_t), st));
-      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(m->ctr + gw::CTR_SDONE, 0, 2 * sizeof(uint32_t), st));  // + CTR_RING_MV
     }
     gw::SweepArgs s{};
     const Grid& G = m->grid[ng];
@@ -1102,7 +1102,6 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.band_zk = keys ? m->band_zk : nullptr;
     s.band_zi = keys ? m->band_zi : nullptr;
     s.band_hd = keys ? m->band_hd : nullptr;
-    s.band_all = m->band_mode == 2 ? 1 : 0;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));

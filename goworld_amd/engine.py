@@ -238,9 +238,9 @@ class Engine:
         check(self._L.gwaoi_debug_set_sweep_lds(self._h, 1 if on else 0))
 
     def debug_set_band(self, mode: int = -1) -> int:
-        """gwaoi_debug_set_band: the band walk of the global-memory movers on (1, default: a cost model picks
-        band or ring per mover), off (0: their whole rings) or for every mover with a band plan (2); returns
-        the movers that took the band walk so far."""
+        """gwaoi_debug_set_band: the band walk of the global-memory movers on (1, default: every mover with a
+        band plan; 2 is the same) or off (0: their whole rings); returns the movers that took the band walk
+        so far."""
         n = ctypes.c_uint64()
         check(self._L.gwaoi_debug_set_band(self._h, int(mode), ctypes.byref(n)))
         return int(n.value)

@@ -76,8 +76,8 @@ int gwaoi_debug_set_build_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* n_fuse
 /* The band walk of the global-memory movers (k_sweep_dense): 1 = on (default: per pass that
  * walks from global memory, the grid's records are sorted per cell by search key and each ordinary move
  * reads only the key windows of the two boxes' symmetric difference), 0 = off (every such mover reads its
- * whole ring of cells), 2 = on for every mover with a band plan (the per-mover cost model off: tests);
- * -1 leaves the mode. *n_band_movers (optional): movers that took the band walk
+ * whole ring of cells), 2 = the same as 1 (there is no per-mover cost model any more: every mover with a
+ * band plan takes the band walk); -1 leaves the mode. *n_band_movers (optional): movers that took the band walk
  * since the manager was made. */
 int gwaoi_debug_set_band(struct gwaoi_mgr* mgr, int mode, uint64_t* n_band_movers);
 /* Sync fan-out path (gwaoi_collect_sync): 0 = the records written straight into their gate packets when

@@ -352,26 +352,23 @@ def test_config2_full_size_enter_and_four_ticks(gpu, po):
     assert eng.debug_relation_mode()[0] == 4, eng.debug_relation_mode()  # every moving tick: updated
 
 
-@pytest.mark.parametrize("path", ["band", "band_all", "ring", "all_global"])
+@pytest.mark.parametrize("path", ["band", "ring", "all_global"])
 def test_skewed_crowd_dense_path(gpu, po, path):
     """Config 5 in miniature: a small-D Space with Gaussian hotspots (~100x the mean
     density) and a large-D Space in one manager. Hotspot tiles and every D=400 tile exceed the sweep's
     LDS region: their movers take the wave-per-mover path (k_sweep_dense) with its reserved event slots,
-    by the band walk where its cost model prefers it (the default: per-cell key windows of the boxes'
-    symmetric difference), by the band walk for every mover with a band plan, by their whole rings (band
-    off), or with every mover of the world on that path (LDS sweep off, band walk for every plan); relation
-    after the enter tick and the last tick, events every tick, against oracle (ii)."""
+    by the band walk (the default: per-cell key windows of the boxes' symmetric difference; the enter tick's
+    movers have no band plan and are handed to the ring walk), by their whole rings (band off), or with every
+    mover of the world on that path (LDS sweep off); relation after the enter tick and the last tick, events
+    every tick, against oracle (ii)."""
     from goworld_amd.engine import Engine
     n, L = 60000, 8500.0  # the mean density of config 5 (1M in 35,000^2)
     spaces = [(50.0, 0x5EED0050), (400.0, 0x5EED0400)]
     eng = Engine(capacity=n * len(spaces), spaces=[(d, (0.0, 0.0, L, L)) for d, _ in spaces])
     if path == "ring":
         eng.debug_set_band(0)
-    elif path == "band_all":
-        eng.debug_set_band(2)
     elif path == "all_global":
         eng.debug_set_sweep_lds(False)
-        eng.debug_set_band(2)
     eng.set_timing(True)
     pos, orcs = [], []
     for k, (d, seed) in enumerate(spaces):
@@ -406,7 +403,7 @@ def test_skewed_crowd_dense_path(gpu, po, path):
     check_relation("last tick")
     st = eng.stats()
     assert st["dense_movers"] > n  # the global-memory path was taken
-    assert (st["band_movers"] > (n if path in ("band_all", "all_global") else 0)) == (path != "ring")
+    assert (st["band_movers"] > n) == (path != "ring")
 
 
 @pytest.mark.parametrize("seed", range(3))
