@@ -2538,8 +2538,40 @@ __device__ __forceinline__ int wave_owner(uint32_t incl, uint32_t k) {
   return lo;
 }
 
+// kBuf: the hot loads (cell starts, search keys, z order, candidate records) through buffer descriptors
+// (32-bit offsets: the walk is VALU-issue bound, and a flat load's 64-bit address costs two or three VALU
+// instructions); the launcher picks it when every array is below 2 GiB
+template <bool kBuf>
 __global__ void __launch_bounds__(kDenseBlock) __attribute__((amdgpu_waves_per_eu(GW_BAND_WPE)))
 k_sweep_band(SweepArgs a) {
+  // x keys and z keys are one allocation (zk = xk + zoff)
+  const uint32_t zoff = (uint32_t)(a.band_zk - a.band_xk);
+  const auto r_cs = __builtin_amdgcn_make_buffer_rsrc((void*)a.g.cs, 0, (int)((a.ncells + 1u) * 4u), 0x00020000);
+  const auto r_key = __builtin_amdgcn_make_buffer_rsrc((void*)a.band_xk, 0, (int)(2u * zoff * 4u), 0x00020000);
+  const auto r_zi = __builtin_amdgcn_make_buffer_rsrc((void*)a.band_zi, 0, (int)(zoff * 4u), 0x00020000);
+  const auto r_rec = __builtin_amdgcn_make_buffer_rsrc((void*)a.g.rec, 0, (int)(a.n_rec * 32u), 0x00020000);
+  auto ld_cs = [&](uint32_t k) -> uint32_t {
+    if constexpr (kBuf) return __builtin_amdgcn_raw_buffer_load_b32(r_cs, k << 2, 0, 0);
+    else return a.g.cs[k];
+  };
+  auto ld_key = [&](int kind, uint32_t i) -> float {  // kind 1: z key
+    if constexpr (kBuf) return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r_key, ((kind == 1 ? zoff : 0u) + i) << 2, 0, 0));
+    else return (kind == 1 ? a.band_zk : a.band_xk)[i];
+  };
+  auto ld_zi = [&](uint32_t i) -> uint32_t {
+    if constexpr (kBuf) return __builtin_amdgcn_raw_buffer_load_b32(r_zi, i << 2, 0, 0);
+    else return a.band_zi[i];
+  };
+  auto ld_rec = [&](uint32_t j, uint4& ra, uint4& rb) {
+    if constexpr (kBuf) {
+      const auto qa = __builtin_amdgcn_raw_buffer_load_b128(r_rec, j << 5, 0, 0);
+      const auto qb = __builtin_amdgcn_raw_buffer_load_b128(r_rec, (j << 5) + 16u, 0, 0);
+      ra = make_uint4(qa[0], qa[1], qa[2], qa[3]);
+      rb = make_uint4(qb[0], qb[1], qb[2], qb[3]);
+    } else {
+      ra = a.g.rec[j].a, rb = a.g.rec[j].b;
+    }
+  };
   const int lane = threadIdx.x & 63;
   const uint32_t wv = threadIdx.x >> 6, nwaves = gridDim.x * (kDenseBlock / 64);
   const uint32_t wave = ((blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u) * (kDenseBlock / 64) + wv;
@@ -2643,8 +2675,8 @@ k_sweep_band(SweepArgs a) {
       for (int u = 0; u < 2; ++u) {  // cell starts of both cells, loads in flight together
         if (kind[u] != 3) {
           const uint32_t ck = p0[u];
-          p0[u] = a.g.cs[ck];
-          p1[u] = a.g.cs[ck + 1 + (uint32_t)span[u]];  // (a run: its last cell's end)
+          p0[u] = ld_cs(ck);
+          p1[u] = ld_cs(ck + 1 + (uint32_t)span[u]);  // (a run: its last cell's end)
         }
       }
 #pragma unroll
@@ -2679,15 +2711,14 @@ k_sweep_band(SweepArgs a) {
         while (__any(lh[0] > ll[0] || uh[0] > ul[0] || lh[1] > ll[1] || uh[1] > ul[1])) {
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
-            const float* arr = kind[u] == 1 ? a.band_zk : a.band_xk;
             const uint32_t sl = (lh[u] - ll[u] + kBandFan - 1) / kBandFan, su = (uh[u] - ul[u] + kBandFan - 1) / kBandFan;
             const bool same = ll[u] == ul[u] && lh[u] == uh[u];
             uint32_t cl = 0, cu = 0, cs = 0;  // probes below the bound (a prefix: the keys are sorted)
 #pragma unroll
             for (uint32_t q = 0; q < kBandFan; ++q) {
               const uint32_t ql = ll[u] + (q + 1) * sl - 1, qu = ul[u] + (q + 1) * su - 1;
-              const float kl = (sl && ql < lh[u]) ? arr[ql] : __builtin_inff();
-              const float ku = (!same && su && qu < uh[u]) ? arr[qu] : __builtin_inff();
+              const float kl = (sl && ql < lh[u]) ? ld_key(kind[u], ql) : __builtin_inff();
+              const float ku = (!same && su && qu < uh[u]) ? ld_key(kind[u], qu) : __builtin_inff();
               cl += kl < w0[u] ? 1u : 0u;
               cs += kl <= w1[u] ? 1u : 0u;
               cu += ku <= w1[u] ? 1u : 0u;
@@ -2738,8 +2769,9 @@ k_sweep_band(SweepArgs a) {
           ev[v] = 0;
           oth[v] = 0;
           if (kc < total) {
-            const uint32_t j = kd == 1 ? a.band_zi[pos] : pos;
-            const uint4 ra = a.g.rec[j].a, rb = a.g.rec[j].b;
+            const uint32_t j = kd == 1 ? ld_zi(pos) : pos;
+            uint4 ra, rb;
+            ld_rec(j, ra, rb);
             bool dup = false;
             if (dl) {
               const float wl0 = pl[wv][mo[v]].w[0], wl1 = pl[wv][mo[v]].w[1];
@@ -3103,7 +3135,13 @@ void launch_sweep(const SweepArgs& a, hipStream_t st) {
   // tick): if this pass lists some after all, the host re-runs the sweep with it (run_pass)
   if (a.dense && a.dense_hint) {
     if (a.band_xk && a.dense2) {  // the band walk, then the ring walk of the movers it hands over
-      hipLaunchKernelGGL(k_sweep_band, dim3(256 * GW_BAND_WPE), dim3(kDenseBlock), 0, st, a);
+      // (buffer loads when every array the band walk reads is below 2 GiB; the keys as one allocation)
+      const bool buf = (uint64_t)a.n_rec * 32u < (1ull << 31) && ((uint64_t)a.ncells + 1u) * 4u < (1ull << 31) &&
+                       (uint64_t)(a.band_zk - a.band_xk) * 8u < (1ull << 31) && a.band_zk > a.band_xk;
+      if (buf)
+        hipLaunchKernelGGL(k_sweep_band<true>, dim3(256 * GW_BAND_WPE), dim3(kDenseBlock), 0, st, a);
+      else
+        hipLaunchKernelGGL(k_sweep_band<false>, dim3(256 * GW_BAND_WPE), dim3(kDenseBlock), 0, st, a);
       hipLaunchKernelGGL(k_sweep_dense<true>, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
     } else {
       hipLaunchKernelGGL(k_sweep_dense<false>, dim3(kDenseGrid), dim3(kDenseBlock), 0, st, a);
