@@ -33,6 +33,8 @@ for f in sorted(glob.glob(prefix + "*/run_counter_collection.csv")):
             name = "k_sweep"
         elif name.startswith("k_sweep_dense<"):
             name = "k_sweep_dense"
+        elif name.startswith("k_sweep_band<"):
+            name = "k_sweep_band"
         vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 lib, n = set(), set()
 for f in sorted(glob.glob(prefix + "*.json")):
