@@ -239,7 +239,6 @@ struct BandArgs {
   uint32_t nspaces;
   uint32_t rec_bound;    // launch bound on the grid's records
   const uint32_t* nrec;  // device: the grid's records (cs[ncells])
-  float2* key2;          // [records] per record {x key, z key}
   Rec* rec_out;          // [records] the grid's records sorted by x key inside each cell (cells over
                          // kBandCellMax records copied as they are); replaces the grid's records
   float* xk;             // [records] their x keys, in rec_out order

@@ -2045,31 +2045,85 @@ __device__ __forceinline__ void band_key(const uint4 ra, const uint4 rb, float& 
   hz = fmaxf(fabsf(sz - mz), fabsf(bz - mz));
 }
 
-// keys in record order and the per-Space spread: grid-stride over the records; the spread is reduced per
-// block in LDS (a Space's records are contiguous in grid order) and raised in global memory once per block,
-// Space and axis, only when it exceeds the current value (one atomic or read per wave on the same two
-// words serialised at the memory side: 1.49 ms, then 0.25 ms per skew50 pass)
-constexpr uint32_t kBandKeyBlocks = 1024;
-__global__ void __launch_bounds__(kBlock) k_band_keys(BandArgs a) {
+// Search keys, the per-Space key spread and each record's rank by x key and by z key inside its cell (ties by
+// record index), in ONE kernel: a block takes kBandSortRecs consecutive records, computes the keys of every
+// record of the cells they lie in (from the start of its first record's cell to the end of its last one's)
+// into LDS, and ranks its own records from there (a hotspot cell's ~50 records read ~50 keys each: from LDS,
+// not L1/L2); each record writes itself into the x-sorted records and keys and the z-sorted keys and indices.
+// Cells over kBandCellMax records are copied in place, unsorted (the walk reads them whole). The spread is
+// reduced per block in LDS and raised in global memory once per block, Space and axis, only when it exceeds
+// the current value (one atomic per wave on the same words serialised at the memory side: 1.49 ms per skew50
+// pass, r05_b2). A range over the LDS stage (a cell over kBandCellMax records at an edge) ranks from the
+// records themselves. (Two kernels before, keys then ranks through a key array: 197 vs 137 us at skew50,
+// r05_c28.)
+constexpr uint32_t kBandSortRecs = 4 * kBlock, kBandSortStage = 1536;
+__device__ __forceinline__ float2 rec_key(const Rec* rec, uint32_t i) {
+  const Rec r = rec[i];
+  float kx, kz, hx, hz;
+  band_key(r.a, r.b, kx, kz, hx, hz);
+  return make_float2(kx, kz);
+}
+__global__ void __launch_bounds__(kBlock) k_band_sort(BandArgs a) {
+  __shared__ float2 kk[kBandSortStage];
+  __shared__ Geom gs[kLdsGeoms];
   __shared__ uint32_t bh[2 * kLdsGeoms];
-  const bool lds = a.nspaces <= kLdsGeoms;
-  if (lds)
-    for (uint32_t i = threadIdx.x; i < 2 * a.nspaces; i += kBlock) bh[i] = 0u;
+  __shared__ uint32_t rng[2];
+  const bool lgeo = a.nspaces <= kLdsGeoms;
+  if (lgeo)
+    for (uint32_t i = threadIdx.x; i < a.nspaces; i += kBlock) gs[i] = a.g.geom[i], bh[2 * i] = 0u, bh[2 * i + 1] = 0u;
   __syncthreads();
   const uint32_t n = min(*a.nrec, a.rec_bound);
-  for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j < n; j += gridDim.x * kBlock) {
+  const uint32_t j0 = blockIdx.x * kBandSortRecs;
+  if (j0 >= n) return;  // block-uniform
+  const uint32_t jl = min(j0 + kBandSortRecs, n) - 1u;
+  auto cell_of = [&](const uint4 ra, uint32_t& s, uint32_t& e) {
+    const uint32_t sp = a.space_of[ra.z & REC_SLOT];
+    const float bx = __uint_as_float(ra.x), bz = __uint_as_float(ra.y);
+    const uint32_t key = lgeo ? cell_key_of(gs[sp], bx, bz) : cell_key_of(a.g.geom[sp], bx, bz);
+    s = a.g.cs[key], e = a.g.cs[key + 1];
+    return sp;
+  };
+  if (threadIdx.x < 2) {
+    uint32_t s, e;
+    cell_of(a.g.rec[threadIdx.x == 0 ? j0 : jl].a, s, e);
+    rng[threadIdx.x] = threadIdx.x == 0 ? s : e;
+  }
+  __syncthreads();
+  const uint32_t lo = rng[0], hi = rng[1];
+  const bool staged = hi - lo <= kBandSortStage;  // block-uniform
+  if (staged)
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) kk[i - lo] = rec_key(a.g.rec, i);
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t j = j0 + k * kBlock + threadIdx.x;
+    if (j >= n || j > jl) continue;
     const Rec r = a.g.rec[j];
+    uint32_t s, e;
+    const uint32_t sp = cell_of(r.a, s, e);
     float kx, kz, hx, hz;
     band_key(r.a, r.b, kx, kz, hx, hz);
-    a.key2[j] = make_float2(kx, kz);
     if (hx > 0.0f || hz > 0.0f) {
-      const uint32_t sp = a.space_of[r.a.z & REC_SLOT];
-      uint32_t* w = lds ? &bh[2 * sp] : &a.hd[2 * sp];
+      uint32_t* w = lgeo ? &bh[2 * sp] : &a.hd[2 * sp];
       if (hx > 0.0f) atomicMax(&w[0], __float_as_uint(hx));
       if (hz > 0.0f) atomicMax(&w[1], __float_as_uint(hz));
     }
+    if (e - s > kBandCellMax) {  // copied in place, unsorted (the walk reads the cell whole)
+      a.rec_out[j] = r;
+      continue;
+    }
+    uint32_t rx = 0, rz = 0;
+    for (uint32_t i = s; i < e; ++i) {
+      const float2 ki = staged ? kk[i - lo] : rec_key(a.g.rec, i);
+      rx += (ki.x < kx || (ki.x == kx && i < j)) ? 1u : 0u;
+      rz += (ki.y < kz || (ki.y == kz && i < j)) ? 1u : 0u;
+    }
+    a.rec_out[s + rx] = r;
+    a.xk[s + rx] = kx;
+    a.zk[s + rz] = kz;
+    a.zi[s + rz] = s + rx;
   }
-  if (!lds) return;
+  if (!lgeo) return;
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < 2 * a.nspaces; i += kBlock) {
     const uint32_t v = bh[i];
@@ -2077,45 +2131,9 @@ __global__ void __launch_bounds__(kBlock) k_band_keys(BandArgs a) {
   }
 }
 
-// per record: its ranks by x key and by z key among its cell's records (ties by record index), from
-// which it writes itself into the two sorted arrays. Cells over kBandCellMax records are left unsorted
-// (the walk reads them whole).
-__global__ void __launch_bounds__(kBlock) k_band_rank(BandArgs a) {
-  __shared__ Geom gs[kLdsGeoms];
-  if (a.nspaces <= kLdsGeoms)
-    for (uint32_t i = threadIdx.x; i < a.nspaces; i += kBlock) gs[i] = a.g.geom[i];
-  __syncthreads();
-  const uint32_t n = min(*a.nrec, a.rec_bound);
-  const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  const uint4 ra = a.g.rec[j].a;
-  const uint32_t sp = a.space_of[ra.z & REC_SLOT];
-  const float bx = __uint_as_float(ra.x), bz = __uint_as_float(ra.y);
-  const uint32_t key = a.nspaces <= kLdsGeoms ? cell_key_of(gs[sp], bx, bz) : cell_key_of(a.g.geom[sp], bx, bz);
-  const uint32_t s = a.g.cs[key], e = a.g.cs[key + 1];
-  const Rec r = a.g.rec[j];
-  if (e - s > kBandCellMax) {  // copied in place, unsorted (the walk reads the cell whole)
-    a.rec_out[j] = r;
-    return;
-  }
-  const float2 kj = a.key2[j];
-  uint32_t rx = 0, rz = 0;
-  for (uint32_t i = s; i < e; ++i) {
-    const float2 ki = a.key2[i];
-    rx += (ki.x < kj.x || (ki.x == kj.x && i < j)) ? 1u : 0u;
-    rz += (ki.y < kj.y || (ki.y == kj.y && i < j)) ? 1u : 0u;
-  }
-  a.rec_out[s + rx] = r;
-  a.xk[s + rx] = kj.x;
-  a.zk[s + rz] = kj.y;
-  a.zi[s + rz] = s + rx;
-}
-
 void launch_band_keys(const BandArgs& b, hipStream_t st) {
   if (!b.rec_bound) return;
-  const uint32_t nb = (b.rec_bound + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_band_keys, dim3(std::min(nb, kBandKeyBlocks)), dim3(kBlock), 0, st, b);
-  hipLaunchKernelGGL(k_band_rank, dim3(nb), dim3(kBlock), 0, st, b);
+  hipLaunchKernelGGL(k_band_sort, dim3((b.rec_bound + kBandSortRecs - 1) / kBandSortRecs), dim3(kBlock), 0, st, b);
 }
 
 // The band walk's plan for one mover (wave-uniform): the union box's cells, the cell columns that can
@@ -2421,8 +2439,8 @@ k_sweep_dense(SweepArgs a) {
 // k_sweep_dense's list walked by the band walk. For an ordinary move only the cells that can hold a judge
 // position in the symmetric difference of the two boxes are read (the x-strip columns of the left / right
 // band over the union's rows, the z-strip rows of the bottom / top band over its columns), and in each
-// such cell only the window of search keys that can (a fanout-8 search per cell: k_band_keys /
-// k_band_rank sorted the cells' records). A hotspot cell of ~50 records yields ~3 candidates instead of 50.
+// such cell only the window of search keys that can (a fanout-4 search per cell: k_band_sort
+// sorted the cells' records). A hotspot cell of ~50 records yields ~3 candidates instead of 50.
 //
 // Every global round trip costs ~3.5k cycles under this load (GW_STAMPS phases, r05_b6), so the walk is
 // flat over the wave's batch of 64 movers: the batch's cells form ONE item stream (2 per lane per round:

@@ -200,7 +200,6 @@ struct gwaoi_mgr {
   // after the grid of every pass that launches k_sweep_dense (gwaoi_debug_set_band: 0 off)
   bool big_sweep = true;  // Spaces over the small LDS sweep's region budget take the big one (debug_set_sweep_lds 3: off)
   int band_mode = 1;  // 0 off, 1 (or 2) on: every mover with a band plan
-  float2* band_key2 = nullptr;
   float *band_xk = nullptr, *band_zk = nullptr;
   uint32_t* band_zi = nullptr;
   uint32_t* band_hd = nullptr;   // [2 nspaces]
@@ -490,12 +489,12 @@ int build_band_keys(gwaoi_mgr* m, int gi, uint32_t bound, bool* built) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < n * 20 + 4ull * m->cap + (64ull << 20)) return GWAOI_OK;
     // (x and z keys in one allocation: the band walk reads both through one buffer descriptor)
-    if (dalloc(&m->band_key2, n) || dalloc(&m->band_xk, 2 * n) || dalloc(&m->band_zi, n) ||
+    if (dalloc(&m->band_xk, 2 * n) || dalloc(&m->band_zi, n) ||
         dalloc(&m->band_hd, 2 * (size_t)m->nspaces) || dalloc(&m->band_dense2, m->cap)) {  // (no room: the ring walk)
-      for (void* p : {(void*)m->band_key2, (void*)m->band_xk, (void*)m->band_zi, (void*)m->band_hd,
+      for (void* p : {(void*)m->band_xk, (void*)m->band_zi, (void*)m->band_hd,
                       (void*)m->band_dense2})
         if (p) hipFree(p);
-      m->band_key2 = nullptr, m->band_xk = m->band_zk = nullptr, m->band_zi = m->band_hd = m->band_dense2 = nullptr;
+      m->band_xk = m->band_zk = nullptr, m->band_zi = m->band_hd = m->band_dense2 = nullptr;
       return GWAOI_OK;
     }
     m->band_zk = m->band_xk + n;
@@ -508,7 +507,6 @@ int build_band_keys(gwaoi_mgr* m, int gi, uint32_t bound, bool* built) {
   b.nspaces = m->nspaces;
   b.rec_bound = (uint32_t)std::min<uint64_t>(bound, m->band_cap);
   b.nrec = G.cs + G.ncells;
-  b.key2 = m->band_key2;
   // the records sorted by x key inside their cells go into the other grid's record buffer (this pass does
   // not read it: it was the build's bucket buffer), which then becomes this grid's
   b.rec_out = m->grid[gi ^ 1].rec;
@@ -1295,7 +1293,7 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->uns, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_key2, m->band_xk, m->band_zi, m->band_hd, m->band_dense2, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_xk, m->band_zi, m->band_hd, m->band_dense2, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
                    m->dx_part, m->dx_out};

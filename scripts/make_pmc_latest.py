@@ -70,7 +70,7 @@ for k, cs in vals.items():
         e["wait_any_frac"] = d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]
     kern[k] = e
 # the workload's roofline kernel(s), as bench.py times them (the pass's sweep stage)
-dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_big", "k_band_keys", "k_band_rank", "k_sweep_band", "k_sweep_dense"])
+dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_big", "k_band_sort", "k_sweep_band", "k_sweep_dense"])
 # (only kernels that ran (nearly) every tick of the passes, >= 3/4 of k_sweep's dispatches: a band walk launched once
 # in a config-2 run, for the bulk Enter pass, is not the tick's)
 per_tick = kern.get("k_sweep", {}).get("dispatches", 0)
