@@ -53,6 +53,14 @@ constexpr int kSweepRegCells = GW_REG_CELLS;  // 48 x 48
 // the big LDS sweep (one 1024-thread block per CU): regions of up to 68 x 68 cells
 constexpr int kSweepBigRows = 68;
 constexpr int kSweepBigCells = kSweepBigRows * kSweepBigRows;
+// the mid sweep (two 512-thread blocks per CU: one stages while the other walks) for regions of up to
+// kSweepMidRows rows and its records' LDS (Geom.pad with kPadMid set)
+#ifndef GW_MID_ROWS
+#define GW_MID_ROWS 56
+#endif
+constexpr int kSweepMidRows = GW_MID_ROWS;
+constexpr int kSweepMidCells = kSweepMidRows * kSweepMidRows;
+constexpr uint32_t kPadMid = 0x80000000u;  // Geom.pad: the Space takes the mid sweep (the halo in the low bits)
 
 // Cell geometry of one Space inside one grid snapshot.
 struct Geom {
@@ -198,6 +206,7 @@ struct SweepArgs {
   uint32_t ncells;     // cells of the grid (cs[ncells] = record count)
   uint32_t ntiles;     // tiles of the grid: blocks [0, ntiles) take one tile each, the rest Leave ops
   uint32_t big_t0, big_n;  // the tiles of the Spaces of the big sweep (Geom.pad): [big_t0, big_t0 + big_n)
+  uint32_t mid_t0, mid_n;  // the tiles of the Spaces of the mid sweep (Geom.pad & kPadMid)
   int use_lds;         // 1: LDS-staged sweep; 0: every mover to k_sweep_dense (tests); 2: staging only (timing)
   const uint32_t* op_slot;    // for the leave path
   const uint8_t* op_kind;     // per op (null: all moves); OP_SILENT movers are applied, not walked

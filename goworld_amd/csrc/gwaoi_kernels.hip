@@ -1004,13 +1004,18 @@ struct SwCfg {
   static constexpr int kBlk = kB, kCap = kCapT, kCells = kCellsT, kRows = kRowsT, kWpe = kWpeT;
   static constexpr int kCellsPT = (kCells + kB - 1) / kB;  // region cells per thread (staging)
   static constexpr int kIters = (kCap + kB - 1) / kB;      // staged records per thread
-  static constexpr bool kBig = kB > 512;
+  static constexpr bool kBig = kB > 512 || kCapT > 1600;  // the big or the mid sweep (Geom.pad)
+  static constexpr bool kMid = kB == 512 && kCapT > 1600;  // the mid sweep (Geom.pad & kPadMid)
 };
 using SwSmall = SwCfg<kSweepBlock, GW_CAP, kSweepRegCells, kMaxRows, GW_SWEEP_WAVES_PER_EU>;
 #ifndef GW_BIG_CAP
 #define GW_BIG_CAP 2800
 #endif
 using SwBig = SwCfg<1024, GW_BIG_CAP, kSweepBigCells, kSweepBigRows, 4>;
+#ifndef GW_MID_CAP
+#define GW_MID_CAP 1850
+#endif
+using SwMid = SwCfg<512, GW_MID_CAP, kSweepMidCells, kSweepMidRows, 4>;
 constexpr float kInner = 3.814697265625e-06f;  // 2^-18: ring margin, relative to |c| + D
 
 template <class C>
@@ -1035,6 +1040,7 @@ using SweepSmem = SweepSmemT<SwSmall>;
 #endif
 static_assert(sizeof(SweepSmem) <= 163840 / GW_SWEEP_BLOCKS_PER_CU - 512, "sweep LDS budget per block");
 static_assert(sizeof(SweepSmemT<SwBig>) <= 163840 - 512, "big sweep: one block per CU");
+static_assert(sizeof(SweepSmemT<SwMid>) <= 163840 / 2 - 512, "mid sweep: two blocks per CU");
 
 size_t sweep_lds_bytes() { return sizeof(SweepSmem); }
 uint32_t sweep_block() { return kSweepBlock; }
@@ -1821,7 +1827,8 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmemT<C>& sm
   const Geom g = uniform_geom(&a.g.geom[sp]);
   // a Space takes the small sweep (reach), the big one (pad) or neither; a tile of the other kernel's
   // Space is left alone entirely (that kernel stores its events and counts)
-  if (C::kBig ? !(g.reach == 0 && g.pad > 0) : (g.reach == 0 && g.pad > 0 && a.use_lds)) return;
+  const bool mid = (g.pad & kPadMid) != 0;
+  if (C::kBig ? !(g.reach == 0 && g.pad > 0 && mid == C::kMid) : (g.reach == 0 && g.pad > 0 && a.use_lds)) return;
   if (a.tile_walk) {
     if (!a.tile_walk[t]) return no_events();  // block-uniform: no reported mover in the tile (k_bin_tsort)
   } else {
@@ -1830,7 +1837,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmemT<C>& sm
     for (uint32_t j = e0 + threadIdx.x; j < e1 && !mine; j += kSweepBlock) mine = is_walker(a, a.g.rec[j].a);
     if (!__syncthreads_or(mine)) return no_events();  // nothing queued: the caller's barrier follows
   }
-  const int reach = C::kBig ? (int)g.pad : g.reach;
+  const int reach = C::kBig ? (int)(g.pad & ~kPadMid) : g.reach;
   bool lds = a.use_lds && reach > 0;
   Region R;
   int tcx = 0, tcz = 0;
@@ -1943,7 +1950,7 @@ k_sweep(SweepArgs a) {
   SweepSmemT<C>& sm = *reinterpret_cast<SweepSmemT<C>*>(smem_raw);
   // one block per tile of [t0, t0 + n) (all tiles; the big sweep: the range of its Spaces' tiles), tiles
   // mapped XCD-aware by block index
-  const uint32_t t0 = C::kBig ? a.big_t0 : 0u, nt = C::kBig ? a.big_n : a.ntiles;
+  const uint32_t t0 = C::kMid ? a.mid_t0 : C::kBig ? a.big_t0 : 0u, nt = C::kMid ? a.mid_n : C::kBig ? a.big_n : a.ntiles;
   if (threadIdx.x == 0) {
     const uint32_t xcd = blockIdx.x % kXcds;
     const uint32_t per = nt / kXcds, rem = nt % kXcds;
@@ -1979,6 +1986,8 @@ void sweep_init() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SweepSmem));
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep<SwBig>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SweepSmemT<SwBig>));
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sweep<SwMid>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SweepSmemT<SwMid>));
 }
 
 // The event queue of the one-thread-per-op global walks (k_sweep_leaves): only the queue in LDS.
@@ -3143,6 +3152,8 @@ uint32_t sweep_ev_lds() { return kEvLds; }
 
 void launch_sweep(const SweepArgs& a, hipStream_t st) {
   if (a.ntiles) hipLaunchKernelGGL(k_sweep<SwSmall>, dim3(a.ntiles), dim3(kSweepBlock), sizeof(SweepSmem), st, a);
+  if (a.mid_n && a.use_lds)
+    hipLaunchKernelGGL(k_sweep<SwMid>, dim3(a.mid_n), dim3(SwMid::kBlk), sizeof(SweepSmemT<SwMid>), st, a);
   if (a.big_n && a.use_lds)
     hipLaunchKernelGGL(k_sweep<SwBig>, dim3(a.big_n), dim3(SwBig::kBlk), sizeof(SweepSmemT<SwBig>), st, a);
   if (a.leave_blocks)

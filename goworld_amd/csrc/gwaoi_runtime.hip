@@ -302,6 +302,10 @@ void space_extent(const SpaceHost& sh, float* x0, float* z0, float* x1, float* z
   *z1 = sh.seen_maxz + 0.125f * wz + D;
 }
 
+#ifndef GW_MID_PLAN
+#define GW_MID_PLAN 1550.0
+#endif
+constexpr double kMidPlanRecs = GW_MID_PLAN;  // the same for the mid sweep (GW_MID_CAP 1850 staged)
 constexpr double kBigPlanRecs = 2400.0;  // planned records of a big-sweep region at most (GW_BIG_CAP 2800 staged)
 constexpr double kCellOccupancy = 0.5;  // planned entities per cell (config 2: 1M in 35,000^2, cells of 25)
 #ifndef GW_TILE_MOVERS
@@ -404,7 +408,11 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
       const double area = ((double)x1 - x0) * ((double)z1 - z0);
       const double pop = sh.pop_hint ? (double)sh.pop_hint : (double)m->cap / std::max<uint32_t>(1, m->nspaces);
       const double per_cell = pop * c * c / std::max(1.0, area);
-      if (m->big_sweep && rw <= gw::kSweepBigRows && (double)(rw * rw) * per_cell <= kBigPlanRecs) g.pad = (uint32_t)reach;
+      // (the mid sweep first: two blocks per CU, when its smaller region and record budget hold)
+      if (m->big_sweep && rw <= gw::kSweepMidRows && (double)(rw * rw) * per_cell <= kMidPlanRecs)
+        g.pad = (uint32_t)reach | gw::kPadMid;
+      else if (m->big_sweep && rw <= gw::kSweepBigRows && (double)(rw * rw) * per_cell <= kBigPlanRecs)
+        g.pad = (uint32_t)reach;
       reach = 0;  // (the small LDS path off for this Space)
     }
     g.reach = reach;
@@ -1054,12 +1062,20 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     {  // the tiles of the big sweep's Spaces, as one range
       uint32_t b0 = ~0u, b1 = 0;
       for (const gw::Geom& sg : G.h_geom)
-        if (sg.reach == 0 && sg.pad > 0) {
+        if (sg.reach == 0 && sg.pad > 0 && !(sg.pad & gw::kPadMid)) {
           b0 = std::min(b0, sg.tile_base);
           b1 = std::max(b1, sg.tile_base + (uint32_t)(sg.ntx * sg.ntz));
         }
       s.big_t0 = b1 > b0 ? b0 : 0u;
       s.big_n = b1 > b0 ? b1 - b0 : 0u;
+      uint32_t m0 = ~0u, m1 = 0;  // and the mid sweep's
+      for (const gw::Geom& sg : G.h_geom)
+        if (sg.reach == 0 && (sg.pad & gw::kPadMid)) {
+          m0 = std::min(m0, sg.tile_base);
+          m1 = std::max(m1, sg.tile_base + (uint32_t)(sg.ntx * sg.ntz));
+        }
+      s.mid_t0 = m1 > m0 ? m0 : 0u;
+      s.mid_n = m1 > m0 ? m1 - m0 : 0u;
     }
     s.ncells = G.ncells;
     s.n_rec = dev_mixed ? n_start + n_ops : n_start + n_new;  // upper bound on records (main + ghost)
