@@ -716,7 +716,7 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
             "band_movers_per_tick": st["band_movers"] / ticks,
             "avg_launch_ms": sweep_ms,
             "kernels_timed": "k_sweep" +
-                             (" + k_sweep<SwBig>" if args.workload in ("skew", "skew50") else "") +
+                             (" + k_sweep<SwMid> + k_sweep<SwBig>" if args.workload in ("skew", "skew50") else "") +
                              (" + k_band_sort + k_sweep_band" if st["band_movers"] else "") +
                              (" + k_sweep_dense" if st["dense_movers"] else "") +
                              " (the pass's sweep stage, hipEvents on the manager's stream)",

@@ -27,10 +27,12 @@ for f in sorted(glob.glob(prefix + "*/run_counter_collection.csv")):
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
         name = name.replace("void ", "").replace("gw::", "").strip()
         # the LDS sweep's two sizes and the ring walk's two lists under stable names
-        if name.startswith("k_sweep<SwCfg<1024"):
-            name = "k_sweep_big"
-        elif name.startswith("k_sweep<SwCfg<"):
-            name = "k_sweep"
+        if name.startswith("k_sweep<SwCfg<"):
+            # SwCfg<threads, record cap, ...>: the small sweep (512, cap <= 1600), the mid one (512, more) and the
+            # big one (1024)
+            args = [x.strip() for x in name[len("k_sweep<SwCfg<"):].split(",")]
+            blk, cap = int(args[0]), int(args[1])
+            name = "k_sweep_big" if blk > 512 else ("k_sweep_mid" if cap > 1600 else "k_sweep")
         elif name.startswith("k_sweep_dense<"):
             name = "k_sweep_dense"
         elif name.startswith("k_sweep_band<"):
@@ -70,7 +72,7 @@ for k, cs in vals.items():
         e["wait_any_frac"] = d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]
     kern[k] = e
 # the workload's roofline kernel(s), as bench.py times them (the pass's sweep stage)
-dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_big", "k_band_sort", "k_sweep_band", "k_sweep_dense"])
+dominant = {"gametick": ["k_fan_dwrite", "k_fan_tile<true>"]}.get(workload, ["k_sweep", "k_sweep_mid", "k_sweep_big", "k_band_sort", "k_sweep_band", "k_sweep_dense"])
 # (only kernels that ran (nearly) every tick of the passes, >= 3/4 of k_sweep's dispatches: a band walk launched once
 # in a config-2 run, for the bulk Enter pass, is not the tick's)
 per_tick = kern.get("k_sweep", {}).get("dispatches", 0)
