@@ -484,25 +484,36 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
     if HS:
         pin_s, pin_x, pin_z = eng.stage_buffers()
         pin_s[:n] = slots_h
+    # The headline ticks stage with gwaoi_stage_moves_pinned_async (ABI 2.1: the DMA copy, the device checks
+    # and the pipeline enqueued back to back, the checks' verdict read by the pass); then `syncpin` ticks
+    # with the synchronous gwaoi_stage_moves_pinned (its verdict read back before the pipeline starts) and
+    # `copyin` ticks with the copy-in gwaoi_stage_moves (host validation), for comparison.
+    async_ok = hasattr(L_, "gwaoi_stage_moves_pinned_async") and args.pin_mode == "async"
     copyin = min(10, HS // 2)
-    stage_ci = []
-    for i in range(HS + copyin):
-        use_pin = i < HS
+    syncpin = min(100, HS // 2) if async_ok else 0
+    stage_ci, lat_sp, stage_sp = [], [], []
+    for i in range(HS + syncpin + copyin):
+        use_pin = i < HS + syncpin
         dx, dz = (pin_x, pin_z) if use_pin else (xh, zh)
         bx, bz = walk_next()  # untimed: the tick's positions into the host arrays
         _lib.check(L_.gwaoi_dev_dtoh(dev, dx.ctypes.data, ctypes.c_void_p(bx), 4 * n))
         _lib.check(L_.gwaoi_dev_dtoh(dev, dz.ctypes.data, ctypes.c_void_p(bz), 4 * n))
         ts = time.perf_counter()
-        if use_pin:
+        if use_pin and async_ok and i < HS:
+            eng.stage_moves_pinned_async(n)
+        elif use_pin:
             eng.stage_moves_pinned(n)
         else:
             eng.stage_moves(slots_h, xh, zh)
         t1 = time.perf_counter()
         ev = eng.tick_raw()
         te = time.perf_counter()
-        if use_pin:
+        if i < HS:
             lat_hs.append(te - ts)
             stage_hs.append(t1 - ts)
+        elif use_pin:
+            lat_sp.append(te - ts)
+            stage_sp.append(t1 - ts)
         else:
             stage_ci.append(t1 - ts)
         if rs is not None and ev.count:
@@ -523,6 +534,26 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         rs.close()
     if rss is not None:
         rss.close()
+
+    # ---- positions arriving over the tick (GameService.go:398-410: one position packet at a time): the tick's
+    # Moved calls written into the pinned arrays in `chunks` parts, each part pushed when it has arrived
+    # (gwaoi_stage_moves_pinned_partial, asynchronous DMA) and the arrivals spread over more time than the
+    # pushes take (the device synchronised, untimed); timed: the Flush, i.e. the async staging of the whole
+    # batch (only the last part still to copy) + gwaoi_tick, to the events in pinned host memory ----
+    lat_ck = []
+    CK = args.chunked_ticks if (HS and async_ok and hasattr(L_, "gwaoi_stage_moves_pinned_partial")) else 0
+    nchunks = max(1, args.chunks)
+    for i in range(CK):
+        bx, bz = walk_next()
+        _lib.check(L_.gwaoi_dev_dtoh(dev, pin_x.ctypes.data, ctypes.c_void_p(bx), 4 * n))
+        _lib.check(L_.gwaoi_dev_dtoh(dev, pin_z.ctypes.data, ctypes.c_void_p(bz), 4 * n))
+        for c in range(1, nchunks):
+            eng.stage_moves_pinned_partial(n * c // nchunks)
+        _lib.check(L_.gwaoi_dev_sync(dev))
+        ts = time.perf_counter()
+        eng.stage_moves_pinned_async(n)
+        eng.tick_raw()
+        lat_ck.append(time.perf_counter() - ts)
 
     # ---- device-resident p50/p99 (p99_tick_ms_device): a fixed loop of P ticks (events left in HBM),
     # independent of --steps ----
@@ -663,6 +694,20 @@ def run_spaces(args, rank, world, dev, sync_all, allmax):
         "p50_tick_ms_host_events": percentile(lat_host, 50) * 1e3 if lat_host else None,
         "p99_tick_ms_host_events": percentile(lat_host, 99) * 1e3 if lat_host else None,
         "host_stage_ms": percentile(stage_hs, 50) * 1e3 if stage_hs else None,
+        "host_staging_call": ("gwaoi_stage_moves_pinned_async" if async_ok else "gwaoi_stage_moves_pinned") if lat_hs else None,
+        "p50_tick_ms_sync_staging": percentile(lat_sp, 50) * 1e3 if lat_sp else None,
+        "p99_tick_ms_sync_staging": percentile(lat_sp, 99) * 1e3 if lat_sp else None,
+        "host_stage_ms_sync_staging": percentile(stage_sp, 50) * 1e3 if stage_sp else None,
+        "sync_staging_note": (f"{len(lat_sp)} host-staged ticks with the synchronous gwaoi_stage_moves_pinned (the "
+                              "device check's verdict read back before the pipeline is launched), after the headline "
+                              "ticks") if lat_sp else None,
+        "p50_flush_ms_chunked": percentile(lat_ck, 50) * 1e3 if lat_ck else None,
+        "p99_flush_ms_chunked": percentile(lat_ck, 99) * 1e3 if lat_ck else None,
+        "chunked_note": (f"positions arriving over the tick: {len(lat_ck)} ticks, each batch written into the pinned "
+                         f"arrays in {nchunks} parts pushed as they arrive (gwaoi_stage_moves_pinned_partial, "
+                         "asynchronous DMA; arrivals slower than the pushes: the device synchronised, untimed); "
+                         "timed from the Flush (gwaoi_stage_moves_pinned_async of the whole batch, only the last "
+                         "part left to copy, + gwaoi_tick) to the events in pinned host memory") if lat_ck else None,
         "host_stage_copyin_ms": percentile(stage_ci, 50) * 1e3 if stage_ci else None,
         "replay_ms": percentile(replay_s, 50) * 1e3 if replay_s else None,
         "replay_ms_sharded": percentile(replay_sh_s, 50) * 1e3 if replay_sh_s else None,
@@ -1200,6 +1245,11 @@ def main():
                     help="extra ticks staged from host arrays (gwaoi_stage_moves), events to host, replayed")
     ap.add_argument("--no-replay", dest="replay", action="store_false",
                     help="skip the C replay of events into per-entity hash sets")
+    ap.add_argument("--pin-mode", choices=["async", "sync"], default="async",
+                    help="host-staged headline ticks: gwaoi_stage_moves_pinned_async (ABI 2.1) or the sync call")
+    ap.add_argument("--chunked-ticks", type=int, default=300,
+                    help="ticks of the chunked-arrival leg (p99_flush_ms_chunked); 0 = off")
+    ap.add_argument("--chunks", type=int, default=16, help="parts of the chunked-arrival leg's batch")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cells-per-dist", type=float, default=None)

@@ -28,12 +28,13 @@ GWAOI_OP_MOVE, GWAOI_OP_ENTER, GWAOI_OP_LEAVE, GWAOI_OP_SILENT = 0, 1, 2, 0x80
 ABI_SYMBOLS = (
     "gwaoi_create", "gwaoi_create_spaces", "gwaoi_destroy", "gwaoi_set_stream", "gwaoi_enter",
     "gwaoi_enter_space", "gwaoi_stage_enters", "gwaoi_leave", "gwaoi_moved", "gwaoi_stage_moves", "gwaoi_stage_moves_device",
-    "gwaoi_stage_buffers", "gwaoi_stage_moves_pinned",
-    "gwaoi_stage_ops_device",
+    "gwaoi_stage_buffers", "gwaoi_stage_moves_pinned", "gwaoi_stage_moves_pinned_partial",
+    "gwaoi_stage_moves_pinned_async", "gwaoi_stage_ops_device",
     "gwaoi_stage_ops_device_spaces",
     "gwaoi_stage_ops_device_n", "gwaoi_adopt_device_state", "gwaoi_set_population_hint",
     "gwaoi_tick", "gwaoi_tick_ex", "gwaoi_count", "gwaoi_export_relation", "gwaoi_export_relation_delta", "gwaoi_relation_device", "gwaoi_set_timing",
     "gwaoi_get_stats", "gwaoi_reset_stats", "gwaoi_version", "gwaoi_last_error", "gwaoi_abi_version",
+    "gwaoi_abi_minor",
 )
 TOOL_SYMBOLS = (
     "gwaoi_device_count", "gwaoi_dev_malloc", "gwaoi_dev_free", "gwaoi_dev_htod", "gwaoi_dev_dtoh",
@@ -43,7 +44,7 @@ TOOL_SYMBOLS = (
     "gwaoi_debug_read_stamps",
     "gwaoi_debug_sweep_occupancy", "gwaoi_wl_pack_ingest", "gwaoi_debug_set_index_limit",
     "gwaoi_debug_set_relation_mode", "gwaoi_debug_set_build_mode", "gwaoi_debug_set_small_pass", "gwaoi_debug_set_fanout_mode",
-    "gwaoi_debug_set_band",
+    "gwaoi_debug_set_band", "gwaoi_debug_sweep_sizes",
 )
 
 
@@ -159,6 +160,8 @@ class Stats(ctypes.Structure):
 _lib = None
 
 
+# ABI 2.1 additions (include/gwaoi.h GWAOI_ABI_MINOR): optional when an older build is loaded for an A/B
+ABI_MINOR_SYMBOLS = ("gwaoi_stage_moves_pinned_partial", "gwaoi_stage_moves_pinned_async", "gwaoi_abi_minor")
 ABI_VERSION = 2  # GWAOI_ABI_VERSION of include/gwaoi.h that these ctypes structs and signatures follow
 
 
@@ -193,6 +196,8 @@ def load(path: str = SO_PATH):
         "gwaoi_stage_buffers": ([vp, ctypes.POINTER(u32p), ctypes.POINTER(f32p), ctypes.POINTER(f32p),
                                  ctypes.POINTER(u32)], ctypes.c_int),
         "gwaoi_stage_moves_pinned": ([vp, u32], ctypes.c_int),
+        "gwaoi_stage_moves_pinned_partial": ([vp, u32], ctypes.c_int),
+        "gwaoi_stage_moves_pinned_async": ([vp, u32], ctypes.c_int),
         "gwaoi_stage_ops_device": ([vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_stage_ops_device_spaces": ([vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
         "gwaoi_stage_ops_device_n": ([vp, vp, vp, vp, vp, vp, vp, u32], ctypes.c_int),
@@ -209,6 +214,7 @@ def load(path: str = SO_PATH):
         "gwaoi_export_relation_delta": ([vp, vp, u64, ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_version": ([], ctypes.c_char_p),
         "gwaoi_abi_version": ([], ctypes.c_int),
+        "gwaoi_abi_minor": ([], ctypes.c_int),
         "gwaoi_last_error": ([], ctypes.c_char_p),
         "gwaoi_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "gwaoi_dev_malloc": ([ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(vp)], ctypes.c_int),
@@ -234,6 +240,7 @@ def load(path: str = SO_PATH):
         "gwaoi_debug_set_small_pass": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_debug_set_fanout_mode": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_debug_set_band": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
+        "gwaoi_debug_sweep_sizes": ([vp, ctypes.c_int, ctypes.POINTER(u64)], ctypes.c_int),
         "gwaoi_strip_init_walk": ([vp, vp, vp, vp, vp, u64, f32], ctypes.c_int),
         "gwaoi_strip_walk": ([vp, vp, vp, vp, vp, vp, vp, u64, u64, f32, f32, vp], ctypes.c_int),
         "gwaoi_strip_ingest": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),
@@ -266,8 +273,8 @@ def load(path: str = SO_PATH):
                                         ctypes.c_int),
     }
     for name, (args, res) in sig.items():
-        if name in TOOL_SYMBOLS and not hasattr(L, name):
-            continue  # a debug tool newer than this build (A/B runs of older libraries)
+        if (name in TOOL_SYMBOLS or name in ABI_MINOR_SYMBOLS) and not hasattr(L, name):
+            continue  # a debug tool or ABI 2.1 call newer than this build (A/B runs of older libraries)
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

@@ -60,6 +60,14 @@ constexpr int kSweepBigCells = kSweepBigRows * kSweepBigRows;
 #endif
 constexpr int kSweepMidRows = GW_MID_ROWS;
 constexpr int kSweepMidCells = kSweepMidRows * kSweepMidRows;
+// records the mid and big sweeps stage at most (the planner keeps a region's planned population below them)
+#ifndef GW_BIG_CAP
+#define GW_BIG_CAP 2800
+#endif
+#ifndef GW_MID_CAP
+#define GW_MID_CAP 1850
+#endif
+constexpr int kSweepBigCap = GW_BIG_CAP, kSweepMidCap = GW_MID_CAP;
 constexpr uint32_t kPadMid = 0x80000000u;  // Geom.pad: the Space takes the mid sweep (the halo in the low bits)
 
 // Cell geometry of one Space inside one grid snapshot.
@@ -235,6 +243,7 @@ struct SweepArgs {
   const float* band_zk;   // per cell by z key: the key, and
   const uint32_t* band_zi;  // the record
   const uint32_t* band_hd;
+  uint32_t* size_tiles;  // debug (gwaoi_debug_sweep_sizes): tiles walked in LDS by the small / mid / big sweep, or null
 };
 
 // Band keys of the pass's grid for k_sweep_dense's band walk. A record's judge position p is
@@ -462,6 +471,10 @@ struct PinCheckArgs {
   uint32_t* out;               // [0] error bits, [1] first repeat (n: none), [2] first bad op, [3] beyond ext
 };
 void launch_pin_check(const PinCheckArgs& a, bool reset_seen, uint32_t nspaces, hipStream_t st);
+// the verdict of a pin check kept on the device (gwaoi_stage_moves_pinned_async): *n_dev = the op count of
+// the sub-pass [seg, cut) (0 for a refused batch), the four out words copied into mapped host memory
+void launch_pin_count(const uint32_t* out, uint32_t n, uint32_t seg, int validate, uint32_t* n_dev,
+                      uint32_t* host_out, hipStream_t st);
 float ord_float(uint32_t k);
 
 // ---- manager view for the callers either side of the path (gwaoi_sync.hip) ----

@@ -206,6 +206,7 @@ struct gwaoi_mgr {
   uint32_t* band_dense2 = nullptr;  // [cap] the dense movers the band walk leaves to the ring walk
   uint64_t band_cap = 0;         // records the arrays hold (0: not allocated)
   uint64_t band_builds = 0, band_movers = 0;
+  uint32_t* d_size_tiles = nullptr;  // [3] gwaoi_debug_sweep_sizes (null: not counted)
   uint32_t* tile_ev = nullptr;   // per tile: events k_sweep queued in the tile's region of ev_tmp
   uint32_t* tile_ent = nullptr;  // per tile: their enter events
   uint32_t nblk = 0;
@@ -260,6 +261,16 @@ struct gwaoi_mgr {
   float4* d_pin_ext = nullptr;     // [nspaces]
   float4* h_pin_ext = nullptr;
   bool pin_seen_dirty = true;
+  // incremental push (gwaoi_stage_moves_pinned_partial): entries [0, pin_pushed) are on the device already
+  uint32_t pin_pushed = 0;
+  // deferred verdict (gwaoi_stage_moves_pinned_async): the batch waits in dv_* as a device-counted batch
+  // whose count k_pin_count writes (0 when refused); run_pass reads the verdict after the pass
+  bool pin_pending = false;
+  bool pin_validated = false;        // the pending sub-pass's check validated the batch (its first)
+  uint32_t pin_n = 0;                // the batch's size
+  uint32_t* d_pin_n = nullptr;       // the sub-pass's op count (device)
+  uint32_t* h_pin_v = nullptr;       // the check's four words, mapped coherent host memory
+  uint32_t* d_pin_v = nullptr;       // its device alias
 
   // relation delta export (gwaoi_export_relation_delta): the last tick's events are still in ev_out
   bool dx_ready = false;         // set by gwaoi_tick, cleared when the next accumulation opens
@@ -307,6 +318,8 @@ void space_extent(const SpaceHost& sh, float* x0, float* z0, float* x1, float* z
 #endif
 constexpr double kMidPlanRecs = GW_MID_PLAN;  // the same for the mid sweep (GW_MID_CAP 1850 staged)
 constexpr double kBigPlanRecs = 2400.0;  // planned records of a big-sweep region at most (GW_BIG_CAP 2800 staged)
+static_assert(kMidPlanRecs < gw::kSweepMidCap && kBigPlanRecs < gw::kSweepBigCap,
+              "a region's planned records must stay below what its sweep stages (else every tile overflows)");
 constexpr double kCellOccupancy = 0.5;  // planned entities per cell (config 2: 1M in 35,000^2, cells of 25)
 #ifndef GW_TILE_MOVERS
 #define GW_TILE_MOVERS 440.0
@@ -399,7 +412,10 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
     const double maxc = std::max({std::fabs((double)x0), std::fabs((double)x1), std::fabs((double)z0),
                                   std::fabs((double)z1)});
     const double span = ((double)sh.desc.dist * (1.0 + 1e-5) + (maxc + sh.desc.dist) * 1e-6) / c;
-    int reach = (int)std::ceil(span) + 1;
+#ifndef GW_REACH_STEP  // A/B: halo cells beyond the box span (movers whose boxes leave the region go global)
+#define GW_REACH_STEP 1.0
+#endif
+    int reach = (int)std::ceil(span + GW_REACH_STEP);
     g.pad = 0;
     const int rw = gw::kTile + 2 * reach;  // region width (cells)
     if (rw * rw > gw::kSweepRegCells) {  // the small LDS sweep's region budget: not this Space
@@ -513,7 +529,9 @@ int build_band_keys(gwaoi_mgr* m, int gi, uint32_t bound, bool* built) {
   b.g = {G.rec, G.cs, G.d_geom, G.d_tile_space};
   b.space_of = m->space_of;
   b.nspaces = m->nspaces;
-  b.rec_bound = (uint32_t)std::min<uint64_t>(bound, m->band_cap);
+  // every record of the grid (the grid holds at most 2 cap records, main + ghost): the records are swapped
+  // in below, so a bound below the grid's real count would publish a half-copied grid
+  b.rec_bound = (uint32_t)m->band_cap;
   b.nrec = G.cs + G.ncells;
   // the records sorted by x key inside their cells go into the other grid's record buffer (this pass does
   // not read it: it was the build's bucket buffer), which then becomes this grid's
@@ -947,10 +965,11 @@ int ensure_grid_current(gwaoi_mgr* m) {
 
 // Run the device pipeline over the staged batch (host ops or the device batch). Events accumulate
 // (device buffer always, host buffer when copy_events) until the next gwaoi_tick returns them.
-int run_pass(gwaoi_mgr* m, bool copy_events) {
+int run_pass_core(gwaoi_mgr* m, bool copy_events) {
   const bool dev = m->dv_n != 0;
   const uint32_t n_ops = dev ? m->dv_n : m->n_ops;
   if (!n_ops) return GWAOI_OK;
+  if (!dev) m->pin_pushed = 0;  // host ops are copied into (or their slots and kinds written to) d_op_*
   if (!m->acc_open) {
     reset_tick(m);
     m->acc_open = true;
@@ -1118,6 +1137,7 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
     s.band_zk = keys ? m->band_zk : nullptr;
     s.band_zi = keys ? m->band_zi : nullptr;
     s.band_hd = keys ? m->band_hd : nullptr;
+    s.size_tiles = m->d_size_tiles;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
@@ -1229,6 +1249,8 @@ int run_pass(gwaoi_mgr* m, bool copy_events) {
   return GWAOI_OK;
 }
 
+int run_pass(gwaoi_mgr* m, bool copy_events);  // run_pass_core + the verdict of an async pinned batch
+
 // Non-finite coordinates are refused (GWAOI_ERR_INVALID). go-aoi accepts them, and a NaN node in its
 // sorted lists stops every Mark walk that reaches it, so third parties lose neighbours (the list
 // restatement in the test suite reproduces that); that behaviour depends on list position, not
@@ -1290,6 +1312,124 @@ void note_coord(gwaoi_mgr* m, uint32_t space, float x, float z) {
   if (x < sh.gx0 || x > sh.gx1 || z < sh.gz0 || z > sh.gz1) m->geom_dirty = true;
 }
 
+// ---- pinned staging: DMA, device checks, and the deferred verdict of the async path ----------------------
+// entries [from, to) of the pinned arrays into the op arrays (asynchronous, on the manager's stream)
+int pin_copy(gwaoi_mgr* m, uint32_t from, uint32_t to) {
+  if (to <= from) return GWAOI_OK;
+  const size_t k = to - from;
+  hipStream_t st = m->stream;
+  HIPCHK(hipMemcpyAsync(m->d_op_slot + from, m->h_pin_slot + from, k * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(m->d_op_x + from, m->h_pin_x + from, k * sizeof(float), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(m->d_op_z + from, m->h_pin_z + from, k * sizeof(float), hipMemcpyHostToDevice, st));
+  return GWAOI_OK;
+}
+
+bool pin_any_auto(const gwaoi_mgr* m) {
+  for (const SpaceHost& sh : m->spaces)
+    if (sh.auto_extent) return true;
+  return false;
+}
+
+// k_pin_check / k_pin_cut over ops [seg, n) of the batch in d_op_* (validate: the batch's first check, over
+// all of it); with `count`, k_pin_count keeps the verdict on the device (the async path)
+int pin_launch(gwaoi_mgr* m, uint32_t n, uint32_t seg, int validate, bool count) {
+  hipStream_t st = m->stream;
+  const bool any_auto = pin_any_auto(m);
+  if (any_auto && validate) {  // the extent each auto-extent Space's grid covers (beyond it: reported)
+    const float inf = std::numeric_limits<float>::infinity();
+    for (uint32_t sp = 0; sp < m->nspaces; ++sp) {
+      const SpaceHost& sh = m->spaces[sp];
+      m->h_pin_ext[sp] = sh.auto_extent ? (sh.seen_any ? make_float4(sh.gx0, sh.gz0, sh.gx1, sh.gz1)
+                                                       : make_float4(inf, inf, -inf, -inf))  // nothing seen yet
+                                        : make_float4(-inf, -inf, inf, inf);
+    }
+    HIPCHK(hipMemcpyAsync(m->d_pin_ext, m->h_pin_ext, m->nspaces * sizeof(float4), hipMemcpyHostToDevice, st));
+  }
+  if (++m->pin_id == 0) {  // ids wrapped: forget every stored id
+    HIPCHK(hipMemsetAsync(m->d_pin_first, 0, (size_t)m->cap * sizeof(unsigned long long), st));
+    m->pin_id = 1;
+  }
+  gw::PinCheckArgs a{};
+  a.slot = m->d_op_slot;
+  a.x = m->d_op_x;
+  a.z = m->d_op_z;
+  a.n = n;
+  a.seg = seg;
+  a.cap = m->cap;
+  a.seq = m->seq;
+  a.space_of = m->space_of;
+  a.first = m->d_pin_first;
+  a.ext = any_auto && validate ? m->d_pin_ext : nullptr;
+  a.seen = m->d_pin_seen;
+  a.out = m->d_pin_out;
+  a.id = m->pin_id;
+  a.validate = validate;
+  gw::launch_pin_check(a, validate && a.ext && m->pin_seen_dirty, m->nspaces, st);
+  if (count) gw::launch_pin_count(m->d_pin_out, n, seg, validate, m->d_pin_n, m->d_pin_v, st);
+  HIPCHK(hipGetLastError());
+  return GWAOI_OK;
+}
+
+// the check's report of coordinates beyond an auto-extent Space's grid: widen what the Space has seen
+int pin_note_extent(gwaoi_mgr* m, uint32_t beyond) {
+  m->pin_seen_dirty = beyond != 0;
+  if (!beyond) return GWAOI_OK;
+  uint32_t* k = m->h_pin_out + 4;
+  HIPCHK(hipMemcpyAsync(k, m->d_pin_seen, 4 * sizeof(uint32_t) * m->nspaces, hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  for (uint32_t sp = 0; sp < m->nspaces; ++sp) {
+    if (!m->spaces[sp].auto_extent || k[4 * sp] > k[4 * sp + 2]) continue;  // none beyond
+    note_coord(m, sp, gw::ord_float(k[4 * sp]), gw::ord_float(k[4 * sp + 1]));
+    note_coord(m, sp, gw::ord_float(k[4 * sp + 2]), gw::ord_float(k[4 * sp + 3]));
+  }
+  return GWAOI_OK;
+}
+
+int pin_refused(const uint32_t* o) {
+  set_err("stage_moves_pinned: entry %u refused (flags 0x%x: 2=slot not in a Space, 4=slot >= capacity, "
+          "64=non-finite coordinate); nothing staged",
+          o[2], o[0]);
+  return (o[0] & (gw::ERR_BAD_SLOT | gw::ERR_BAD_COORD)) ? GWAOI_ERR_INVALID : GWAOI_ERR_STATE;
+}
+
+// The pipeline pass, plus the deferred verdict of an async pinned batch: the pass ran as a device-counted
+// batch of the sub-pass's ops (none when the check refused the batch); after its end-of-pass sync the check's
+// words are in mapped host memory: a refusal is reported now (nothing of the batch was applied), coordinates
+// beyond an auto-extent Space widen its extent for the next pass (clamped cells keep this one exact), and a
+// repeated slot starts the next sub-pass at the repeat (checked again from there), as the sync path does.
+int run_pass(gwaoi_mgr* m, bool copy_events) {
+  if (!m->pin_pending) return run_pass_core(m, copy_events);
+  for (;;) {
+    const int r = run_pass_core(m, copy_events);
+    if (r) {
+      m->pin_pending = false;
+      return r;
+    }
+    uint32_t o[4];
+    std::memcpy(o, (const void*)m->h_pin_v, sizeof(o));
+    if (m->pin_validated) {
+      if (o[0]) {
+        m->pin_pending = false;
+        return pin_refused(o);
+      }
+      RCHK(pin_note_extent(m, o[3]));
+      m->pin_validated = false;
+    }
+    const uint32_t n = m->pin_n, cut = std::min(o[1], n);
+    if (cut >= n) {
+      m->pin_pending = false;
+      return GWAOI_OK;
+    }
+    // op `cut` repeats a slot of the sub-pass that ran: the rest of the batch from there
+    RCHK(pin_launch(m, n, cut, 0, true));
+    m->dv_slot = m->d_op_slot + cut;
+    m->dv_x = m->d_op_x + cut;
+    m->dv_z = m->d_op_z + cut;
+    m->dv_count = m->d_pin_n;
+    m->dv_n = n - cut;
+  }
+}
+
 void stage(gwaoi_mgr* m, uint32_t slot, uint8_t kind, float x, float z, uint32_t space) {
   const uint32_t i = m->n_ops++;
   m->h_op_slot[i] = slot;
@@ -1311,7 +1451,7 @@ void free_all(gwaoi_mgr* m) {
                    m->d_op_kind, m->rank_cnt, m->uns, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
                    m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_xk, m->band_zi, m->band_hd, m->band_dense2, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
-                   m->d_pin_seen, m->d_pin_ext, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
+                   m->d_pin_seen, m->d_pin_ext, m->d_pin_n, m->d_size_tiles, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
                    m->dx_part, m->dx_out};
   for (void* p : dptrs)
     if (p) hipFree(p);
@@ -1322,7 +1462,7 @@ void free_all(gwaoi_mgr* m) {
       if (p) hipFree(p);
   }
   void* hptrs[] = {m->h_op_slot, m->h_op_x, m->h_op_z, m->h_op_kind, m->h_op_space, m->h_leaves, m->h_ctr,
-                   m->h_ev, m->h_pub, m->h_pin_slot, m->h_pin_x, m->h_pin_z, m->h_pin_out, m->h_pin_ext};
+                   m->h_ev, m->h_pub, m->h_pin_slot, m->h_pin_x, m->h_pin_z, m->h_pin_out, m->h_pin_ext, m->h_pin_v};
   for (void* p : hptrs)
     if (p) hipHostFree(p);
   for (auto& e : m->tev)
@@ -1517,6 +1657,20 @@ int create_impl(const gwaoi_space_desc* spaces, uint32_t nspaces, uint32_t capac
   return GWAOI_OK;
 }
 
+int pin_args_ok(gwaoi_mgr* m, uint32_t n, const char* what) {
+  RCHK(check_mgr(m));
+  RCHK(host_staging_ok(m));
+  if (!m->h_pin_slot) {
+    set_err("%s: no staging buffers (call gwaoi_stage_buffers first)", what);
+    return GWAOI_ERR_STATE;
+  }
+  if (n > m->cap) {
+    set_err("%s: %u moves > capacity %u", what, n, m->cap);
+    return GWAOI_ERR_INVALID;
+  }
+  return set_dev(m);
+}
+
 }  // namespace
 
 // ================================================================================================
@@ -1591,6 +1745,7 @@ extern "C" {
 // the source stamp (goworld_amd/build.py source_hash) ties measurements to the build they came from
 const char* gwaoi_version(void) { return "gwaoi 0.4.0 (gfx950, abi 2) src " GWAOI_SRC_HASH; }
 int gwaoi_abi_version(void) { return GWAOI_ABI_VERSION; }
+int gwaoi_abi_minor(void) { return GWAOI_ABI_MINOR; }
 const char* gwaoi_last_error(void) { return g_err.c_str(); }
 
 int gwaoi_create(float dist, uint32_t capacity, int device, gwaoi_mgr** out) {
@@ -1785,10 +1940,24 @@ int gwaoi_stage_buffers(gwaoi_mgr* m, uint32_t** slots, float** x, float** z, ui
     if (!r) r = dalloc(&m->d_pin_out, 4);
     if (!r) r = dalloc(&m->d_pin_seen, 4 * (size_t)ns);
     if (!r) r = dalloc(&m->d_pin_ext, ns);
+    if (!r) r = dalloc(&m->d_pin_n, 1);
     if (r) return r;  // freed with the manager
+    // the async path's verdict words: mapped coherent host memory written by k_pin_count (without it,
+    // gwaoi_stage_moves_pinned_async takes the synchronous path)
+    void* dp = nullptr;
+    if (hipHostMalloc((void**)&m->h_pin_v, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) ==
+            hipSuccess &&
+        hipHostGetDevicePointer(&dp, m->h_pin_v, 0) == hipSuccess) {
+      m->d_pin_v = (uint32_t*)dp;
+    } else {
+      (void)hipGetLastError();
+      if (m->h_pin_v) (void)hipHostFree(m->h_pin_v);
+      m->h_pin_v = nullptr;
+    }
     HIPCHK(hipMemsetAsync(m->d_pin_first, 0, (size_t)m->cap * sizeof(unsigned long long), m->stream));
     m->pin_id = 0;
     m->pin_seen_dirty = true;
+    m->pin_pushed = 0;
   }
   *slots = m->h_pin_slot;
   *x = m->h_pin_x;
@@ -1797,84 +1966,41 @@ int gwaoi_stage_buffers(gwaoi_mgr* m, uint32_t** slots, float** x, float** z, ui
   return GWAOI_OK;
 }
 
-// The Moved batch in the pinned buffers: one DMA copy, then k_pin_check validates it on the GPU and
-// finds the first repeated slot; nothing changes unless the whole batch is acceptable. Runs of the
-// batch without a repeat are staged as device batches (all but the last run as sub-passes now).
-int gwaoi_stage_moves_pinned(gwaoi_mgr* m, uint32_t n) {
-  RCHK(check_mgr(m));
-  RCHK(host_staging_ok(m));
-  if (!m->h_pin_slot) {
-    set_err("stage_moves_pinned: no staging buffers (call gwaoi_stage_buffers first)");
-    return GWAOI_ERR_STATE;
-  }
-  if (n > m->cap) {
-    set_err("stage_moves_pinned: %u moves > capacity %u", n, m->cap);
+// Incremental push: entries [pushed, upto) to the device now (asynchronous DMA), so the final call copies
+// only the tail. Ops staged earlier run first, as they would at the final call (a pass of host ops would
+// overwrite the device copy of what was pushed: pin_pushed restarts then).
+int gwaoi_stage_moves_pinned_partial(gwaoi_mgr* m, uint32_t upto) {
+  RCHK(pin_args_ok(m, upto, "stage_moves_pinned_partial"));
+  if (m->n_ops || m->dv_n) RCHK(run_pass(m, true));
+  if (upto < m->pin_pushed) {
+    set_err("stage_moves_pinned_partial: %u entries < the %u already pushed", upto, m->pin_pushed);
     return GWAOI_ERR_INVALID;
   }
-  if (!n) return GWAOI_OK;
-  RCHK(set_dev(m));
+  RCHK(pin_copy(m, m->pin_pushed, upto));
+  m->pin_pushed = upto;
+  return GWAOI_OK;
+}
+
+// The Moved batch in the pinned buffers: one DMA copy (of what was not pushed yet), then k_pin_check
+// validates it on the GPU and finds the first repeated slot; nothing changes unless the whole batch is
+// acceptable. Runs of the batch without a repeat are staged as device batches (all but the last run as
+// sub-passes now).
+int gwaoi_stage_moves_pinned(gwaoi_mgr* m, uint32_t n) {
+  RCHK(pin_args_ok(m, n, "stage_moves_pinned"));
   if (m->n_ops || m->dv_n) RCHK(run_pass(m, true));  // ops staged earlier come first
+  const uint32_t pushed = std::min(m->pin_pushed, n);
+  m->pin_pushed = 0;
+  if (!n) return GWAOI_OK;
   hipStream_t st = m->stream;
-  HIPCHK(hipMemcpyAsync(m->d_op_slot, m->h_pin_slot, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(m->d_op_x, m->h_pin_x, (size_t)n * sizeof(float), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(m->d_op_z, m->h_pin_z, (size_t)n * sizeof(float), hipMemcpyHostToDevice, st));
-  bool any_auto = false;
-  for (const SpaceHost& sh : m->spaces) any_auto |= sh.auto_extent;
-  if (any_auto) {  // the extent each auto-extent Space's grid covers (beyond it: reported, geometry redone)
-    const float inf = std::numeric_limits<float>::infinity();
-    for (uint32_t sp = 0; sp < m->nspaces; ++sp) {
-      const SpaceHost& sh = m->spaces[sp];
-      m->h_pin_ext[sp] = sh.auto_extent ? (sh.seen_any ? make_float4(sh.gx0, sh.gz0, sh.gx1, sh.gz1)
-                                                       : make_float4(inf, inf, -inf, -inf))  // nothing seen yet
-                                        : make_float4(-inf, -inf, inf, inf);
-    }
-    HIPCHK(hipMemcpyAsync(m->d_pin_ext, m->h_pin_ext, m->nspaces * sizeof(float4), hipMemcpyHostToDevice, st));
-  }
-  gw::PinCheckArgs a{};
-  a.slot = m->d_op_slot;
-  a.x = m->d_op_x;
-  a.z = m->d_op_z;
-  a.n = n;
-  a.cap = m->cap;
-  a.seq = m->seq;
-  a.space_of = m->space_of;
-  a.first = m->d_pin_first;
-  a.ext = any_auto ? m->d_pin_ext : nullptr;
-  a.seen = m->d_pin_seen;
-  a.out = m->d_pin_out;
+  RCHK(pin_copy(m, pushed, n));
   uint32_t seg = 0;
   for (int validate = 1;; validate = 0) {
-    if (++m->pin_id == 0) {  // ids wrapped: forget every stored id
-      HIPCHK(hipMemsetAsync(m->d_pin_first, 0, (size_t)m->cap * sizeof(unsigned long long), st));
-      m->pin_id = 1;
-    }
-    a.seg = seg;
-    a.id = m->pin_id;
-    a.validate = validate;
-    gw::launch_pin_check(a, validate && m->pin_seen_dirty, m->nspaces, st);
-    HIPCHK(hipGetLastError());
+    RCHK(pin_launch(m, n, seg, validate, false));
     HIPCHK(hipMemcpyAsync(m->h_pin_out, m->d_pin_out, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t* o = m->h_pin_out;
-    if (validate && o[0]) {
-      set_err("stage_moves_pinned: entry %u refused (flags 0x%x: 2=slot not in a Space, 4=slot >= capacity, "
-              "64=non-finite coordinate); nothing staged",
-              o[2], o[0]);
-      return (o[0] & (gw::ERR_BAD_SLOT | gw::ERR_BAD_COORD)) ? GWAOI_ERR_INVALID : GWAOI_ERR_STATE;
-    }
-    if (validate) {
-      m->pin_seen_dirty = o[3] != 0;
-      if (o[3]) {  // coordinates beyond an auto-extent Space's grid: widen what it has seen
-        uint32_t* k = m->h_pin_out + 4;
-        HIPCHK(hipMemcpyAsync(k, m->d_pin_seen, 4 * sizeof(uint32_t) * m->nspaces, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        for (uint32_t sp = 0; sp < m->nspaces; ++sp) {
-          if (!m->spaces[sp].auto_extent || k[4 * sp] > k[4 * sp + 2]) continue;  // none beyond
-          note_coord(m, sp, gw::ord_float(k[4 * sp]), gw::ord_float(k[4 * sp + 1]));
-          note_coord(m, sp, gw::ord_float(k[4 * sp + 2]), gw::ord_float(k[4 * sp + 3]));
-        }
-      }
-    }
+    if (validate && o[0]) return pin_refused(o);
+    if (validate) RCHK(pin_note_extent(m, o[3]));
     const uint32_t cut = std::min(o[1], n);
     m->dv_slot = m->d_op_slot + seg;
     m->dv_x = m->d_op_x + seg;
@@ -1884,6 +2010,30 @@ int gwaoi_stage_moves_pinned(gwaoi_mgr* m, uint32_t n) {
     RCHK(run_pass(m, true));  // op `cut` repeats a slot of this run: the run is a sub-pass
     seg = cut;
   }
+  return GWAOI_OK;
+}
+
+// The same without the host round trip: the DMA copy, the checks and k_pin_count are enqueued, and the batch
+// is staged as a device-counted batch whose count the check decides on the device. The verdict is read by
+// the pass that runs it (run_pass): a refused batch applies nothing and that call (gwaoi_tick, or a call
+// that flushes) returns the refusal; repeats split it into sub-passes there.
+int gwaoi_stage_moves_pinned_async(gwaoi_mgr* m, uint32_t n) {
+  RCHK(pin_args_ok(m, n, "stage_moves_pinned_async"));
+  if (!m->h_pin_v) return gwaoi_stage_moves_pinned(m, n);  // no mapped verdict words: the sync path
+  if (m->n_ops || m->dv_n) RCHK(run_pass(m, true));  // ops staged earlier come first
+  const uint32_t pushed = std::min(m->pin_pushed, n);
+  m->pin_pushed = 0;
+  if (!n) return GWAOI_OK;
+  RCHK(pin_copy(m, pushed, n));
+  RCHK(pin_launch(m, n, 0, 1, true));
+  m->pin_pending = true;
+  m->pin_validated = true;
+  m->pin_n = n;
+  m->dv_slot = m->d_op_slot;
+  m->dv_x = m->d_op_x;
+  m->dv_z = m->d_op_z;
+  m->dv_count = m->d_pin_n;
+  m->dv_n = n;
   return GWAOI_OK;
 }
 
@@ -2497,6 +2647,27 @@ int gwaoi_debug_set_band(gwaoi_mgr* m, int mode, uint64_t* n_band_movers) {
   }
   if (mode >= 0) m->band_mode = mode;
   if (n_band_movers) *n_band_movers = m->band_movers;
+  return GWAOI_OK;
+}
+
+int gwaoi_debug_sweep_sizes(gwaoi_mgr* m, int enable, uint64_t* tiles) {
+  RCHK(check_mgr(m));
+  RCHK(set_dev(m));
+  if (enable > 0 && !m->d_size_tiles) {
+    RCHK(dalloc(&m->d_size_tiles, 4));
+    HIPCHK(hipMemsetAsync(m->d_size_tiles, 0, 4 * sizeof(uint32_t), m->stream));
+  }
+  uint32_t h[4] = {0, 0, 0, 0};
+  if (m->d_size_tiles) {
+    HIPCHK(hipStreamSynchronize(m->stream));
+    HIPCHK(hipMemcpy(h, m->d_size_tiles, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  if (tiles)
+    for (int k = 0; k < 3; ++k) tiles[k] = h[k];
+  if (enable == 0 && m->d_size_tiles) {
+    HIPCHK(hipFree(m->d_size_tiles));
+    m->d_size_tiles = nullptr;
+  }
   return GWAOI_OK;
 }
 

@@ -107,6 +107,16 @@ class Engine:
         """The first n entries of the pinned staging arrays as n Moved calls (validated on the device)."""
         check(self._L.gwaoi_stage_moves_pinned(self._h, int(n)))
 
+    def stage_moves_pinned_partial(self, upto: int):
+        """Push entries [pushed, upto) of the pinned arrays to the device now (ABI 2.1: asynchronous DMA,
+        nothing staged); the final stage_moves_pinned[_async](n) copies only the rest."""
+        check(self._L.gwaoi_stage_moves_pinned_partial(self._h, int(upto)))
+
+    def stage_moves_pinned_async(self, n: int):
+        """stage_moves_pinned without the host round trip (ABI 2.1): a refused batch applies nothing and is
+        reported by the next call that runs the pass (tick, or a flushing call)."""
+        check(self._L.gwaoi_stage_moves_pinned_async(self._h, int(n)))
+
     def stage_moves_device(self, d_slots: int, d_x: int, d_z: int, n: int):
         check(self._L.gwaoi_stage_moves_device(self._h, ctypes.c_void_p(d_slots), ctypes.c_void_p(d_x),
                                                 ctypes.c_void_p(d_z), n))
@@ -244,6 +254,13 @@ class Engine:
         n = ctypes.c_uint64()
         check(self._L.gwaoi_debug_set_band(self._h, int(mode), ctypes.byref(n)))
         return int(n.value)
+
+    def debug_sweep_sizes(self, enable: int = -1):
+        """gwaoi_debug_sweep_sizes: tiles the LDS sweeps walked (small, mid, big) since counting was enabled
+        (1: count; 0: read and stop; -1: read)."""
+        t = (ctypes.c_uint64 * 3)()
+        check(self._L.gwaoi_debug_sweep_sizes(self._h, int(enable), t))
+        return tuple(int(v) for v in t)
 
     def debug_small_pass(self, mode: int = -1) -> int:
         """Small passes (gwaoi_debug_set_small_pass): mode 0 off, 1 auto, 2 whenever possible, -1 keep;

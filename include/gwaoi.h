@@ -113,6 +113,21 @@ int gwaoi_stage_moves(gwaoi_mgr* mgr, const uint32_t* slots, const float* x, con
  * rewritten. */
 int gwaoi_stage_buffers(gwaoi_mgr* mgr, uint32_t** slots, float** x, float** z, uint32_t* capacity);
 int gwaoi_stage_moves_pinned(gwaoi_mgr* mgr, uint32_t n);
+/* ABI 2.1. Incremental push for a wrapper whose Moved calls arrive over the tick (GameService.go:398-410
+ * handles one position packet at a time): entries [pushed, upto) of the pinned arrays are copied to the
+ * device NOW (asynchronous DMA; nothing validated, nothing staged), so the final
+ * gwaoi_stage_moves_pinned[_async](n) copies only entries [upto, n). Entries below `upto` must not be
+ * rewritten before that call; `upto` never decreases within a batch (GWAOI_ERR_INVALID). Ops staged before
+ * it run first, as at the final call; a pass of host-staged ops in between discards what was pushed (the
+ * final call copies it again). */
+int gwaoi_stage_moves_pinned_partial(gwaoi_mgr* mgr, uint32_t upto);
+/* ABI 2.1. gwaoi_stage_moves_pinned without the host round trip: the copy, the device checks and the
+ * repeat search are enqueued and the batch is staged at once; the pass that runs it (gwaoi_tick, or any
+ * call that flushes staged ops) applies none of it if the checks refused it and then returns
+ * GWAOI_ERR_INVALID / GWAOI_ERR_STATE (what gwaoi_stage_moves_pinned would have returned; the manager
+ * stays usable). A repeated slot splits the batch into sub-passes exactly as gwaoi_stage_moves_pinned
+ * does. When it returns, the buffers may be rewritten. */
+int gwaoi_stage_moves_pinned_async(gwaoi_mgr* mgr, uint32_t n);
 /* Same, from DEVICE arrays (inputs resident in HBM). Must be the only ops of the batch; slots must be
  * distinct and present — checked on the device, reported by gwaoi_tick as GWAOI_ERR_DEVICE_CHECK
  * (the manager is then unusable and must be destroyed). The arrays must stay valid until gwaoi_tick. */
@@ -211,8 +226,11 @@ typedef struct {
   uint64_t grid_records;   /* records of the passes' cell-sorted grids (main + ghost) */
   uint64_t grid_cells;     /* cells of those grids */
   uint64_t dense_movers;   /* movers swept one wave each (boxes beyond their tile's LDS region) */
-  uint64_t band_movers;    /* of the dense movers, those that took the band walk; this was
+  union {                  /* of the dense movers, those that took the band walk; this was
                               * the reserved refined_cells word of ABI 2 (always 0 there): same layout */
+    uint64_t band_movers;
+    uint64_t chunked_movers; /* deprecated alias (ABI 2.0 round 4 name) */
+  };
 } gwaoi_stats;
 int gwaoi_set_timing(gwaoi_mgr* mgr, int enable);
 int gwaoi_get_stats(const gwaoi_mgr* mgr, gwaoi_stats* out);
@@ -224,9 +242,16 @@ const char* gwaoi_version(void);
  * checks gwaoi_abi_version() == GWAOI_ABI_VERSION once at start-up: a struct that grew
  * (e.g. gwaoi_ingest_result.n_nonfinite, ABI 2) would otherwise be written past its end.
  *   1: round-1 surface;  2: gwaoi_ingest_result.n_nonfinite, gwaoi_strip_absorb_n's d_err,
- *   gwaoi_stage_buffers / gwaoi_stage_moves_pinned, gwaoi_export_relation_delta. */
+ *   gwaoi_stage_buffers / gwaoi_stage_moves_pinned, gwaoi_export_relation_delta.
+ * Minor revisions add calls and keep every struct layout (a binding of 2.0 runs against 2.1):
+ *   2.1: gwaoi_stage_moves_pinned_partial, gwaoi_stage_moves_pinned_async, gwaoi_abi_minor;
+ *        gwaoi_stats.band_movers is the round-4 name chunked_movers (kept as an alias, same word);
+ *        gwaoi_tools.h: gwaoi_debug_set_chunked (removed in 2.0's last revision) is replaced by
+ *        gwaoi_debug_set_band (mode, out counter), a test hook outside the ABI proper. */
 #define GWAOI_ABI_VERSION 2
+#define GWAOI_ABI_MINOR 1
 int gwaoi_abi_version(void);
+int gwaoi_abi_minor(void);
 const char* gwaoi_last_error(void);
 
 #ifdef __cplusplus

@@ -85,6 +85,10 @@ int gwaoi_debug_set_band(struct gwaoi_mgr* mgr, int mode, uint64_t* n_band_mover
  * (optional): direct collects whose packet buffer was too small and were written again. Requires
  * gwaoi_sync_enable. */
 int gwaoi_debug_set_fanout_mode(struct gwaoi_mgr* mgr, int mode, uint64_t* direct_reruns);
+/* Count the tiles the LDS sweeps walked, per sweep size: tiles[0] small, [1] mid, [2] big,
+ * accumulated over the passes since counting was enabled (enable 1: start, or keep, counting; 0: read and
+ * stop; -1: read). One atomic per tile when on; the product path does not count. */
+int gwaoi_debug_sweep_sizes(struct gwaoi_mgr* mgr, int enable, uint64_t* tiles);
 /* Diagnostics: resident sweep workgroups per CU (HIP occupancy API) and the sweep's LDS bytes. */
 int gwaoi_debug_sweep_occupancy(int device, int* blocks_per_cu, int* lds_bytes);
 

@@ -90,17 +90,19 @@ def gpu_tick(eng, ops) -> np.ndarray:
     return eng.tick()
 
 
-def gpu_tick_pinned(eng, ops) -> np.ndarray:
+def gpu_tick_pinned(eng, ops, mode="sync", chunk=0) -> np.ndarray:
     """The cgo wrapper's batching: Moved calls are written into the manager's pinned
     staging arrays and pushed with ONE gwaoi_stage_moves_pinned before the next Enter/Leave and at the
-    flush; a slot moved twice stays in the batch (the device splits it into sub-passes)."""
+    flush; a slot moved twice stays in the batch (the device splits it into sub-passes). mode "async":
+    gwaoi_stage_moves_pinned_async (the verdict read by the pass); chunk > 0: every `chunk` Moved calls
+    are pushed early with gwaoi_stage_moves_pinned_partial (ABI 2.1)."""
     ps, px, pz = eng.stage_buffers()
     k = 0
 
     def push():
         nonlocal k
         if k:
-            eng.stage_moves_pinned(k)
+            (eng.stage_moves_pinned_async if mode == "async" else eng.stage_moves_pinned)(k)
             k = 0
 
     for kind, slot, x, z in ops:
@@ -109,6 +111,8 @@ def gpu_tick_pinned(eng, ops) -> np.ndarray:
             k += 1
             if k == len(ps):
                 push()
+            elif chunk and k % chunk == 0:
+                eng.stage_moves_pinned_partial(k)
             continue
         push()
         if kind == ENTER:

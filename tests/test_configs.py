@@ -228,6 +228,7 @@ def test_config5_4x100k_vs_grid_oracle(gpu, oracle_lib, band):
         assert np.array_equal(grp - grp[0], orp.astype(np.int64)), f"space {s} row lengths"
         assert np.array_equal(cols[grp[0]:grp[-1]] - np.uint32(s * N), ocols), f"space {s} neighbours"
     slots = np.arange(N, dtype=np.uint32)
+    eng.debug_sweep_sizes(1)  # count the tiles each LDS sweep size walks in the moving ticks
     for t in (1, 2):
         want = []
         for s, o in enumerate(orcs):
@@ -244,6 +245,10 @@ def test_config5_4x100k_vs_grid_oracle(gpu, oracle_lib, band):
         assert np.array_equal(got, want), f"tick {t}: " + H.fmt_diff(got, want)
     st = eng.stats()
     assert st["dense_movers"] > 0 and (st["band_movers"] > 0) == bool(band)  # the path under test
+    small, mid, big = eng.debug_sweep_sizes(0)
+    # every LDS sweep size took part (D 50 / 100: small, D 200: mid, D 400: big): a planner or
+    # cap change that reroutes a Space would drop a size's parity coverage here
+    assert small > 0 and mid > 0 and big > 0, (small, mid, big)
 
 
 def test_config5_full_size_two_grids_agree(gpu):

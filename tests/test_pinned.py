@@ -18,11 +18,15 @@ def assert_same(a, b, what):
     assert np.array_equal(a, b), what + ": " + H.fmt_diff(a, b)
 
 
-@pytest.mark.parametrize("seed,bounded", [(31, True), (32, False), (33, False)])
-def test_pinned_random_ops_vs_oracle(gpu, oracle_lib, seed, bounded):
+@pytest.mark.parametrize("seed,bounded,mode,chunk", [(31, True, "sync", 0), (32, False, "sync", 0),
+                                                    (33, False, "sync", 0), (34, False, "async", 0),
+                                                    (35, True, "async", 7), (36, False, "sync", 5),
+                                                    (37, False, "async", 64)])
+def test_pinned_random_ops_vs_oracle(gpu, oracle_lib, seed, bounded, mode, chunk):
     """Random Enter/Leave/Moved mixes with slots moved up to three times per tick, teleports and
     lattice ties; unbounded managers (NewXZListAOIManager(d): auto extent) see coordinates far outside
-    their grid, reported by the device check."""
+    their grid, reported by the device check. mode "async": the verdict and the repeat cut stay on the
+    device (gwaoi_stage_moves_pinned_async); chunk: incremental pushes every `chunk` Moved calls."""
     from goworld_amd.engine import Engine
     case = H.case_random_ops(seed=seed, n=300, nticks=10, ops_per_tick=400, world=300.0, dist=40.0)
     eng = Engine(case["dist"], capacity=case["cap"], bounds=(-400.0, -400.0, 400.0, 400.0) if bounded else None)
@@ -43,7 +47,7 @@ def test_pinned_random_ops_vs_oracle(gpu, oracle_lib, seed, bounded):
             extra.append((H.MOVE, int(s), float(np.float32(x)), float(np.float32(z))))
         ops = ops + extra
         want = H.oracle_tick(orc, ops)
-        got = H.gpu_tick_pinned(eng, ops)
+        got = H.gpu_tick_pinned(eng, ops, mode=mode, chunk=chunk)
         assert_same(got, want, f"seed {seed} tick {t}")
     rg, ro = eng.relation(), orc.relation()
     assert np.array_equal(rg[0], ro[0]) and np.array_equal(rg[1], ro[1])
@@ -118,4 +122,107 @@ def test_pinned_refuses_bad_batch_and_stages_nothing(gpu):
     ps[:2], px[:2], pz[:2] = (0, 1), (150.0, 20.0), (0.0, 0.0)
     eng.stage_moves_pinned(2)
     assert eng.tick().tolist() == [[0, 1]]  # slot 0 leaves slot 1's box: the manager still works
+    eng.close()
+
+
+@pytest.mark.parametrize("chunk", [0, 4096])
+def test_pinned_async_walk_with_sub_passes(gpu, oracle_lib, chunk):
+    """The async path on a config-1-style walk: equal to gwaoi_stage_moves and oracle (i) every tick,
+    including a tick whose batch moves every slot twice (the repeat cut found on the device and the
+    second half run as a sub-pass by the pass that reads the verdict), with and without incremental
+    pushes of the arrays."""
+    from goworld_amd.engine import Engine
+    n, L = 20_000, 4000.0
+    po = oracle_lib
+    x, z = po.workload_init(0x5EED00A2, n, L)
+    a = Engine(100.0, capacity=2 * n, bounds=(0.0, 0.0, L, L))
+    b = Engine(100.0, capacity=2 * n, bounds=(0.0, 0.0, L, L))
+    slots = np.arange(n, dtype=np.uint32)
+    a.stage_enters(slots, x, z)
+    b.stage_enters(slots, x, z)
+    assert np.array_equal(a.tick(), b.tick())
+    orc = po.XZListOracle(100.0, 2 * n)
+    orc.bulk_enter(slots, x, z)
+    orc.take_events()
+    ps, px, pz = b.stage_buffers()
+    for t in range(1, 5):
+        po.workload_step(0x5EED00A2, t, x, z, L, 1.0)
+        if t == 3:  # every slot twice in ONE batch of 2n
+            x2 = (x + np.float32(0.5)).astype(np.float32)
+            ss, xs, zs = np.concatenate([slots, slots]), np.concatenate([x, x2]), np.concatenate([z, z])
+            m = 2 * n
+            x[:] = x2
+        else:
+            ss, xs, zs = slots, x.copy(), z.copy()
+            m = n
+        a.stage_moves(ss, xs, zs)
+        ps[:m], px[:m], pz[:m] = ss, xs, zs
+        if chunk:
+            for k in range(chunk, m, chunk):
+                b.stage_moves_pinned_partial(k)
+        b.stage_moves_pinned_async(m)
+        ops = [(H.MOVE, int(ss[i]), float(xs[i]), float(zs[i])) for i in range(m)]
+        ea, eb = a.tick(), b.tick()
+        assert_same(eb, ea, f"tick {t} async vs stage_moves")
+        assert_same(eb, H.oracle_tick(orc, ops), f"tick {t} vs oracle (i)")
+        assert len(eb) > 100
+    a.close()
+    b.close()
+
+
+def test_pinned_async_refusal_reported_by_tick(gpu):
+    """gwaoi_stage_moves_pinned_async: the same refusals as the sync call (codes and message), reported by
+    the pass that reads the device's verdict; nothing of the batch applied, ops staged before it still run,
+    the manager stays usable."""
+    from goworld_amd import _lib
+    from goworld_amd.engine import Engine
+    eng = Engine(100.0, 64)
+    eng.enter(0, 0.0, 0.0)
+    eng.enter(1, 10.0, 0.0)
+    assert eng.tick().tolist() == [[1, 0 | H.EV_ENTER]]
+    ps, px, pz = eng.stage_buffers()
+    cases = [((0, 5), (1.0, 2.0), _lib.GWAOI_ERR_STATE),
+             ((0, 64), (1.0, 2.0), _lib.GWAOI_ERR_INVALID),
+             ((0, 1), (1.0, float("nan")), _lib.GWAOI_ERR_INVALID),
+             ((1, 1), (150.0, float("inf")), _lib.GWAOI_ERR_INVALID)]  # refused although it repeats a slot
+    for sl, xs, code in cases:
+        eng.moved(1, 20.0, 0.0)  # staged before the batch: runs first
+        ps[:2], px[:2], pz[:2] = sl, xs, (0.0, 0.0)
+        eng.stage_moves_pinned_async(2)
+        with pytest.raises(_lib.GwaoiError) as e:
+            eng.tick()
+        assert e.value.code == code, (sl, xs)
+        assert "nothing staged" in str(e.value)
+        assert eng.tick().tolist() == []  # nothing of the batch was applied
+    ps[:2], px[:2], pz[:2] = (0, 1), (150.0, 20.0), (0.0, 0.0)
+    eng.stage_moves_pinned_async(2)
+    assert eng.tick().tolist() == [[0, 1]]
+    eng.close()
+
+
+def test_pinned_partial_push_discarded_by_host_pass(gpu, oracle_lib):
+    """An incremental push followed by a pass of host-staged ops (which writes the device op arrays): the
+    final call copies the pushed entries again, so the batch is still exact against oracle (i)."""
+    from goworld_amd.engine import Engine
+    eng = Engine(40.0, 256)
+    orc = oracle_lib.XZListOracle(40.0, 256)
+    rng = np.random.default_rng(7)
+    pos = rng.uniform(-100, 100, (200, 2)).astype(np.float32)
+    ops = [(H.ENTER, i, float(pos[i, 0]), float(pos[i, 1])) for i in range(200)]
+    assert_same(H.gpu_tick(eng, ops), H.oracle_tick(orc, ops), "enter")
+    ps, px, pz = eng.stage_buffers()
+    for mode in ("sync", "async"):
+        mv = rng.uniform(-100, 100, (150, 2)).astype(np.float32)
+        ps[:150], px[:150], pz[:150] = np.arange(150, dtype=np.uint32), mv[:, 0], mv[:, 1]
+        eng.stage_moves_pinned_partial(100)
+        e1 = [(H.ENTER, 210, 5.0, 5.0)]  # a host-staged Enter run on its own (gwaoi_enter + tick)
+        assert_same(H.gpu_tick(eng, e1), H.oracle_tick(orc, e1), "enter between push and flush")
+        orc_ops = [(H.LEAVE, 210, 0.0, 0.0)]
+        assert_same(H.gpu_tick(eng, orc_ops), H.oracle_tick(orc, orc_ops), "leave")
+        (eng.stage_moves_pinned_async if mode == "async" else eng.stage_moves_pinned)(150)
+        ops = [(H.MOVE, i, float(mv[i, 0]), float(mv[i, 1])) for i in range(150)]
+        assert_same(eng.tick(), H.oracle_tick(orc, ops), mode)
+    with pytest.raises(Exception):
+        eng.stage_moves_pinned_partial(10)
+        eng.stage_moves_pinned_partial(5)  # below what was pushed
     eng.close()
