@@ -323,6 +323,23 @@ def small_pass_leg(eng, n, L, xs, zs, reps, seed):
                 "host_ms_p50": percentile([r[2] for r in v], 50),
                 "events_mean": float(np.mean([r[3] for r in v])),
             }
+        if mode == 1:
+            # the same 1-op passes with timing off (no hipEvent records between the kernels) and the events
+            # delivered to the host, as the Go wrapper's flushed Enter / Leave (gwaoi_tick)
+            eng.set_timing(False)
+            hl, he = [], []
+            for _ in range(reps):
+                s = int(rng.integers(n))
+                for lst, stage in ((hl, lambda: eng.leave(s)), (he, lambda: eng.enter(s, float(xs[s]), float(zs[s])))):
+                    t0 = time.perf_counter()
+                    stage()
+                    eng.tick_raw()
+                    lst.append((time.perf_counter() - t0) * 1e3)
+            res["leave_1op"]["host_ms_p50_host_events_no_timing"] = percentile(hl, 50)
+            res["enter_1op"]["host_ms_p50_host_events_no_timing"] = percentile(he, 50)
+            res["leave_1op"]["host_ms_p99_host_events_no_timing"] = percentile(hl, 99)
+            res["enter_1op"]["host_ms_p99_host_events_no_timing"] = percentile(he, 99)
+            eng.set_timing(True)
         out[tag] = res
     eng.debug_small_pass(1)
     eng.set_timing(False)
@@ -331,7 +348,9 @@ def small_pass_leg(eng, n, L, xs, zs, reps, seed):
         "Moved pass (<= 1 unit each), host-staged, events in HBM, into the full manager; device = the pass's "
         "hipEvents (first to last: the event records between the kernels included), sweep_stage = the hipEvents "
         "around the sweep kernel (a single op: the whole pass, apply + sweep + order + publication, is that one "
-        "kernel); host = stage + tick wall time; small_passes = passes that took the small path")
+        "kernel); host = stage + tick wall time; small_passes = passes that took the small path; "
+        "host_ms_*_host_events_no_timing: the same 1-op passes with timing off and the events delivered to "
+        "host memory (gwaoi_tick, the Go wrapper's flushed Enter / Leave)")
     return out
 
 

@@ -243,6 +243,8 @@ struct SweepArgs {
   const float* band_zk;   // per cell by z key: the key, and
   const uint32_t* band_zi;  // the record
   const uint32_t* band_hd;
+  const uint8_t* band_tab;   // key tables (BandArgs.tab), or null: the key windows are searched
+  uint32_t band_tab_half;
   uint32_t* size_tiles;  // debug (gwaoi_debug_sweep_sizes): tiles walked in LDS by the small / mid / big sweep, or null
 };
 
@@ -263,9 +265,16 @@ struct BandArgs {
   float* zk;             // [records] per cell by z key: the key,
   uint32_t* zi;          // and the record's index in rec_out
   uint32_t* hd;          // [2 nspaces] per Space: max |p - key| (float bits; zeroed by the caller), x then z
+  uint8_t* tab;          // key tables (GW_BAND_TABLE): x tables, then z tables at tab + tab_half; a sorted cell
+  uint32_t tab_half;     // of kBandSearchMin.. records starting at record s owns bytes [(s / 4) * 64, + 64)
 };
-// cells of more records than this are not sorted: the band walk reads them whole
-constexpr uint32_t kBandCellMax = 256;
+// cells of more records than this are not sorted: the band walk reads them whole (255: a key table's
+// offsets are bytes)
+constexpr uint32_t kBandCellMax = 255;
+// key table of a sorted cell, per axis: byte b (1..63) = the number of the cell's keys k whose bucket
+// band_bucket(k) is below b, i.e. the sorted position of the first key of bucket b (buckets: 64 equal parts of
+// the cell's side); the band walk reads the keys of a window [w0, w1] as positions [tab[b(w0)], tab[b(w1) + 1])
+constexpr int kBandBuckets = 64;
 void launch_band_keys(const BandArgs& b, hipStream_t st);
 
 struct RelArgs {
@@ -418,6 +427,11 @@ struct SmallArgs {
   int one_op;
   ApplyArgs ap;
   OrderArgs od;
+  // one_op: the op itself by value (the host staged it: no PCIe read of the pinned staging arrays), and the
+  // slice also written into the mapped host event buffer (od.host_out) before the publication, so a
+  // host-delivered pass needs no copy-out kernel and no stream synchronisation
+  uint32_t one_slot, one_space, one_kind;
+  float one_x, one_z;
 };
 void launch_sweep_small(const SmallArgs& a, hipStream_t st);
 // k_place (+ zeroing side jobs, duplicate-slot check) -> k_slice_sort (+ batch check, publication of

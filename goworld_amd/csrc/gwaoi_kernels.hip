@@ -2205,6 +2205,20 @@ __global__ void __launch_bounds__(kBlock) k_sweep_leaves(SweepArgs a) {
 // acted in this pass and was present at the start: judge() then meets it at its start OR its end position
 // (which one depends on the mover's rank), both in the binned cell, and the key is their midpoint; hd
 // (per Space and axis) bounds |p - key| over all records.
+#ifndef GW_BAND_SEARCH_MIN  // cells of fewer records are read whole instead of searched
+#define GW_BAND_SEARCH_MIN 4u
+#endif
+constexpr uint32_t kBandSearchMin = GW_BAND_SEARCH_MIN;
+#ifndef GW_BAND_TABLE  // 1: key tables (one lookup per searched cell); 0: the fanout-4 key search (A/B)
+#define GW_BAND_TABLE 1
+#endif
+// The bucket of key k inside cell c (column for x keys, row for z keys) of a Space with origin o and 1 / side
+// inv: 64 equal parts of the cell, clamped (keys of a clamped border cell lie outside it). Monotone in k (every
+// step is), which is all the key tables need: the builder (k_band_sort) and the walk use this one function.
+__device__ __forceinline__ int band_bucket(float k, float o, float inv, int c) {
+  const float f = ((k - o) * inv - (float)c) * (float)kBandBuckets;
+  return f >= (float)(kBandBuckets - 1) ? kBandBuckets - 1 : (f > 0.0f ? (int)f : 0);
+}
 __device__ __forceinline__ void band_key(const uint4 ra, const uint4 rb, float& kx, float& kz, float& hx, float& hz) {
   const float bx = __uint_as_float(ra.x), bz = __uint_as_float(ra.y);
   kx = bx, kz = bz, hx = 0.0f, hz = 0.0f;
@@ -2284,15 +2298,37 @@ __global__ void __launch_bounds__(kBlock) k_band_sort(BandArgs a) {
       continue;
     }
     uint32_t rx = 0, rz = 0;
+    float px = -__builtin_inff(), pz = -__builtin_inff();  // the largest keys ranked below this one
     for (uint32_t i = s; i < e; ++i) {
       const float2 ki = staged ? kk[i - lo] : rec_key(a.g.rec, i);
-      rx += (ki.x < kx || (ki.x == kx && i < j)) ? 1u : 0u;
-      rz += (ki.y < kz || (ki.y == kz && i < j)) ? 1u : 0u;
+      const bool bx = ki.x < kx || (ki.x == kx && i < j), bz = ki.y < kz || (ki.y == kz && i < j);
+      rx += bx ? 1u : 0u;
+      rz += bz ? 1u : 0u;
+      px = bx ? fmaxf(px, ki.x) : px;
+      pz = bz ? fmaxf(pz, ki.y) : pz;
     }
     a.rec_out[s + rx] = r;
     a.xk[s + rx] = kx;
     a.zk[s + rz] = kz;
     a.zi[s + rz] = s + rx;
+    const uint32_t nc = e - s;
+    if (a.tab && nc >= kBandSearchMin) {
+      // this key's share of its cell's tables: byte b = rank for the buckets b after the predecessor's bucket up
+      // to its own (every byte 1..63 of a table is written by exactly one key of the cell; the largest key
+      // also writes the buckets above its own with the cell's count)
+      const Geom gg = lgeo ? gs[sp] : a.g.geom[sp];
+      const int cx = cellc(__uint_as_float(r.a.x), gg.x0, gg.inv_c, gg.ncx);
+      const int cz = cellc(__uint_as_float(r.a.y), gg.z0, gg.inv_c, gg.ncz);
+      uint8_t* tb = a.tab + (size_t)(s >> 2) * kBandBuckets;
+      auto fill = [&](uint8_t* t, uint32_t rk, float k, float pk, float o, int c) {
+        const int ib = band_bucket(k, o, gg.inv_c, c), pb = rk ? band_bucket(pk, o, gg.inv_c, c) : 0;
+        for (int b = pb + 1; b <= ib; ++b) t[b] = (uint8_t)rk;
+        if (rk == nc - 1)
+          for (int b = ib + 1; b < kBandBuckets; ++b) t[b] = (uint8_t)nc;
+      };
+      fill(tb, rx, kx, px, gg.x0, cx);
+      fill(tb + a.tab_half, rz, kz, pz, gg.z0, cz);
+    }
   }
   if (!lgeo) return;
   __syncthreads();
@@ -2623,10 +2659,6 @@ k_sweep_dense(SweepArgs a) {
 #ifndef GW_BAND_WPE  // 4 waves per SIMD: 118 VGPRs (two cells and two candidates per lane in flight)
 #define GW_BAND_WPE 5
 #endif
-#ifndef GW_BAND_SEARCH_MIN  // cells of fewer records are read whole instead of searched
-#define GW_BAND_SEARCH_MIN 4u
-#endif
-constexpr uint32_t kBandSearchMin = GW_BAND_SEARCH_MIN;
 #ifndef GW_BAND_FAN
 #define GW_BAND_FAN 4
 #endif
@@ -2750,6 +2782,11 @@ k_sweep_band(SweepArgs a) {
     if constexpr (kBuf) return __builtin_amdgcn_raw_buffer_load_b32(r_zi, i << 2, 0, 0);
     else return a.band_zi[i];
   };
+  const auto r_tab = __builtin_amdgcn_make_buffer_rsrc((void*)a.band_tab, 0, (int)(2u * a.band_tab_half), 0x00020000);
+  auto ld_tab = [&](uint32_t i) -> uint32_t {
+    if constexpr (kBuf) return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r_tab, i, 0, 0);
+    else return a.band_tab[i];
+  };
   auto ld_rec = [&](uint32_t j, uint4& ra, uint4& rb) {
     if constexpr (kBuf) {
       const auto qa = __builtin_amdgcn_raw_buffer_load_b128(r_rec, j << 5, 0, 0);
@@ -2838,6 +2875,10 @@ k_sweep_band(SweepArgs a) {
       uint32_t p0[2], p1[2], mk[2];
       float w0[2], w1[2];
       int kind[2], dd[2], iow[2], span[2];
+#if GW_BAND_TABLE
+      int cl[2];     // the cell's column (x-strip item) or row (z-strip item): its key table's buckets
+      float4 gq[2];  // the mover's Space: {x0, z0, 1 / cell side, D}
+#endif
       stream_owners(orow[wv], iexcl, nit, ib, iow[0], iow[1]);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -2848,11 +2889,24 @@ k_sweep_band(SweepArgs a) {
         mk[u] = (uint32_t)k;
         p0[u] = p1[u] = 0u;
         kind[u] = 3, dd[u] = 0, span[u] = 0, w0[u] = w1[u] = 0.0f;
+#if GW_BAND_TABLE
+        cl[u] = 0;
+        gq[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#endif
         if (it < N) {
           const BandPlan P = plan_load(pl[wv][k]);
           const uint2 sg = pg[wv][k];
           int c, r;
           band_item(P, it - kex, c, r, w0[u], w1[u], kind[u], dd[u], span[u]);
+#if GW_BAND_TABLE
+          // an x-strip cell in a z-strip row (a corner cell): its candidates are judged only when their x key lies
+          // in the window (the key table's range is the window's buckets, a superset), so that the z-strip item
+          // of the same cell judges exactly the rest (dd 1 / 2: the left / right window)
+          if (kind[u] == 0 && ((r >= P.rb0 && r <= P.rb1) || (r >= P.rt0 && r <= P.rt1)))
+            dd[u] = c >= P.cl0 && c <= P.cl1 ? 1 : 2;
+          cl[u] = kind[u] == 1 ? r : c;
+          gq[u] = *reinterpret_cast<const float4*>(&a.g.geom[mb[wv][k][0].y]);  // (x0, z0, inv_c, D lead Geom)
+#endif
           // (cell_key on the Space's base and tile columns)
           p0[u] = sg.x + ((uint32_t)((r >> kTileShift) * (int)sg.y + (c >> kTileShift)) << kTileCellShift) +
                   (uint32_t)(((r & (kTile - 1)) << kTileShift) | (c & (kTile - 1)));  // (the key until its starts load)
@@ -2876,9 +2930,10 @@ k_sweep_band(SweepArgs a) {
         const uint32_t nc = p1[u] - p0[u];
         if (kind[u] == 4) {
           kind[u] = 2;  // a run: read whole (no x-strip column in it: no dedupe)
-        } else if (kind[u] != 3 && (nc > kBandCellMax || nc < kBandSearchMin)) {
+        } else if (kind[u] != 3 && (nc > kBandCellMax || nc < kBandSearchMin || (GW_BAND_TABLE && !a.band_tab))) {
+          if (dd[u] && kind[u] == 1) p1[u] = p0[u];
+          if (kind[u] == 0) dd[u] = 0;  // (an x-strip cell read whole: no window test)
           kind[u] = 2;
-          if (dd[u]) p1[u] = p0[u];
         }
       }
 #if GW_STAMPS
@@ -2888,6 +2943,22 @@ k_sweep_band(SweepArgs a) {
       }
 #endif
       GW_DPH(2);
+#if GW_BAND_TABLE
+      // key windows of the sorted cells from their key tables: the window's first and last bucket, two bytes
+      // (one round trip for both cells); the range is a superset of the window by under a bucket each side
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (kind[u] < 2) {
+          const float o = kind[u] == 1 ? gq[u].y : gq[u].x;
+          const int i0 = band_bucket(w0[u], o, gq[u].z, cl[u]), i1 = band_bucket(w1[u], o, gq[u].z, cl[u]);
+          const uint32_t tb = (kind[u] == 1 ? a.band_tab_half : 0u) + (p0[u] >> 2) * (uint32_t)kBandBuckets;
+          const uint32_t lo = i0 ? ld_tab(tb + (uint32_t)i0) : 0u;
+          const uint32_t hi = i1 < kBandBuckets - 1 ? ld_tab(tb + (uint32_t)i1 + 1u) : p1[u] - p0[u];
+          p1[u] = p0[u] + max(hi, lo);
+          p0[u] += lo;
+        }
+      }
+#else
       {  // key windows of the sorted cells: fanout kBandFan, both bounds of both cells per round trip; while
          // both bounds are still in the same key range (a narrow window: mostly), one set of probes serves both
         uint32_t ll[2], lh[2], ul[2], uh[2];
@@ -2926,6 +2997,7 @@ k_sweep_band(SweepArgs a) {
         for (int u = 0; u < 2; ++u)
           if (kind[u] < 2) p0[u] = ll[u], p1[u] = max(ul[u], ll[u]);
       }
+#endif
       GW_DPH(3);
       // ---- the round's candidates: one stream over both cells of every lane, 2 per lane per round ----
       const uint32_t c0 = p1[0] - p0[0], cnt = c0 + (p1[1] - p0[1]);
@@ -2962,11 +3034,13 @@ k_sweep_band(SweepArgs a) {
             ld_rec(j, ra, rb);
             bool dup = false;
             if (dl) {
+              // a corner cell: its z-strip item (kd 1) skips the records whose x key lies in the x-strip's window,
+              // its searched x-strip item (kd 0, key tables) judges only those (the same float test on the same key)
               const float wl0 = pl[wv][mo[v]].w[0], wl1 = pl[wv][mo[v]].w[1];
               const float wr0 = pl[wv][mo[v]].w[2], wr1 = pl[wv][mo[v]].w[3];
               float kx, kz, hx, hz;
               band_key(ra, rb, kx, kz, hx, hz);
-              dup = ((dl & 1) && kx >= wl0 && kx <= wl1) || ((dl & 2) && kx >= wr0 && kx <= wr1);
+              dup = (((dl & 1) && kx >= wl0 && kx <= wl1) || ((dl & 2) && kx >= wr0 && kx <= wr1)) == (kd == 1);
             }
             if (!dup) {
               const uint4 u0 = mb[wv][mo[v]][0], u1 = mb[wv][mo[v]][1];
@@ -3082,11 +3156,11 @@ __global__ void __launch_bounds__(kW == 1 ? kBlock : 64 * kW) k_sweep_small(Smal
   if (kW > 1 && threadIdx.x == 0) sloc = 0;
   if (kOne && threadIdx.x == 0) {  // k_apply for the op (host-staged: validated on the host)
     const ApplyArgs& p = a.ap;
-    // the op over PCIe, all four loads in flight; then the slot's state, all loads in flight
-    const uint32_t s = p.op_slot[0];
-    const uint8_t raw = p.op_kind[0], kind = raw & OP_KIND;
-    const float ox = p.op_x[0], oz = p.op_z[0];
-    const uint32_t osp = p.op_space ? p.op_space[0] : 0u;
+    // the op from the kernel's arguments; then the slot's state, all loads in flight
+    const uint32_t s = a.one_slot;
+    const uint8_t raw = (uint8_t)a.one_kind, kind = raw & OP_KIND;
+    const float ox = a.one_x, oz = a.one_z;
+    const uint32_t osp = a.one_space;
     const uint32_t q = p.base, q0 = p.seq[s], sp0 = p.space_of[s], tag = p.ov_tag[s], oidx = p.ov_idx[s];
     const float x0 = p.pos_x[s], z0 = p.pos_z[s];
     p.cp_slot[0] = s;  // (a re-run of the sweep reads the op from the device copies)
@@ -3280,6 +3354,7 @@ __global__ void __launch_bounds__(kW == 1 ? kBlock : 64 * kW) k_sweep_small(Smal
           pos += (kk < v.y || (kk == v.y && k < e)) ? 1u : 0u;
         }
         o.ev_out[pos] = v;
+        if (o.host_out) o.host_out[pos] = v;  // (mapped host memory: visible at the publication below)
       }
     }
   }

@@ -205,6 +205,8 @@ struct gwaoi_mgr {
   uint32_t* band_hd = nullptr;   // [2 nspaces]
   uint32_t* band_dense2 = nullptr;  // [cap] the dense movers the band walk leaves to the ring walk
   uint64_t band_cap = 0;         // records the arrays hold (0: not allocated)
+  uint8_t* band_tab = nullptr;   // key tables (BandArgs.tab): 2 x band_tab_half bytes, or null
+  uint32_t band_tab_half = 0;
   uint64_t band_builds = 0, band_movers = 0;
   uint32_t* d_size_tiles = nullptr;  // [3] gwaoi_debug_sweep_sizes (null: not counted)
   uint32_t* tile_ev = nullptr;   // per tile: events k_sweep queued in the tile's region of ev_tmp
@@ -504,6 +506,11 @@ int ensure_events(gwaoi_mgr* m, uint64_t need_out, uint32_t need_tmp, uint64_t k
 // The band walk's keys over grid gi (records <= bound): per record its {x, z} search keys, per cell the
 // records sorted by each, per Space the keys' spread. The arrays are allocated on first use for
 // the grid's largest size (2 records per slot); without the memory the dense walk reads whole rings.
+#ifndef GW_BAND_TABLE
+#define GW_BAND_TABLE_HOST 1
+#else
+#define GW_BAND_TABLE_HOST GW_BAND_TABLE
+#endif
 int build_band_keys(gwaoi_mgr* m, int gi, uint32_t bound, bool* built) {
   *built = false;
   Grid& G = m->grid[gi];
@@ -523,6 +530,16 @@ int build_band_keys(gwaoi_mgr* m, int gi, uint32_t bound, bool* built) {
     }
     m->band_zk = m->band_xk + n;
     m->band_cap = n;
+    // the key tables: 64 B per axis per 4 records of address space (only the sorted cells of >= 4 records
+    // write theirs); without them (no room) the walk reads its cells whole
+    const uint64_t half = (n / 4 + 1) * (uint64_t)gw::kBandBuckets;
+    if (GW_BAND_TABLE_HOST && half < (1ull << 30) && hipMemGetInfo(&fr, &tot) == hipSuccess && fr > 2 * half + (64ull << 20) &&
+        dalloc(&m->band_tab, 2 * half) == GWAOI_OK) {
+      m->band_tab_half = (uint32_t)half;
+    } else {
+      (void)hipGetLastError();
+      m->band_tab = nullptr;
+    }
   }
   HIPCHK(hipMemsetAsync(m->band_hd, 0, 2 * (size_t)m->nspaces * sizeof(uint32_t), m->stream));
   gw::BandArgs b{};
@@ -540,6 +557,8 @@ int build_band_keys(gwaoi_mgr* m, int gi, uint32_t bound, bool* built) {
   b.zk = m->band_zk;
   b.zi = m->band_zi;
   b.hd = m->band_hd;
+  b.tab = m->band_tab;
+  b.tab_half = m->band_tab_half;
   gw::launch_band_keys(b, m->stream);
   HIPCHK(hipGetLastError());
   std::swap(G.rec, m->grid[gi ^ 1].rec);
@@ -848,7 +867,9 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
     o.tile_acted = nullptr;
     o.ntiles_acted = 0;
     o.n_dev = a.n_dev;
-    o.pub_seq = publish_seq(m, copy_events);
+    // (a single op's pass publishes even with host delivery: its kernel writes the slice into the mapped
+    // host buffer itself, before the publication)
+    o.pub_seq = publish_seq(m, copy_events && !one);
     o.pub = o.pub_seq ? m->d_pub : nullptr;
     o.sorted_hint = !o.check_ops ? 1 : 0;  // few blocks: a small pass sorts few slices
     o.place_blocks = 16;
@@ -877,11 +898,18 @@ int run_small_pass(gwaoi_mgr* m, bool copy_events, uint32_t base, uint32_t n_ops
     sa.one_op = one ? 1 : 0;
     sa.ap = a;
     sa.od = o;
+    if (one) {
+      sa.one_slot = m->h_op_slot[0];
+      sa.one_kind = m->h_op_kind[0];
+      sa.one_x = m->h_op_x[0];
+      sa.one_z = m->h_op_z[0];
+      sa.one_space = m->h_op_space[0];
+    }
     gw::launch_sweep_small(sa, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));
     if (one) {
-      gw::launch_copy_out(o, st);
+      if (!o.pub) gw::launch_copy_out(o, st);  // (published: the kernel wrote the host slice itself)
     } else {
       if (!fused) gw::launch_scan(m->scan, m->rank_cnt, n_ops + 1, st);
       if (fused)
@@ -1137,6 +1165,8 @@ int run_pass_core(gwaoi_mgr* m, bool copy_events) {
     s.band_zk = keys ? m->band_zk : nullptr;
     s.band_zi = keys ? m->band_zi : nullptr;
     s.band_hd = keys ? m->band_hd : nullptr;
+    s.band_tab = keys ? m->band_tab : nullptr;
+    s.band_tab_half = m->band_tab_half;
     s.size_tiles = m->d_size_tiles;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
@@ -1449,7 +1479,7 @@ void free_all(gwaoi_mgr* m) {
   void* dptrs[] = {m->pos_x, m->pos_z, m->old_x, m->old_z, m->seq, m->space_of, m->old_seq, m->opq,
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->uns, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
-                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_xk, m->band_zi, m->band_hd, m->band_dense2, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
+                   m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_xk, m->band_zi, m->band_hd, m->band_dense2, m->band_tab, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
                    m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->d_pin_n, m->d_size_tiles, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
                    m->dx_part, m->dx_out};

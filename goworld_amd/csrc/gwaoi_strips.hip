@@ -123,17 +123,22 @@ __global__ void __launch_bounds__(kSBlock) k_strip_ingest(gwaoi_strip_geom g, ui
 // reserves its range of each list with ONE atomic per list, then writes. (One wave-aggregated atomic
 // per wave with a selection serialised on the two counters when the world's ids are spread over many
 // strips: 270 us for a 16M-id world at 8 strips.)
-constexpr int kSelItems = 64;
-constexpr uint32_t kSelChunk = kSBlock * kSelItems;
+// Rounds per block (items): enough blocks to fill the device (~1k: 2M ids -> 8 rounds; a 16M-id world at
+// most 64), so a small world is not walked by two blocks per CU (64 rounds at 2M ids: 122 blocks, 40 us).
+constexpr int kSelItems = 64;  // at most (one bit per round in two 64-bit masks)
+inline uint32_t sel_items(uint32_t n) {
+  const uint32_t want = (n + 1024u * kSBlock - 1) / (1024u * kSBlock);
+  return want < 4 ? 4u : want > (uint32_t)kSelItems ? (uint32_t)kSelItems : want;
+}
 __global__ void __launch_bounds__(kSBlock) k_strip_select(gwaoi_strip_geom g, const uint8_t* flags, const float* sx,
                                                           const float* ex, const float* ez, uint4* left,
                                                           uint4* right, uint32_t cap, uint32_t* counts,
-                                                          uint32_t* err) {
+                                                          uint32_t* err, uint32_t items) {
   __shared__ uint32_t base_sh[2];
-  const uint32_t c0 = blockIdx.x * kSelChunk + threadIdx.x;
+  const uint32_t c0 = blockIdx.x * kSBlock * items + threadIdx.x;
   unsigned long long ml = 0, mr = 0;
 #pragma unroll 4
-  for (int r = 0; r < kSelItems; ++r) {
+  for (int r = 0; r < (int)items; ++r) {
     const uint32_t i = c0 + (uint32_t)r * kSBlock;
     if (i >= g.n) break;
     const uint8_t f = flags[i];
@@ -399,6 +404,12 @@ __global__ void __launch_bounds__(kSBlock) k_translate(const uint32_t* l2g, uint
 }
 
 inline dim3 blocks_for(uint32_t n) { return dim3((n + kSBlock - 1) / kSBlock); }
+// the free-slot ring of cap_l local slots: the next power of two entries (index mask)
+inline uint32_t ring_mask(uint32_t cap_l) {
+  uint32_t r = 1;
+  while (r < cap_l) r <<= 1;
+  return r - 1;
+}
 inline uint32_t emit_blocks(uint32_t n) { return (n + kSChunk - 1) / kSChunk; }
 
 }  // namespace
@@ -438,11 +449,12 @@ int gwaoi_strip_select(void* stream, const gwaoi_strip_geom* g, const uint8_t* f
                        uint32_t* d_err) {
   if (!g || !flags || !sx || !ex || !ez || !d_left || !d_right || !d_counts || !d_err) return GWAOI_ERR_INVALID;
   if (hipMemsetAsync(d_counts, 0, 2 * sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return GWAOI_ERR_HIP;
-  if (g->n)
-    hipLaunchKernelGGL(gw::k_strip_select, dim3((g->n + gw::kSelChunk - 1) / gw::kSelChunk), dim3(gw::kSBlock), 0,
-                       (hipStream_t)stream, *g, flags,
-                       sx, ex, ez, reinterpret_cast<uint4*>(d_left), reinterpret_cast<uint4*>(d_right), cap, d_counts,
-                       d_err);
+  if (g->n) {
+    const uint32_t items = gw::sel_items(g->n), chunk = gw::kSBlock * items;
+    hipLaunchKernelGGL(gw::k_strip_select, dim3((g->n + chunk - 1) / chunk), dim3(gw::kSBlock), 0, (hipStream_t)stream,
+                       *g, flags, sx, ex, ez, reinterpret_cast<uint4*>(d_left), reinterpret_cast<uint4*>(d_right), cap,
+                       d_counts, d_err, items);
+  }
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 
@@ -500,7 +512,7 @@ int gwaoi_strip_emit(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, fl
 }
 
 int gwaoi_strip_local_init(void* stream, uint32_t n, uint32_t cap_l, uint32_t* g2l, uint32_t* fq, uint32_t* ctr) {
-  if (!g2l || !fq || !ctr || !cap_l || (cap_l & (cap_l - 1))) return GWAOI_ERR_INVALID;
+  if (!g2l || !fq || !ctr || !cap_l || cap_l > 0x80000000u) return GWAOI_ERR_INVALID;
   const uint32_t m = n > cap_l ? n : cap_l;
   hipLaunchKernelGGL(gw::k_local_init, gw::blocks_for(m), dim3(gw::kSBlock), 0, (hipStream_t)stream, n, cap_l, g2l, fq,
                      ctr);
@@ -512,8 +524,9 @@ int gwaoi_strip_emit_local(void* stream, const gwaoi_strip_geom* g, uint8_t* fla
                            uint8_t* d_kinds, uint32_t* d_scratch, uint32_t* d_n_ops, uint32_t* g2l, uint32_t* l2g,
                            uint32_t* fq, uint32_t* pend, uint32_t cap_l, uint32_t* ctr) {
   if (!g || !flags || !sx || !sz || !ex || !ez || !d_slots || !d_x || !d_z || !d_kinds || !d_scratch || !d_n_ops ||
-      !g2l || !l2g || !fq || !pend || !ctr || !cap_l || (cap_l & (cap_l - 1)))
+      !g2l || !l2g || !fq || !pend || !ctr || !cap_l || cap_l > 0x80000000u)
     return GWAOI_ERR_INVALID;
+  const uint32_t mask = gw::ring_mask(cap_l);
   hipStream_t st = (hipStream_t)stream;
   const uint32_t nb = gw::emit_blocks(g->n);
   uint32_t* blk = d_scratch;  // [nb + 1]
@@ -521,14 +534,14 @@ int gwaoi_strip_emit_local(void* stream, const gwaoi_strip_geom* g, uint8_t* fla
   sc.status = d_scratch + nb + 1;
   if (hipMemsetAsync(blk + nb, 0, sizeof(uint32_t), st) != hipSuccess) return GWAOI_ERR_HIP;
   uint32_t* spare = d_scratch + nb + 1 + gw::scan_part_words(nb + 1);  // 4 words (gwaoi_strip_scratch_words)
-  hipLaunchKernelGGL(gw::k_local_release, dim3(1), dim3(1024), 0, st, fq, (const uint32_t*)pend, cap_l - 1, ctr, spare);
+  hipLaunchKernelGGL(gw::k_local_release, dim3(1), dim3(1024), 0, st, fq, (const uint32_t*)pend, mask, ctr, spare);
   if (nb) {
     hipLaunchKernelGGL(gw::k_strip_count, dim3(nb), dim3(gw::kSBlock), 0, st, flags, g->n, blk, spare + 1);
     gw::launch_scan(sc, blk, nb + 1, st);
     // writes *d_n_ops (0 when the Enters do not fit the free slots)
     hipLaunchKernelGGL(gw::k_strip_emit_local, dim3(nb), dim3(gw::kSBlock), 0, st, *g, flags, sx, sz, ex, ez,
                        (const uint32_t*)blk, d_slots, d_x, d_z, d_kinds, g2l, l2g, (const uint32_t*)fq, pend,
-                       cap_l - 1, ctr, (const uint32_t*)spare, nb, d_n_ops);
+                       mask, ctr, (const uint32_t*)spare, nb, d_n_ops);
   } else if (hipMemsetAsync(d_n_ops, 0, sizeof(uint32_t), st) != hipSuccess) {
     return GWAOI_ERR_HIP;
   }

@@ -145,16 +145,19 @@ class StripNode:
         share = n * (hi - lo) / layout.L if layout.uniform else n / layout.world * (hi - lo) / own_w
         # Local slots (include/gwaoi_strips.h): the manager indexes the region's entities by a slot of
         # its own, so its per-pass work follows the region's population, not the world's id range.
-        # cap_l: a power of two with room for crowds drifting in (1.5x the share + 8k), at most n.
-        want = min(n, int(share * 1.5) + 8192) if local_slots else n
+        # cap_l: room for crowds drifting in (1.25x the share + 8k), at most n; the manager's capacity, so
+        # every pass's per-slot work (grid build) follows it (ABI 2.1: any count, the free ring rounded up to
+        # a power of two; 2.0 rounded cap_l itself: a 2M region took 4M slots)
+        want = min(n, int(share * 1.25) + 8192) if local_slots else n
         if cap_l is not None:  # explicit (tests: a region that overflows its slots)
             want = int(cap_l)
-        self.cap_l = 1 << max(0, (max(1, want) - 1).bit_length())
+        self.cap_l = max(1, want)
         self.local = bool(local_slots)
         if self.local:
+            ring = 1 << max(0, (self.cap_l - 1).bit_length())
             self.g2l = torch.empty(n, dtype=i32, device=dev)
             self.l2g = torch.zeros(self.cap_l, dtype=i32, device=dev)
-            self.fq = torch.empty(self.cap_l, dtype=i32, device=dev)
+            self.fq = torch.empty(ring, dtype=i32, device=dev)
             self.pend = torch.empty(self.cap_l, dtype=i32, device=dev)
             self.lctr = torch.zeros(4, dtype=i32, device=dev)
             self.h_lctr = torch.zeros(4, dtype=i32).pin_memory()
@@ -168,6 +171,10 @@ class StripNode:
         self.eng.set_population_hint(0, max(1, min(n, int(share * 1.05))))
         self.tick_no = 0
         self.xev = []  # (start, end) hipEvents of timed exchanges (tick_rccl(time_exchange=True))
+        # per-tick device time of the strip's own kernels (walk + select, absorb + emit), when timing
+        # (scripts/strips_loopback_bench.py): hipEvents on the node's stream, read by strip_kernel_ms()
+        self.timing = False
+        self.sev = []
 
     # ---- raw kernel calls ----
     def _s(self):
@@ -192,6 +199,10 @@ class StripNode:
             self.h_lctr.copy_(self.lctr, non_blocking=True)
         else:
             check(L.gwaoi_strip_emit(*common))
+        f1 = self._mark()
+        if f1 is not None and getattr(self, "_f0", None) is not None and getattr(self, "_ev_prep", (None, None))[1]:
+            self.sev.append((self._ev_prep[0], self._ev_prep[1], self._f0, f1))
+        self._f0 = None
         self.h_counts.copy_(self.counts, non_blocking=True)  # stream-ordered before the tick's kernels
         n_bound = max(1, min(self.cap_l if self.local else self.n, int(n_bound)))
         self.eng.stage_ops_device(self.ids.data_ptr(), self.ox.data_ptr(), self.oz.data_ptr(),
@@ -258,8 +269,27 @@ class StripNode:
         with torch.cuda.stream(self.stream):
             return self._prepare(t, step, moves)
 
+    def _mark(self):
+        if not self.timing:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(self.stream)
+        return e
+
+    def strip_kernel_ms(self) -> Optional[dict]:
+        """Mean device time per timed tick of the strip kernels: prepare (walk or ingest + select) and finish
+        (absorb + emit), from the hipEvents recorded while `timing` was on."""
+        if not self.sev:
+            return None
+        self.stream.synchronize()
+        k = len(self.sev)
+        prep = sum(a.elapsed_time(b) for a, b, _, _ in self.sev) / k
+        fin = sum(c.elapsed_time(d) for _, _, c, d in self.sev) / k
+        return {"ms_strip_prepare": round(prep, 4), "ms_strip_finish": round(fin, 4), "ticks": k}
+
     def _prepare(self, t, step, moves):
         L = self._L
+        self._ev_prep = (self._mark(),)
         if moves is None:
             check(L.gwaoi_strip_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz),
                                      _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed), ctypes.c_uint64(t),
@@ -271,6 +301,7 @@ class StripNode:
         check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
                                    _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
                                    ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+        self._ev_prep = (self._ev_prep[0], self._mark())
         self.tick_no = t
         if not (self.g.has_left or self.g.has_right):  # nothing to send: no round trip (errors: finish)
             return self.left[:0], self.right[:0]
@@ -284,6 +315,7 @@ class StripNode:
         (n, 2) host array of the owned movers' events in canonical order."""
         self.stream.wait_stream(torch.cuda.current_stream(self.device))  # received on the caller's stream
         with torch.cuda.stream(self.stream):
+            f0 = self._mark()
             nin = 0
             for recs in (left_in, right_in):
                 if recs is not None and recs.numel():
@@ -292,6 +324,7 @@ class StripNode:
                     nin += int(recs.shape[0])
                     check(self._L.gwaoi_strip_absorb(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
                                                      _ptr(recs), int(recs.shape[0])))
+            self._f0 = f0
             return self._emit_and_tick(host_events, self.eng.count()[0] + nin)
 
     def tick_rccl(self, t: int, comm: "StripComm", host_events: bool = False, step: float = 1.0,

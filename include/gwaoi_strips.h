@@ -88,7 +88,9 @@ size_t gwaoi_strip_scratch_words(uint32_t n);
  * on 8 GPUs: ~2M present per rank). The op list stays in global id order (that order is what makes
  * the merged events equal one manager's), only the slot the manager sees changes. State (device):
  * g2l[n] (global id -> local slot, GWAOI_STRIP_NO_SLOT = none), l2g[cap_l], a ring of free slots
- * fq[cap_l] (cap_l a power of two), pend[cap_l] (slots of this tick's Leaves, returned to the ring at
+ * fq[cap_l rounded up to a power of two] (any cap_l >= 1 since ABI 2.1; 2.0 required a power of two, so
+ * the manager's capacity, and with it every pass's per-slot work, was up to 2x the slots needed),
+ * pend[cap_l] (slots of this tick's Leaves, returned to the ring at
  * the next emit, after the caller has translated the tick's events with l2g) and ctr[4] =
  * {allocations, releases, pending, error bits}. */
 #define GWAOI_STRIP_NO_SLOT 0xFFFFFFFFu

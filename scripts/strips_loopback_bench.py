@@ -32,6 +32,7 @@ for t in range(1, 4):
 for nd in nodes:
     nd.eng.set_timing(True)
     nd.eng.reset_stats()
+    nd.timing = True  # the strip kernels' own device time (walk + select, absorb + emit)
 torch.cuda.synchronize()
 halo = [0] * world
 t0 = time.perf_counter()
@@ -49,11 +50,16 @@ for nd in nodes:
     st = nd.eng.stats()
     k = max(1, st["ticks"])
     rows.append({key: round(st[key] / k, 4) for key in ("ms_apply", "ms_grid", "ms_sweep", "ms_order", "ms_total")})
+    rows[-1].update(nd.strip_kernel_ms() or {})
+    rows[-1]["ms_device_total"] = round(rows[-1]["ms_total"] + rows[-1].get("ms_strip_prepare", 0.0)
+                                        + rows[-1].get("ms_strip_finish", 0.0), 4)
     rows[-1]["ops"] = nd.last_ops
     rows[-1]["halo_records_sent_per_tick"] = halo[nd.rank] / ticks
     nd.close()
 print(json.dumps({"world": world, "per_gpu": per, "ticks": ticks, "halo_records_per_tick": sum(halo) / ticks,
                   "wall_ms_per_tick_all_strips": wall,
                   "note": "W strips of one world on ONE GPU, halo records handed over in-process (LoopbackExchange); "
-                          "per strip: its pipeline stages (hipEvents) and the records it sends its neighbours",
+                          "per strip: its pipeline stages (hipEvents), its strip kernels (prepare = walk + select, finish = "
+                          "absorb + emit, hipEvents on its stream), their sum (ms_device_total) and the records it sends "
+                          "its neighbours",
                   "per_strip": rows}))
