@@ -41,6 +41,10 @@ type Manager struct {
 	pinX    []float32
 	pinZ    []float32
 	nmv     int
+	pushed  int // pending calls already copied to the device (gwaoi_stage_moves_pinned_partial)
+	// PushEvery > 0: every PushEvery Moved calls the filled part of the staging arrays is copied to the
+	// device while the tick goes on (ABI 2.1), so Flush copies only the tail
+	PushEvery int
 	// SyncEnterLeave flushes inside Enter/Leave so their callbacks fire before Space.enter runs the
 	// user hooks (Space.go:211-217), exactly as with the list manager.
 	SyncEnterLeave bool
@@ -57,7 +61,11 @@ func NewXZListAOIManager(aoidist aoi.Coord, capacity uint32, device int) *Manage
 	if v := int(C.gwaoi_abi_version()); v != int(C.GWAOI_ABI_VERSION) {
 		gwlog.Panicf("gwaoi: libgwaoi.so has ABI %d, these headers %d", v, int(C.GWAOI_ABI_VERSION))
 	}
-	g := &Manager{bySlot: make([]*aoi.AOI, capacity), slotOf: map[*aoi.AOI]uint32{}, SyncEnterLeave: true}
+	if int(C.gwaoi_abi_minor()) < 1 {
+		gwlog.Panicf("gwaoi: libgwaoi.so predates ABI 2.1 (gwaoi_stage_moves_pinned_async / _partial)")
+	}
+	g := &Manager{bySlot: make([]*aoi.AOI, capacity), slotOf: map[*aoi.AOI]uint32{}, SyncEnterLeave: true,
+		PushEvery: 65536}
 	for s := int(capacity) - 1; s >= 0; s-- {
 		g.free = append(g.free, uint32(s))
 	}
@@ -73,12 +81,15 @@ func NewXZListAOIManager(aoidist aoi.Coord, capacity uint32, device int) *Manage
 	return g
 }
 
-// pushMoves hands the pending Moved calls to the manager: one cgo crossing, one DMA copy.
+// pushMoves hands the pending Moved calls to the manager: one cgo crossing, one DMA copy of what was not
+// pushed yet. The device checks the batch and its verdict is read by the pass that runs it
+// (gwaoi_stage_moves_pinned_async): a refused batch panics at the next gwaoi_tick, with nothing of it
+// applied, as it would have here.
 func (g *Manager) pushMoves() {
 	if g.nmv > 0 {
 		n := g.nmv
-		g.nmv = 0
-		chk(C.gwaoi_stage_moves_pinned(g.m, C.uint32_t(n)))
+		g.nmv, g.pushed = 0, 0
+		chk(C.gwaoi_stage_moves_pinned_async(g.m, C.uint32_t(n)))
 	}
 }
 
@@ -123,6 +134,10 @@ func (g *Manager) Moved(a *aoi.AOI, x, y aoi.Coord) {
 	g.nmv = k + 1
 	if g.nmv == len(g.pinSlot) {
 		g.pushMoves()
+	} else if g.PushEvery > 0 && g.nmv-g.pushed >= g.PushEvery {
+		// the filled part travels now (asynchronous DMA, nothing staged yet): Flush copies only the tail
+		chk(C.gwaoi_stage_moves_pinned_partial(g.m, C.uint32_t(g.nmv)))
+		g.pushed = g.nmv
 	}
 }
 

@@ -245,6 +245,7 @@ struct SweepArgs {
   const uint32_t* band_hd;
   const uint8_t* band_tab;   // key tables (BandArgs.tab), or null: the key windows are searched
   uint32_t band_tab_half;
+  uint32_t nspaces;      // Spaces of the grid (geom[nspaces])
   uint32_t* size_tiles;  // debug (gwaoi_debug_sweep_sizes): tiles walked in LDS by the small / mid / big sweep, or null
 };
 

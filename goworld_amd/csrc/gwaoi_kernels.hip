@@ -1569,156 +1569,6 @@ __device__ __forceinline__ uint32_t sweep_lds(const SweepArgs& a, S& sm, const M
   return local;
 }
 
-// ---- A/B (verdict r5 #2): the ring walk with G lanes per mover ------------------------------------------
-// GW_SWEEP_GROUP = G > 1: a group of G consecutive lanes walks ONE mover; lane gl of the group judges the
-// candidates gl, gl + G, gl + 2G, ... of the mover's two ring streams, so the lanes of a group read
-// consecutive LDS records (rows of the row stream are contiguous LDS ranges: conflict-free b128 reads)
-// and a mover's ~15 candidates take ~15 / G steps instead of ~15. The mover's setup (slot state, boxes,
-// ring plan, judge) is computed by every lane of its group. Events: one queue range per wave as in
-// emit_masks, numbered inside the group (group prefix of the per-lane counts), then renumbered in the
-// canonical order over the group's contiguous queue range.
-#ifndef GW_SWEEP_GROUP
-#define GW_SWEEP_GROUP 1
-#endif
-constexpr int kSweepGroup = GW_SWEEP_GROUP;
-static_assert(kSweepGroup == 1 || kSweepGroup == 2 || kSweepGroup == 4 || kSweepGroup == 8, "lanes per mover");
-
-// judge candidates b + gl + G i (i < 64: bit i of the mask) of one stream
-template <int G, class S, class IdxF>
-__device__ __forceinline__ unsigned long long judge_chunk_g(const S& sm, const Judge& J, uint32_t b, uint32_t total,
-                                                            uint32_t gl, IdxF&& idx) {
-  const uint32_t s = b + gl;
-  const uint32_t n = s < total ? min((total - s + (uint32_t)G - 1u) / (uint32_t)G, 64u) : 0u;
-  unsigned long long hit = 0;
-  uint32_t i = 0;
-  for (; i + 1 < n; i += 2) {
-    const uint32_t j0 = idx(s + (uint32_t)G * i), j1 = idx(s + (uint32_t)G * (i + 1));
-    const uint4 p0 = sm.rp[j0], p1 = sm.rp[j1];
-    const uint2 q0 = sm.rm[j0], q1 = sm.rm[j1];
-    bool n0, n1;
-    bool h0 = judge_fast(J, p0, q0, n0), h1 = judge_fast(J, p1, q1, n1);
-    if (GW_JUDGE_EXACT || __builtin_expect(n0 | n1, 0)) {
-      h0 = judge_lds(J, p0, q0) != 0;
-      h1 = judge_lds(J, p1, q1) != 0;
-    }
-    hit |= (unsigned long long)((uint32_t)h0 | ((uint32_t)h1 << 1)) << i;
-  }
-  if (i < n) {
-    const uint32_t j0 = idx(s + (uint32_t)G * i);
-    hit |= (unsigned long long)(judge_lds(J, sm.rp[j0], sm.rm[j0]) != 0) << i;
-  }
-  return hit;
-}
-
-// Queue the events of two hit masks (candidates ia(bit), ib(bit)) for every lane of the wave that reached
-// the call (whole groups: a group's lanes are active together); local = lbase + the group prefix. With
-// kSortLocal the group's events (one contiguous queue range) are renumbered in the canonical order.
-// Returns the group's event count (the same in each lane of the group).
-template <int G, bool kSortLocal, class S, class IdxA, class IdxB>
-__device__ __forceinline__ uint32_t emit_masks_g(const SweepArgs& a, S& sm, const Mover& m, const Judge& J,
-                                                 unsigned long long hA, IdxA&& ia, unsigned long long hB, IdxB&& ib,
-                                                 uint32_t lbase, uint32_t& nent, bool sort_on = true) {
-  const uint32_t c = (uint32_t)(__popcll(hA) + __popcll(hB));
-  const int lane = threadIdx.x & 63;
-  const unsigned long long below = (1ull << lane) - 1ull;
-  uint32_t pre = 0, tot = 0;
-  for (int bit = 0; __any((c >> bit) != 0u); ++bit) {
-    const unsigned long long mb = __ballot((c >> bit) & 1u);
-    pre += (uint32_t)__popcll(mb & below) << bit;
-    tot += (uint32_t)__popcll(mb) << bit;
-  }
-  if (tot == 0u) return 0u;  // wave-uniform
-  const int g0 = lane & ~(G - 1);
-  const uint32_t gpre = (uint32_t)__shfl((int)pre, g0, 64);
-  const uint32_t gcnt = (uint32_t)__shfl((int)(pre + c), g0 + G - 1, 64) - gpre;
-  const int leader = __ffsll((long long)__ballot(1)) - 1;
-  uint32_t q0 = 0;
-  if (lane == leader) q0 = atomicAdd(&sm.n, tot);
-  q0 = __builtin_amdgcn_readfirstlane(q0);
-  const uint32_t qs = max(q0, S::kEv);
-  uint32_t g0i = 0;
-  if (q0 + tot > qs) {
-    if (lane == leader) g0i = atomicAdd(&a.ctr[CTR_EVENTS], q0 + tot - qs);
-    g0i = __builtin_amdgcn_readfirstlane(g0i);
-  }
-  uint32_t p = q0 + pre;
-  uint32_t local = lbase + (pre - gpre);
-  auto put = [&](unsigned long long h, auto&& idx) {
-    while (h) {
-      const int bit = __ffsll((long long)h) - 1;
-      const uint32_t j = idx((uint32_t)bit);
-      const bool enter = judge_lds(J, sm.rp[j], sm.rm[j]) == 2;
-      const uint32_t eb = enter ? 0x80000000u : 0u;
-      nent += enter ? 1u : 0u;
-      if (p < S::kEv) {
-        sm.ev[p] = make_uint4(m.rank, local, m.slot, sm.rslot[j] | eb);
-      } else {
-        const uint32_t gi = g0i + (p - qs);
-        if (gi < a.ev_cap) a.ev_tmp[gi] = make_uint4(m.rank, local, m.slot, sm.rslot[j] | eb);
-        asm volatile("" ::: "memory");  // two stores, not one FLAT store (emit_masks)
-      }
-      ++local;
-      ++p;
-      h &= h - 1ull;
-    }
-  };
-  put(hA, ia);
-  put(hB, ib);
-  if (kSortLocal && sort_on && gcnt >= 2u) {
-    const uint32_t p0 = q0 + gpre;  // the group's queue range [p0, p0 + gcnt)
-    if (gcnt <= kSortMax && p0 + gcnt <= S::kEv) {
-      __builtin_amdgcn_wave_barrier();  // the group's writes before its reads (one wave: LDS in order)
-      for (uint32_t i = q0 + pre; i < q0 + pre + c; ++i) {
-        const uint32_t ki = sm.ev[i].w;
-        uint32_t rk = 0;
-        for (uint32_t k = 0; k < gcnt; ++k) rk += sm.ev[p0 + k].w < ki ? 1u : 0u;
-        sm.ev[i].y = lbase + rk;
-      }
-    } else {
-      if ((lane & (G - 1)) == 0) flag_op(a, m.rank);
-      sm.unsorted = 1u;
-    }
-  }
-  return gcnt;
-}
-
-// sweep_lds for lane gl of the mover's G-lane group; returns the mover's event count (every lane of the
-// group). The non-ring walk (rare at config 2: teleports, Enters) runs on the group's first lane alone.
-template <int G, class S>
-__device__ __forceinline__ uint32_t sweep_lds_group(const SweepArgs& a, S& sm, const Mover& m, const Walk& w,
-                                                    const Region& R, uint32_t gl, uint32_t& nent) {
-  const Judge J = make_judge(m, a.base);
-  RingStream Rs, Cs;
-  if (ring_plan(w, R, sm, Rs, Cs)) {
-    auto ri = [&](uint32_t k) { return stream_at(Rs, k); };
-    auto ci = [&](uint32_t k) { return (uint32_t)sm.cidx[stream_at(Cs, k)]; };
-    // (the usual ring: both streams in one chunk of 64 G candidates, one emission, canonical numbering;
-    // longer streams chunk by chunk, numbered in walk order and flagged for k_slice_sort)
-    const bool one = __all(Rs.total <= 64u * G && Cs.total <= 64u * G);
-    uint32_t local = 0;
-    for (uint32_t b = 0; __any(b < Rs.total || b < Cs.total); b += 64u * G) {
-      const unsigned long long hR = judge_chunk_g<G>(sm, J, b, Rs.total, gl, ri);
-      const unsigned long long hC = judge_chunk_g<G>(sm, J, b, Cs.total, gl, ci);
-      local += emit_masks_g<G, true>(
-          a, sm, m, J, hR, [&](uint32_t i) { return ri(b + gl + (uint32_t)G * i); }, hC,
-          [&](uint32_t i) { return ci(b + gl + (uint32_t)G * i); }, local, nent, one);
-    }
-    if (!one && local > 1u && gl == 0) flag_op(a, m.rank), sm.unsorted = 1u;
-    return local;
-  }
-  uint32_t local = 0;
-  if (gl == 0) {
-    walk_cells(w, [&](int r, int c0, int c1) {
-      const int b = (r - R.zr0) * R.ncols - R.xr0;
-      const uint32_t j = sm.lcs[b + c0];
-      const uint32_t e = (c0 <= c1) ? (uint32_t)sm.lcs[b + c1 + 1] : j;
-      judge_stream(a, sm, J, m, e - j, [&](uint32_t k) { return j + k; }, local, nent);
-    });
-    if (local > 1u) flag_op(a, m.rank), sm.unsorted = 1u;
-  }
-  return local;
-}
-
 // exclusive scan of v over a kB-thread block; *total = block sum (LDS scratch `ws`)
 template <int kB = kSweepBlock>
 __device__ __forceinline__ uint32_t block_excl_scan_big(uint32_t v, uint32_t* ws, uint32_t* total) {
@@ -2039,24 +1889,7 @@ __device__ __forceinline__ void sweep_item(const SweepArgs& a, SweepSmemT<C>& sm
     }
   } else {
     const uint32_t nm = sm.nmv;
-    if (kSweepGroup > 1 && a.use_lds != 2) {  // A/B: G lanes per mover (sweep_lds_group)
-      constexpr uint32_t G = (uint32_t)kSweepGroup, kGroups = (uint32_t)kSweepBlock / G;
-      const uint32_t gl = threadIdx.x & (G - 1u), gi = threadIdx.x / G;
-      for (uint32_t r = 0; r * kGroups < nm; ++r) {
-        const uint32_t p = r * kGroups + ((r & 1u) ? kGroups - 1u - gi : gi);
-        if (p >= nm) continue;  // (whole groups)
-        const Mover m = lds_mover(sm, sm.mv[p], a.base, g.D);
-        const CellBox A0 = qbox(g, m.mx0, m.mz0), A1 = qbox(g, m.mx1, m.mz1);
-        const bool in_lds = R.holds(A1) && (!m.valid0 || R.holds(A0));
-        const uint32_t di = wave_append(&a.ctr[CTR_DENSE], !in_lds && gl == 0u);
-        if (!in_lds) {
-          if (gl == 0u && di < a.dense_cap) a.dense[di] = m.slot;
-          continue;
-        }
-        const uint32_t cnt = sweep_lds_group<kSweepGroup>(a, sm, m, make_walk(m, g, A0, A1), R, gl, nent);
-        if (gl == 0u) put_count(a.rank_cnt, m.rank, cnt);
-      }
-    } else if (a.use_lds != 2) {  // 2: ablation (timing only), staging and ordering without the walk
+    if (a.use_lds != 2) {  // 2: ablation (timing only), staging and ordering without the walk
       // (one wave per mover for a tile's few movers beyond a full round: measured 110 -> 123 us; the
       // planner sizes tiles below one round instead, compute_geometry)
       for (uint32_t r = 0; r * kSweepBlock < nm; ++r) {
@@ -2212,6 +2045,7 @@ constexpr uint32_t kBandSearchMin = GW_BAND_SEARCH_MIN;
 #ifndef GW_BAND_TABLE  // 1: key tables (one lookup per searched cell); 0: the fanout-4 key search (A/B)
 #define GW_BAND_TABLE 1
 #endif
+constexpr uint32_t kBandLdsGeoms = 16;  // Spaces whose geometry the band walk keeps in LDS
 // The bucket of key k inside cell c (column for x keys, row for z keys) of a Space with origin o and 1 / side
 // inv: 64 equal parts of the cell, clamped (keys of a clamped border cell lie outside it). Monotone in k (every
 // step is), which is all the key tables need: the builder (k_band_sort) and the walk use this one function.
@@ -2810,6 +2644,16 @@ k_sweep_band(SweepArgs a) {
   __shared__ float2 je[kDenseBlock / 64][64];    // per batch mover: {D, eps} of its judge
   __shared__ uint32_t lc[kDenseBlock / 64][64];  // per batch mover: its events so far
   __shared__ uint32_t orow[kDenseBlock / 64][128];  // stream_owners' marks
+#if GW_BAND_TABLE
+  // the Spaces' {x0, z0, 1 / cell side, D} for the key tables' buckets, in LDS (a global load per item round
+  // was one more dependent round trip before the tables could be read); more Spaces: read from the grid
+  __shared__ float4 sgq[kBandLdsGeoms];
+  const bool lgq = a.nspaces <= kBandLdsGeoms;
+  if (lgq)
+    for (uint32_t k = threadIdx.x; k < a.nspaces; k += kDenseBlock)
+      sgq[k] = *reinterpret_cast<const float4*>(&a.g.geom[k]);
+  __syncthreads();
+#endif
 #if GW_STAMPS
   unsigned long long dph[16] = {}, dt0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2905,7 +2749,8 @@ k_sweep_band(SweepArgs a) {
           if (kind[u] == 0 && ((r >= P.rb0 && r <= P.rb1) || (r >= P.rt0 && r <= P.rt1)))
             dd[u] = c >= P.cl0 && c <= P.cl1 ? 1 : 2;
           cl[u] = kind[u] == 1 ? r : c;
-          gq[u] = *reinterpret_cast<const float4*>(&a.g.geom[mb[wv][k][0].y]);  // (x0, z0, inv_c, D lead Geom)
+          const uint32_t sp = mb[wv][k][0].y;
+          gq[u] = lgq ? sgq[sp] : *reinterpret_cast<const float4*>(&a.g.geom[sp]);  // (x0, z0, inv_c, D lead Geom)
 #endif
           // (cell_key on the Space's base and tile columns)
           p0[u] = sg.x + ((uint32_t)((r >> kTileShift) * (int)sg.y + (c >> kTileShift)) << kTileCellShift) +

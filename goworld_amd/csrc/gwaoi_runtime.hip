@@ -414,10 +414,7 @@ void compute_geometry(gwaoi_mgr* m, std::vector<gw::Geom>& out) {
     const double maxc = std::max({std::fabs((double)x0), std::fabs((double)x1), std::fabs((double)z0),
                                   std::fabs((double)z1)});
     const double span = ((double)sh.desc.dist * (1.0 + 1e-5) + (maxc + sh.desc.dist) * 1e-6) / c;
-#ifndef GW_REACH_STEP  // A/B: halo cells beyond the box span (movers whose boxes leave the region go global)
-#define GW_REACH_STEP 1.0
-#endif
-    int reach = (int)std::ceil(span + GW_REACH_STEP);
+    int reach = (int)std::ceil(span) + 1;  // (ceil(span + 0.25): config 2 -0.7%, skew +1.3%, r06_a2: not kept)
     g.pad = 0;
     const int rw = gw::kTile + 2 * reach;  // region width (cells)
     if (rw * rw > gw::kSweepRegCells) {  // the small LDS sweep's region budget: not this Space
@@ -1168,6 +1165,7 @@ int run_pass_core(gwaoi_mgr* m, bool copy_events) {
     s.band_tab = keys ? m->band_tab : nullptr;
     s.band_tab_half = m->band_tab_half;
     s.size_tiles = m->d_size_tiles;
+    s.nspaces = m->nspaces;
     gw::launch_sweep(s, st);
     HIPCHK(hipGetLastError());
     if (m->timing) HIPCHK(hipEventRecord(m->tev[3], st));

@@ -86,9 +86,11 @@ __global__ void __launch_bounds__(kSBlock) k_strip_init_skew(gwaoi_strip_geom g,
 
 __global__ void __launch_bounds__(kSBlock) k_strip_walk(gwaoi_strip_geom g, uint8_t* flags, const float* sx,
                                                         const float* sz, float* ex, float* ez, uint64_t seed,
-                                                        uint64_t tick, float L, float step, uint32_t* err) {
-  const uint32_t i = blockIdx.x * kSBlock + threadIdx.x;
-  if (i >= g.n) return;
+                                                        uint64_t tick, float L, float step, uint32_t* err,
+                                                        const uint32_t* rl, const uint32_t* nrl) {
+  const uint32_t k = blockIdx.x * kSBlock + threadIdx.x;
+  if (k >= (rl ? *nrl : g.n)) return;
+  const uint32_t i = rl ? rl[k] : k;  // (a region list: list position k)
   const uint8_t f = flags[i];
   if (!(f & GWAOI_STRIP_OWNED)) return;
   const float x0 = sx[i];
@@ -130,17 +132,21 @@ inline uint32_t sel_items(uint32_t n) {
   const uint32_t want = (n + 1024u * kSBlock - 1) / (1024u * kSBlock);
   return want < 4 ? 4u : want > (uint32_t)kSelItems ? (uint32_t)kSelItems : want;
 }
+// rl (region list, ABI 2.1): the positions walked are list positions (ids rl[k], k < *nrl), not ids
 __global__ void __launch_bounds__(kSBlock) k_strip_select(gwaoi_strip_geom g, const uint8_t* flags, const float* sx,
                                                           const float* ex, const float* ez, uint4* left,
                                                           uint4* right, uint32_t cap, uint32_t* counts,
-                                                          uint32_t* err, uint32_t items) {
+                                                          uint32_t* err, uint32_t items, const uint32_t* rl,
+                                                          const uint32_t* nrl) {
   __shared__ uint32_t base_sh[2];
   const uint32_t c0 = blockIdx.x * kSBlock * items + threadIdx.x;
+  const uint32_t n = rl ? *nrl : g.n;
   unsigned long long ml = 0, mr = 0;
 #pragma unroll 4
   for (int r = 0; r < (int)items; ++r) {
-    const uint32_t i = c0 + (uint32_t)r * kSBlock;
-    if (i >= g.n) break;
+    const uint32_t k = c0 + (uint32_t)r * kSBlock;
+    if (k >= n) break;
+    const uint32_t i = rl ? rl[k] : k;
     const uint8_t f = flags[i];
     if ((f & GWAOI_STRIP_OWNED) && (f & GWAOI_STRIP_END)) {
       const float x0 = sx[i], x1 = ex[i];
@@ -162,7 +168,7 @@ __global__ void __launch_bounds__(kSBlock) k_strip_select(gwaoi_strip_geom g, co
   while (m) {
     const int r = __ffsll((long long)m) - 1;
     m &= m - 1ull;
-    const uint32_t i = c0 + (uint32_t)r * kSBlock;
+    const uint32_t i = rl ? rl[c0 + (uint32_t)r * kSBlock] : c0 + (uint32_t)r * kSBlock;
     const uint4 rec = make_uint4(i, __float_as_uint(ex[i]), __float_as_uint(ez[i]), 0u);
     if ((ml >> r) & 1ull) {
       if (pl < cap) left[pl] = rec;
@@ -177,8 +183,11 @@ __global__ void __launch_bounds__(kSBlock) k_strip_select(gwaoi_strip_geom g, co
   }
 }
 
+// nw (region list, ABI 2.1): the received ids not present in the region at the start of the tick (they
+// enter it) are appended to nw (count nctr[0]; beyond cap_new: nctr[1] |= GWAOI_STRIP_ERR_NEWLIST)
 __global__ void __launch_bounds__(kSBlock) k_strip_absorb(uint8_t* flags, float* ex, float* ez, const uint4* recs,
-                                                          uint32_t n, const uint32_t* d_n, uint32_t* err) {
+                                                          uint32_t n, const uint32_t* d_n, uint32_t* err, uint32_t* nw,
+                                                          uint32_t* nctr, uint32_t cap_new) {
   const uint32_t k = blockIdx.x * kSBlock + threadIdx.x;
   if (d_n) {  // received count (device): the launch covers the message's capacity
     const uint32_t got = *d_n;
@@ -187,11 +196,22 @@ __global__ void __launch_bounds__(kSBlock) k_strip_absorb(uint8_t* flags, float*
     if (got > n && k == 0 && err) atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
     n = min(n, got);
   }
-  if (k >= n) return;
-  const uint4 r = recs[k];
-  ex[r.x] = __uint_as_float(r.y);
-  ez[r.x] = __uint_as_float(r.z);
-  flags[r.x] |= GWAOI_STRIP_END;
+  bool fresh = false;
+  uint4 r = make_uint4(0u, 0u, 0u, 0u);
+  if (k < n) {
+    r = recs[k];
+    const uint8_t f = flags[r.x];
+    fresh = !(f & GWAOI_STRIP_PRESENT);
+    ex[r.x] = __uint_as_float(r.y);
+    ez[r.x] = __uint_as_float(r.z);
+    flags[r.x] = f | GWAOI_STRIP_END;
+  }
+  if (!nw) return;  // grid-uniform
+  const uint32_t j = wave_append_s(&nctr[0], fresh);
+  if (fresh) {
+    if (j < cap_new) nw[j] = r.x;
+    else atomicOr(&nctr[1], GWAOI_STRIP_ERR_NEWLIST);
+  }
 }
 
 // 16 flags of thread `t` of block `b` (ids b * kSChunk + t * 16 ...), zero beyond n
@@ -403,6 +423,177 @@ __global__ void __launch_bounds__(kSBlock) k_translate(const uint32_t* l2g, uint
   ev[2 * k + 1] = l2g[o & 0x7FFFFFFFu] | (o & 0x80000000u);
 }
 
+// ---- region lists (ABI 2.1): the per-tick kernels over the ids present in the region, not the id range ----
+// List counters (gwaoi_strip_list.ctr): [0] length of rl, [1] 1 when the last list emit emitted, [2] new ids
+// (nw), [3] error bits.
+constexpr uint32_t kNewSortCap = 16384;  // ids one tick may bring into the region (one block's LDS sort)
+
+// the tick's new ids sorted ascending in place (one 1024-thread block, bitonic in LDS); more than fit: the
+// error bit, and the emit emits nothing
+__global__ void __launch_bounds__(1024) k_sl_sort_new(uint32_t* nw, uint32_t* lc, uint32_t cap_new) {
+  __shared__ uint32_t sk[kNewSortCap];
+  const uint32_t n = lc[2];
+  if (n > cap_new || n > kNewSortCap) {
+    if (threadIdx.x == 0) atomicOr(&lc[3], GWAOI_STRIP_ERR_NEWLIST);
+    return;
+  }
+  if (n < 2) return;
+  uint32_t P = 64;
+  while (P < n) P <<= 1;
+  for (uint32_t i = threadIdx.x; i < P; i += 1024) sk[i] = i < n ? nw[i] : 0xFFFFFFFFu;
+  __syncthreads();
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < P; i += 1024) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const uint32_t u = sk[i], v = sk[l];
+          if ((u > v) == ((i & k) == 0)) sk[i] = v, sk[l] = u;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < n; i += 1024) nw[i] = sk[i];
+}
+
+// first index of a[0, n) (ascending) not below v
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t v) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// k_strip_emit_local over the merge of the region list rl (present: Moved or Leave) and the sorted new ids
+// (Enter): thread t takes list entry t (t < nrl) or new id t - nrl, and places its op at its merged position
+// (its own index + the other list's entries below it, a binary search), so the op list is in global id order
+// as the id-range emit's. The tick's Enters are exactly the new ids: they must fit the free slots.
+__global__ void __launch_bounds__(kSBlock) k_sl_emit_local(gwaoi_strip_geom g, const uint32_t* rl, const uint32_t* nw,
+                                                           uint32_t* lc, uint8_t* flags, float* sx, float* sz,
+                                                           const float* ex, const float* ez, uint32_t* slots, float* ox,
+                                                           float* oz, uint8_t* kinds, uint32_t* g2l, uint32_t* l2g,
+                                                           const uint32_t* fq, uint32_t* pend, uint32_t mask,
+                                                           uint32_t* ctr, const uint32_t* sc, uint32_t* n_ops) {
+  const uint32_t t = blockIdx.x * kSBlock + threadIdx.x;
+  const uint32_t nrl = lc[0], nnew = lc[2], total = nrl + nnew;
+  const uint32_t tail = ctr[1];
+  const bool fits = !(lc[3] & GWAOI_STRIP_ERR_NEWLIST) && nnew <= sc[0];  // grid-uniform
+  if (t == 0) {
+    *n_ops = fits ? total : 0u;
+    lc[1] = fits ? 1u : 0u;
+    if (!fits && !(lc[3] & GWAOI_STRIP_ERR_NEWLIST)) atomicOr(&ctr[3], GWAOI_STRIP_ERR_SLOTS);
+  }
+  if (!fits) return;
+  uint32_t i = 0, q = 0;
+  uint8_t f = 0;
+  const bool op = t < total;
+  if (op) {
+    if (t < nrl) {
+      i = rl[t];
+      q = t + lower_bound_u32(nw, nnew, i);
+    } else {
+      i = nw[t - nrl];
+      q = (t - nrl) + lower_bound_u32(rl, nrl, i);
+    }
+    f = flags[i];
+  }
+  const bool p = f & GWAOI_STRIP_PRESENT, e = f & GWAOI_STRIP_END;
+  const uint32_t ka = wave_append_s(&ctr[0], op && !p);       // Enter: allocation index
+  const uint32_t kl = wave_append_s(&ctr[2], op && p && !e);  // Leave: pending index
+  if (!op) return;
+  uint8_t kind = p ? (e ? GWAOI_OP_MOVE : GWAOI_OP_LEAVE) : GWAOI_OP_ENTER;
+  if (!(f & GWAOI_STRIP_OWNED)) kind |= GWAOI_OP_SILENT;
+  uint32_t l;
+  if (!p) {
+    if ((int)(tail - ka) <= 0) {  // ring empty (excluded by the check above; kept as a guard)
+      atomicOr(&ctr[3], GWAOI_STRIP_ERR_SLOTS);
+      l = 0u;
+    } else {
+      l = fq[ka & mask];
+      g2l[i] = l;
+      l2g[l] = i;
+    }
+  } else {
+    l = g2l[i];
+    if (!e) {
+      pend[kl] = l;
+      g2l[i] = GWAOI_STRIP_NO_SLOT;
+    }
+  }
+  float x = 0.f, z = 0.f;
+  uint8_t nf = 0;
+  if (e) {
+    x = ex[i];
+    z = ez[i];
+    sx[i] = x;
+    sz[i] = z;
+    nf = GWAOI_STRIP_PRESENT | (in_range(x, g.xa, g.xb) ? GWAOI_STRIP_OWNED : 0);
+  }
+  slots[q] = l;
+  ox[q] = x;
+  oz[q] = z;
+  kinds[q] = kind;
+  flags[i] = nf;
+}
+
+// The next tick's region list from a tick's op list: the ids of the ops that are not Leaves, in op (= id)
+// order. Counts per kSChunk ops, a scan, then each chunk's ids written (ballot ranks, wave totals in LDS).
+// The id of an op: l2g[slot] (local slots; a Leave's slot is recycled only at the next emit) or the slot.
+__device__ __forceinline__ bool keeps(uint8_t k) { return (k & OP_KIND) != GWAOI_OP_LEAVE; }
+__global__ void __launch_bounds__(kSBlock) k_sl_keep_count(const uint8_t* kinds, const uint32_t* n_ops, uint32_t* blk) {
+  const uint32_t n = *n_ops;
+  uint32_t c = 0;
+  for (int r = 0; r < kSItems; ++r) {
+    const uint32_t q = blockIdx.x * kSChunk + (uint32_t)r * kSBlock + threadIdx.x;
+    c += (q < n && keeps(kinds[q])) ? 1u : 0u;
+  }
+  uint32_t tot;
+  block_scan_s(c, &tot);
+  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+// nb: the count kernel's chunks. lc[1] == 0 (the list emit emitted nothing: new ids over the list path's
+// capacity, or no free slots): rl is copied unchanged, so the caller's swap keeps the list of the tick.
+__global__ void __launch_bounds__(kSBlock) k_sl_keep_write(const uint8_t* kinds, const uint32_t* slots,
+                                                           const uint32_t* l2g, const uint32_t* n_ops,
+                                                           const uint32_t* blk, uint32_t nb, const uint32_t* rl,
+                                                           uint32_t* rl_next, uint32_t* lc, int from_emit) {
+  __shared__ uint32_t wsum[2][kSBlock / 64];
+  if (from_emit && !lc[1]) {  // grid-uniform
+    const uint32_t nrl = lc[0];
+    for (uint32_t k = blockIdx.x * kSBlock + threadIdx.x; k < nrl; k += gridDim.x * kSBlock) rl_next[k] = rl[k];
+    return;
+  }
+  const uint32_t n = *n_ops;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  uint32_t pos = blk[blockIdx.x];
+  for (int r = 0; r < kSItems; ++r) {
+    const uint32_t q = blockIdx.x * kSChunk + (uint32_t)r * kSBlock + threadIdx.x;
+    const bool keep = q < n && keeps(kinds[q]);
+    const unsigned long long m = __ballot(keep);
+    if (lane == 0) wsum[r & 1][w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSBlock / 64; ++k) {
+      const uint32_t v = wsum[r & 1][k];
+      off += k < w ? v : 0u;
+      tot += v;
+    }
+    if (keep) rl_next[pos + off + (uint32_t)__popcll(m & below)] = l2g ? l2g[slots[q]] : slots[q];
+    pos += tot;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next tick's list length; no new ids yet (lc[1]: the emit's)
+    lc[0] = blk[nb];
+    lc[2] = 0u;
+  }
+}
+
 inline dim3 blocks_for(uint32_t n) { return dim3((n + kSBlock - 1) / kSBlock); }
 // the free-slot ring of cap_l local slots: the next power of two entries (index mask)
 inline uint32_t ring_mask(uint32_t cap_l) {
@@ -431,7 +622,7 @@ int gwaoi_strip_walk(void* stream, const gwaoi_strip_geom* g, uint8_t* flags, co
   if (!g || !flags || !sx || !sz || !ex || !ez || !d_err) return GWAOI_ERR_INVALID;
   if (g->n)
     hipLaunchKernelGGL(gw::k_strip_walk, gw::blocks_for(g->n), dim3(gw::kSBlock), 0, (hipStream_t)stream, *g, flags,
-                       sx, sz, ex, ez, seed, tick, L, step, d_err);
+                       sx, sz, ex, ez, seed, tick, L, step, d_err, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 
@@ -453,7 +644,7 @@ int gwaoi_strip_select(void* stream, const gwaoi_strip_geom* g, const uint8_t* f
     const uint32_t items = gw::sel_items(g->n), chunk = gw::kSBlock * items;
     hipLaunchKernelGGL(gw::k_strip_select, dim3((g->n + chunk - 1) / chunk), dim3(gw::kSBlock), 0, (hipStream_t)stream,
                        *g, flags, sx, ex, ez, reinterpret_cast<uint4*>(d_left), reinterpret_cast<uint4*>(d_right), cap,
-                       d_counts, d_err, items);
+                       d_counts, d_err, items, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
   }
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
@@ -462,7 +653,8 @@ int gwaoi_strip_absorb(void* stream, uint8_t* flags, float* ex, float* ez, const
   if (!flags || !ex || !ez || (n && !d_recs)) return GWAOI_ERR_INVALID;
   if (n)
     hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n), dim3(gw::kSBlock), 0, (hipStream_t)stream, flags, ex, ez,
-                       reinterpret_cast<const uint4*>(d_recs), n, (const uint32_t*)nullptr, (uint32_t*)nullptr);
+                       reinterpret_cast<const uint4*>(d_recs), n, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr, (uint32_t*)nullptr, 0u);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 
@@ -471,7 +663,8 @@ int gwaoi_strip_absorb_n(void* stream, uint8_t* flags, float* ex, float* ez, con
   if (!flags || !ex || !ez || !d_n || (n_max && !d_recs)) return GWAOI_ERR_INVALID;
   // one block at least: the overflow check runs even for a zero-capacity message
   hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n_max ? n_max : 1u), dim3(gw::kSBlock), 0, (hipStream_t)stream,
-                     flags, ex, ez, reinterpret_cast<const uint4*>(d_recs), n_max, d_n, d_err);
+                     flags, ex, ez, reinterpret_cast<const uint4*>(d_recs), n_max, d_n, d_err, (uint32_t*)nullptr,
+                     (uint32_t*)nullptr, 0u);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 
@@ -546,6 +739,90 @@ int gwaoi_strip_emit_local(void* stream, const gwaoi_strip_geom* g, uint8_t* fla
     return GWAOI_ERR_HIP;
   }
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+// ---- region lists (ABI 2.1) ----
+static bool list_ok(const gwaoi_strip_list* L) {
+  return L && L->rl && L->rl_next && L->nw && L->ctr && L->scratch && L->cap && L->cap_new &&
+         L->cap_new <= gw::kNewSortCap && L->cap <= 0x7fffffffu - gw::kNewSortCap;
+}
+
+// (the emit's op list holds up to cap + cap_new ops: the list's ids and the new ones, Leaves included)
+size_t gwaoi_strip_list_scratch_words(uint32_t cap) { return gwaoi_strip_scratch_words(cap + gw::kNewSortCap) + 4; }
+
+// rl_next from a tick's op list (the caller swaps rl and rl_next afterwards): the list after a full
+// (id-range) emit, e.g. the Enter pass of tick 0
+static int list_keep(hipStream_t st, const gwaoi_strip_list* L, const uint8_t* kinds, const uint32_t* slots,
+                     const uint32_t* l2g, const uint32_t* d_n_ops, int from_emit) {
+  const uint32_t nb = gw::emit_blocks(L->cap + L->cap_new);  // the op list's bound
+  uint32_t* blk = L->scratch + 4;  // [nb + 1]
+  gw::ScanCtx sc;
+  sc.status = blk + nb + 1;
+  if (!nb) return GWAOI_OK;
+  hipLaunchKernelGGL(gw::k_sl_keep_count, dim3(nb), dim3(gw::kSBlock), 0, st, kinds, d_n_ops, blk);
+  if (hipMemsetAsync(blk + nb, 0, sizeof(uint32_t), st) != hipSuccess) return GWAOI_ERR_HIP;
+  gw::launch_scan(sc, blk, nb + 1, st);
+  hipLaunchKernelGGL(gw::k_sl_keep_write, dim3(nb), dim3(gw::kSBlock), 0, st, kinds, slots, l2g, d_n_ops,
+                     (const uint32_t*)blk, nb, (const uint32_t*)L->rl, L->rl_next, L->ctr, from_emit);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_list_from_ops(void* stream, const gwaoi_strip_list* L, const uint32_t* d_slots, const uint8_t* d_kinds,
+                              const uint32_t* l2g, const uint32_t* d_n_ops) {
+  if (!list_ok(L) || !d_slots || !d_kinds || !d_n_ops) return GWAOI_ERR_INVALID;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(L->ctr, 0, 4 * sizeof(uint32_t), st) != hipSuccess) return GWAOI_ERR_HIP;
+  return list_keep(st, L, d_kinds, d_slots, l2g, d_n_ops, 0);
+}
+
+int gwaoi_strip_walk_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, uint8_t* flags,
+                          const float* sx, const float* sz, float* ex, float* ez, uint64_t seed, uint64_t tick,
+                          float Lw, float step, uint32_t* d_err) {
+  if (!g || !list_ok(L) || !flags || !sx || !sz || !ex || !ez || !d_err) return GWAOI_ERR_INVALID;
+  hipLaunchKernelGGL(gw::k_strip_walk, gw::blocks_for(L->cap), dim3(gw::kSBlock), 0, (hipStream_t)stream, *g, flags,
+                     sx, sz, ex, ez, seed, tick, Lw, step, d_err, (const uint32_t*)L->rl, (const uint32_t*)L->ctr);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_select_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, const uint8_t* flags,
+                            const float* sx, const float* ex, const float* ez, uint32_t* d_left, uint32_t* d_right,
+                            uint32_t cap, uint32_t* d_counts, uint32_t* d_err) {
+  if (!g || !list_ok(L) || !flags || !sx || !ex || !ez || !d_left || !d_right || !d_counts || !d_err)
+    return GWAOI_ERR_INVALID;
+  if (hipMemsetAsync(d_counts, 0, 2 * sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return GWAOI_ERR_HIP;
+  const uint32_t items = gw::sel_items(L->cap), chunk = gw::kSBlock * items;
+  hipLaunchKernelGGL(gw::k_strip_select, dim3((L->cap + chunk - 1) / chunk), dim3(gw::kSBlock), 0, (hipStream_t)stream,
+                     *g, flags, sx, ex, ez, reinterpret_cast<uint4*>(d_left), reinterpret_cast<uint4*>(d_right), cap,
+                     d_counts, d_err, items, (const uint32_t*)L->rl, (const uint32_t*)L->ctr);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_absorb_list(void* stream, const gwaoi_strip_list* L, uint8_t* flags, float* ex, float* ez,
+                            const uint32_t* d_recs, const uint32_t* d_n, uint32_t n_max, uint32_t* d_err) {
+  if (!list_ok(L) || !flags || !ex || !ez || (n_max && !d_recs)) return GWAOI_ERR_INVALID;
+  hipLaunchKernelGGL(gw::k_strip_absorb, gw::blocks_for(n_max ? n_max : 1u), dim3(gw::kSBlock), 0, (hipStream_t)stream,
+                     flags, ex, ez, reinterpret_cast<const uint4*>(d_recs), n_max, d_n, d_err, L->nw, L->ctr + 2,
+                     L->cap_new);
+  return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
+}
+
+int gwaoi_strip_emit_local_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, uint8_t* flags,
+                                float* sx, float* sz, const float* ex, const float* ez, uint32_t* d_slots, float* d_x,
+                                float* d_z, uint8_t* d_kinds, uint32_t* d_n_ops, uint32_t* g2l, uint32_t* l2g,
+                                uint32_t* fq, uint32_t* pend, uint32_t cap_l, uint32_t* ctr) {
+  if (!g || !list_ok(L) || !flags || !sx || !sz || !ex || !ez || !d_slots || !d_x || !d_z || !d_kinds || !d_n_ops ||
+      !g2l || !l2g || !fq || !pend || !ctr || !cap_l || cap_l > 0x80000000u)
+    return GWAOI_ERR_INVALID;
+  hipStream_t st = (hipStream_t)stream;
+  const uint32_t mask = gw::ring_mask(cap_l);
+  uint32_t* spare = L->scratch;  // [4]: free slots after the release
+  hipLaunchKernelGGL(gw::k_local_release, dim3(1), dim3(1024), 0, st, fq, (const uint32_t*)pend, mask, ctr, spare);
+  hipLaunchKernelGGL(gw::k_sl_sort_new, dim3(1), dim3(1024), 0, st, L->nw, L->ctr, L->cap_new);
+  hipLaunchKernelGGL(gw::k_sl_emit_local, gw::blocks_for(L->cap + L->cap_new), dim3(gw::kSBlock), 0, st, *g,
+                     (const uint32_t*)L->rl, (const uint32_t*)L->nw, L->ctr, flags, sx, sz, ex, ez, d_slots, d_x, d_z,
+                     d_kinds, g2l, l2g, (const uint32_t*)fq, pend, mask, ctr, (const uint32_t*)spare, d_n_ops);
+  if (hipGetLastError() != hipSuccess) return GWAOI_ERR_HIP;
+  return list_keep(st, L, d_kinds, d_slots, l2g, d_n_ops, 1);
 }
 
 int gwaoi_strip_translate_events(void* stream, const uint32_t* l2g, uint32_t* d_events, uint32_t n) {

@@ -30,6 +30,7 @@ from .engine import Engine
 
 f32 = np.float32
 STRIP_ERR_SLOTS = 8  # GWAOI_STRIP_ERR_SLOTS (include/gwaoi_strips.h)
+STRIP_ERR_NEWLIST = 16  # GWAOI_STRIP_ERR_NEWLIST
 
 
 class StripLayout:
@@ -108,9 +109,13 @@ class StripNode:
 
     def __init__(self, layout: StripLayout, rank: int, n: int, device: int = 0, seed: int = 0x5EED0004,
                  halo_cap: Optional[int] = None, skew: Optional[Tuple[int, float, int]] = None,
-                 local_slots: bool = True, cap_l: Optional[int] = None):
+                 local_slots: bool = True, cap_l: Optional[int] = None, region_list: bool = True,
+                 cap_new: int = 16384):
         """skew = (nhot, sigma, hot_every): the skewed-crowd placement of config 5 instead of uniform.
-        local_slots: the manager sees local slots (gwaoi_strip_emit_local); False: slot = global id."""
+        local_slots: the manager sees local slots (gwaoi_strip_emit_local); False: slot = global id.
+        region_list (local slots only, ABI 2.1): the per-tick strip kernels walk the ids present in the region
+        (gwaoi_strip_*_list) instead of the world's id range; cap_new: ids one tick may bring into the region
+        on that path (more: that tick is emitted by id range and the list rebuilt)."""
         self.layout, self.rank, self.n, self.seed = layout, int(rank), int(n), int(seed)
         self.skew = skew
         self.g = layout.geom(rank, n)
@@ -165,6 +170,20 @@ class StripNode:
             check(self._L.gwaoi_strip_local_init(ctypes.c_void_p(0), n, self.cap_l, _ptr(self.g2l), _ptr(self.fq),
                                                  _ptr(self.lctr)))
             torch.cuda.synchronize(dev)
+        self.lst = None
+        if self.local and region_list and hasattr(self._L, "gwaoi_strip_emit_local_list"):
+            cn = max(1, min(int(cap_new), 16384))
+            self.rl = torch.zeros(self.cap_l, dtype=i32, device=dev)
+            self.rl_next = torch.zeros(self.cap_l, dtype=i32, device=dev)
+            self.nw = torch.zeros(cn, dtype=i32, device=dev)
+            self.lctr2 = torch.zeros(4, dtype=i32, device=dev)
+            self.h_lctr2 = torch.zeros(4, dtype=i32).pin_memory()
+            self.lscratch = torch.zeros(int(self._L.gwaoi_strip_list_scratch_words(self.cap_l)), dtype=i32, device=dev)
+            self.lst = _lib.StripList()
+            self.lst.nw, self.lst.ctr = self.nw.data_ptr(), self.lctr2.data_ptr()
+            self.lst.scratch, self.lst.cap, self.lst.cap_new = self.lscratch.data_ptr(), self.cap_l, cn
+            self._set_list()
+            torch.cuda.synchronize(dev)
         self.eng = Engine(layout.dist, capacity=self.cap_l if self.local else n, device=device,
                           bounds=(lo, 0.0, hi, layout.L))
         self.eng.set_stream(self.stream.cuda_stream)
@@ -177,6 +196,21 @@ class StripNode:
         self.sev = []
 
     # ---- raw kernel calls ----
+    def _set_list(self):
+        self.lst.rl, self.lst.rl_next = self.rl.data_ptr(), self.rl_next.data_ptr()
+
+    def _swap_list(self):
+        """The emit wrote the next tick's list into rl_next: it becomes rl."""
+        self.rl, self.rl_next = self.rl_next, self.rl
+        self._set_list()
+
+    def _list_from_ops(self):
+        """The region list from the tick's op list (after an id-range emit: tick 0, or a tick with more new
+        ids than the list emit takes)."""
+        check(self._L.gwaoi_strip_list_from_ops(self._s(), ctypes.byref(self.lst), _ptr(self.ids), _ptr(self.kinds),
+                                                _ptr(self.l2g), ctypes.c_void_p(self.counts.data_ptr() + 8)))
+        self._swap_list()
+
     def _s(self):
         return ctypes.c_void_p(self.stream.cuda_stream)
 
@@ -186,16 +220,31 @@ class StripNode:
     def _err(self):
         return ctypes.c_void_p(self.counts.data_ptr() + 12)
 
-    def _emit_and_tick(self, host_events: bool, n_bound: int):
+    def _emit_and_tick(self, host_events: bool, n_bound: int, by_range: bool = False):
         """The op list goes to the manager with its count in device memory (no host round trip);
-        n_bound bounds it: entities present at the start + records received this tick."""
+        n_bound bounds it: entities present at the start + records received this tick. With a region list
+        the emit merges the list with the tick's new ids (by_range: the id-range emit, then the list is
+        rebuilt from the op list: tick 0, or the recovery of a tick with too many new ids)."""
         L = self._L
         common = (self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz), _ptr(self.ex), _ptr(self.ez),
                   _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds), _ptr(self.scratch),
                   ctypes.c_void_p(self.counts.data_ptr() + 8))
-        if self.local:
+        use_list = self.lst is not None and not by_range
+        if use_list:
+            check(L.gwaoi_strip_emit_local_list(self._s(), self._g(), ctypes.byref(self.lst), _ptr(self.flags),
+                                                _ptr(self.sx), _ptr(self.sz), _ptr(self.ex), _ptr(self.ez),
+                                                _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds),
+                                                ctypes.c_void_p(self.counts.data_ptr() + 8), _ptr(self.g2l),
+                                                _ptr(self.l2g), _ptr(self.fq), _ptr(self.pend), self.cap_l,
+                                                _ptr(self.lctr)))
+            self._swap_list()
+            self.h_lctr.copy_(self.lctr, non_blocking=True)
+            self.h_lctr2.copy_(self.lctr2, non_blocking=True)
+        elif self.local:
             check(L.gwaoi_strip_emit_local(*common, _ptr(self.g2l), _ptr(self.l2g), _ptr(self.fq), _ptr(self.pend),
                                            self.cap_l, _ptr(self.lctr)))
+            if self.lst is not None:
+                self._list_from_ops()
             self.h_lctr.copy_(self.lctr, non_blocking=True)
         else:
             check(L.gwaoi_strip_emit(*common))
@@ -213,6 +262,11 @@ class StripNode:
         else:
             ev = self.eng.tick() if host_events else self.eng.tick_device()
         c = self.h_counts  # complete: the tick waited for every kernel after the copy
+        if use_list and int(self.h_lctr2[3]) & STRIP_ERR_NEWLIST and not int(self.h_lctr[3]) and not int(c[3]):
+            # more ids came into the region than the list emit takes: it emitted nothing (the manager ran an
+            # empty pass, the state did not advance); the same tick by id range, then the list again
+            self.list_fallbacks = getattr(self, "list_fallbacks", 0) + 1
+            return self._emit_and_tick(host_events, n_bound, by_range=True)
         if int(c[3]) or (self.local and int(self.h_lctr[3])):
             flags = int(c[3]) | (int(self.h_lctr[3]) if self.local else 0)
             why = " (the region holds more entities than its local slots, cap_l = %d: nothing of this tick was " \
@@ -259,7 +313,7 @@ class StripNode:
                                                     _ptr(self.ez), ctypes.c_uint64(self.seed),
                                                     ctypes.c_float(self.layout.L)))
             self.tick_no = 0
-            return self._emit_and_tick(host_events, self.n)
+            return self._emit_and_tick(host_events, self.n, by_range=True)  # (then the region list from its ops)
 
     def prepare(self, t: int, step: float = 1.0, moves: Optional[Tuple[torch.Tensor, ...]] = None):
         """End positions of the owned entities (the seeded walk's tick t, or `moves` = (ids, x, z)
@@ -287,20 +341,52 @@ class StripNode:
         fin = sum(c.elapsed_time(d) for _, _, c, d in self.sev) / k
         return {"ms_strip_prepare": round(prep, 4), "ms_strip_finish": round(fin, 4), "ticks": k}
 
+    def _walk(self, t, step):
+        L = self._L
+        if self.lst is not None:
+            check(L.gwaoi_strip_walk_list(self._s(), self._g(), ctypes.byref(self.lst), _ptr(self.flags), _ptr(self.sx),
+                                          _ptr(self.sz), _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed),
+                                          ctypes.c_uint64(t), ctypes.c_float(self.layout.L), ctypes.c_float(step),
+                                          self._err()))
+        else:
+            check(L.gwaoi_strip_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz),
+                                     _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed), ctypes.c_uint64(t),
+                                     ctypes.c_float(self.layout.L), ctypes.c_float(step), self._err()))
+
+    def _select(self):
+        L = self._L
+        if self.lst is not None:
+            check(L.gwaoi_strip_select_list(self._s(), self._g(), ctypes.byref(self.lst), _ptr(self.flags), _ptr(self.sx),
+                                            _ptr(self.ex), _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
+                                            ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+        else:
+            check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
+                                       _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
+                                       ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+
+    def _absorb(self, recs, n_max: int, d_n=None):
+        L = self._L
+        if self.lst is not None:
+            check(L.gwaoi_strip_absorb_list(self._s(), ctypes.byref(self.lst), _ptr(self.flags), _ptr(self.ex),
+                                            _ptr(self.ez), _ptr(recs), d_n, int(n_max),
+                                            self._err() if d_n is not None else None))
+        elif d_n is not None:
+            check(L.gwaoi_strip_absorb_n(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez), _ptr(recs), d_n,
+                                         int(n_max), self._err()))
+        else:
+            check(L.gwaoi_strip_absorb(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez), _ptr(recs),
+                                       int(n_max)))
+
     def _prepare(self, t, step, moves):
         L = self._L
         self._ev_prep = (self._mark(),)
         if moves is None:
-            check(L.gwaoi_strip_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz),
-                                     _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed), ctypes.c_uint64(t),
-                                     ctypes.c_float(self.layout.L), ctypes.c_float(step), self._err()))
+            self._walk(t, step)
         else:
             ids, x, z = moves
             check(L.gwaoi_strip_ingest(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
                                        _ptr(self.ez), _ptr(ids), _ptr(x), _ptr(z), int(ids.numel()), self._err()))
-        check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
-                                   _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
-                                   ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+        self._select()
         self._ev_prep = (self._ev_prep[0], self._mark())
         self.tick_no = t
         if not (self.g.has_left or self.g.has_right):  # nothing to send: no round trip (errors: finish)
@@ -322,8 +408,7 @@ class StripNode:
                     recs = recs.to(self.device).contiguous()
                     recs.record_stream(self.stream)
                     nin += int(recs.shape[0])
-                    check(self._L.gwaoi_strip_absorb(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
-                                                     _ptr(recs), int(recs.shape[0])))
+                    self._absorb(recs, int(recs.shape[0]))
             self._f0 = f0
             return self._emit_and_tick(host_events, self.eng.count()[0] + nin)
 
@@ -348,16 +433,12 @@ class StripNode:
         L = self._L
         with torch.cuda.stream(self.stream):
             if moves is None:
-                check(L.gwaoi_strip_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz),
-                                         _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed), ctypes.c_uint64(t),
-                                         ctypes.c_float(self.layout.L), ctypes.c_float(step), self._err()))
+                self._walk(t, step)
             else:
                 ids, x, z = moves
                 check(L.gwaoi_strip_ingest(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
                                            _ptr(self.ez), _ptr(ids), _ptr(x), _ptr(z), int(ids.numel()), self._err()))
-            check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
-                                       _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
-                                       ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+            self._select()
             if time_exchange:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -370,9 +451,7 @@ class StripNode:
                 self.xev.append((e0, e1))
             for k, recs in enumerate((self.left_in, self.right_in)):
                 if peers[k] >= 0:
-                    check(L.gwaoi_strip_absorb_n(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez),
-                                                 _ptr(recs), ctypes.c_void_p(self.counts_in.data_ptr() + 4 * k),
-                                                 self.cap, self._err()))
+                    self._absorb(recs, self.cap, ctypes.c_void_p(self.counts_in.data_ptr() + 4 * k))
             self.tick_no = t
             return self._emit_and_tick(host_events, self.eng.count()[0] + 2 * self.cap)
 

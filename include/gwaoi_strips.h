@@ -114,6 +114,45 @@ int gwaoi_strip_init_skew(void* stream, const gwaoi_strip_geom* g, uint8_t* flag
 int gwaoi_strip_absorb_n(void* stream, uint8_t* flags, float* ex, float* ez, const uint32_t* d_recs,
                          const uint32_t* d_n, uint32_t n_max, uint32_t* d_err);
 
+/* ---- region lists (ABI 2.1) ----
+ * The per-tick kernels above sweep the whole id range (g->n): with a 16M-id world on 8 GPUs every rank
+ * scans 16M ids to find its ~2M. With a region list they walk the ids present in the region instead:
+ * walk and select over the list, absorb appends the ids that come into the region, and the emit merges the
+ * list with the sorted new ids (the op list stays in global id order) and writes the next tick's list. Per
+ * tick the work follows the region, not the world. Local slots only (gwaoi_strip_emit_local_list). */
+#define GWAOI_STRIP_ERR_NEWLIST 16u /* more ids came into the region in one tick than the list emit takes
+                                       (cap_new, at most 16384): nothing emitted; emit by id range instead,
+                                       then rebuild the list (gwaoi_strip_list_from_ops) */
+typedef struct {
+  uint32_t* rl;       /* [cap] ids present in the region at the start of the tick, ascending */
+  uint32_t* rl_next;  /* [cap] the next tick's list, written by the emit: the caller swaps rl and rl_next */
+  uint32_t* nw;       /* [cap_new] ids that came into the region this tick (absorbed while not present) */
+  uint32_t* ctr;      /* [4] device: {list length, emitted, new ids, GWAOI_STRIP_ERR_* bits} */
+  uint32_t* scratch;  /* [gwaoi_strip_list_scratch_words(cap)] */
+  uint32_t cap;       /* largest region population (the manager's local slot count, cap_l) */
+  uint32_t cap_new;   /* new ids per tick at most (<= 16384) */
+} gwaoi_strip_list;
+size_t gwaoi_strip_list_scratch_words(uint32_t cap);
+/* rl_next (and the counters) from a tick's op list, e.g. tick 0's Enter pass or an id-range emit; then swap */
+int gwaoi_strip_list_from_ops(void* stream, const gwaoi_strip_list* L, const uint32_t* d_slots, const uint8_t* d_kinds,
+                              const uint32_t* l2g, const uint32_t* d_n_ops);
+int gwaoi_strip_walk_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, uint8_t* flags,
+                          const float* sx, const float* sz, float* ex, float* ez, uint64_t seed, uint64_t tick,
+                          float Lw, float step, uint32_t* d_err);
+int gwaoi_strip_select_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, const uint8_t* flags,
+                            const float* sx, const float* ex, const float* ez, uint32_t* d_left, uint32_t* d_right,
+                            uint32_t cap, uint32_t* d_counts, uint32_t* d_err);
+/* gwaoi_strip_absorb_n (d_n may be NULL: n_max records) that also lists the ids coming into the region */
+int gwaoi_strip_absorb_list(void* stream, const gwaoi_strip_list* L, uint8_t* flags, float* ex, float* ez,
+                            const uint32_t* d_recs, const uint32_t* d_n, uint32_t n_max, uint32_t* d_err);
+/* gwaoi_strip_emit_local over the list: the op list in id order, the state advance and rl_next. With
+ * GWAOI_STRIP_ERR_NEWLIST (or no free slots: GWAOI_STRIP_ERR_SLOTS in ctr[3]) nothing is emitted and rl_next
+ * is a copy of rl. */
+int gwaoi_strip_emit_local_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, uint8_t* flags,
+                                float* sx, float* sz, const float* ex, const float* ez, uint32_t* d_slots, float* d_x,
+                                float* d_z, uint8_t* d_kinds, uint32_t* d_n_ops, uint32_t* g2l, uint32_t* l2g,
+                                uint32_t* fq, uint32_t* pend, uint32_t cap_l, uint32_t* ctr);
+
 /* ---- the halo exchange over RCCL (xGMI), device-resident end to end ----
  * One communicator per strip world, one rank per GPU. Rank 0 makes the id; the caller hands the 128
  * bytes to every rank over whatever channel the deployment has (the game processes' own transport,

@@ -5,9 +5,11 @@
  *
  *   Enter      -> gwaoi_enter, then Flush (SyncEnterLeave: the callbacks fire inside Space.enter,
  *                 /root/reference/engine/entity/Space.go:211-217)
- *   Moved      -> written into the manager's pinned staging arrays (gwaoi_stage_buffers); Flush pushes
- *                 them with ONE gwaoi_stage_moves_pinned call (validated on the device). The scenario
- *                 runs a second time with host slices and ONE gwaoi_stage_moves call (the copy-in path).
+ *   Moved      -> written into the manager's pinned staging arrays (gwaoi_stage_buffers); every 16 calls
+ *                 the filled part is pushed early (gwaoi_stage_moves_pinned_partial, ABI 2.1) and Flush
+ *                 pushes the rest with ONE gwaoi_stage_moves_pinned_async call (checked on the device, the
+ *                 verdict read by gwaoi_tick). The scenario runs again with the synchronous
+ *                 gwaoi_stage_moves_pinned, and with host slices and ONE gwaoi_stage_moves call (copy-in).
  *   Flush      -> push the pending moves + gwaoi_tick, events replayed in order
  *   Leave      -> pending moves first (call order), gwaoi_leave, then Flush
  *
@@ -87,7 +89,8 @@ static int failures;
   } while (0)
 
 static void push(void) {
-  if (npend && pinned) CHK(gwaoi_stage_moves_pinned(mgr, npend));
+  if (npend && pinned == 2) CHK(gwaoi_stage_moves_pinned_async(mgr, npend)); /* ABI 2.1: the Go wrapper's push */
+  if (npend && pinned == 1) CHK(gwaoi_stage_moves_pinned(mgr, npend));
   if (npend && !pinned) CHK(gwaoi_stage_moves(mgr, pend_slot, pend_x, pend_z, npend));
   npend = 0;
 }
@@ -118,6 +121,7 @@ static void moved(uint32_t s, float x, float z) { /* staged on the host side, li
   pend_x[npend] = x;
   pend_z[npend] = z;
   ++npend;
+  if (pinned == 2 && npend % 16 == 0) CHK(gwaoi_stage_moves_pinned_partial(mgr, npend)); /* incremental push */
   model_op(0, (int)s, x, z);
 }
 
@@ -163,7 +167,13 @@ static void scenario(int use_pinned) {
   if (pinned) { /* a refused pinned batch stages nothing (slot 80 is not in a Space) */
     pend_slot[0] = 0, pend_x[0] = 0.f, pend_z[0] = 0.f;
     pend_slot[1] = 80, pend_x[1] = 1.f, pend_z[1] = 1.f;
-    if (gwaoi_stage_moves_pinned(mgr, 2) != GWAOI_ERR_STATE) ++failures, fprintf(stderr, "pinned absent accepted\n");
+    if (pinned == 1 && gwaoi_stage_moves_pinned(mgr, 2) != GWAOI_ERR_STATE)
+      ++failures, fprintf(stderr, "pinned absent accepted\n");
+    if (pinned == 2) { /* async: the pass that reads the device's verdict reports it, nothing applied */
+      gwaoi_events e2;
+      CHK(gwaoi_stage_moves_pinned_async(mgr, 2));
+      if (gwaoi_tick(mgr, &e2) != GWAOI_ERR_STATE) ++failures, fprintf(stderr, "async absent accepted\n");
+    }
     flush("refused batch");
   }
   /* misuse is reported, not crashed on: Enter twice, Moved/Leave of an absent slot, NaN */
@@ -188,6 +198,7 @@ int main(void) {
     fprintf(stderr, "abi_smoke: library ABI %d, headers %d\n", gwaoi_abi_version(), GWAOI_ABI_VERSION);
     return 4;
   }
+  scenario(2); /* the Go wrapper of ABI 2.1: async push, incremental pushes */
   scenario(1);
   scenario(0);
   if (failures) {

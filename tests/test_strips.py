@@ -92,17 +92,24 @@ def test_cpu_gloo_world(oracle_lib, tmp_path, world):
 # ------------------------------------------------------------------------------------------------ GPU
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,local", [(1, True), (3, True), (4, True), (3, False)])
-def test_gpu_strips_loopback(gpu, oracle_lib, world, local):
+@pytest.mark.parametrize("world,local,lst", [(1, True, 1), (3, True, 1), (4, True, 1), (3, True, 0), (3, False, 0),
+                                             (3, True, 2)])
+def test_gpu_strips_loopback(gpu, oracle_lib, world, local, lst):
     """HIP strip kernels + one libgwaoi manager per strip, all on cuda:0; every step's op list equals
     the CPU restatement's and the merged events equal one manager over the whole world. local: the
-    managers index their entities by local slot (gwaoi_strip_emit_local), events translated back."""
+    managers index their entities by local slot (gwaoi_strip_emit_local), events translated back.
+    lst 1: the per-tick kernels over the region list (ABI 2.1: walk / select / absorb / merge emit over the
+    ids present in the region); 0: over the id range; 2: the region list with room for 1 new id per tick,
+    so most ticks take the fallback (nothing emitted by the list, the tick emitted by id range, the list
+    rebuilt)."""
     from goworld_amd.strips import LoopbackExchange, StripNode
     po = oracle_lib
     n, Lw = 12000, 3800.0
     want = SC.global_events(po, n, Lw, D, SEED, TICKS)
     lay = _layout(world, Lw)
-    nodes = [StripNode(lay, r, n, device=0, seed=SEED, local_slots=local) for r in range(world)]
+    nodes = [StripNode(lay, r, n, device=0, seed=SEED, local_slots=local, region_list=lst > 0,
+                       cap_new=1 if lst == 2 else 16384) for r in range(world)]
+    assert all((nd.lst is not None) == (lst > 0) for nd in nodes)
     cpu = [SC.CPUStripNode(lay, r, n, po, SEED) for r in range(world)]
     got = [SC.merge_sorted([nd.start(host_events=True) for nd in nodes])]
     for c in cpu:
@@ -134,6 +141,10 @@ def test_gpu_strips_loopback(gpu, oracle_lib, world, local):
             evs.append(e)
         got.append(SC.merge_sorted(evs))
         assert np.array_equal(got[t], want[t]), f"world {world} tick {t}: {len(got[t])} vs {len(want[t])}"
+    if lst == 2 and world > 1:  # the fallback ran (halo entities come into the regions every tick)
+        assert sum(getattr(nd, "list_fallbacks", 0) for nd in nodes) > 0
+    if lst == 1:
+        assert sum(getattr(nd, "list_fallbacks", 0) for nd in nodes) == 0
     for nd in nodes:
         nd.close()
 
