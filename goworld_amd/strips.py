@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -109,7 +110,7 @@ class StripNode:
 
     def __init__(self, layout: StripLayout, rank: int, n: int, device: int = 0, seed: int = 0x5EED0004,
                  halo_cap: Optional[int] = None, skew: Optional[Tuple[int, float, int]] = None,
-                 local_slots: bool = True, cap_l: Optional[int] = None, region_list: bool = True,
+                 local_slots: bool = True, cap_l: Optional[int] = None, region_list: Optional[bool] = None,
                  cap_new: int = 16384):
         """skew = (nhot, sigma, hot_every): the skewed-crowd placement of config 5 instead of uniform.
         local_slots: the manager sees local slots (gwaoi_strip_emit_local); False: slot = global id.
@@ -171,6 +172,12 @@ class StripNode:
                                                  _ptr(self.lctr)))
             torch.cuda.synchronize(dev)
         self.lst = None
+        if region_list is None:
+            # auto: the list path where the world's id range is well beyond the region (a 16M-id world in 8
+            # strips: select 81 -> 41 us per strip; a 2M world in one strip: the list's merge and compaction
+            # cost ~20 us more than the id-range emit, r06_a5); GWAOI_STRIP_LIST=0 / 1 forces it (A/B)
+            env = os.environ.get("GWAOI_STRIP_LIST")
+            region_list = (env != "0") if env is not None else n > 2 * want
         if self.local and region_list and hasattr(self._L, "gwaoi_strip_emit_local_list"):
             cn = max(1, min(int(cap_new), 16384))
             self.rl = torch.zeros(self.cap_l, dtype=i32, device=dev)
