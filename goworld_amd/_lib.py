@@ -54,8 +54,8 @@ STRIP_SYMBOLS = (
     "gwaoi_strip_absorb", "gwaoi_strip_emit", "gwaoi_strip_scratch_words", "gwaoi_strip_init_skew",
     "gwaoi_strip_absorb_n", "gwaoi_strip_comm_id", "gwaoi_strip_comm_init", "gwaoi_strip_comm_destroy",
     "gwaoi_strip_exchange", "gwaoi_strip_local_init", "gwaoi_strip_emit_local", "gwaoi_strip_translate_events",
-    "gwaoi_strip_list_scratch_words", "gwaoi_strip_list_from_ops", "gwaoi_strip_walk_list",
-    "gwaoi_strip_select_list", "gwaoi_strip_absorb_list", "gwaoi_strip_emit_local_list",
+    "gwaoi_strip_region_init", "gwaoi_strip_region_start", "gwaoi_strip_region_walk", "gwaoi_strip_region_ingest",
+    "gwaoi_strip_region_select", "gwaoi_strip_region_absorb", "gwaoi_strip_region_emit",
 )
 
 
@@ -111,11 +111,15 @@ class StripGeom(ctypes.Structure):
     ]
 
 
-class StripList(ctypes.Structure):
-    """gwaoi_strip_list (include/gwaoi_strips.h, ABI 2.1): a strip's region list."""
-    _fields_ = [("rl", ctypes.c_void_p), ("rl_next", ctypes.c_void_p), ("nw", ctypes.c_void_p),
-                ("ctr", ctypes.c_void_p), ("scratch", ctypes.c_void_p), ("cap", ctypes.c_uint32),
-                ("cap_new", ctypes.c_uint32)]
+class StripRegion(ctypes.Structure):
+    """gwaoi_strip_region (include/gwaoi_strips.h, ABI 2.1): a strip's state in local-slot order."""
+    _fields_ = [("flags", ctypes.c_void_p), ("sx", ctypes.c_void_p), ("sz", ctypes.c_void_p),
+                ("ex", ctypes.c_void_p), ("ez", ctypes.c_void_p), ("g2l", ctypes.c_void_p), ("l2g", ctypes.c_void_p),
+                ("fq", ctypes.c_void_p), ("pend", ctypes.c_void_p), ("lctr", ctypes.c_void_p),
+                ("rl", ctypes.c_void_p * 2), ("rs", ctypes.c_void_p * 2), ("nw", ctypes.c_void_p),
+                ("lv", ctypes.c_void_p), ("srt", ctypes.c_void_p), ("ctr", ctypes.c_void_p),
+                ("scratch", ctypes.c_void_p), ("n", ctypes.c_uint32), ("cap_l", ctypes.c_uint32),
+                ("cap_new", ctypes.c_uint32), ("chunk", ctypes.c_uint32), ("cur", ctypes.c_uint32)]
 
 
 class GwaoiError(RuntimeError):
@@ -171,8 +175,9 @@ _lib = None
 
 # ABI 2.1 additions (include/gwaoi.h GWAOI_ABI_MINOR): optional when an older build is loaded for an A/B
 ABI_MINOR_SYMBOLS = ("gwaoi_stage_moves_pinned_partial", "gwaoi_stage_moves_pinned_async", "gwaoi_abi_minor",
-                     "gwaoi_strip_list_scratch_words", "gwaoi_strip_list_from_ops", "gwaoi_strip_walk_list",
-                     "gwaoi_strip_select_list", "gwaoi_strip_absorb_list", "gwaoi_strip_emit_local_list")
+                     "gwaoi_strip_region_init", "gwaoi_strip_region_start", "gwaoi_strip_region_walk",
+                     "gwaoi_strip_region_ingest", "gwaoi_strip_region_select", "gwaoi_strip_region_absorb",
+                     "gwaoi_strip_region_emit")
 ABI_VERSION = 2  # GWAOI_ABI_VERSION of include/gwaoi.h that these ctypes structs and signatures follow
 
 
@@ -263,13 +268,13 @@ def load(path: str = SO_PATH):
         "gwaoi_strip_emit_local": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp],
                                    ctypes.c_int),
         "gwaoi_strip_translate_events": ([vp, vp, vp, u32], ctypes.c_int),
-        "gwaoi_strip_list_scratch_words": ([u32], ctypes.c_size_t),
-        "gwaoi_strip_list_from_ops": ([vp, vp, vp, vp, vp, vp], ctypes.c_int),
-        "gwaoi_strip_walk_list": ([vp, vp, vp, vp, vp, vp, vp, vp, u64, u64, f32, f32, vp], ctypes.c_int),
-        "gwaoi_strip_select_list": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp], ctypes.c_int),
-        "gwaoi_strip_absorb_list": ([vp, vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),
-        "gwaoi_strip_emit_local_list": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp],
-                                        ctypes.c_int),
+        "gwaoi_strip_region_init": ([vp, vp], ctypes.c_int),
+        "gwaoi_strip_region_start": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
+        "gwaoi_strip_region_walk": ([vp, vp, vp, u64, u64, f32, f32, vp], ctypes.c_int),
+        "gwaoi_strip_region_ingest": ([vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),
+        "gwaoi_strip_region_select": ([vp, vp, vp, vp, vp, u32, vp, vp], ctypes.c_int),
+        "gwaoi_strip_region_absorb": ([vp, vp, vp, vp, u32, vp], ctypes.c_int),
+        "gwaoi_strip_region_emit": ([vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "gwaoi_strip_init_skew": ([vp, vp, vp, vp, vp, u64, f32, u32, f32, u32], ctypes.c_int),
         "gwaoi_strip_absorb_n": ([vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),
         "gwaoi_strip_comm_id": ([vp], ctypes.c_int),

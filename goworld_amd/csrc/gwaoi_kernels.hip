@@ -3288,6 +3288,10 @@ __device__ __forceinline__ bool ev_fits(const OrderArgs& o, uint32_t* slots, uin
   return *slots <= o.g.tmp_cap && o.g.keep + *n <= o.g.out_cap;
 }
 
+#ifndef GW_PLACE_UNROLL
+#define GW_PLACE_UNROLL 8
+#endif
+constexpr int kPlaceU = GW_PLACE_UNROLL;
 __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
   const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
   uint32_t slots, n;
@@ -3342,17 +3346,30 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
     if (threadIdx.x == 0 && tot != o.g.ctr[CTR_NOPS] && !o.g.ctr[CTR_BOVF])
       atomicOr(const_cast<uint32_t*>(&o.g.ctr[CTR_ERR]), ERR_DUP_SLOT);
   }
-  for (uint32_t i = tid; i < slots; i += nth) {
-    const uint4 e = o.ev_tmp[i];
-    if (e.x != kEvHole) o.ev_out[o.rank_off[e.x] + e.y] = make_uint2(e.z, e.w);
+  // kPlaceU slots per thread and round, every load of a round issued before the first use: one event at a
+  // time, each thread's chain (the slot, then its op's offset, then the store) waited out two memory round
+  // trips per event (skew50's 21M events: 180 us)
+  for (uint32_t i0 = tid; i0 < slots; i0 += kPlaceU * nth) {
+    uint4 e[kPlaceU];
+#pragma unroll
+    for (int k = 0; k < kPlaceU; ++k) {
+      const uint32_t i = i0 + (uint32_t)k * nth;
+      e[k] = i < slots ? o.ev_tmp[i] : make_uint4(kEvHole, 0u, 0u, 0u);
+    }
+    uint32_t ro[kPlaceU];
+#pragma unroll
+    for (int k = 0; k < kPlaceU; ++k) ro[k] = e[k].x != kEvHole ? o.rank_off[e[k].x] : 0u;
+#pragma unroll
+    for (int k = 0; k < kPlaceU; ++k)
+      if (e[k].x != kEvHole) o.ev_out[ro[k] + e[k].y] = make_uint2(e[k].z, e[k].w);
   }
 }
 
 // Per-op slices are sorted by .y (other | ENTER bit: LEAVE first, then other ascending), inside one
 // kernel without global atomics (a shared work-list counter bumped by every wave serialises at ~88
 // returning atomics per us): slices of up to kSmallSlice events (config 2: ~0.3 per op) are sorted in
-// registers by their op's thread (an odd-even transposition network, static indices only); up to 64
-// by the op's wave (each lane holds one event and counts the events ordered before it); longer ones
+// registers by their op's thread (an odd-even transposition network, static indices only); up to
+// GW_MED_MAX by the op's wave (each lane holds events and counts the events ordered before them); longer ones
 // (crowds: hundreds per mover) by the whole block: chunks of kBigChunk events are bitonic-sorted in
 // LDS, and a slice of several chunks is merged by rank: an element's final index is its index in its
 // sorted chunk plus, for every other chunk, the count of elements ordered before it there (binary
@@ -3360,6 +3377,15 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
 // free once k_place has run (its uint2 view has 2 x slots >= n entries).
 constexpr uint32_t kSmallSlice = 8;
 constexpr uint32_t kBigChunk = 2048;
+// diagnosis only (A/B of where k_slice_sort's time goes; the result is then NOT sorted): 1 skips the wave
+// windows, 2 the block sorts, 3 the register sorts, 4 every sort
+#ifndef GW_DIAG_SORT
+#define GW_DIAG_SORT 0
+#endif
+// longest slice ranked by one wave in its LDS window (below: the block's bitonic sort). Round 6: 64 -> 256
+#ifndef GW_MED_MAX
+#define GW_MED_MAX 256u
+#endif
 __device__ __forceinline__ uint32_t seg_key(const uint2 v) { return v.y; }
 __device__ __forceinline__ uint32_t seg_key(const uint32_t v) { return v; }
 template <class T> __device__ __forceinline__ T seg_pad();
@@ -3434,7 +3460,7 @@ template <class T>
 __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uint32_t len, T* sk, uint2* bigq,
                          uint32_t* nbig) {
   if (threadIdx.x == 0) *nbig = 0;
-  if (len >= 2u && len <= kSmallSlice) {
+  if (GW_DIAG_SORT != 3 && GW_DIAG_SORT != 4 && len >= 2u && len <= kSmallSlice) {
     T v[kSmallSlice];
 #pragma unroll
     for (uint32_t i = 0; i < kSmallSlice; ++i) v[i] = i < len ? d[b + i] : seg_pad<T>();
@@ -3452,20 +3478,22 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
     for (uint32_t i = 0; i < kSmallSlice; ++i)
       if (i < len) d[b + i] = v[i];
   }
-  // medium segments (kSmallSlice < len <= 64): the wave's together, in windows of up to kMedWin elements
+  // medium segments (kSmallSlice < len <= GW_MED_MAX): the wave's together, in windows of up to kMedWin elements
   // (whole segments, in lane order) staged in the wave's share of sk with all loads in flight at once; an
   // element's final index is the count of its segment's elements ordered before it (key, then position:
   // stable), read from the window (the lanes of one segment read the same element at a time: broadcast).
   // (One segment at a time, the wave paid a dependent global round trip per segment: skew50's ~1M medium
-  // slices made k_slice_sort 338 us.)
+  // slices made k_slice_sort 338 us. Slices of 65..256 went to the block's bitonic sort, one slice at a time
+  // with a barrier per stage; in a wave window each costs ~len / 64 rounds of len LDS reads.)
   constexpr uint32_t kMedWin = kBigChunk / (kBlock / 64);
   constexpr uint32_t kMedRounds = kMedWin / 64u;
   const uint32_t lane = threadIdx.x & 63u;
   T* win = sk + (threadIdx.x >> 6) * kMedWin;
-  const uint32_t lm = (len > kSmallSlice && len <= 64u) ? len : 0u;
+  static_assert(GW_MED_MAX <= kMedWin, "a medium slice fits one wave window");
+  const uint32_t lm = (len > kSmallSlice && len <= (uint32_t)GW_MED_MAX) ? len : 0u;
   const uint32_t incl = wave_incl_scan(lm), excl = incl - lm;
   const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  for (uint32_t w0 = 0; w0 < tot;) {  // wave-uniform; each window holds the next segment at least
+  for (uint32_t w0 = 0; w0 < ((GW_DIAG_SORT == 1 || GW_DIAG_SORT == 4) ? 0u : tot);) {  // wave-uniform; each window holds the next segment at least
     const unsigned long long fit = __ballot(incl <= w0 + kMedWin);  // a prefix of the lanes
     const int last = __builtin_amdgcn_readfirstlane(63 - __clzll((long long)fit));
     const uint32_t wend = (uint32_t)__builtin_amdgcn_readlane((int)incl, last);
@@ -3510,10 +3538,10 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
   }
   // long segments: the whole block
   __syncthreads();
-  if (len > 64u) bigq[atomicAdd(nbig, 1u)] = make_uint2(b, len);  // LDS atomic
+  if (len > (uint32_t)GW_MED_MAX) bigq[atomicAdd(nbig, 1u)] = make_uint2(b, len);  // LDS atomic
   __syncthreads();
   const uint32_t nb = *nbig;
-  for (uint32_t q = 0; q < nb; ++q) {
+  for (uint32_t q = 0; q < ((GW_DIAG_SORT == 2 || GW_DIAG_SORT == 4) ? 0u : nb); ++q) {
     const uint2 sg = bigq[q];
     seg_sort_long(d + sg.x, tmp + sg.x, sg.y, sk);
   }

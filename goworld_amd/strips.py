@@ -31,7 +31,7 @@ from .engine import Engine
 
 f32 = np.float32
 STRIP_ERR_SLOTS = 8  # GWAOI_STRIP_ERR_SLOTS (include/gwaoi_strips.h)
-STRIP_ERR_NEWLIST = 16  # GWAOI_STRIP_ERR_NEWLIST
+STRIP_ERR_NEWLIST = 16  # GWAOI_STRIP_ERR_NEWLIST (region state)
 
 
 class StripLayout:
@@ -110,13 +110,14 @@ class StripNode:
 
     def __init__(self, layout: StripLayout, rank: int, n: int, device: int = 0, seed: int = 0x5EED0004,
                  halo_cap: Optional[int] = None, skew: Optional[Tuple[int, float, int]] = None,
-                 local_slots: bool = True, cap_l: Optional[int] = None, region_list: Optional[bool] = None,
-                 cap_new: int = 16384):
+                 local_slots: bool = True, cap_l: Optional[int] = None, region_state: Optional[bool] = None,
+                 cap_new: int = 65536, sort_chunk: int = 0):
         """skew = (nhot, sigma, hot_every): the skewed-crowd placement of config 5 instead of uniform.
         local_slots: the manager sees local slots (gwaoi_strip_emit_local); False: slot = global id.
-        region_list (local slots only, ABI 2.1): the per-tick strip kernels walk the ids present in the region
-        (gwaoi_strip_*_list) instead of the world's id range; cap_new: ids one tick may bring into the region
-        on that path (more: that tick is emitted by id range and the list rebuilt)."""
+        region_state (local slots only, ABI 2.1, default on; GWAOI_STRIP_REGION=0 / 1 forces it): the strip's
+        state in local-slot order and the per-tick kernels over the region (gwaoi_strip_region_*), not over the
+        world's id range; cap_new: ids that may come into (and Leaves that may leave) the region per tick;
+        sort_chunk: the LDS sort's chunk of those (0: 16384; tests use small chunks to cover the merge)."""
         self.layout, self.rank, self.n, self.seed = layout, int(rank), int(n), int(seed)
         self.skew = skew
         self.g = layout.geom(rank, n)
@@ -124,11 +125,6 @@ class StripNode:
         self._L = _lib.load()
         dev = self.device
         u8, i32, fl = torch.uint8, torch.int32, torch.float32
-        self.flags = torch.zeros(n, dtype=u8, device=dev)
-        self.sx, self.sz, self.ex, self.ez = (torch.zeros(n, dtype=fl, device=dev) for _ in range(4))
-        self.ids = torch.zeros(n, dtype=i32, device=dev)
-        self.ox, self.oz = torch.zeros(n, dtype=fl, device=dev), torch.zeros(n, dtype=fl, device=dev)
-        self.kinds = torch.zeros(n, dtype=u8, device=dev)
         # the halo of one side holds ~ 2 H L density entities; keep room for several times that (a skewed
         # crowd can put a hotspot on an edge: more)
         cap = halo_cap or max(4096, int((32 if skew else 8) * layout.halo * layout.L * n / (layout.L * layout.L)) + 4096)
@@ -159,6 +155,17 @@ class StripNode:
             want = int(cap_l)
         self.cap_l = max(1, want)
         self.local = bool(local_slots)
+        if region_state is None:
+            env = os.environ.get("GWAOI_STRIP_REGION")
+            region_state = env != "0" if env is not None else True
+        self.R = None
+        # state: per local slot (region state) or per global id; the op list: at most cap_l ops (region state)
+        m = self.cap_l if (self.local and region_state) else n
+        self.flags = torch.zeros(m, dtype=u8, device=dev)
+        self.sx, self.sz, self.ex, self.ez = (torch.zeros(m, dtype=fl, device=dev) for _ in range(4))
+        self.ids = torch.zeros(m, dtype=i32, device=dev)
+        self.ox, self.oz = torch.zeros(m, dtype=fl, device=dev), torch.zeros(m, dtype=fl, device=dev)
+        self.kinds = torch.zeros(m, dtype=u8, device=dev)
         if self.local:
             ring = 1 << max(0, (self.cap_l - 1).bit_length())
             self.g2l = torch.empty(n, dtype=i32, device=dev)
@@ -168,34 +175,36 @@ class StripNode:
             self.lctr = torch.zeros(4, dtype=i32, device=dev)
             self.h_lctr = torch.zeros(4, dtype=i32).pin_memory()
             torch.cuda.synchronize(dev)
-            check(self._L.gwaoi_strip_local_init(ctypes.c_void_p(0), n, self.cap_l, _ptr(self.g2l), _ptr(self.fq),
-                                                 _ptr(self.lctr)))
-            torch.cuda.synchronize(dev)
-        self.lst = None
-        if region_list is None:
-            # auto: the list path where the world's id range is well beyond the region (a 16M-id world in 8
-            # strips: select 81 -> 41 us per strip; a 2M world in one strip: the list's merge and compaction
-            # cost ~20 us more than the id-range emit, r06_a5); GWAOI_STRIP_LIST=0 / 1 forces it (A/B)
-            env = os.environ.get("GWAOI_STRIP_LIST")
-            region_list = (env != "0") if env is not None else n > 2 * want
-        if self.local and region_list and hasattr(self._L, "gwaoi_strip_emit_local_list"):
-            cn = max(1, min(int(cap_new), 16384))
-            self.rl = torch.zeros(self.cap_l, dtype=i32, device=dev)
-            self.rl_next = torch.zeros(self.cap_l, dtype=i32, device=dev)
-            self.nw = torch.zeros(cn, dtype=i32, device=dev)
-            self.lctr2 = torch.zeros(4, dtype=i32, device=dev)
-            self.h_lctr2 = torch.zeros(4, dtype=i32).pin_memory()
-            self.lscratch = torch.zeros(int(self._L.gwaoi_strip_list_scratch_words(self.cap_l)), dtype=i32, device=dev)
-            self.lst = _lib.StripList()
-            self.lst.nw, self.lst.ctr = self.nw.data_ptr(), self.lctr2.data_ptr()
-            self.lst.scratch, self.lst.cap, self.lst.cap_new = self.lscratch.data_ptr(), self.cap_l, cn
-            self._set_list()
+            if region_state:
+                cn = max(1, min(int(cap_new), 8 * (int(sort_chunk) or 16384)))
+                self.rl = [torch.zeros(self.cap_l, dtype=i32, device=dev) for _ in range(2)]
+                self.rs = [torch.zeros(self.cap_l, dtype=i32, device=dev) for _ in range(2)]
+                self.nw = torch.zeros(2 * cn, dtype=i32, device=dev)
+                self.lv = torch.zeros(cn, dtype=i32, device=dev)
+                self.srt = torch.zeros(3 * cn, dtype=i32, device=dev)
+                self.rctr = torch.zeros(8, dtype=i32, device=dev)
+                self.h_rctr = torch.zeros(8, dtype=i32).pin_memory()
+                R = _lib.StripRegion()
+                for f in ("flags", "sx", "sz", "ex", "ez", "g2l", "l2g", "fq", "pend", "lctr", "nw", "lv", "srt",
+                          "scratch"):
+                    setattr(R, f, getattr(self, f).data_ptr())
+                R.rl[0], R.rl[1] = self.rl[0].data_ptr(), self.rl[1].data_ptr()
+                R.rs[0], R.rs[1] = self.rs[0].data_ptr(), self.rs[1].data_ptr()
+                R.ctr = self.rctr.data_ptr()
+                R.n, R.cap_l, R.cap_new, R.chunk = n, self.cap_l, cn, int(sort_chunk)
+                self.R = R
+                torch.cuda.synchronize(dev)
+                check(self._L.gwaoi_strip_region_init(ctypes.c_void_p(0), ctypes.byref(R)))
+            else:
+                check(self._L.gwaoi_strip_local_init(ctypes.c_void_p(0), n, self.cap_l, _ptr(self.g2l),
+                                                     _ptr(self.fq), _ptr(self.lctr)))
             torch.cuda.synchronize(dev)
         self.eng = Engine(layout.dist, capacity=self.cap_l if self.local else n, device=device,
                           bounds=(lo, 0.0, hi, layout.L))
         self.eng.set_stream(self.stream.cuda_stream)
         self.eng.set_population_hint(0, max(1, min(n, int(share * 1.05))))
         self.tick_no = 0
+        self.max_new = 0  # region state: the most new ids or Leaves of one tick so far
         self.xev = []  # (start, end) hipEvents of timed exchanges (tick_rccl(time_exchange=True))
         # per-tick device time of the strip's own kernels (walk + select, absorb + emit), when timing
         # (scripts/strips_loopback_bench.py): hipEvents on the node's stream, read by strip_kernel_ms()
@@ -203,21 +212,6 @@ class StripNode:
         self.sev = []
 
     # ---- raw kernel calls ----
-    def _set_list(self):
-        self.lst.rl, self.lst.rl_next = self.rl.data_ptr(), self.rl_next.data_ptr()
-
-    def _swap_list(self):
-        """The emit wrote the next tick's list into rl_next: it becomes rl."""
-        self.rl, self.rl_next = self.rl_next, self.rl
-        self._set_list()
-
-    def _list_from_ops(self):
-        """The region list from the tick's op list (after an id-range emit: tick 0, or a tick with more new
-        ids than the list emit takes)."""
-        check(self._L.gwaoi_strip_list_from_ops(self._s(), ctypes.byref(self.lst), _ptr(self.ids), _ptr(self.kinds),
-                                                _ptr(self.l2g), ctypes.c_void_p(self.counts.data_ptr() + 8)))
-        self._swap_list()
-
     def _s(self):
         return ctypes.c_void_p(self.stream.cuda_stream)
 
@@ -227,31 +221,26 @@ class StripNode:
     def _err(self):
         return ctypes.c_void_p(self.counts.data_ptr() + 12)
 
-    def _emit_and_tick(self, host_events: bool, n_bound: int, by_range: bool = False):
+    def _emit_and_tick(self, host_events: bool, n_bound: int, start=None):
         """The op list goes to the manager with its count in device memory (no host round trip);
-        n_bound bounds it: entities present at the start + records received this tick. With a region list
-        the emit merges the list with the tick's new ids (by_range: the id-range emit, then the list is
-        rebuilt from the op list: tick 0, or the recovery of a tick with too many new ids)."""
+        n_bound bounds it: entities present at the start + records received this tick. start: tick 0's
+        global-id arrays (flags, ex, ez) with a region state."""
         L = self._L
         common = (self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz), _ptr(self.ex), _ptr(self.ez),
                   _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds), _ptr(self.scratch),
                   ctypes.c_void_p(self.counts.data_ptr() + 8))
-        use_list = self.lst is not None and not by_range
-        if use_list:
-            check(L.gwaoi_strip_emit_local_list(self._s(), self._g(), ctypes.byref(self.lst), _ptr(self.flags),
-                                                _ptr(self.sx), _ptr(self.sz), _ptr(self.ex), _ptr(self.ez),
-                                                _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds),
-                                                ctypes.c_void_p(self.counts.data_ptr() + 8), _ptr(self.g2l),
-                                                _ptr(self.l2g), _ptr(self.fq), _ptr(self.pend), self.cap_l,
-                                                _ptr(self.lctr)))
-            self._swap_list()
+        ops = (_ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds), ctypes.c_void_p(self.counts.data_ptr() + 8))
+        if self.R is not None:
+            if start is not None:
+                check(L.gwaoi_strip_region_start(self._s(), self._g(), ctypes.byref(self.R), *(_ptr(a) for a in start),
+                                                 *ops))
+            else:
+                check(L.gwaoi_strip_region_emit(self._s(), self._g(), ctypes.byref(self.R), *ops))
             self.h_lctr.copy_(self.lctr, non_blocking=True)
-            self.h_lctr2.copy_(self.lctr2, non_blocking=True)
+            self.h_rctr.copy_(self.rctr, non_blocking=True)
         elif self.local:
             check(L.gwaoi_strip_emit_local(*common, _ptr(self.g2l), _ptr(self.l2g), _ptr(self.fq), _ptr(self.pend),
                                            self.cap_l, _ptr(self.lctr)))
-            if self.lst is not None:
-                self._list_from_ops()
             self.h_lctr.copy_(self.lctr, non_blocking=True)
         else:
             check(L.gwaoi_strip_emit(*common))
@@ -269,18 +258,21 @@ class StripNode:
         else:
             ev = self.eng.tick() if host_events else self.eng.tick_device()
         c = self.h_counts  # complete: the tick waited for every kernel after the copy
-        if use_list and int(self.h_lctr2[3]) & STRIP_ERR_NEWLIST and not int(self.h_lctr[3]) and not int(c[3]):
-            # more ids came into the region than the list emit takes: it emitted nothing (the manager ran an
-            # empty pass, the state did not advance); the same tick by id range, then the list again
-            self.list_fallbacks = getattr(self, "list_fallbacks", 0) + 1
-            return self._emit_and_tick(host_events, n_bound, by_range=True)
-        if int(c[3]) or (self.local and int(self.h_lctr[3])):
-            flags = int(c[3]) | (int(self.h_lctr[3]) if self.local else 0)
-            why = " (the region holds more entities than its local slots, cap_l = %d: nothing of this tick was " \
-                  "applied)" % self.cap_l if flags & STRIP_ERR_SLOTS else ""
+        flags = int(c[3]) | (int(self.h_lctr[3]) if self.local else 0) | (int(self.h_rctr[6]) if self.R is not None else 0)
+        if flags:
+            why = ""
+            if flags & STRIP_ERR_SLOTS:
+                why = " (the region holds more entities than its local slots, cap_l = %d: nothing of this tick was " \
+                      "applied)" % self.cap_l
+            elif flags & STRIP_ERR_NEWLIST:
+                why = " (more than cap_new = %d entities came into or left the region in one tick: nothing of this " \
+                      "tick was applied, the region state is not usable any more)" % self.R.cap_new
             raise _lib.GwaoiError(_lib.GWAOI_ERR_STATE, f"strip {self.rank}: protocol check failed (flags "
                                   f"{flags}){why}")
         self.last_ops = int(c[2])
+        if self.R is not None:  # (the emit flipped cur: the tick's new ids were counted on the other side)
+            cur = int(self.R.cur)
+            self.max_new = max(self.max_new, int(self.h_rctr[2 + (cur ^ 1)]), int(self.h_rctr[4 + cur]))
         return ev
 
     def _events_to_host(self, ev) -> np.ndarray:
@@ -309,18 +301,21 @@ class StripNode:
     def start(self, host_events: bool = False):
         """Tick 0: every entity of the region enters (the seeded workload's initial placement)."""
         with torch.cuda.stream(self.stream):
+            if self.R is not None:  # the workload's tick 0 by global id, only for the start
+                gf = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+                gx, gz = (torch.zeros(self.n, dtype=torch.float32, device=self.device) for _ in range(2))
+            else:
+                gf, gx, gz = self.flags, self.ex, self.ez
             if self.skew:
                 nhot, sigma, every = self.skew
-                check(self._L.gwaoi_strip_init_skew(self._s(), self._g(), _ptr(self.flags), _ptr(self.ex),
-                                                    _ptr(self.ez), ctypes.c_uint64(self.seed),
-                                                    ctypes.c_float(self.layout.L), int(nhot), ctypes.c_float(sigma),
-                                                    int(every)))
+                check(self._L.gwaoi_strip_init_skew(self._s(), self._g(), _ptr(gf), _ptr(gx), _ptr(gz),
+                                                    ctypes.c_uint64(self.seed), ctypes.c_float(self.layout.L),
+                                                    int(nhot), ctypes.c_float(sigma), int(every)))
             else:
-                check(self._L.gwaoi_strip_init_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.ex),
-                                                    _ptr(self.ez), ctypes.c_uint64(self.seed),
-                                                    ctypes.c_float(self.layout.L)))
+                check(self._L.gwaoi_strip_init_walk(self._s(), self._g(), _ptr(gf), _ptr(gx), _ptr(gz),
+                                                    ctypes.c_uint64(self.seed), ctypes.c_float(self.layout.L)))
             self.tick_no = 0
-            return self._emit_and_tick(host_events, self.n, by_range=True)  # (then the region list from its ops)
+            return self._emit_and_tick(host_events, self.n, start=(gf, gx, gz) if self.R is not None else None)
 
     def prepare(self, t: int, step: float = 1.0, moves: Optional[Tuple[torch.Tensor, ...]] = None):
         """End positions of the owned entities (the seeded walk's tick t, or `moves` = (ids, x, z)
@@ -350,22 +345,31 @@ class StripNode:
 
     def _walk(self, t, step):
         L = self._L
-        if self.lst is not None:
-            check(L.gwaoi_strip_walk_list(self._s(), self._g(), ctypes.byref(self.lst), _ptr(self.flags), _ptr(self.sx),
-                                          _ptr(self.sz), _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed),
-                                          ctypes.c_uint64(t), ctypes.c_float(self.layout.L), ctypes.c_float(step),
-                                          self._err()))
+        if self.R is not None:
+            check(L.gwaoi_strip_region_walk(self._s(), self._g(), ctypes.byref(self.R), ctypes.c_uint64(self.seed),
+                                            ctypes.c_uint64(t), ctypes.c_float(self.layout.L), ctypes.c_float(step),
+                                            self._err()))
         else:
             check(L.gwaoi_strip_walk(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz),
                                      _ptr(self.ex), _ptr(self.ez), ctypes.c_uint64(self.seed), ctypes.c_uint64(t),
                                      ctypes.c_float(self.layout.L), ctypes.c_float(step), self._err()))
 
+    def _ingest(self, moves):
+        ids, x, z = moves
+        if self.R is not None:
+            check(self._L.gwaoi_strip_region_ingest(self._s(), self._g(), ctypes.byref(self.R), _ptr(ids), _ptr(x),
+                                                    _ptr(z), int(ids.numel()), self._err()))
+        else:
+            check(self._L.gwaoi_strip_ingest(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
+                                             _ptr(self.ez), _ptr(ids), _ptr(x), _ptr(z), int(ids.numel()),
+                                             self._err()))
+
     def _select(self):
         L = self._L
-        if self.lst is not None:
-            check(L.gwaoi_strip_select_list(self._s(), self._g(), ctypes.byref(self.lst), _ptr(self.flags), _ptr(self.sx),
-                                            _ptr(self.ex), _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
-                                            ctypes.c_void_p(self.counts.data_ptr()), self._err()))
+        if self.R is not None:
+            check(L.gwaoi_strip_region_select(self._s(), self._g(), ctypes.byref(self.R), _ptr(self.left),
+                                              _ptr(self.right), self.cap, ctypes.c_void_p(self.counts.data_ptr()),
+                                              self._err()))
         else:
             check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
                                        _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
@@ -373,10 +377,9 @@ class StripNode:
 
     def _absorb(self, recs, n_max: int, d_n=None):
         L = self._L
-        if self.lst is not None:
-            check(L.gwaoi_strip_absorb_list(self._s(), ctypes.byref(self.lst), _ptr(self.flags), _ptr(self.ex),
-                                            _ptr(self.ez), _ptr(recs), d_n, int(n_max),
-                                            self._err() if d_n is not None else None))
+        if self.R is not None:
+            check(L.gwaoi_strip_region_absorb(self._s(), ctypes.byref(self.R), _ptr(recs), d_n, int(n_max),
+                                              self._err() if d_n is not None else None))
         elif d_n is not None:
             check(L.gwaoi_strip_absorb_n(self._s(), _ptr(self.flags), _ptr(self.ex), _ptr(self.ez), _ptr(recs), d_n,
                                          int(n_max), self._err()))
@@ -385,14 +388,11 @@ class StripNode:
                                        int(n_max)))
 
     def _prepare(self, t, step, moves):
-        L = self._L
         self._ev_prep = (self._mark(),)
         if moves is None:
             self._walk(t, step)
         else:
-            ids, x, z = moves
-            check(L.gwaoi_strip_ingest(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
-                                       _ptr(self.ez), _ptr(ids), _ptr(x), _ptr(z), int(ids.numel()), self._err()))
+            self._ingest(moves)
         self._select()
         self._ev_prep = (self._ev_prep[0], self._mark())
         self.tick_no = t
@@ -437,19 +437,16 @@ class StripNode:
             peers = (self.rank - 1 if self.g.has_left else -1, self.rank + 1 if self.g.has_right else -1)
         if moves is not None:
             self.stream.wait_stream(torch.cuda.current_stream(self.device))
-        L = self._L
         with torch.cuda.stream(self.stream):
             if moves is None:
                 self._walk(t, step)
             else:
-                ids, x, z = moves
-                check(L.gwaoi_strip_ingest(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
-                                           _ptr(self.ez), _ptr(ids), _ptr(x), _ptr(z), int(ids.numel()), self._err()))
+                self._ingest(moves)
             self._select()
             if time_exchange:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            check(L.gwaoi_strip_exchange(comm.handle, self._s(), int(peers[0]), int(peers[1]), _ptr(self.left),
+            check(self._L.gwaoi_strip_exchange(comm.handle, self._s(), int(peers[0]), int(peers[1]), _ptr(self.left),
                                          _ptr(self.right), _ptr(self.counts), self.cap, _ptr(self.left_in),
                                          _ptr(self.right_in), _ptr(self.counts_in)))
             if time_exchange:

@@ -114,44 +114,63 @@ int gwaoi_strip_init_skew(void* stream, const gwaoi_strip_geom* g, uint8_t* flag
 int gwaoi_strip_absorb_n(void* stream, uint8_t* flags, float* ex, float* ez, const uint32_t* d_recs,
                          const uint32_t* d_n, uint32_t n_max, uint32_t* d_err);
 
-/* ---- region lists (ABI 2.1) ----
- * The per-tick kernels above sweep the whole id range (g->n): with a 16M-id world on 8 GPUs every rank
- * scans 16M ids to find its ~2M. With a region list they walk the ids present in the region instead:
- * walk and select over the list, absorb appends the ids that come into the region, and the emit merges the
- * list with the sorted new ids (the op list stays in global id order) and writes the next tick's list. Per
- * tick the work follows the region, not the world. Local slots only (gwaoi_strip_emit_local_list). */
-#define GWAOI_STRIP_ERR_NEWLIST 16u /* more ids came into the region in one tick than the list emit takes
-                                       (cap_new, at most 16384): nothing emitted; emit by id range instead,
-                                       then rebuild the list (gwaoi_strip_list_from_ops) */
+/* ---- region state (ABI 2.1) ----
+ * The per-tick kernels above index the strip's state by global id and sweep the whole id range (g->n): a
+ * 16M-id world on 8 GPUs makes every rank scan 16M ids to find its ~2M, and the ids of one region are spread
+ * over the id space, so each 64-byte line of a state array holds about two of them. With a region state the
+ * strip's state lives in LOCAL-slot order (the manager's own slots): walk and select sweep the cap_l slots
+ * (contiguous), absorb maps the few received ids through g2l (an entity new to the region takes a free slot
+ * there), and the emit walks the region list (the last op list: ids ascending, with their slots) merged with
+ * the tick's new ids, so the op list stays in global id order. Per tick the work follows the region, and
+ * every sweep reads whole lines. Tick 0 (gwaoi_strip_region_start) enters the region's entities from the
+ * global-id arrays of gwaoi_strip_init_walk / _init_skew, which are not needed afterwards.
+ *   Limits: at most cap_new ids may come into the region, and at most cap_new Leaves leave it, per tick (the
+ * halo crossings of one tick: hundreds at the bench sizes); cap_new <= 8 x chunk, chunk <= 16384 (one
+ * block's LDS sort per chunk of the tick's new ids or Leaves). Past either limit, or with no free slot for a
+ * new id, ctr[6] gets GWAOI_STRIP_ERR_NEWLIST / lctr[3] GWAOI_STRIP_ERR_SLOTS, the emit emits nothing and the
+ * region state is no longer consistent: the caller stops the strip (the manager itself stays usable). */
+#define GWAOI_STRIP_ERR_NEWLIST 16u /* region state: more than cap_new new ids or Leaves in one tick */
+#define GWAOI_STRIP_TOMB 0x80000000u /* region list: the entry left the region (a Leave of the last emit) */
 typedef struct {
-  uint32_t* rl;       /* [cap] ids present in the region at the start of the tick, ascending */
-  uint32_t* rl_next;  /* [cap] the next tick's list, written by the emit: the caller swaps rl and rl_next */
-  uint32_t* nw;       /* [cap_new] ids that came into the region this tick (absorbed while not present) */
-  uint32_t* ctr;      /* [4] device: {list length, emitted, new ids, GWAOI_STRIP_ERR_* bits} */
-  uint32_t* scratch;  /* [gwaoi_strip_list_scratch_words(cap)] */
-  uint32_t cap;       /* largest region population (the manager's local slot count, cap_l) */
-  uint32_t cap_new;   /* new ids per tick at most (<= 16384) */
-} gwaoi_strip_list;
-size_t gwaoi_strip_list_scratch_words(uint32_t cap);
-/* rl_next (and the counters) from a tick's op list, e.g. tick 0's Enter pass or an id-range emit; then swap */
-int gwaoi_strip_list_from_ops(void* stream, const gwaoi_strip_list* L, const uint32_t* d_slots, const uint8_t* d_kinds,
-                              const uint32_t* l2g, const uint32_t* d_n_ops);
-int gwaoi_strip_walk_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, uint8_t* flags,
-                          const float* sx, const float* sz, float* ex, float* ez, uint64_t seed, uint64_t tick,
-                          float Lw, float step, uint32_t* d_err);
-int gwaoi_strip_select_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, const uint8_t* flags,
-                            const float* sx, const float* ex, const float* ez, uint32_t* d_left, uint32_t* d_right,
-                            uint32_t cap, uint32_t* d_counts, uint32_t* d_err);
-/* gwaoi_strip_absorb_n (d_n may be NULL: n_max records) that also lists the ids coming into the region */
-int gwaoi_strip_absorb_list(void* stream, const gwaoi_strip_list* L, uint8_t* flags, float* ex, float* ez,
-                            const uint32_t* d_recs, const uint32_t* d_n, uint32_t n_max, uint32_t* d_err);
-/* gwaoi_strip_emit_local over the list: the op list in id order, the state advance and rl_next. With
- * GWAOI_STRIP_ERR_NEWLIST (or no free slots: GWAOI_STRIP_ERR_SLOTS in ctr[3]) nothing is emitted and rl_next
- * is a copy of rl. */
-int gwaoi_strip_emit_local_list(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_list* L, uint8_t* flags,
-                                float* sx, float* sz, const float* ex, const float* ez, uint32_t* d_slots, float* d_x,
-                                float* d_z, uint8_t* d_kinds, uint32_t* d_n_ops, uint32_t* g2l, uint32_t* l2g,
-                                uint32_t* fq, uint32_t* pend, uint32_t cap_l, uint32_t* ctr);
+  uint8_t* flags;     /* [cap_l] GWAOI_STRIP_* per local slot (0: free) */
+  float *sx, *sz;     /* [cap_l] start-of-tick positions */
+  float *ex, *ez;     /* [cap_l] end-of-tick positions */
+  uint32_t* g2l;      /* [n] global id -> local slot (GWAOI_STRIP_NO_SLOT) */
+  uint32_t* l2g;      /* [cap_l] local slot -> global id */
+  uint32_t* fq;       /* [cap_l rounded up to a power of two] free-slot ring */
+  uint32_t* pend;     /* [cap_l] slots of the last emit's Leaves (back to the ring at the next emit) */
+  uint32_t* lctr;     /* [4] ring counters, as gwaoi_strip_local_init */
+  uint32_t* rl[2];    /* [cap_l] region list (ids ascending, GWAOI_STRIP_TOMB on Leaves), double buffered */
+  uint32_t* rs[2];    /* [cap_l] the list entries' slots */
+  uint32_t* nw;       /* [2 * cap_new] the tick's new ids, then their slots (absorb appends) */
+  uint32_t* lv;       /* [cap_new] list positions of the last emit's Leaves */
+  uint32_t* srt;      /* [3 * cap_new] the emit's sorted copies: new ids, their slots, Leave positions */
+  uint32_t* ctr;      /* [8] device, per list buffer p: [p] list length, [2 + p] new ids, [4 + p] tombstones;
+                         [6] GWAOI_STRIP_ERR_* bits */
+  uint32_t* scratch;  /* [gwaoi_strip_scratch_words(n)] (gwaoi_strip_region_start) */
+  uint32_t n, cap_l, cap_new, chunk; /* chunk: 0 = 16384, else a power of two in [16, 16384] */
+  uint32_t cur;       /* the current list buffer (flipped by gwaoi_strip_region_emit) */
+} gwaoi_strip_region;
+/* Zero the slot flags and counters, empty g2l and fill the ring (every pointer above allocated) */
+int gwaoi_strip_region_init(void* stream, gwaoi_strip_region* R);
+/* Tick 0: every entity of the region (global-id arrays flags / ex / ez of gwaoi_strip_init_walk) enters, in
+ * id order, taking slots 0, 1, ...; the op list (local slots) and the region list. More than cap_l: nothing
+ * emitted (*d_n_ops = 0), lctr[3] |= GWAOI_STRIP_ERR_SLOTS. */
+int gwaoi_strip_region_start(void* stream, const gwaoi_strip_geom* g, gwaoi_strip_region* R, const uint8_t* flags,
+                             const float* ex, const float* ez, uint32_t* d_slots, float* d_x, float* d_z,
+                             uint8_t* d_kinds, uint32_t* d_n_ops);
+int gwaoi_strip_region_walk(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_region* R, uint64_t seed,
+                            uint64_t tick, float Lw, float step, uint32_t* d_err);
+int gwaoi_strip_region_ingest(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_region* R,
+                              const uint32_t* d_ids, const float* d_x, const float* d_z, uint32_t n, uint32_t* d_err);
+int gwaoi_strip_region_select(void* stream, const gwaoi_strip_geom* g, const gwaoi_strip_region* R, uint32_t* d_left,
+                              uint32_t* d_right, uint32_t cap, uint32_t* d_counts, uint32_t* d_err);
+/* as gwaoi_strip_absorb_n (d_n may be NULL: n_max records) */
+int gwaoi_strip_region_absorb(void* stream, const gwaoi_strip_region* R, const uint32_t* d_recs, const uint32_t* d_n,
+                              uint32_t n_max, uint32_t* d_err);
+/* The op list (local slots) in global id order, the state advance and the next region list (R->cur flips) */
+int gwaoi_strip_region_emit(void* stream, const gwaoi_strip_geom* g, gwaoi_strip_region* R, uint32_t* d_slots,
+                            float* d_x, float* d_z, uint8_t* d_kinds, uint32_t* d_n_ops);
 
 /* ---- the halo exchange over RCCL (xGMI), device-resident end to end ----
  * One communicator per strip world, one rank per GPU. Rank 0 makes the id; the caller hands the 128

@@ -54,8 +54,7 @@ for nd in nodes:
     rows[-1]["ms_device_total"] = round(rows[-1]["ms_total"] + rows[-1].get("ms_strip_prepare", 0.0)
                                         + rows[-1].get("ms_strip_finish", 0.0), 4)
     rows[-1]["ops"] = nd.last_ops
-    rows[-1]["region_list"] = nd.lst is not None  # the strip kernels over the region's ids (ABI 2.1)
-    rows[-1]["list_fallbacks"] = getattr(nd, "list_fallbacks", 0)
+    rows[-1]["region_state"] = nd.R is not None  # the strip's state in local-slot order (ABI 2.1)
     rows[-1]["halo_records_sent_per_tick"] = halo[nd.rank] / ticks
     nd.close()
 print(json.dumps({"world": world, "per_gpu": per, "ticks": ticks, "halo_records_per_tick": sum(halo) / ticks,

@@ -92,32 +92,33 @@ def test_cpu_gloo_world(oracle_lib, tmp_path, world):
 # ------------------------------------------------------------------------------------------------ GPU
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,local,lst", [(1, True, 1), (3, True, 1), (4, True, 1), (3, True, 0), (3, False, 0),
+@pytest.mark.parametrize("world,local,reg", [(1, True, 1), (3, True, 1), (4, True, 1), (3, True, 0), (3, False, 0),
                                              (3, True, 2)])
-def test_gpu_strips_loopback(gpu, oracle_lib, world, local, lst):
+def test_gpu_strips_loopback(gpu, oracle_lib, world, local, reg):
     """HIP strip kernels + one libgwaoi manager per strip, all on cuda:0; every step's op list equals
     the CPU restatement's and the merged events equal one manager over the whole world. local: the
     managers index their entities by local slot (gwaoi_strip_emit_local), events translated back.
-    lst 1: the per-tick kernels over the region list (ABI 2.1: walk / select / absorb / merge emit over the
-    ids present in the region); 0: over the id range; 2: the region list with room for 1 new id per tick,
-    so most ticks take the fallback (nothing emitted by the list, the tick emitted by id range, the list
-    rebuilt)."""
-    from goworld_amd.strips import LoopbackExchange, StripNode
+    reg 1: the region state (ABI 2.1: state in local-slot order, the emit merging the region list with the
+    tick's new ids); 0: state by global id, kernels over the id range; 2: the region state with 16-entry sort
+    chunks and steps of up to 40 units, so the tick's new ids and Leaves span several chunks (the merge's
+    multi-chunk counts)."""
+    from goworld_amd.strips import LoopbackExchange, StripLayout, StripNode
     po = oracle_lib
     n, Lw = 12000, 3800.0
-    want = SC.global_events(po, n, Lw, D, SEED, TICKS)
-    lay = _layout(world, Lw)
-    nodes = [StripNode(lay, r, n, device=0, seed=SEED, local_slots=local, region_list=lst > 0,
-                       cap_new=1 if lst == 2 else 16384) for r in range(world)]
-    assert all((nd.lst is not None) == (lst > 0) for nd in nodes)
+    step = 40.0 if reg == 2 else 1.0
+    want = SC.global_events(po, n, Lw, D, SEED, TICKS, step=step)
+    lay = StripLayout(world, Lw, D, step)
+    nodes = [StripNode(lay, r, n, device=0, seed=SEED, local_slots=local, region_state=reg > 0,
+                       sort_chunk=16 if reg == 2 else 0, cap_new=128 if reg == 2 else 65536) for r in range(world)]
+    assert all((nd.R is not None) == (reg > 0) for nd in nodes)
     cpu = [SC.CPUStripNode(lay, r, n, po, SEED) for r in range(world)]
     got = [SC.merge_sorted([nd.start(host_events=True) for nd in nodes])]
     for c in cpu:
         c.start()
     assert np.array_equal(got[0], want[0])
     for t in range(1, TICKS):
-        outs = [nd.prepare(t) for nd in nodes]
-        couts = [c.prepare(t) for c in cpu]
+        outs = [nd.prepare(t, step) for nd in nodes]
+        couts = [c.prepare(t, step) for c in cpu]
         for (a, b), (ca, cb) in zip(outs, couts):  # same records to send (order free)
             for x, y in ((a, ca), (b, cb)):
                 xs = x.cpu().numpy().view(np.uint32)
@@ -141,10 +142,8 @@ def test_gpu_strips_loopback(gpu, oracle_lib, world, local, lst):
             evs.append(e)
         got.append(SC.merge_sorted(evs))
         assert np.array_equal(got[t], want[t]), f"world {world} tick {t}: {len(got[t])} vs {len(want[t])}"
-    if lst == 2 and world > 1:  # the fallback ran (halo entities come into the regions every tick)
-        assert sum(getattr(nd, "list_fallbacks", 0) for nd in nodes) > 0
-    if lst == 1:
-        assert sum(getattr(nd, "list_fallbacks", 0) for nd in nodes) == 0
+    if reg == 2:  # the tick's new ids took several sort chunks somewhere
+        assert max(nd.max_new for nd in nodes) > 16
     for nd in nodes:
         nd.close()
 
