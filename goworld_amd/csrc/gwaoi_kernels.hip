@@ -2496,7 +2496,7 @@ k_sweep_dense(SweepArgs a) {
 #ifndef GW_BAND_FAN
 #define GW_BAND_FAN 4
 #endif
-constexpr uint32_t kBandFan = GW_BAND_FAN;  // probes per search level (cells of up to kBandFan keys: one level)
+[[maybe_unused]] constexpr uint32_t kBandFan = GW_BAND_FAN;  // probes per search level (cells of up to kBandFan keys: one level)
 #ifndef GW_BAND_RUN
 #define GW_BAND_RUN 4.0f
 #endif
@@ -2612,6 +2612,7 @@ k_sweep_band(SweepArgs a) {
     if constexpr (kBuf) return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r_key, ((kind == 1 ? zoff : 0u) + i) << 2, 0, 0));
     else return (kind == 1 ? a.band_zk : a.band_xk)[i];
   };
+  (void)ld_key;  // (the search path, GW_BAND_TABLE=0)
   auto ld_zi = [&](uint32_t i) -> uint32_t {
     if constexpr (kBuf) return __builtin_amdgcn_raw_buffer_load_b32(r_zi, i << 2, 0, 0);
     else return a.band_zi[i];
@@ -3378,7 +3379,8 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
 constexpr uint32_t kSmallSlice = 8;
 constexpr uint32_t kBigChunk = 2048;
 // diagnosis only (A/B of where k_slice_sort's time goes; the result is then NOT sorted): 1 skips the wave
-// windows, 2 the block sorts, 3 the register sorts, 4 every sort
+// windows, 2 the block sorts, 3 the register sorts, 4 every sort; 5 the windows' ranking and stores (loads
+// only), 6 the windows' stores
 #ifndef GW_DIAG_SORT
 #define GW_DIAG_SORT 0
 #endif
@@ -3514,6 +3516,15 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
     for (uint32_t k = 0; k < kMedRounds; ++k)
       if (k * 64u + lane < n) win[k * 64u + lane] = v[k];
     __builtin_amdgcn_wave_barrier();  // the window's writes before its reads
+    if (GW_DIAG_SORT == 5) {
+      __builtin_amdgcn_wave_barrier();
+      w0 = wend;
+      continue;
+    }
+    // (Reading the window 4, 8 or 16 keys per step, with each element's segment found once per window, did
+    // not change the kernel, r06_a9; the diagnosis builds put ~100 us of its 198 at skew50 in this ranking,
+    // ~32 in the window loads, ~15 in the stores, r06_a10; a range sort, one block per 2,048 consecutive
+    // events with every slice of up to 256 ranked in LDS, took 243 us, r06_a11.)
 #pragma unroll
     for (uint32_t k = 0; k < kMedRounds; ++k) {
       const uint32_t i = k * 64u + lane;
@@ -3529,7 +3540,8 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
             const uint32_t kj = seg_key(win[s0 + j]);
             pos += (kj < kv || (kj == kv && j < o)) ? 1u : 0u;
           }
-          d[sb + pos] = v[k];
+          if (GW_DIAG_SORT != 6) d[sb + pos] = v[k];
+          else if (pos == 0xFFFFFFFFu) d[0] = v[k];  // (keeps the ranking)
         }
       }
     }
@@ -3805,7 +3817,8 @@ __global__ void __launch_bounds__(kBlock) k_relation(RelArgs a) {
       for (int r = B.z0; r <= B.z1; ++r) {
         const int rb = (r - cz0) * W - cx0;
         const uint32_t e = cst[rb + B.x1 + 1];
-        for (uint32_t p = cst[rb + B.x0]; p < e; ++p) {
+        uint32_t p = cst[rb + B.x0];
+        for (; p < e; ++p) {  // (four reads per step, issued together: 167 -> 188 us, r06_a10)
           const uint4 c = rl[p];
           judge(c.w, c.z, __uint_as_float(c.x), __uint_as_float(c.y));
         }
@@ -4210,12 +4223,23 @@ __device__ __forceinline__ int2 rd_long_sums_lds(const uint32_t* ch, const int32
 }
 
 constexpr int kRdRegChunks = 36;  // chunks of a group held in registers (config 2: 33 +- 1)
+// staged groups: each entry's row (0..63) in a per-wave LDS map, written by the rows' lanes, instead of a walk
+// over the rows each chunk touches (readlanes per row and chunk)
+#ifndef GW_RD_ROWMAP
+#define GW_RD_ROWMAP 1
+#endif
+// diagnosis only (A/B of where k_rd_merge's time goes; the view is then wrong): 1 skips the row search
+#ifndef GW_DIAG_MERGE
+#define GW_DIAG_MERGE 0
+#endif
 __global__ void __launch_bounds__(kBlock) k_rd_merge(RelDeltaArgs a) {
   __shared__ uint32_t chs_all[kBlock / 64][kRdWaveCh];
   __shared__ int32_t pss_all[kBlock / 64][kRdWaveCh];
+  __shared__ uint8_t rid_all[kBlock / 64][GW_RD_ROWMAP ? kRdRegChunks * 64 : 1];
   const int lane = threadIdx.x & 63;
   uint32_t* chs = chs_all[threadIdx.x >> 6];
   int32_t* pss = pss_all[threadIdx.x >> 6];
+  uint8_t* rid = rid_all[threadIdx.x >> 6];
   const uint32_t r0 = ((blockIdx.x * kBlock + threadIdx.x) >> 6) * 64u;
   if (r0 >= a.cap || *a.flag) return;  // wave-uniform
   const uint32_t nr = min(64u, a.cap - r0);
@@ -4242,7 +4266,14 @@ __global__ void __launch_bounds__(kBlock) k_rd_merge(RelDeltaArgs a) {
     const bool act = e < G1;
     const uint32_t cend = min(b + 64u, G1);
     uint32_t ri = L0, mos = 0, mns = 0, mcs = 0, mce = 0;
-    for (uint32_t L = L0; L < nr; ++L) {
+    if (kStaged && GW_RD_ROWMAP) {  // the entry's row from the wave's LDS map, its bounds from that row's lane
+      ri = act ? (uint32_t)rid[e - G0] : 0u;
+      mos = (uint32_t)__shfl((int)os, (int)ri, 64);
+      mns = (uint32_t)__shfl((int)ns, (int)ri, 64);
+      mcs = (uint32_t)__shfl((int)cs, (int)ri, 64);
+      mce = (uint32_t)__shfl((int)ce, (int)ri, 64);
+    }
+    for (uint32_t L = L0; L < ((GW_DIAG_MERGE == 1 || (kStaged && GW_RD_ROWMAP)) ? 0u : nr); ++L) {
       const uint32_t osL = __builtin_amdgcn_readlane(os, L);
       if (osL >= cend) break;  // wave-uniform
       const uint32_t nsL = __builtin_amdgcn_readlane(ns, L), csL = __builtin_amdgcn_readlane(cs, L),
@@ -4289,6 +4320,12 @@ __global__ void __launch_bounds__(kBlock) k_rd_merge(RelDeltaArgs a) {
     }
     for (uint32_t k = lane; k < C1 - C0; k += 64) chs[k] = a.dch[C0 + k];
     for (uint32_t k = lane; k < C1 - C0; k += 64) pss[k] = a.psum[C0 + k];  // (meaningful for long rows)
+    if (GW_RD_ROWMAP) {  // row L's entries [os, next row's os) -> L
+      const uint32_t nxt = (uint32_t)__shfl_down((int)os, 1, 64);
+      const uint32_t oe = (uint32_t)lane + 1u < nr ? nxt : G1;
+      if ((uint32_t)lane < nr)
+        for (uint32_t k = os - G0; k < oe - G0; ++k) rid[k] = (uint8_t)lane;
+    }
     // every load complete before the first store: the walk's uses of vv then wait on nothing (a wait
     // for one of them after stores were issued would be vmcnt(0), i.e. for the stores too)
     __builtin_amdgcn_s_waitcnt(0);
