@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 #include "gwaoi_device.h"
 #include "gwaoi_internal.h"
@@ -3376,6 +3377,29 @@ __global__ void __launch_bounds__(kBlock) k_place(OrderArgs o) {
 // sorted chunk plus, for every other chunk, the count of elements ordered before it there (binary
 // search; ties go to the earlier chunk, so the merge is stable). The chunks are parked in ev_tmp,
 // free once k_place has run (its uint2 view has 2 x slots >= n entries).
+// Ascending sort of N registers by Batcher's odd-even merge network for any N (comparators past N
+// dropped): 191 / 305 / 384 / 543 compare-exchanges for N = 32 / 40 / 48 / 64 (bitonic 64: 672).
+template <int N>
+__device__ __forceinline__ void net_sort(uint32_t (&r)[N]) {
+#pragma unroll
+  for (int p = 1; p < N; p <<= 1) {
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1) {
+#pragma unroll
+      for (int j = k % p; j + k < N; j += 2 * k) {
+#pragma unroll
+        for (int i = 0; i < k && i + j + k < N; ++i) {
+          if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            const uint32_t x = r[i + j], y = r[i + j + k];
+            r[i + j] = min(x, y);
+            r[i + j + k] = max(x, y);
+          }
+        }
+      }
+    }
+  }
+}
+
 constexpr uint32_t kSmallSlice = 8;
 constexpr uint32_t kBigChunk = 2048;
 // diagnosis only (A/B of where k_slice_sort's time goes; the result is then NOT sorted): 1 skips the wave
@@ -3383,6 +3407,12 @@ constexpr uint32_t kBigChunk = 2048;
 // only), 6 the windows' stores
 #ifndef GW_DIAG_SORT
 #define GW_DIAG_SORT 0
+#endif
+// The window ranking is VALU-bound (skew50: ~98 M VALU instructions per launch, ~4 cycles each on a SIMD):
+// GW_MED_SPLIT ranks without the tie test (two loops around the element's own index) and finds each element's
+// owner lane once per window.
+#ifndef GW_MED_SPLIT
+#define GW_MED_SPLIT 1
 #endif
 // longest slice ranked by one wave in its LDS window (below: the block's bitonic sort). Round 6: 64 -> 256
 #ifndef GW_MED_MAX
@@ -3462,7 +3492,23 @@ template <class T>
 __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uint32_t len, T* sk, uint2* bigq,
                          uint32_t* nbig) {
   if (threadIdx.x == 0) *nbig = 0;
-  if (GW_DIAG_SORT != 3 && GW_DIAG_SORT != 4 && len >= 2u && len <= kSmallSlice) {
+  if (GW_DIAG_SORT != 3 && GW_DIAG_SORT != 4 && len >= 2u && len <= kSmallSlice &&
+      std::is_same<T, uint2>::value && GW_MED_SPLIT) {
+    // an event slice: .x is its mover for every element, so only the keys move (Batcher's network, 19
+    // min / max pairs for 8; equal keys are equal events)
+    uint32_t y[kSmallSlice];
+    uint32_t x0 = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kSmallSlice; ++i) {
+      const T e = i < len ? d[b + i] : seg_pad<T>();
+      y[i] = seg_key(e);
+      if (i == 0) x0 = reinterpret_cast<const uint2&>(e).x;
+    }
+    net_sort<kSmallSlice>(y);
+#pragma unroll
+    for (uint32_t i = 0; i < kSmallSlice; ++i)
+      if (i < len) reinterpret_cast<uint2*>(d)[b + i] = make_uint2(x0, y[i]);
+  } else if (GW_DIAG_SORT != 3 && GW_DIAG_SORT != 4 && len >= 2u && len <= kSmallSlice) {
     T v[kSmallSlice];
 #pragma unroll
     for (uint32_t i = 0; i < kSmallSlice; ++i) v[i] = i < len ? d[b + i] : seg_pad<T>();
@@ -3501,13 +3547,16 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
     const uint32_t wend = (uint32_t)__builtin_amdgcn_readlane((int)incl, last);
     const uint32_t n = wend - w0;
     T v[kMedRounds];
+    int own[kMedRounds];  // (GW_MED_SPLIT) the lane owning the round's element, found once per window
 #pragma unroll
     for (uint32_t k = 0; k < kMedRounds; ++k) {
       const uint32_t i = k * 64u + lane;
       v[k] = seg_pad<T>();
+      own[k] = 0;
       if (k * 64u < n) {  // wave-uniform: every lane takes part in the lane moves
         const uint32_t g = w0 + min(i, n - 1u);
         const int L = wave_owner(incl, g);
+        own[k] = L;
         const uint32_t sb = (uint32_t)__shfl((int)b, L, 64), se = (uint32_t)__shfl((int)excl, L, 64);
         if (i < n) v[k] = d[sb + (g - se)];
       }
@@ -3530,15 +3579,20 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
       const uint32_t i = k * 64u + lane;
       if (k * 64u < n) {
         const uint32_t g = w0 + min(i, n - 1u);
-        const int L = wave_owner(incl, g);
+        const int L = GW_MED_SPLIT ? own[k] : wave_owner(incl, g);
         const uint32_t sb = (uint32_t)__shfl((int)b, L, 64), se = (uint32_t)__shfl((int)excl, L, 64);
         const uint32_t sl = (uint32_t)__shfl((int)lm, L, 64);
         if (i < n) {
           const uint32_t kv = seg_key(v[k]), o = g - se, s0 = se - w0;
           uint32_t pos = 0;
-          for (uint32_t j = 0; j < sl; ++j) {
-            const uint32_t kj = seg_key(win[s0 + j]);
-            pos += (kj < kv || (kj == kv && j < o)) ? 1u : 0u;
+          if (GW_MED_SPLIT) {  // the elements before this one count when <=, the ones after when < (stable)
+            for (uint32_t j = 0; j < o; ++j) pos += seg_key(win[s0 + j]) <= kv ? 1u : 0u;
+            for (uint32_t j = o + 1u; j < sl; ++j) pos += seg_key(win[s0 + j]) < kv ? 1u : 0u;
+          } else {
+            for (uint32_t j = 0; j < sl; ++j) {
+              const uint32_t kj = seg_key(win[s0 + j]);
+              pos += (kj < kv || (kj == kv && j < o)) ? 1u : 0u;
+            }
           }
           if (GW_DIAG_SORT != 6) d[sb + pos] = v[k];
           else if (pos == 0xFFFFFFFFu) d[0] = v[k];  // (keeps the ranking)
@@ -3574,6 +3628,9 @@ struct SegSmem {
 // 3,907 blocks at config 2, serialises on the one counter: 9 -> 15 us measured with 1,024 blocks.)
 // Otherwise one thread per op, and k_publish after it.
 constexpr uint32_t kSortFewBlocks = 32;
+#ifndef GW_SORT_BLOCKS
+#define GW_SORT_BLOCKS 0  // a sorting pass's grid at most (0: one block per kBlock ops)
+#endif
 __global__ void __launch_bounds__(kBlock) k_slice_sort(OrderArgs o) {
   __shared__ uint2 sk[kBigChunk];
   __shared__ SegSmem ss;
@@ -3633,7 +3690,8 @@ __global__ void __launch_bounds__(kBlock) k_copy_out(OrderArgs o) {
 void launch_order(const OrderArgs& o, hipStream_t st) {
   hipLaunchKernelGGL(k_place, dim3(o.place_blocks ? o.place_blocks : 1024u), dim3(kBlock), 0, st, o);
   const uint32_t per_op = std::max(1u, (o.n_ops + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_slice_sort, dim3(o.sorted_hint ? std::min(per_op, kSortFewBlocks) : per_op), dim3(kBlock), 0,
+  const uint32_t full = GW_SORT_BLOCKS ? std::min(per_op, (uint32_t)GW_SORT_BLOCKS) : per_op;  // (grid-stride)
+  hipLaunchKernelGGL(k_slice_sort, dim3(o.sorted_hint ? std::min(per_op, kSortFewBlocks) : full), dim3(kBlock), 0,
                      st, o);
   if (o.host_out) hipLaunchKernelGGL(k_copy_out, dim3(512), dim3(kBlock), 0, st, o);
   if (o.pub && !o.sorted_hint) launch_publish(o.g.ctr, o.pub, o.pub_seq, st);
@@ -3891,29 +3949,6 @@ void launch_relation(const RelArgs& a, hipStream_t st) {
 // sort in LDS, 0.88 ms; the network over unpadded LDS rows, 0.18 ms, bank conflicts.)
 constexpr uint32_t kRowNetMax = 64;  // longest row sorted by the register network
 constexpr int kRowPitch = 65;
-
-// Ascending sort of N registers by Batcher's odd-even merge network for any N (comparators past N
-// dropped): 191 / 305 / 384 / 543 compare-exchanges for N = 32 / 40 / 48 / 64 (bitonic 64: 672).
-template <int N>
-__device__ __forceinline__ void net_sort(uint32_t (&r)[N]) {
-#pragma unroll
-  for (int p = 1; p < N; p <<= 1) {
-#pragma unroll
-    for (int k = p; k >= 1; k >>= 1) {
-#pragma unroll
-      for (int j = k % p; j + k < N; j += 2 * k) {
-#pragma unroll
-        for (int i = 0; i < k && i + j + k < N; ++i) {
-          if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
-            const uint32_t x = r[i + j], y = r[i + j + k];
-            r[i + j] = min(x, y);
-            r[i + j + k] = max(x, y);
-          }
-        }
-      }
-    }
-  }
-}
 
 template <int N>
 __device__ __forceinline__ void sort_row_net(uint32_t* ww, int lane, uint32_t len) {
