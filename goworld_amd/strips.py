@@ -111,13 +111,15 @@ class StripNode:
     def __init__(self, layout: StripLayout, rank: int, n: int, device: int = 0, seed: int = 0x5EED0004,
                  halo_cap: Optional[int] = None, skew: Optional[Tuple[int, float, int]] = None,
                  local_slots: bool = True, cap_l: Optional[int] = None, region_state: Optional[bool] = None,
-                 cap_new: int = 65536, sort_chunk: int = 0):
+                 cap_new: int = 65536, sort_chunk: int = 0, stream: Optional[torch.cuda.Stream] = None):
         """skew = (nhot, sigma, hot_every): the skewed-crowd placement of config 5 instead of uniform.
         local_slots: the manager sees local slots (gwaoi_strip_emit_local); False: slot = global id.
         region_state (local slots only, ABI 2.1, default on; GWAOI_STRIP_REGION=0 / 1 forces it): the strip's
         state in local-slot order and the per-tick kernels over the region (gwaoi_strip_region_*), not over the
         world's id range; cap_new: ids that may come into (and Leaves that may leave) the region per tick;
-        sort_chunk: the LDS sort's chunk of those (0: 16384; tests use small chunks to cover the merge)."""
+        sort_chunk: the LDS sort's chunk of those (0: 16384; tests use small chunks to cover the merge).
+        stream: a (non-null) stream to run on, e.g. one shared by several strips of a single-GPU loopback run so
+        that their kernels do not overlap and each strip's hipEvents time its own work; default: its own."""
         self.layout, self.rank, self.n, self.seed = layout, int(rank), int(n), int(seed)
         self.skew = skew
         self.g = layout.geom(rank, n)
@@ -137,7 +139,7 @@ class StripNode:
         self.scratch = torch.zeros(int(self._L.gwaoi_strip_scratch_words(n)), dtype=i32, device=dev)
         # a stream of the node's own (never the null stream: the manager would take that as "its
         # own stream" and the strip kernels and the pipeline would no longer be ordered)
-        self.stream = torch.cuda.Stream(dev)
+        self.stream = stream if stream is not None else torch.cuda.Stream(dev)
         torch.cuda.synchronize(dev)  # the buffers above were zeroed on the current stream
         lo = max(self.g.ra, 0.0)
         hi = min(self.g.rb, layout.L)

@@ -2,7 +2,10 @@
 """Per-strip pipeline cost of a W-strip world on ONE GPU (loopback exchange): what each rank of a
 W-GPU strips run would pay per tick, stage by stage (hipEvents). Used to see how the per-rank tick
 grows with the world size (the manager's slot space is the whole world's id range).
-usage: strips_loopback_bench.py [world=8] [per_gpu=2000000] [ticks=20]"""
+usage: strips_loopback_bench.py [world=8] [per_gpu=2000000] [ticks=20] [streams=shared|own]
+shared (default): every strip on one stream, so no strip's kernels overlap another's and its hipEvents time
+what its own GPU would run; own: a stream per strip (kernels of different strips overlap, so each strip's
+stage times include the others' contention)."""
 import json
 import math
 import os
@@ -17,11 +20,13 @@ from goworld_amd.strips import LoopbackExchange, StripLayout, StripNode  # noqa:
 world = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 per = int(sys.argv[2]) if len(sys.argv) > 2 else 2_000_000
 ticks = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+shared = (sys.argv[4] if len(sys.argv) > 4 else "shared") == "shared"
 n = per * world
 L = math.sqrt(n / (1_000_000 / 35000.0 ** 2))
 lay = StripLayout(world, L, 100.0, 1.0)
 t0 = time.perf_counter()
-nodes = [StripNode(lay, r, n, device=0, seed=0x5EED0004) for r in range(world)]
+st = torch.cuda.Stream(0) if shared else None
+nodes = [StripNode(lay, r, n, device=0, seed=0x5EED0004, stream=st) for r in range(world)]
 for nd in nodes:
     nd.start(host_events=False)
 print(f"setup {time.perf_counter() - t0:.1f}s, world {n}, L {L:.0f}", file=sys.stderr, flush=True)
@@ -53,11 +58,13 @@ for nd in nodes:
     rows[-1].update(nd.strip_kernel_ms() or {})
     rows[-1]["ms_device_total"] = round(rows[-1]["ms_total"] + rows[-1].get("ms_strip_prepare", 0.0)
                                         + rows[-1].get("ms_strip_finish", 0.0), 4)
+    rows[-1]["device_total_over_pipeline"] = round(rows[-1]["ms_device_total"] / max(1e-9, rows[-1]["ms_total"]), 4)
     rows[-1]["ops"] = nd.last_ops
     rows[-1]["region_state"] = nd.R is not None  # the strip's state in local-slot order (ABI 2.1)
     rows[-1]["halo_records_sent_per_tick"] = halo[nd.rank] / ticks
     nd.close()
-print(json.dumps({"world": world, "per_gpu": per, "ticks": ticks, "halo_records_per_tick": sum(halo) / ticks,
+print(json.dumps({"world": world, "per_gpu": per, "ticks": ticks, "streams": "shared" if shared else "own",
+                  "halo_records_per_tick": sum(halo) / ticks,
                   "wall_ms_per_tick_all_strips": wall,
                   "note": "W strips of one world on ONE GPU, halo records handed over in-process (LoopbackExchange); "
                           "per strip: its pipeline stages (hipEvents), its strip kernels (prepare = walk + select, finish = "
