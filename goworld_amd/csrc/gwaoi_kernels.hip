@@ -2084,6 +2084,7 @@ __device__ __forceinline__ float2 rec_key(const Rec* rec, uint32_t i) {
   return make_float2(kx, kz);
 }
 __global__ void __launch_bounds__(kBlock) k_band_sort(BandArgs a) {
+  // (the staged keys as two float arrays instead of float2 pairs: 174.8 us either way at skew50, r06_a15)
   __shared__ float2 kk[kBandSortStage];
   __shared__ Geom gs[kLdsGeoms];
   __shared__ uint32_t bh[2 * kLdsGeoms];
@@ -3408,12 +3409,6 @@ constexpr uint32_t kBigChunk = 2048;
 #ifndef GW_DIAG_SORT
 #define GW_DIAG_SORT 0
 #endif
-// The window ranking is VALU-bound (skew50: ~98 M VALU instructions per launch, ~4 cycles each on a SIMD):
-// GW_MED_SPLIT ranks without the tie test (two loops around the element's own index) and finds each element's
-// owner lane once per window.
-#ifndef GW_MED_SPLIT
-#define GW_MED_SPLIT 1
-#endif
 // longest slice ranked by one wave in its LDS window (below: the block's bitonic sort). Round 6: 64 -> 256
 #ifndef GW_MED_MAX
 #define GW_MED_MAX 256u
@@ -3493,7 +3488,7 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
                          uint32_t* nbig) {
   if (threadIdx.x == 0) *nbig = 0;
   if (GW_DIAG_SORT != 3 && GW_DIAG_SORT != 4 && len >= 2u && len <= kSmallSlice &&
-      std::is_same<T, uint2>::value && GW_MED_SPLIT) {
+      std::is_same<T, uint2>::value) {
     // an event slice: .x is its mover for every element, so only the keys move (Batcher's network, 19
     // min / max pairs for 8; equal keys are equal events)
     uint32_t y[kSmallSlice];
@@ -3547,7 +3542,7 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
     const uint32_t wend = (uint32_t)__builtin_amdgcn_readlane((int)incl, last);
     const uint32_t n = wend - w0;
     T v[kMedRounds];
-    int own[kMedRounds];  // (GW_MED_SPLIT) the lane owning the round's element, found once per window
+    int own[kMedRounds];  // the lane owning the round's element, found once per window
 #pragma unroll
     for (uint32_t k = 0; k < kMedRounds; ++k) {
       const uint32_t i = k * 64u + lane;
@@ -3570,29 +3565,26 @@ __device__ void seg_sort(T* __restrict__ d, T* __restrict__ tmp, uint32_t b, uin
       w0 = wend;
       continue;
     }
-    // (Reading the window 4, 8 or 16 keys per step, with each element's segment found once per window, did
-    // not change the kernel, r06_a9; the diagnosis builds put ~100 us of its 198 at skew50 in this ranking,
-    // ~32 in the window loads, ~15 in the stores, r06_a10; a range sort, one block per 2,048 consecutive
-    // events with every slice of up to 256 ranked in LDS, took 243 us, r06_a11.)
+    // (The owner lanes found once per window (own[]) and the key-only network for short event slices: 198 ->
+    // 180 us at skew50, r06_a15. Not kept: the window read 4, 8 or 16 keys per step, r06_a9; the ranking split
+    // into two loops around the element without the tie test (lanes of one slice then read different words:
+    // bank conflicts 3% -> 15%), r06_a12; a range sort, one block per 2,048 consecutive events with every slice
+    // of up to 256 ranked in LDS, 243 us, r06_a11. The diagnosis builds put ~100 us of 198 in this ranking, ~32
+    // in the window loads, ~15 in the stores, r06_a10.)
 #pragma unroll
     for (uint32_t k = 0; k < kMedRounds; ++k) {
       const uint32_t i = k * 64u + lane;
       if (k * 64u < n) {
         const uint32_t g = w0 + min(i, n - 1u);
-        const int L = GW_MED_SPLIT ? own[k] : wave_owner(incl, g);
+        const int L = own[k];
         const uint32_t sb = (uint32_t)__shfl((int)b, L, 64), se = (uint32_t)__shfl((int)excl, L, 64);
         const uint32_t sl = (uint32_t)__shfl((int)lm, L, 64);
         if (i < n) {
           const uint32_t kv = seg_key(v[k]), o = g - se, s0 = se - w0;
           uint32_t pos = 0;
-          if (GW_MED_SPLIT) {  // the elements before this one count when <=, the ones after when < (stable)
-            for (uint32_t j = 0; j < o; ++j) pos += seg_key(win[s0 + j]) <= kv ? 1u : 0u;
-            for (uint32_t j = o + 1u; j < sl; ++j) pos += seg_key(win[s0 + j]) < kv ? 1u : 0u;
-          } else {
-            for (uint32_t j = 0; j < sl; ++j) {
-              const uint32_t kj = seg_key(win[s0 + j]);
-              pos += (kj < kv || (kj == kv && j < o)) ? 1u : 0u;
-            }
+          for (uint32_t j = 0; j < sl; ++j) {
+            const uint32_t kj = seg_key(win[s0 + j]);
+            pos += (kj < kv || (kj == kv && j < o)) ? 1u : 0u;
           }
           if (GW_DIAG_SORT != 6) d[sb + pos] = v[k];
           else if (pos == 0xFFFFFFFFu) d[0] = v[k];  // (keeps the ranking)
