@@ -48,10 +48,14 @@ for w in ("config3", "strips", "strips_skew", "skew", "skew50", "gametick"):
         note = f"p99 {x.get('p99_tick_ms') or 0:.3f} host-staged"
     if w in ("skew", "skew50"):
         note = f"{(x.get('events_per_tick') or 0) / 1e6:.1f} M events per tick"
+    st = stages(x)
     if w == "gametick":
-        gt = x.get("gametick") or {}
-        note = ", ".join(f"{k} {v:.3f}" for k, v in gt.items() if isinstance(v, float) and k.endswith("_ms"))[:200]
-    rows.append(f"| {names[w]} | **{x['ms_per_step']:.4f}** | {x['value']:.3g} | {stages(x)} | {note} |")
+        g = x.get("stage_ms") or {}
+        st = ""
+        note = f"ingest {g.get('ingest', 0):.3f}, AOI tick {g.get('aoi_tick', 0):.3f}, sync fan-out {g.get('collect_sync', 0):.3f} ms"
+    if w == "strips":
+        note = f"p99 {x.get('p99_tick_ms') or 0:.3f}; RCCL exchange {1e3 * (x.get('exchange_ms') or 0):.1f} µs per tick (one rank)"
+    rows.append(f"| {names[w]} | **{x['ms_per_step']:.4f}** | {x['value']:.3g} | {st} | {note} |")
 lp = load(loop)
 if lp:
     ps = lp["per_strip"]
