@@ -368,6 +368,8 @@ class StripNode:
 
     def _select(self):
         L = self._L
+        if not (self.g.has_left or self.g.has_right):  # a one-strip world: nothing to send (counts stay 0)
+            return
         if self.R is not None:
             check(L.gwaoi_strip_region_select(self._s(), self._g(), ctypes.byref(self.R), _ptr(self.left),
                                               _ptr(self.right), self.cap, ctypes.c_void_p(self.counts.data_ptr()),
@@ -445,16 +447,17 @@ class StripNode:
             else:
                 self._ingest(moves)
             self._select()
-            if time_exchange:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-            check(self._L.gwaoi_strip_exchange(comm.handle, self._s(), int(peers[0]), int(peers[1]), _ptr(self.left),
-                                         _ptr(self.right), _ptr(self.counts), self.cap, _ptr(self.left_in),
-                                         _ptr(self.right_in), _ptr(self.counts_in)))
-            if time_exchange:
-                e1 = torch.cuda.Event(enable_timing=True)
-                e1.record()
-                self.xev.append((e0, e1))
+            if peers[0] >= 0 or peers[1] >= 0:  # (no neighbour: no RCCL call at all)
+                if time_exchange:
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                check(self._L.gwaoi_strip_exchange(comm.handle, self._s(), int(peers[0]), int(peers[1]),
+                                                   _ptr(self.left), _ptr(self.right), _ptr(self.counts), self.cap,
+                                                   _ptr(self.left_in), _ptr(self.right_in), _ptr(self.counts_in)))
+                if time_exchange:
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    self.xev.append((e0, e1))
             for k, recs in enumerate((self.left_in, self.right_in)):
                 if peers[k] >= 0:
                     self._absorb(recs, self.cap, ctypes.c_void_p(self.counts_in.data_ptr() + 4 * k))

@@ -387,7 +387,8 @@ def test_rccl_exchange_loopback(gpu):
 
 def test_strip_tick_rccl_single_rank_matches(gpu):
     """StripNode.tick_rccl (select -> RCCL exchange -> absorb_n -> emit -> tick, all on the stream) on a
-    one-strip world equals the host-driven path tick for tick."""
+    one-strip world equals the host-driven path tick for tick. The strip exchanges with itself (peers (0, 0):
+    a loopback RCCL group; with no peer at all the node makes no RCCL call)."""
     import torch
     from goworld_amd.strips import StripComm, StripLayout, StripNode
     os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
@@ -399,7 +400,7 @@ def test_strip_tick_rccl_single_rank_matches(gpu):
     assert np.array_equal(a.start(host_events=True), b.start(host_events=True))
     for t in range(1, 5):
         ea = a.finish(*a.prepare(t), host_events=True)
-        eb = b.tick_rccl(t, comm, host_events=True)
+        eb = b.tick_rccl(t, comm, host_events=True, peers=(0, 0))
         assert np.array_equal(ea, eb), f"tick {t}"
         assert len(ea) > 1000
     torch.cuda.synchronize()
@@ -428,6 +429,37 @@ def test_strip_local_slots_exhausted_keeps_manager_usable(gpu):
     assert len(ev) == 0
     torch.cuda.synchronize()
     nd.close()
+
+
+def test_strip_region_new_ids_over_cap_raises(gpu):
+    """Region state (ABI 2.1): a tick that brings more ids into a region than cap_new emits nothing and the strip
+    raises, naming GWAOI_STRIP_ERR_NEWLIST; the manager still runs passes. (3 strips, 40-unit steps: tens of halo
+    crossings per tick against a cap_new of 2.)"""
+    import torch
+    from goworld_amd import _lib
+    from goworld_amd.strips import LoopbackExchange, StripLayout, StripNode
+    n, L, step = 12000, 3800.0, 40.0
+    lay = StripLayout(3, L, 100.0, step)
+    nodes = [StripNode(lay, r, n, device=0, seed=0x5EED0079, cap_new=2, sort_chunk=16) for r in range(3)]
+    assert all(nd.R is not None for nd in nodes)
+    for nd in nodes:
+        nd.start()
+    raised = []
+    for t in range(1, 4):
+        ins = LoopbackExchange.exchange([nd.prepare(t, step) for nd in nodes])
+        for nd, i in zip(nodes, ins):
+            try:
+                nd.finish(*i)
+            except _lib.GwaoiError as e:
+                raised.append(str(e))
+        if raised:
+            break
+    assert raised and all("flags 16" in m and "cap_new = 2" in m for m in raised), raised
+    for nd in nodes:
+        assert len(nd.eng.tick()) == 0  # the manager is not poisoned: an empty pass runs
+    torch.cuda.synchronize()
+    for nd in nodes:
+        nd.close()
 
 
 def test_strip_absorb_n_flags_a_cut_list(gpu):
