@@ -1357,7 +1357,16 @@ def main():
         # its own deadline: the headline line is already measured, so a strips run that does not finish
         # (a hung RCCL peer) is reported in it, and every rank ends cleanly, instead of losing the line
         guard = arm_deadline(120.0 + 0.05 * args.strips_steps, rank, result)
-        sub = strips_submeasurement(args, rank, world, dev, sync_all, allmax, backend)
+        try:
+            sub = strips_submeasurement(args, rank, world, dev, sync_all, allmax, backend)
+        except Exception as e:  # a failed strips run is reported in the already-measured line, never loses it
+            log(f"[rank {rank}] strips sub-measurement failed: {e!r}")
+            if rank == 0:
+                result["strips"] = {"error": f"failed on rank 0: {e!r} (the headline line above it was measured "
+                                             "before it started)"}
+                print(json.dumps(result), file=_stdout_for_json(), flush=True)
+            # (the other ranks may wait in a collective of the strips run: their deadline ends them, status 0)
+            os._exit(0)
         guard.cancel()
         if rank == 0:
             result["strips"] = sub
