@@ -55,7 +55,7 @@ STRIP_SYMBOLS = (
     "gwaoi_strip_absorb_n", "gwaoi_strip_comm_id", "gwaoi_strip_comm_init", "gwaoi_strip_comm_destroy",
     "gwaoi_strip_exchange", "gwaoi_strip_local_init", "gwaoi_strip_emit_local", "gwaoi_strip_translate_events",
     "gwaoi_strip_region_init", "gwaoi_strip_region_start", "gwaoi_strip_region_walk", "gwaoi_strip_region_ingest",
-    "gwaoi_strip_region_select", "gwaoi_strip_region_absorb", "gwaoi_strip_region_emit",
+    "gwaoi_strip_region_select", "gwaoi_strip_region_absorb", "gwaoi_strip_region_emit", "gwaoi_strip_region_absorb2",
 )
 
 
@@ -177,7 +177,7 @@ _lib = None
 ABI_MINOR_SYMBOLS = ("gwaoi_stage_moves_pinned_partial", "gwaoi_stage_moves_pinned_async", "gwaoi_abi_minor",
                      "gwaoi_strip_region_init", "gwaoi_strip_region_start", "gwaoi_strip_region_walk",
                      "gwaoi_strip_region_ingest", "gwaoi_strip_region_select", "gwaoi_strip_region_absorb",
-                     "gwaoi_strip_region_emit")
+                     "gwaoi_strip_region_emit", "gwaoi_strip_region_absorb2")
 ABI_VERSION = 2  # GWAOI_ABI_VERSION of include/gwaoi.h that these ctypes structs and signatures follow
 
 
@@ -274,6 +274,7 @@ def load(path: str = SO_PATH):
         "gwaoi_strip_region_ingest": ([vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),
         "gwaoi_strip_region_select": ([vp, vp, vp, vp, vp, u32, vp, vp], ctypes.c_int),
         "gwaoi_strip_region_absorb": ([vp, vp, vp, vp, u32, vp], ctypes.c_int),
+        "gwaoi_strip_region_absorb2": ([vp, vp, vp, vp, u32, vp, vp, u32, vp], ctypes.c_int),
         "gwaoi_strip_region_emit": ([vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),
         "gwaoi_strip_init_skew": ([vp, vp, vp, vp, vp, u64, f32, u32, f32, u32], ctypes.c_int),
         "gwaoi_strip_absorb_n": ([vp, vp, vp, vp, vp, vp, u32, vp], ctypes.c_int),

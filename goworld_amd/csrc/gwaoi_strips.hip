@@ -511,23 +511,27 @@ __global__ void __launch_bounds__(kSBlock) k_rs_start(gwaoi_strip_geom g, RsDev 
 }
 
 // received records into the slot state; an id new to the region takes a free slot and is appended to the
-// tick's new ids (nw: ids, then their slots at nw + cap_new)
-__global__ void __launch_bounds__(kSBlock) k_rs_absorb(RsDev R, const uint4* recs, uint32_t n, const uint32_t* d_n,
+// tick's new ids (nw: ids, then their slots at nw + cap_new). Two messages in one launch (both neighbours'):
+// threads [0, na) take message a, the rest message b; a count in device memory (d_n*) clamps its message.
+__global__ void __launch_bounds__(kSBlock) k_rs_absorb(RsDev R, const uint4* recs_a, uint32_t na, const uint32_t* d_na,
+                                                       const uint4* recs_b, uint32_t nb, const uint32_t* d_nb,
                                                        uint32_t* err) {
-  const uint32_t k = blockIdx.x * kSBlock + threadIdx.x;
-  if (d_n) {
-    const uint32_t got = *d_n;
-    if (got > n && k == 0 && err) atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
-    n = min(n, got);
+  const uint32_t t = blockIdx.x * kSBlock + threadIdx.x;
+  if (t == 0 && err) {  // a sender past its capacity kept counting: its list was cut (the receiver fails too)
+    if ((d_na && *d_na > na) || (d_nb && *d_nb > nb)) atomicOr(err, GWAOI_STRIP_ERR_OVERFLOW);
   }
+  const bool second = t >= na;
+  const uint32_t k = second ? t - na : t;
+  const uint32_t* d_n = second ? d_nb : d_na;
+  uint32_t n = second ? nb : na;
+  if (d_n) n = min(n, *d_n);
   const uint32_t tail = R.lctr[1];  // (releases run in the emit, after every absorb of the tick)
   uint4 r = make_uint4(0u, 0u, 0u, 0u);
   uint32_t l = GWAOI_STRIP_NO_SLOT;
   if (k < n) {
-    r = recs[k];
+    r = (second ? recs_b : recs_a)[k];
     l = R.g2l[r.x];
-  }
-  const bool fresh = k < n && l == GWAOI_STRIP_NO_SLOT;
+  }  const bool fresh = k < n && l == GWAOI_STRIP_NO_SLOT;
   const uint32_t ka = wave_append_s(&R.lctr[0], fresh);
   const bool got_slot = fresh && (int)(tail - ka) > 0;
   if (fresh && !got_slot) atomicOr(&R.lctr[3], GWAOI_STRIP_ERR_SLOTS);
@@ -909,9 +913,19 @@ int gwaoi_strip_region_select(void* stream, const gwaoi_strip_geom* g, const gwa
 
 int gwaoi_strip_region_absorb(void* stream, const gwaoi_strip_region* R, const uint32_t* d_recs, const uint32_t* d_n,
                               uint32_t n_max, uint32_t* d_err) {
-  if (!region_ok(R) || (n_max && !d_recs)) return GWAOI_ERR_INVALID;
-  hipLaunchKernelGGL(gw::k_rs_absorb, gw::blocks_for(n_max ? n_max : 1u), dim3(gw::kSBlock), 0, (hipStream_t)stream,
-                     region_dev(R), reinterpret_cast<const uint4*>(d_recs), n_max, d_n, d_err);
+  return gwaoi_strip_region_absorb2(stream, R, d_recs, d_n, n_max, nullptr, nullptr, 0u, d_err);
+}
+
+int gwaoi_strip_region_absorb2(void* stream, const gwaoi_strip_region* R, const uint32_t* d_left, const uint32_t* d_nl,
+                               uint32_t nl_max, const uint32_t* d_right, const uint32_t* d_nr, uint32_t nr_max,
+                               uint32_t* d_err) {
+  if (!region_ok(R) || (nl_max && !d_left) || (nr_max && !d_right) || nl_max > 0x7fffffffu || nr_max > 0x7fffffffu)
+    return GWAOI_ERR_INVALID;
+  // one block at least: a count check runs even for zero-capacity messages
+  const uint32_t tot = nl_max + nr_max;
+  hipLaunchKernelGGL(gw::k_rs_absorb, gw::blocks_for(tot ? tot : 1u), dim3(gw::kSBlock), 0, (hipStream_t)stream,
+                     region_dev(R), reinterpret_cast<const uint4*>(d_left), nl_max, d_nl,
+                     reinterpret_cast<const uint4*>(d_right), nr_max, d_nr, d_err);
   return hipGetLastError() == hipSuccess ? GWAOI_OK : GWAOI_ERR_HIP;
 }
 

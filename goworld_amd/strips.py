@@ -414,12 +414,25 @@ class StripNode:
         with torch.cuda.stream(self.stream):
             f0 = self._mark()
             nin = 0
+            got = []
             for recs in (left_in, right_in):
                 if recs is not None and recs.numel():
                     recs = recs.to(self.device).contiguous()
                     recs.record_stream(self.stream)
                     nin += int(recs.shape[0])
-                    self._absorb(recs, int(recs.shape[0]))
+                    got.append(recs)
+                else:
+                    got.append(None)
+            if self.R is not None and any(g is not None for g in got):  # both messages, one launch
+                (a, b) = got
+                check(self._L.gwaoi_strip_region_absorb2(
+                    self._s(), ctypes.byref(self.R), _ptr(a) if a is not None else None, None,
+                    int(a.shape[0]) if a is not None else 0, _ptr(b) if b is not None else None, None,
+                    int(b.shape[0]) if b is not None else 0, None))
+            elif self.R is None:
+                for recs in got:
+                    if recs is not None:
+                        self._absorb(recs, int(recs.shape[0]))
             self._f0 = f0
             return self._emit_and_tick(host_events, self.eng.count()[0] + nin)
 
@@ -458,9 +471,17 @@ class StripNode:
                     e1 = torch.cuda.Event(enable_timing=True)
                     e1.record()
                     self.xev.append((e0, e1))
-            for k, recs in enumerate((self.left_in, self.right_in)):
-                if peers[k] >= 0:
-                    self._absorb(recs, self.cap, ctypes.c_void_p(self.counts_in.data_ptr() + 4 * k))
+            if self.R is not None:  # both messages, one launch (an absent peer: an empty message)
+                cin = self.counts_in.data_ptr()
+                on = (peers[0] >= 0, peers[1] >= 0)
+                check(self._L.gwaoi_strip_region_absorb2(
+                    self._s(), ctypes.byref(self.R), _ptr(self.left_in), ctypes.c_void_p(cin) if on[0] else None,
+                    self.cap if on[0] else 0, _ptr(self.right_in), ctypes.c_void_p(cin + 4) if on[1] else None,
+                    self.cap if on[1] else 0, self._err()))
+            else:
+                for k, recs in enumerate((self.left_in, self.right_in)):
+                    if peers[k] >= 0:
+                        self._absorb(recs, self.cap, ctypes.c_void_p(self.counts_in.data_ptr() + 4 * k))
             self.tick_no = t
             return self._emit_and_tick(host_events, self.eng.count()[0] + 2 * self.cap)
 

@@ -168,6 +168,10 @@ int gwaoi_strip_region_select(void* stream, const gwaoi_strip_geom* g, const gwa
 /* as gwaoi_strip_absorb_n (d_n may be NULL: n_max records) */
 int gwaoi_strip_region_absorb(void* stream, const gwaoi_strip_region* R, const uint32_t* d_recs, const uint32_t* d_n,
                               uint32_t n_max, uint32_t* d_err);
+/* both neighbours' messages in one launch (either may be empty: n_max 0) */
+int gwaoi_strip_region_absorb2(void* stream, const gwaoi_strip_region* R, const uint32_t* d_left, const uint32_t* d_nl,
+                               uint32_t nl_max, const uint32_t* d_right, const uint32_t* d_nr, uint32_t nr_max,
+                               uint32_t* d_err);
 /* The op list (local slots) in global id order, the state advance and the next region list (R->cur flips) */
 int gwaoi_strip_region_emit(void* stream, const gwaoi_strip_geom* g, gwaoi_strip_region* R, uint32_t* d_slots,
                             float* d_x, float* d_z, uint8_t* d_kinds, uint32_t* d_n_ops);
