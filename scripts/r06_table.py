@@ -54,7 +54,9 @@ for w in ("config3", "strips", "strips_skew", "skew", "skew50", "gametick"):
         st = ""
         note = f"ingest {g.get('ingest', 0):.3f}, AOI tick {g.get('aoi_tick', 0):.3f}, sync fan-out {g.get('collect_sync', 0):.3f} ms"
     if w == "strips":
-        note = f"p99 {x.get('p99_tick_ms') or 0:.3f}; RCCL exchange {1e3 * (x.get('exchange_ms') or 0):.1f} µs per tick (one rank)"
+        xm = x.get("exchange_ms")
+        note = f"p99 {x.get('p99_tick_ms') or 0:.3f}; " + (f"RCCL exchange {1e3 * xm:.1f} µs per tick" if xm is not None
+                                                          else "one strip: no halo, no select, no RCCL call")
     rows.append(f"| {names[w]} | **{x['ms_per_step']:.4f}** | {x['value']:.3g} | {st} | {note} |")
 lp = load(loop)
 if lp:
