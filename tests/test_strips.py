@@ -164,3 +164,44 @@ def test_gpu_strips_two_processes(gpu, oracle_lib, tmp_path):
     for t in range(TICKS):
         got = SC.merge_sorted([p[f"arr_{t}"] for p in per])
         assert np.array_equal(got, want[t]), f"tick {t}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("reg", [1, 0])
+def test_gpu_strips_ingest_external_moves(gpu, oracle_lib, reg):
+    """Strips driven by external moves (gwaoi_strip_ingest / gwaoi_strip_region_ingest: the owned entities' end
+    positions handed in as (ids, x, z) device arrays, in a shuffled order) instead of the seeded walk kernel; the
+    merged events equal one manager over the whole world, tick by tick. The CPU restatement supplies each tick's
+    owned ids and their end positions."""
+    import torch
+    from goworld_amd.strips import LoopbackExchange, StripNode
+    po = oracle_lib
+    n, Lw, world = 12000, 3800.0, 3
+    want = SC.global_events(po, n, Lw, D, SEED, TICKS)
+    lay = _layout(world, Lw)
+    nodes = [StripNode(lay, r, n, device=0, seed=SEED, region_state=reg > 0) for r in range(world)]
+    assert all((nd.R is not None) == (reg > 0) for nd in nodes)
+    cpu = [SC.CPUStripNode(lay, r, n, po, SEED) for r in range(world)]
+    got = [SC.merge_sorted([nd.start(host_events=True) for nd in nodes])]
+    for c in cpu:
+        c.start()
+    assert np.array_equal(got[0], want[0])
+    rng = np.random.default_rng(7)
+    dev = torch.device("cuda", 0)
+    for t in range(1, TICKS):
+        outs, couts = [], []
+        for nd, c in zip(nodes, cpu):
+            own = np.nonzero(c.flags & SC.O)[0]  # owned at the start of the tick
+            couts.append(c.prepare(t))           # the walk's end positions (c.wx, c.wz) and the CPU's records
+            perm = rng.permutation(len(own))
+            ids = torch.from_numpy(own[perm].astype(np.int32)).to(dev)
+            x = torch.from_numpy(np.ascontiguousarray(c.wx[own][perm])).to(dev)
+            z = torch.from_numpy(np.ascontiguousarray(c.wz[own][perm])).to(dev)
+            outs.append(nd.prepare(t, moves=(ids, x, z)))
+        ins = LoopbackExchange.exchange(outs)
+        got.append(SC.merge_sorted([nd.finish(*i, host_events=True) for nd, i in zip(nodes, ins)]))
+        assert np.array_equal(got[t], want[t]), f"tick {t}: {len(got[t])} vs {len(want[t])}"
+        for c, ci in zip(cpu, LoopbackExchange.exchange(couts)):  # the restatement advances too
+            c.finish(*ci)
+    for nd in nodes:
+        nd.close()
