@@ -446,6 +446,9 @@ constexpr uint32_t kOrderSmallOps = 1024;
 void launch_order_small(const OrderArgs& o, hipStream_t st);
 void launch_copy_out(const OrderArgs& o, hipStream_t st);  // k_copy_out alone (host event delivery)
 void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_t st);
+// a[0, na) then b[0, nb) (na + nb <= kPubWords) into pub, then seq into pub[kPubWords]
+void launch_publish_words(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* pub,
+                          uint32_t seq, hipStream_t st);
 void launch_relation(const RelArgs& a, hipStream_t st);
 // Rows of cols (filled by the fill pass) sorted in place.
 void launch_row_sort(const uint32_t* row_ptr, uint32_t cap, uint32_t* cols, uint32_t* tmp, hipStream_t st);

@@ -3801,6 +3801,24 @@ void launch_publish(const uint32_t* ctr, uint32_t* pub, uint32_t seq, hipStream_
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, ctr, pub, seq);
 }
 
+// A few device words the host must read between launches (the relation's sizes), published the same
+// way: words a[0, na) then b[0, nb), then the sequence word.
+__global__ void k_publish_words(const uint32_t* __restrict__ a, uint32_t na, const uint32_t* __restrict__ b,
+                                uint32_t nb, uint32_t* pub, uint32_t seq) {
+  const uint32_t i = threadIdx.x;
+  if (i < na + nb) {
+    __hip_atomic_store(&pub[i], i < na ? a[i] : b[i - na], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
+  __syncthreads();
+  if (i == 0) __hip_atomic_store(&pub[kPubWords], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_publish_words(const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* pub,
+                          uint32_t seq, hipStream_t st) {
+  hipLaunchKernelGGL(k_publish_words, dim3(1), dim3(64), 0, st, a, na, b, nb, pub, seq);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Relation export: row s = {o : N(s,o)} = {o : in(L, F)}, L = later actor, over the END-of-pass
 // state (main records only). Count pass (row_ptr null) then fill pass; rows sorted afterwards.

@@ -158,7 +158,7 @@ struct gwaoi_mgr {
   uint32_t *rel_rp = nullptr, *rel_cols = nullptr, *rel_tmp = nullptr;
   uint64_t rel_cap = 0, rel_tmp_cap = 0;  // capacities of rel_cols / rel_tmp (swapped by the incremental path)
   // incremental view (relation_delta): the view is valid for the state after pass `rel_passes`
-  uint32_t *rel_rp2 = nullptr, *rel_dn = nullptr, *rel_dcur = nullptr, *rel_dch = nullptr, *rel_flag = nullptr;
+  uint32_t *rel_rp2 = nullptr, *rel_dn = nullptr, *rel_dcur = nullptr, *rel_dch = nullptr, *rel_flag = nullptr;  // rel_dcur, rel_flag: inside rel_dn's allocation
   uint64_t rel_dch_cap = 0;  // changes rel_dch (and its row array behind it) hold
   bool rel_valid = false;
   uint64_t rel_passes = 0, rel_nnz = 0;
@@ -725,13 +725,8 @@ uint32_t publish_seq(gwaoi_mgr* m, bool copy_events) {
   return ++m->pub_seq ? m->pub_seq : ++m->pub_seq;  // never 0 (the initial value)
 }
 
-int finish_pass(gwaoi_mgr* m, uint32_t seq) {
+int wait_pub(gwaoi_mgr* m, uint32_t seq) {
   hipStream_t st = m->stream;
-  if (!seq) {
-    HIPCHK(hipMemcpyAsync(m->h_ctr, m->ctr, gw::CTR_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return GWAOI_OK;
-  }
   volatile uint32_t* flag = m->h_pub + gw::kPubWords;
   for (uint64_t spin = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++spin) {
     if ((spin & 0xFFFF) == 0) {
@@ -747,7 +742,40 @@ int finish_pass(gwaoi_mgr* m, uint32_t seq) {
     }
     __builtin_ia32_pause();
   }
+  return GWAOI_OK;
+}
+
+int finish_pass(gwaoi_mgr* m, uint32_t seq) {
+  hipStream_t st = m->stream;
+  if (!seq) {
+    HIPCHK(hipMemcpyAsync(m->h_ctr, m->ctr, gw::CTR_N * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return GWAOI_OK;
+  }
+  RCHK(wait_pub(m, seq));
   std::memcpy(m->h_ctr, m->h_pub, gw::kPubWords * sizeof(uint32_t));
+  return GWAOI_OK;
+}
+
+#ifndef GW_RD_MAPPED
+#define GW_RD_MAPPED 1
+#endif
+// Device words a[0, na) and b[0, nb) to the host, every kernel launched before complete: through the
+// publication buffer (a one-thread kernel, the host spins on the sequence word) when there is one,
+// else DMA copies and a stream synchronisation. The relation's size read-backs between its launches.
+int read_words(gwaoi_mgr* m, const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* out) {
+  hipStream_t st = m->stream;
+  if (GW_RD_MAPPED && m->h_pub && na + nb <= (uint32_t)gw::kPubWords) {
+    const uint32_t seq = ++m->pub_seq ? m->pub_seq : ++m->pub_seq;
+    gw::launch_publish_words(a, na, b, nb, m->d_pub, seq, st);
+    HIPCHK(hipGetLastError());
+    RCHK(wait_pub(m, seq));
+    std::memcpy(out, m->h_pub, (na + nb) * sizeof(uint32_t));
+    return GWAOI_OK;
+  }
+  if (na) HIPCHK(hipMemcpyAsync(out, a, na * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (nb) HIPCHK(hipMemcpyAsync(out + na, b, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   return GWAOI_OK;
 }
 
@@ -1478,7 +1506,7 @@ void free_all(gwaoi_mgr* m) {
                    m->key_of, m->local_of, m->d_op_slot, m->d_op_space, m->d_leaves, m->d_dense, m->d_op_x, m->d_op_z,
                    m->d_op_kind, m->rank_cnt, m->uns, m->part, m->thist, m->ttot, m->tstart, m->ctr_buf, m->ev_tmp, m->ev_out,
                    m->rel_rp, m->rel_cols, m->rel_tmp, m->tile_walk, m->tile_acted, m->band_xk, m->band_zi, m->band_hd, m->band_dense2, m->band_tab, m->ov_tag, m->ov_idx, m->ov_rec, m->ov_count, m->tile_ev, m->tile_ent, m->rel_tot, m->rel_tstat, m->rel_slab, m->rel_fix,
-                   m->rel_rp2, m->rel_dn, m->rel_dcur, m->rel_dch, m->rel_flag, m->d_pin_first, m->d_pin_out,
+                   m->rel_rp2, m->rel_dn, m->rel_dch, m->d_pin_first, m->d_pin_out,
                    m->d_pin_seen, m->d_pin_ext, m->d_pin_n, m->d_size_tiles, m->dx_keys, m->dx_cnt, m->dx_last, m->dx_slot, m->dx_flags,
                    m->dx_part, m->dx_out};
   for (void* p : dptrs)
@@ -2188,9 +2216,11 @@ int relation_delta(gwaoi_mgr* m, bool* done) {
   if (bound > m->index_limit) return GWAOI_OK;
   const size_t n1 = (size_t)m->cap + 1;
   if (!m->rel_rp2) RCHK(dalloc(&m->rel_rp2, n1));
-  if (!m->rel_dn) RCHK(dalloc(&m->rel_dn, n1));
-  if (!m->rel_dcur) RCHK(dalloc(&m->rel_dcur, n1));
-  if (!m->rel_flag) RCHK(dalloc(&m->rel_flag, 2));  // [0] flag, [1] long rows
+  if (!m->rel_dn) {  // one allocation, zeroed by one memset: change counts, row cursors, flags
+    RCHK(dalloc(&m->rel_dn, 2 * n1 + 2));
+    m->rel_dcur = m->rel_dn + n1;
+    m->rel_flag = m->rel_dn + 2 * n1;  // [0] flag, [1] long rows
+  }
   if (2 * nev > m->rel_dch_cap) {
     if (m->rel_dch) hipFree(m->rel_dch);
     m->rel_dch = nullptr;
@@ -2226,17 +2256,14 @@ int relation_delta(gwaoi_mgr* m, bool* done) {
   a.longrows = m->rel_dch + 3 * m->rel_dch_cap;
   a.nlong = m->rel_flag + 1;
   a.long_cap = (uint32_t)(m->rel_dch_cap / 32 + 1);
-  HIPCHK(hipMemsetAsync(m->rel_dn, 0, n1 * sizeof(uint32_t), st));
-  HIPCHK(hipMemsetAsync(m->rel_dcur, 0, n1 * sizeof(uint32_t), st));
-  HIPCHK(hipMemsetAsync(m->rel_flag, 0, 2 * sizeof(uint32_t), st));
+  HIPCHK(hipMemsetAsync(m->rel_dn, 0, (2 * n1 + 2) * sizeof(uint32_t), st));
   gw::launch_rel_delta_count(a, st);
   gw::launch_scan(m->scan, m->rel_dn, m->cap + 1, st);
   gw::launch_rel_delta_apply(a, m->scan, st);
   HIPCHK(hipGetLastError());
-  uint32_t flag = 0, nnz_new = 0;
-  HIPCHK(hipMemcpyAsync(&flag, m->rel_flag, sizeof flag, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&nnz_new, m->rel_rp2 + m->cap, sizeof nnz_new, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  uint32_t w[2] = {0, 0};
+  RCHK(read_words(m, m->rel_flag, 1, m->rel_rp2 + m->cap, 1, w));
+  const uint32_t flag = w[0], nnz_new = w[1];
   m->rel_why = 7;
   if (flag) return GWAOI_OK;
   m->rel_why = 8;
@@ -2368,8 +2395,8 @@ int gwaoi_relation_device(gwaoi_mgr* m, gwaoi_relation_view* out) {
   HIPCHK(hipMemsetAsync(m->rel_tot, 0, 3 * sizeof(unsigned long long), st));
   gw::launch_relation(a, st);
   unsigned long long tot[2] = {0, 0};
-  HIPCHK(hipMemcpyAsync(tot, m->rel_tot, sizeof tot, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  RCHK(read_words(m, reinterpret_cast<const uint32_t*>(m->rel_tot), 4, nullptr, 0,
+                  reinterpret_cast<uint32_t*>(tot)));
   const unsigned long long total64 = tot[0];
   const uint32_t maxlen = (uint32_t)tot[1];
   if (total64 > m->index_limit) {  // row_ptr is uint32: a scan past 2^32 - 1 would wrap
