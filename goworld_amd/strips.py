@@ -133,9 +133,12 @@ class StripNode:
         self.cap = min(cap, n) if n else 1
         self.left = torch.zeros((self.cap, 4), dtype=i32, device=dev)
         self.right = torch.zeros((self.cap, 4), dtype=i32, device=dev)
-        self.counts = torch.zeros(4, dtype=i32, device=dev)  # [left, right, n_ops, err]
+        # the node's counters in one device block, read back by ONE copy per tick into one pinned block:
+        # [0, 4) counts [left, right, n_ops, err], [4, 8) local-slot counters, [8, 16) region-state counters
+        self.ctrs = torch.zeros(16, dtype=i32, device=dev)
+        self.h_ctrs = torch.zeros(16, dtype=i32).pin_memory()
+        self.counts, self.h_counts = self.ctrs[0:4], self.h_ctrs[0:4]  # h_counts: read after each tick, no extra sync
         self.left_in, self.right_in, self.counts_in = None, None, None  # RCCL receive buffers (tick_rccl)
-        self.h_counts = torch.zeros(4, dtype=i32).pin_memory()  # read after each tick, no extra sync
         self.scratch = torch.zeros(int(self._L.gwaoi_strip_scratch_words(n)), dtype=i32, device=dev)
         # a stream of the node's own (never the null stream: the manager would take that as "its
         # own stream" and the strip kernels and the pipeline would no longer be ordered)
@@ -174,8 +177,7 @@ class StripNode:
             self.l2g = torch.zeros(self.cap_l, dtype=i32, device=dev)
             self.fq = torch.empty(ring, dtype=i32, device=dev)
             self.pend = torch.empty(self.cap_l, dtype=i32, device=dev)
-            self.lctr = torch.zeros(4, dtype=i32, device=dev)
-            self.h_lctr = torch.zeros(4, dtype=i32).pin_memory()
+            self.lctr, self.h_lctr = self.ctrs[4:8], self.h_ctrs[4:8]
             torch.cuda.synchronize(dev)
             if region_state:
                 cn = max(1, min(int(cap_new), 8 * (int(sort_chunk) or 16384)))
@@ -184,8 +186,7 @@ class StripNode:
                 self.nw = torch.zeros(2 * cn, dtype=i32, device=dev)
                 self.lv = torch.zeros(cn, dtype=i32, device=dev)
                 self.srt = torch.zeros(3 * cn, dtype=i32, device=dev)
-                self.rctr = torch.zeros(8, dtype=i32, device=dev)
-                self.h_rctr = torch.zeros(8, dtype=i32).pin_memory()
+                self.rctr, self.h_rctr = self.ctrs[8:16], self.h_ctrs[8:16]
                 R = _lib.StripRegion()
                 for f in ("flags", "sx", "sz", "ex", "ez", "g2l", "l2g", "fq", "pend", "lctr", "nw", "lv", "srt",
                           "scratch"):
@@ -212,16 +213,25 @@ class StripNode:
         # (scripts/strips_loopback_bench.py): hipEvents on the node's stream, read by strip_kernel_ms()
         self.timing = False
         self.sev = []
+        # the ctypes arguments that never change, built once (the per-tick calls' host time is the gap
+        # between the strip kernels on the stream)
+        self._c_s = ctypes.c_void_p(self.stream.cuda_stream)
+        self._c_g = ctypes.byref(self.g)
+        self._c_err = ctypes.c_void_p(self.counts.data_ptr() + 12)
+        self._c_R = ctypes.byref(self.R) if self.R is not None else None
+        self._c_sel = (_ptr(self.left), _ptr(self.right), self.cap, ctypes.c_void_p(self.counts.data_ptr()))
+        self._c_ops = (_ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds),
+                       ctypes.c_void_p(self.counts.data_ptr() + 8))
 
     # ---- raw kernel calls ----
     def _s(self):
-        return ctypes.c_void_p(self.stream.cuda_stream)
+        return self._c_s
 
     def _g(self):
-        return ctypes.byref(self.g)
+        return self._c_g
 
     def _err(self):
-        return ctypes.c_void_p(self.counts.data_ptr() + 12)
+        return self._c_err
 
     def _emit_and_tick(self, host_events: bool, n_bound: int, start=None):
         """The op list goes to the manager with its count in device memory (no host round trip);
@@ -231,26 +241,22 @@ class StripNode:
         common = (self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.sz), _ptr(self.ex), _ptr(self.ez),
                   _ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds), _ptr(self.scratch),
                   ctypes.c_void_p(self.counts.data_ptr() + 8))
-        ops = (_ptr(self.ids), _ptr(self.ox), _ptr(self.oz), _ptr(self.kinds), ctypes.c_void_p(self.counts.data_ptr() + 8))
+        ops = self._c_ops
         if self.R is not None:
             if start is not None:
-                check(L.gwaoi_strip_region_start(self._s(), self._g(), ctypes.byref(self.R), *(_ptr(a) for a in start),
-                                                 *ops))
+                check(L.gwaoi_strip_region_start(self._s(), self._g(), self._c_R, *(_ptr(a) for a in start), *ops))
             else:
-                check(L.gwaoi_strip_region_emit(self._s(), self._g(), ctypes.byref(self.R), *ops))
-            self.h_lctr.copy_(self.lctr, non_blocking=True)
-            self.h_rctr.copy_(self.rctr, non_blocking=True)
+                check(L.gwaoi_strip_region_emit(self._s(), self._g(), self._c_R, *ops))
         elif self.local:
             check(L.gwaoi_strip_emit_local(*common, _ptr(self.g2l), _ptr(self.l2g), _ptr(self.fq), _ptr(self.pend),
                                            self.cap_l, _ptr(self.lctr)))
-            self.h_lctr.copy_(self.lctr, non_blocking=True)
         else:
             check(L.gwaoi_strip_emit(*common))
+        self.h_ctrs.copy_(self.ctrs, non_blocking=True)  # every counter, stream-ordered before the tick's kernels
         f1 = self._mark()
         if f1 is not None and getattr(self, "_f0", None) is not None and getattr(self, "_ev_prep", (None, None))[1]:
             self.sev.append((self._ev_prep[0], self._ev_prep[1], self._f0, f1))
         self._f0 = None
-        self.h_counts.copy_(self.counts, non_blocking=True)  # stream-ordered before the tick's kernels
         n_bound = max(1, min(self.cap_l if self.local else self.n, int(n_bound)))
         self.eng.stage_ops_device(self.ids.data_ptr(), self.ox.data_ptr(), self.oz.data_ptr(),
                                   self.kinds.data_ptr(), n_bound, d_count=self.counts.data_ptr() + 8)
@@ -348,7 +354,7 @@ class StripNode:
     def _walk(self, t, step):
         L = self._L
         if self.R is not None:
-            check(L.gwaoi_strip_region_walk(self._s(), self._g(), ctypes.byref(self.R), ctypes.c_uint64(self.seed),
+            check(L.gwaoi_strip_region_walk(self._s(), self._g(), self._c_R, ctypes.c_uint64(self.seed),
                                             ctypes.c_uint64(t), ctypes.c_float(self.layout.L), ctypes.c_float(step),
                                             self._err()))
         else:
@@ -371,9 +377,7 @@ class StripNode:
         if not (self.g.has_left or self.g.has_right):  # a one-strip world: nothing to send (counts stay 0)
             return
         if self.R is not None:
-            check(L.gwaoi_strip_region_select(self._s(), self._g(), ctypes.byref(self.R), _ptr(self.left),
-                                              _ptr(self.right), self.cap, ctypes.c_void_p(self.counts.data_ptr()),
-                                              self._err()))
+            check(L.gwaoi_strip_region_select(self._s(), self._g(), self._c_R, *self._c_sel, self._err()))
         else:
             check(L.gwaoi_strip_select(self._s(), self._g(), _ptr(self.flags), _ptr(self.sx), _ptr(self.ex),
                                        _ptr(self.ez), _ptr(self.left), _ptr(self.right), self.cap,
@@ -412,7 +416,6 @@ class StripNode:
         (n, 2) host array of the owned movers' events in canonical order."""
         self.stream.wait_stream(torch.cuda.current_stream(self.device))  # received on the caller's stream
         with torch.cuda.stream(self.stream):
-            f0 = self._mark()
             nin = 0
             got = []
             for recs in (left_in, right_in):
@@ -423,10 +426,11 @@ class StripNode:
                     got.append(recs)
                 else:
                     got.append(None)
+            f0 = self._mark()  # (from the first strip kernel's launch)
             if self.R is not None and any(g is not None for g in got):  # both messages, one launch
                 (a, b) = got
                 check(self._L.gwaoi_strip_region_absorb2(
-                    self._s(), ctypes.byref(self.R), _ptr(a) if a is not None else None, None,
+                    self._s(), self._c_R, _ptr(a) if a is not None else None, None,
                     int(a.shape[0]) if a is not None else 0, _ptr(b) if b is not None else None, None,
                     int(b.shape[0]) if b is not None else 0, None))
             elif self.R is None:
